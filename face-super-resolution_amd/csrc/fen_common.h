@@ -1,0 +1,152 @@
+// Shared device helpers for the FaceEnhanceNet gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fen.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// Per-dtype constants.  Every LDS "panel" row is 128 B: 64 bf16 or 32 f32 channels.
+template <typename T> struct Tr;
+template <> struct Tr<float> { static constexpr int CK = 32; static constexpr int EPC = 4; };
+template <> struct Tr<bf16>  { static constexpr int CK = 64; static constexpr int EPC = 8; };
+
+// Byte offset of 16-B chunk `chunk` (0..7) of row `p` in a 128-B-row LDS image.  The XOR
+// key (p>>1)&7 puts 16 consecutive rows read at the same chunk on 16 distinct 16-B slots
+// of the 256-B bank row, so ds_read_b128 fragment reads are conflict-free.
+__device__ __forceinline__ int swz(int p, int chunk) {
+    return (p << 7) + ((chunk ^ ((p >> 1) & 7)) << 4);
+}
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(((unsigned)u) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+    bf16 h = (bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN-preserving
+    return __builtin_bit_cast(unsigned short, h);
+}
+
+template <typename T> __device__ __forceinline__ float tof(T v);
+template <> __device__ __forceinline__ float tof<float>(float v) { return v; }
+template <> __device__ __forceinline__ float tof<bf16>(bf16 v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T fromf(float v);
+template <> __device__ __forceinline__ float fromf<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 fromf<bf16>(float v) { return (bf16)v; }
+
+// 4 consecutive elements <-> float[4]
+template <typename T> __device__ __forceinline__ void ld4(const void* p, float v[4]);
+template <> __device__ __forceinline__ void ld4<float>(const void* p, float v[4]) {
+    float4 x = *(const float4*)p;
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+}
+template <> __device__ __forceinline__ void ld4<bf16>(const void* p, float v[4]) {
+    uint2 x = *(const uint2*)p;
+    v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+    v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+}
+template <typename T> __device__ __forceinline__ void st4(void* p, const float v[4]);
+template <> __device__ __forceinline__ void st4<float>(void* p, const float v[4]) {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> __device__ __forceinline__ void st4<bf16>(void* p, const float v[4]) {
+    uint2 x;
+    x.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    x.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    *(uint2*)p = x;
+}
+
+// 16-B vector of EPC elements <-> float[EPC]
+template <typename T> __device__ __forceinline__ void unpack16(const uint4& u, float* v);
+template <> __device__ __forceinline__ void unpack16<float>(const uint4& u, float* v) {
+    v[0] = __uint_as_float(u.x); v[1] = __uint_as_float(u.y);
+    v[2] = __uint_as_float(u.z); v[3] = __uint_as_float(u.w);
+}
+template <> __device__ __forceinline__ void unpack16<bf16>(const uint4& u, float* v) {
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+template <typename T> __device__ __forceinline__ uint4 pack16(const float* v);
+template <> __device__ __forceinline__ uint4 pack16<float>(const float* v) {
+    return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                      __float_as_uint(v[3]));
+}
+template <> __device__ __forceinline__ uint4 pack16<bf16>(const float* v) {
+    uint4 u;
+    u.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    u.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    u.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+    u.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+    return u;
+}
+
+// acc += A * B for one 16-byte fragment pair: one 16x16x32 bf16 MFMA, or four
+// 16x16x4 f32 MFMAs (exact f32; element s of the 16 B is the k-step s).
+template <typename T> __device__ __forceinline__ void mma16(f32x4& acc, const uint4& a, const uint4& b);
+template <> __device__ __forceinline__ void mma16<bf16>(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+template <> __device__ __forceinline__ void mma16<float>(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Keys cubic convolution, A = -0.75 (torch upsample_bicubic2d coefficients)
+__device__ __forceinline__ void cubic_coeffs(float t, float c[4]) {
+    const float A = -0.75f;
+    float x1 = t + 1.0f;
+    c[0] = ((A * x1 - 5.0f * A) * x1 + 8.0f * A) * x1 - 4.0f * A;
+    c[1] = ((A + 2.0f) * t - (A + 3.0f)) * t * t + 1.0f;
+    float x2 = 1.0f - t;
+    c[2] = ((A + 2.0f) * x2 - (A + 3.0f)) * x2 * x2 + 1.0f;
+    float x3 = 2.0f - t;
+    c[3] = ((A * x3 - 5.0f * A) * x3 + 8.0f * A) * x3 - 4.0f * A;
+}
+
+// Bicubic sample of plane img[hin][win] at output (oy, ox) for resize scale 1/inv_scale,
+// align_corners=False, border-clamped taps; rows interpolated along x first, then along y.
+__device__ __forceinline__ float bicubic_sample(const float* img, int hin, int win, int oy, int ox,
+                                                float inv_scale) {
+    float sy = ((float)oy + 0.5f) * inv_scale - 0.5f;
+    float sx = ((float)ox + 0.5f) * inv_scale - 0.5f;
+    float fy = floorf(sy), fx = floorf(sx);
+    float cy[4], cx[4];
+    cubic_coeffs(sy - fy, cy);
+    cubic_coeffs(sx - fx, cx);
+    int iy = (int)fy, ix = (int)fx;
+    int xs[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xs[j] = min(max(ix - 1 + j, 0), win - 1);
+    float out = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float* row = img + (size_t)min(max(iy - 1 + i, 0), hin - 1) * win;
+        float r = row[xs[0]] * cx[0] + row[xs[1]] * cx[1] + row[xs[2]] * cx[2] + row[xs[3]] * cx[3];
+        out += r * cy[i];
+    }
+    return out;
+}
+
+#define FEN_CHECK_LAUNCH()                                    \
+    do {                                                      \
+        if (hipGetLastError() != hipSuccess) return FEN_EHIP; \
+    } while (0)

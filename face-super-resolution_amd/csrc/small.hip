@@ -1,0 +1,704 @@
+// Bandwidth-bound kernels of the FaceEnhanceNet hot path (gfx950): conv_first (K=27),
+// conv_last data-gradient (K=27) fused with PReLU backward + PixelShuffle inverse, the
+// channel-attention (SE) forward/backward pieces, the bicubic /4 LR synthesis, weight
+// packing, deterministic column reductions and the fused clip_grad_norm_ + AdamW.
+// All vector accesses are 16 B per lane.
+#include "fen_common.h"
+
+namespace {
+
+inline int nblk(size_t n, int t = 256) { return (int)((n + t - 1) / t); }
+
+// ------------------------------ conv_first (3 -> C) ------------------------------
+// reference custom.py:91-94,164; thread per (pixel, 8 output channels)
+template <typename T>
+__global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
+                             const float* __restrict__ w, const float* __restrict__ bias, T* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) float sw[];  // [Ci*9][C]
+    const int K = Ci * 9;
+    for (int i = threadIdx.x; i < K * C; i += blockDim.x) {
+        const int co = i % C, k = i / C;            // k = ci*9 + tap
+        sw[i] = w[(size_t)co * K + k];
+    }
+    __syncthreads();
+    const int G = C / 8;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)B * H * W * G) return;
+    const int g = (int)(idx % G);
+    const size_t px = idx / G;
+    const int wq = (int)(px % W), hq = (int)((px / W) % H), b = (int)(px / ((size_t)W * H));
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = bias[g * 8 + j];
+    for (int ci = 0; ci < Ci; ++ci) {
+        const float* xp = x + ((size_t)b * Ci + ci) * H * W;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int hh = hq + t / 3 - 1, ww = wq + t % 3 - 1;
+            const float v = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? xp[(size_t)hh * W + ww] : 0.f;
+            const float4* wp = (const float4*)(sw + (ci * 9 + t) * C + g * 8);
+            const float4 w0 = wp[0], w1 = wp[1];
+            acc[0] += v * w0.x; acc[1] += v * w0.y; acc[2] += v * w0.z; acc[3] += v * w0.w;
+            acc[4] += v * w1.x; acc[5] += v * w1.y; acc[6] += v * w1.z; acc[7] += v * w1.w;
+        }
+    }
+    char* o = (char*)y + (px * C + g * 8) * sizeof(T);
+    if constexpr (sizeof(T) == 2) {
+        *(uint4*)o = pack16<bf16>(acc);
+    } else {
+        *(uint4*)o = pack16<float>(acc);
+        *(uint4*)(o + 16) = pack16<float>(acc + 4);
+    }
+}
+
+// conv_first weight gradient: wave = one pixel at a time (uniform x loads), lane = co
+constexpr int CF_BLOCKS = 512;
+template <typename T>
+__global__ __launch_bounds__(256) void k_conv_first_wgrad(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
+                                   const T* __restrict__ dy, float* __restrict__ part) {
+    __shared__ float red[4][28 * 2][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float acc[2][28];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int k = 0; k < 28; ++k) acc[j][k] = 0.f;
+    const size_t npx = (size_t)B * H * W;
+    const int nc = (C + 63) / 64;
+    for (size_t px = (size_t)blockIdx.x * 4 + wave; px < npx; px += (size_t)gridDim.x * 4) {
+        const size_t pu = __builtin_amdgcn_readfirstlane((unsigned)px);
+        const int wq = (int)(pu % W), hq = (int)((pu / W) % H), b = (int)(pu / ((size_t)W * H));
+        float g[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int co = lane + 64 * j;
+            g[j] = (j < nc && co < C) ? tof<T>(dy[pu * C + co]) : 0.f;
+        }
+        for (int ci = 0; ci < Ci; ++ci) {
+            const float* xp = x + ((size_t)b * Ci + ci) * H * W;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int hh = hq + t / 3 - 1, ww = wq + t % 3 - 1;
+                const float v = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? xp[(size_t)hh * W + ww] : 0.f;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[j][ci * 9 + t] += g[j] * v;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j][27] += g[j];
+    }
+    for (int j = 0; j < nc; ++j)
+        for (int k = 0; k < 28; ++k) red[wave][j * 28 + k][lane] = acc[j][k];
+    __syncthreads();
+    for (int i = threadIdx.x; i < nc * 28 * 64; i += 256) {
+        const int lanei = i & 63, jk = i >> 6;
+        const float s = red[0][jk][lanei] + red[1][jk][lanei] + red[2][jk][lanei] + red[3][jk][lanei];
+        const int j = jk / 28, k = jk % 28, co = lanei + 64 * j;
+        if (co < C) part[((size_t)blockIdx.x * 28 + k) * C + co] = s;
+    }
+}
+
+__global__ void k_conv_first_finalize(int nb, int Ci, int C, const float* part, float* dw, float* db, int accum) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over 28*C
+    if (i >= 28 * C) return;
+    const int k = i / C, co = i % C;
+    if (k >= Ci * 9 && k != 27) return;
+    float s = 0.f;
+    for (int r = 0; r < nb; ++r) s += part[((size_t)r * 28 + k) * C + co];
+    if (k == 27) {
+        if (db) db[co] = accum ? db[co] + s : s;
+    } else {
+        float* o = dw + (size_t)co * Ci * 9 + k;
+        *o = accum ? *o + s : s;
+    }
+}
+
+// --------------- conv_last dgrad + PReLU backward + PixelShuffle inverse ---------------
+// dout NHWC16 [B,H,W,16], w [Co][C][3][3] -> da[px][c] -> dv = da*(pre>0?1:alpha[c])
+// -> du[b][h/2][w/2][4c + 2(h&1) + (w&1)];  block = 16x16 source px = 8x8 du px
+template <typename T>
+__global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, int C, int Co, const T* __restrict__ dout,
+                                  const float* __restrict__ w, const T* __restrict__ pre,
+                                  const float* __restrict__ alpha, T* __restrict__ du, float* __restrict__ part) {
+    __shared__ float4 sd[18 * 18];          // dout tile + halo, channels 0..2 (3 = pad)
+    __shared__ float sdal[256 * 2];
+    const int tid = threadIdx.x;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
+    const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+    for (int i = tid; i < 18 * 18; i += 256) {
+        const int r = i / 18, c = i % 18;
+        const int gh = h0 + r - 1, gw = w0 + c - 1;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) {
+            float t4[4];
+            ld4<T>((const char*)dout + ((size_t)(b * H + gh) * W + gw) * 16 * sizeof(T), t4);
+            v = make_float4(t4[0], Co > 1 ? t4[1] : 0.f, Co > 2 ? t4[2] : 0.f, 0.f);
+        }
+        sd[i] = v;
+    }
+    const int K2 = C / 2;
+    const int k = tid % K2;                 // channel pair (2k, 2k+1), fixed per thread
+    float wr[2][3][9];
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int co = 0; co < 3; ++co)
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                wr[e][co][t] = co < Co ? w[((size_t)co * C + 2 * k + e) * 9 + t] : 0.f;
+    const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
+    __syncthreads();
+    float dal0 = 0.f, dal1 = 0.f;
+    const int Hh = H >> 1, Wh = W >> 1;
+    for (int i = tid; i < 64 * K2; i += 256) {
+        const int dp = i / K2;
+        const int hh = dp >> 3, ww = dp & 7;
+        const int gh2 = (h0 >> 1) + hh, gw2 = (w0 >> 1) + ww;
+        if (gh2 >= Hh || gw2 >= Wh) continue;
+        float out[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int sh = 2 * hh + (t >> 1), sw = 2 * ww + (t & 1);   // local source pixel
+            float da0 = 0.f, da1 = 0.f;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const float4 g = sd[(sh - kh + 2) * 18 + (sw - kw + 2)];
+                    const int tp = kh * 3 + kw;
+                    da0 += g.x * wr[0][0][tp] + g.y * wr[0][1][tp] + g.z * wr[0][2][tp];
+                    da1 += g.x * wr[1][0][tp] + g.y * wr[1][1][tp] + g.z * wr[1][2][tp];
+                }
+            const size_t pi = ((size_t)(b * H + h0 + sh) * W + w0 + sw) * C + 2 * k;
+            const float p0 = tof<T>(pre[pi]), p1 = tof<T>(pre[pi + 1]);
+            dal0 += p0 > 0.f ? 0.f : da0 * p0;
+            dal1 += p1 > 0.f ? 0.f : da1 * p1;
+            out[t] = p0 > 0.f ? da0 : da0 * al0;
+            out[4 + t] = p1 > 0.f ? da1 : da1 * al1;
+        }
+        char* o = (char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 8 * k) * sizeof(T);
+        if constexpr (sizeof(T) == 2) {
+            *(uint4*)o = pack16<bf16>(out);
+        } else {
+            *(uint4*)o = pack16<float>(out);
+            *(uint4*)(o + 16) = pack16<float>(out + 4);
+        }
+    }
+    sdal[tid * 2] = dal0;
+    sdal[tid * 2 + 1] = dal1;
+    __syncthreads();
+    if (tid < C) {
+        const int kk = tid >> 1, e = tid & 1;
+        float s = 0.f;
+        for (int r = kk; r < 256; r += K2) s += sdal[r * 2 + e];
+        part[(size_t)blockIdx.x * C + tid] = s;
+    }
+}
+
+// ------------------------------- channel attention -------------------------------
+// blocks.py:83-92: mean -> fc0 (C->Cr, no bias) -> ReLU -> fc2 (Cr->C) -> sigmoid
+__global__ void k_se_fwd(int C, int Cr, int nparts, float inv_hw, const float* __restrict__ part,
+                         const float* __restrict__ w1, const float* __restrict__ w2, float* mean,
+                         float* hid, float* s) {
+    __shared__ float sm[512], sh[128];
+    const int b = blockIdx.x, t = threadIdx.x;
+    for (int c = t; c < C; c += blockDim.x) {
+        float a = 0.f;
+        for (int p = 0; p < nparts; ++p) a += part[((size_t)b * nparts + p) * C + c];
+        a *= inv_hw;
+        sm[c] = a;
+        if (mean) mean[(size_t)b * C + c] = a;
+    }
+    __syncthreads();
+    for (int j = t; j < Cr; j += blockDim.x) {
+        float a = 0.f;
+        for (int c = 0; c < C; ++c) a += w1[(size_t)j * C + c] * sm[c];
+        a = fmaxf(a, 0.f);
+        sh[j] = a;
+        if (hid) hid[(size_t)b * Cr + j] = a;
+    }
+    __syncthreads();
+    for (int c = t; c < C; c += blockDim.x) {
+        float a = 0.f;
+        for (int j = 0; j < Cr; ++j) a += w2[(size_t)c * Cr + j] * sh[j];
+        s[(size_t)b * C + c] = 1.f / (1.f + expf(-a));
+    }
+}
+
+// y = t * s[b,c] * rs + x   or (bwd)  dt = dy * s[b,c] * rs + g[b,c]
+template <typename T, bool BWD>
+__global__ void k_se_apply(size_t nvec, int HW, int C, const T* __restrict__ t, const float* __restrict__ s,
+                           float rs, const void* __restrict__ x, T* __restrict__ y) {
+    constexpr int V = 16 / sizeof(T);
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nvec) return;
+    const size_t e0 = i * V;
+    const int c0 = (int)(e0 % C);
+    const size_t b = e0 / ((size_t)HW * C);
+    float tv[V], o[V];
+    unpack16<T>(*(const uint4*)(t + e0), tv);
+    const float* sp = s + b * C + c0;
+    if constexpr (!BWD) {
+        float xv[V];
+        unpack16<T>(*(const uint4*)((const T*)x + e0), xv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = tv[j] * sp[j] * rs + xv[j];
+    } else {
+        const float* gp = (const float*)x + b * C + c0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = tv[j] * rs * sp[j] + gp[j];
+    }
+    *(uint4*)(y + e0) = pack16<T>(o);
+}
+
+// part[b][chunk][c] = sum over the chunk's pixels of a*b_ (or a)
+template <typename T>
+__global__ __launch_bounds__(256) void k_pool_dot(int HW, int C, int nchunk, const T* __restrict__ a,
+                                                  const T* __restrict__ bb, float* __restrict__ part) {
+    constexpr int V = 16 / sizeof(T);
+    __shared__ float red[256][V];
+    const int TP = C / V;                    // threads per pixel
+    const int R = 256 / TP;                  // pixels per iteration
+    const int tid = threadIdx.x, cv = tid % TP, pr = tid / TP;
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int per = (HW + nchunk - 1) / nchunk;
+    const int p0 = ch * per, p1 = min(p0 + per, HW);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+    if (pr < R) {
+        for (int p = p0 + pr; p < p1; p += R) {
+            const size_t e = ((size_t)b * HW + p) * C + cv * V;
+            float av[V];
+            unpack16<T>(*(const uint4*)(a + e), av);
+            if (bb) {
+                float bv[V];
+                unpack16<T>(*(const uint4*)(bb + e), bv);
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] += av[j] * bv[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] += av[j];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[tid][j] = acc[j];
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        const int cvv = c / V, j = c % V;
+        float sum = 0.f;
+        for (int r = 0; r < R; ++r) sum += red[r * TP + cvv][j];
+        part[((size_t)b * nchunk + ch) * C + c] = sum;
+    }
+}
+
+// SE backward for one image (block per b)
+__global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, const float* __restrict__ part,
+                         const float* __restrict__ mean, const float* __restrict__ hid, const float* __restrict__ s,
+                         const float* __restrict__ w1, const float* __restrict__ w2, float* g, float* dw1p,
+                         float* dw2p) {
+    __shared__ float dz[512], dh[128];
+    const int b = blockIdx.x, t = threadIdx.x;
+    for (int c = t; c < C; c += blockDim.x) {
+        float a = 0.f;
+        for (int p = 0; p < nparts; ++p) a += part[((size_t)b * nparts + p) * C + c];
+        const float sv = s[(size_t)b * C + c];
+        dz[c] = a * rs * sv * (1.f - sv);                 // through sigmoid
+    }
+    __syncthreads();
+    for (int j = t; j < Cr; j += blockDim.x) {
+        float a = 0.f;
+        for (int c = 0; c < C; ++c) a += w2[(size_t)c * Cr + j] * dz[c];
+        const float h = hid[(size_t)b * Cr + j];
+        dh[j] = h > 0.f ? a : 0.f;                         // through ReLU
+    }
+    __syncthreads();
+    for (int i = t; i < C * Cr; i += blockDim.x) {
+        const int c = i / Cr, j = i % Cr;
+        dw2p[(size_t)b * C * Cr + i] = dz[c] * hid[(size_t)b * Cr + j];          // [C][Cr]
+        const int jj = i / C, cc = i % C;
+        dw1p[(size_t)b * C * Cr + i] = dh[jj] * mean[(size_t)b * C + cc];        // [Cr][C]
+    }
+    for (int c = t; c < C; c += blockDim.x) {
+        float a = 0.f;
+        for (int j = 0; j < Cr; ++j) a += w1[(size_t)j * C + c] * dh[j];
+        g[(size_t)b * C + c] = a * inv_hw;
+    }
+}
+
+// ------------------------------ resampling / layout ------------------------------
+__global__ void k_bicubic_down4(int B, int C, int H, int W, const float* __restrict__ hr, float* __restrict__ lr) {
+    const int Ho = H / 4, Wo = W / 4;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)B * C * Ho * Wo) return;
+    const int ox = (int)(i % Wo), oy = (int)((i / Wo) % Ho);
+    const size_t plane = i / ((size_t)Wo * Ho);
+    lr[i] = bicubic_sample(hr + plane * H * W, H, W, oy, ox, 4.0f);
+}
+
+template <typename T>
+__global__ void k_nchw_to_nhwc(int B, int C, int H, int W, const float* __restrict__ x, T* __restrict__ y) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // NHWC order
+    if (i >= (size_t)B * C * H * W) return;
+    const int c = (int)(i % C);
+    const size_t px = i / C;
+    const int w = (int)(px % W), h = (int)((px / W) % H), b = (int)(px / ((size_t)W * H));
+    y[i] = fromf<T>(x[(((size_t)b * C + c) * H + h) * W + w]);
+}
+template <typename T>
+__global__ void k_nhwc_to_nchw(int B, int C, int H, int W, const T* __restrict__ x, float* __restrict__ y) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // NCHW order
+    if (i >= (size_t)B * C * H * W) return;
+    const int w = (int)(i % W), h = (int)((i / W) % H), c = (int)((i / ((size_t)W * H)) % C);
+    const size_t b = i / ((size_t)W * H * C);
+    y[i] = tof<T>(x[((b * H + h) * W + w) * C + c]);
+}
+
+template <typename T>
+__global__ void k_pack(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mode == 2) {  // [9][Cin_pad][Cout], row = ci, taps flipped
+        const int co = (int)(i % Cout);
+        const int ci = (int)((i / Cout) % ((Cin + 15) & ~15));
+        const int tap = (int)(i / ((size_t)Cout * ((Cin + 15) & ~15)));
+        const int kh = 2 - tap / 3, kw = 2 - tap % 3;
+        out[i] = fromf<T>(ci < Cin ? w[(((size_t)co * Cin + ci) * 3 + kh) * 3 + kw] : 0.f);
+    } else {          // [9][Cout_pad][Cin], row = co (mode 1: shuffle-permuted rows)
+        const int coutp = (Cout + 15) & ~15;
+        const int ci = (int)(i % Cin);
+        const int cp = (int)((i / Cin) % coutp);
+        const int tap = (int)(i / ((size_t)Cin * coutp));
+        int co = cp;
+        if (mode == 1) { const int Cq = Cout / 4; co = 4 * (cp % Cq) + cp / Cq; }
+        out[i] = fromf<T>(cp < Cout ? w[(((size_t)co * Cin + ci) * 3 + tap / 3) * 3 + tap % 3] : 0.f);
+    }
+}
+
+// ------------------------------ reductions / optimizer ------------------------------
+// stage 1: block (cb, rb) sums rows [rb*RB, rb*RB+RB) of 64 columns into row rb*RB (in place)
+constexpr int COLSUM_RB = 256;
+__global__ void k_colsum1(int rows, int cols, float* part) {
+    __shared__ float red[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    const int r0 = blockIdx.y * COLSUM_RB, r1 = min(r0 + COLSUM_RB, rows);
+    float s = 0.f;
+    if (c < cols)
+        for (int r = r0 + g; r < r1; r += 4) s += part[(size_t)r * cols + c];
+    red[g][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (g == 0 && c < cols) part[(size_t)r0 * cols + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void k_colsum2(int rows, int cols, const float* part, float scale, float* out, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    float s = 0.f;
+    for (int r = 0; r < rows; r += COLSUM_RB) s += part[(size_t)r * cols + c];
+    s *= scale;
+    out[c] = accumulate ? out[c] + s : s;
+}
+
+constexpr int SUMSQ_BLOCKS_MAX = 1024;
+__global__ void k_sumsq(size_t n, const float* __restrict__ g, float* part) {
+    __shared__ float red[4];
+    float s = 0.f;
+    const size_t n4 = n / 4;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 v = ((const float4*)g)[i];
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    if (blockIdx.x == 0)
+        for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += g[i] * g[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ void k_optim_prepare(int nparts, const float* part, float max_norm, float b1, float b2, float wd,
+                                float* scal) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += part[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+        float coef = 1.f;
+        if (max_norm > 0.f) coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+        const float step = scal[2] + 1.f;
+        const float lr = scal[3];
+        scal[0] = norm;
+        scal[1] = coef;
+        scal[2] = step;
+        scal[4] = 1.f - lr * wd;
+        scal[5] = lr / (1.f - powf(b1, step));
+        scal[6] = 1.f / sqrtf(1.f - powf(b2, step));
+    }
+}
+__global__ void k_adamw(size_t n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                        float* __restrict__ v, const float* __restrict__ scal, float b1, float b2, float eps) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float coef = scal[1], decay = scal[4], step_size = scal[5], rbc2 = scal[6];
+    const float gi = g[i] * coef;
+    float pi = p[i] * decay;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);    // lerp
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    const float denom = sqrtf(vi) * rbc2 + eps;
+    pi = pi - step_size * mi / denom;
+    p[i] = pi; m[i] = mi; v[i] = vi;
+}
+__global__ void k_scale(size_t n, float* y, float s) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] *= s;
+}
+
+}  // namespace
+
+// =================================== C-ABI ===================================
+#define STREAM ((hipStream_t)stream)
+
+extern "C" int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x, const float* w,
+                                  const float* bias, void* y, void* stream) {
+    if (!x || !w || !bias || !y || B <= 0 || Ci <= 0 || Ci > 3 || C % 8 || C > 128) return FEN_EINVAL;
+    const size_t n = (size_t)B * H * W * (C / 8);
+    const size_t lds = (size_t)Ci * 9 * C * sizeof(float);
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_conv_first<bf16>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias, (bf16*)y);
+    else if (dtype == FEN_F32)
+        hipLaunchKernelGGL(k_conv_first<float>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias, (float*)y);
+    else
+        return FEN_EINVAL;
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C) {
+    return (size_t)CF_BLOCKS * 28 * C;
+}
+
+extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const float* x, const void* dy,
+                                    float* dw, float* db, int accumulate, float* work, void* stream) {
+    if (!x || !dy || !dw || !work || Ci > 3 || C > 128 || B <= 0) return FEN_EINVAL;
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_conv_first_wgrad<bf16>, dim3(CF_BLOCKS), dim3(256), 0, STREAM, B, Ci, H, W, C, x,
+                           (const bf16*)dy, work);
+    else if (dtype == FEN_F32)
+        hipLaunchKernelGGL(k_conv_first_wgrad<float>, dim3(CF_BLOCKS), dim3(256), 0, STREAM, B, Ci, H, W, C, x,
+                           (const float*)dy, work);
+    else
+        return FEN_EINVAL;
+    FEN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_conv_first_finalize, dim3(nblk(28 * C)), dim3(256), 0, STREAM, CF_BLOCKS, Ci, C, work, dw,
+                       db, accumulate);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" size_t fen_conv_last_dgrad_part_rows(int B, int H, int W) {
+    return (size_t)B * ((H + 15) / 16) * ((W + 15) / 16);
+}
+
+extern "C" int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const void* dout, const float* w,
+                                   const void* pre, const float* alpha, void* du, float* part, void* stream) {
+    if (!dout || !w || !pre || !alpha || !du || !part || Co > 3 || C < 32 || C > 256 || 256 % (C / 2) || (H | W) & 1)
+        return FEN_EINVAL;
+    const int nb = (int)fen_conv_last_dgrad_part_rows(B, H, W);
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_conv_last_dgrad<bf16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co, (const bf16*)dout,
+                           w, (const bf16*)pre, alpha, (bf16*)du, part);
+    else if (dtype == FEN_F32)
+        hipLaunchKernelGGL(k_conv_last_dgrad<float>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co,
+                           (const float*)dout, w, (const float*)pre, alpha, (float*)du, part);
+    else
+        return FEN_EINVAL;
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_se_fwd(int B, int C, int Cr, int nparts, float inv_hw, const float* part, const float* w1,
+                          const float* w2, float* mean, float* hid, float* s, void* stream) {
+    if (!part || !w1 || !w2 || !s || C > 512 || Cr > 128 || B <= 0) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_se_fwd, dim3(B), dim3(256), 0, STREAM, C, Cr, nparts, inv_hw, part, w1, w2, mean, hid, s);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_se_apply(int dtype, int B, int HW, int C, const void* t, const float* s, float res_scale,
+                            const void* x, void* y, void* stream) {
+    if (!t || !s || !x || !y) return FEN_EINVAL;
+    const int V = dtype == FEN_BF16 ? 8 : 4;
+    if (C % V) return FEN_EUNSUPPORTED;
+    const size_t nvec = (size_t)B * HW * C / V;
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL((k_se_apply<bf16, false>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
+                           (const bf16*)t, s, res_scale, x, (bf16*)y);
+    else
+        hipLaunchKernelGGL((k_se_apply<float, false>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
+                           (const float*)t, s, res_scale, x, (float*)y);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" size_t fen_pool_parts(int HW) {
+    int n = HW / 256;
+    if (n < 1) n = 1;
+    if (n > 64) n = 64;
+    return (size_t)n;
+}
+
+extern "C" int fen_pool_dot(int dtype, int B, int HW, int C, const void* a, const void* b_, float* part,
+                            void* stream) {
+    const int V = dtype == FEN_BF16 ? 8 : 4;
+    if (!a || !part || C % V || C / V > 256) return FEN_EINVAL;
+    const int nchunk = (int)fen_pool_parts(HW);
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_pool_dot<bf16>, dim3(nchunk, B), dim3(256), 0, STREAM, HW, C, nchunk, (const bf16*)a,
+                           (const bf16*)b_, part);
+    else
+        hipLaunchKernelGGL(k_pool_dot<float>, dim3(nchunk, B), dim3(256), 0, STREAM, HW, C, nchunk, (const float*)a,
+                           (const float*)b_, part);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_se_bwd(int B, int C, int Cr, int nparts, float inv_hw, float res_scale, const float* part,
+                          const float* mean, const float* hid, const float* s, const float* w1, const float* w2,
+                          float* g, float* dw1p, float* dw2p, void* stream) {
+    if (!part || !mean || !hid || !s || !w1 || !w2 || !g || !dw1p || !dw2p || C > 512 || Cr > 128) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_se_bwd, dim3(B), dim3(256), 0, STREAM, C, Cr, nparts, inv_hw, res_scale, part, mean, hid, s,
+                       w1, w2, g, dw1p, dw2p);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy, const float* s, float res_scale,
+                                const float* g, void* dt, void* stream) {
+    if (!dy || !s || !g || !dt) return FEN_EINVAL;
+    const int V = dtype == FEN_BF16 ? 8 : 4;
+    if (C % V) return FEN_EUNSUPPORTED;
+    const size_t nvec = (size_t)B * HW * C / V;
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL((k_se_apply<bf16, true>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
+                           (const bf16*)dy, s, res_scale, (const void*)g, (bf16*)dt);
+    else
+        hipLaunchKernelGGL((k_se_apply<float, true>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
+                           (const float*)dy, s, res_scale, (const void*)g, (float*)dt);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, float* lr, void* stream) {
+    if (!hr || !lr || H < 4 || W < 4) return FEN_EINVAL;
+    const size_t n = (size_t)B * C * (H / 4) * (W / 4);
+    hipLaunchKernelGGL(k_bicubic_down4, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, hr, lr);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_colsum(int rows, int cols, const float* part, float scale, float* out, int accumulate,
+                          void* stream) {
+    if (!part || !out || rows <= 0 || cols <= 0) return FEN_EINVAL;
+    float* p = const_cast<float*>(part);  // stage 1 reduces in place (documented: part is clobbered)
+    hipLaunchKernelGGL(k_colsum1, dim3((cols + 63) / 64, (rows + COLSUM_RB - 1) / COLSUM_RB), dim3(256), 0, STREAM,
+                       rows, cols, p);
+    FEN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_colsum2, dim3(nblk(cols)), dim3(256), 0, STREAM, rows, cols, (const float*)p, scale, out,
+                       accumulate);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" size_t fen_packed_elems(int mode, int Cout, int Cin) {
+    if (mode == 2) return (size_t)9 * ((Cin + 15) & ~15) * Cout;
+    return (size_t)9 * ((Cout + 15) & ~15) * Cin;
+}
+
+extern "C" int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const float* w, void* out, void* stream) {
+    if (!w || !out || mode < 0 || mode > 2 || (mode == 1 && Cout % 4)) return FEN_EINVAL;
+    const size_t n = fen_packed_elems(mode, Cout, Cin);
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_pack<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, mode, Cout, Cin, w, (bf16*)out, n);
+    else if (dtype == FEN_F32)
+        hipLaunchKernelGGL(k_pack<float>, dim3(nblk(n)), dim3(256), 0, STREAM, mode, Cout, Cin, w, (float*)out, n);
+    else
+        return FEN_EINVAL;
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_nchw_to_nhwc(int dtype, int B, int C, int H, int W, const float* x, void* y, void* stream) {
+    if (!x || !y) return FEN_EINVAL;
+    const size_t n = (size_t)B * C * H * W;
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_nchw_to_nhwc<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, x, (bf16*)y);
+    else
+        hipLaunchKernelGGL(k_nchw_to_nhwc<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, x, (float*)y);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_nhwc_to_nchw(int dtype, int B, int C, int H, int W, const void* x, float* y, void* stream) {
+    if (!x || !y) return FEN_EINVAL;
+    const size_t n = (size_t)B * C * H * W;
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_nhwc_to_nchw<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, (const bf16*)x, y);
+    else
+        hipLaunchKernelGGL(k_nhwc_to_nchw<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, (const float*)x, y);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_sumsq_parts(size_t n) {
+    size_t b = (n / 4 + 255) / 256;
+    if (b < 1) b = 1;
+    if (b > SUMSQ_BLOCKS_MAX) b = SUMSQ_BLOCKS_MAX;
+    return (int)b;
+}
+
+extern "C" int fen_sumsq(size_t n, const float* g, float* part, void* stream) {
+    if (!g || !part || ((uintptr_t)g & 15)) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_sumsq, dim3(fen_sumsq_parts(n)), dim3(256), 0, STREAM, n, g, part);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_optim_prepare(int nparts, const float* part, float max_norm, float beta1, float beta2, float wd,
+                                 float* scal, void* stream) {
+    if (!part || !scal || nparts <= 0) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_optim_prepare, dim3(1), dim3(256), 0, STREAM, nparts, part, max_norm, beta1, beta2, wd, scal);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_adamw(size_t n, float* p, const float* g, float* m, float* v, const float* scal, float beta1,
+                         float beta2, float eps, void* stream) {
+    if (!p || !g || !m || !v || !scal) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_adamw, dim3(nblk(n)), dim3(256), 0, STREAM, n, p, g, m, v, scal, beta1, beta2, eps);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_scale(size_t n, float* y, float s, void* stream) {
+    if (!y) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_scale, dim3(nblk(n)), dim3(256), 0, STREAM, n, y, s);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" const char* fen_status_string(int code) {
+    switch (code) {
+        case FEN_OK: return "FEN_OK";
+        case FEN_EINVAL: return "FEN_EINVAL: invalid pointer, shape or alignment";
+        case FEN_EUNSUPPORTED: return "FEN_EUNSUPPORTED: configuration not implemented by the gfx950 kernels";
+        case FEN_EHIP: return "FEN_EHIP: HIP kernel launch failed";
+        default: return "FEN_?: unknown status";
+    }
+}
+
+extern "C" const char* fen_build_info(void) {
+    return "libfen_hip gfx950 (CDNA4) MFMA kernels, built " __DATE__ " " __TIME__;
+}

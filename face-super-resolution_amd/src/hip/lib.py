@@ -1,0 +1,114 @@
+"""ctypes binding of libfen_hip.so (include/fen.h) -- the only way the package reaches the GPU.
+
+The shared library is built in-tree (`face-super-resolution_amd/csrc/Makefile`, or
+`__graft_entry__.build()`).  There is no fallback: if the library is missing every HIP
+op raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_float, c_int, c_size_t, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FEN_HIP_LIB", os.path.join(_HERE, "libfen_hip.so"))
+
+F32, BF16 = 0, 1
+
+EPI_BIAS = 1
+EPI_PRELU = 2
+EPI_SHUFFLE = 4
+EPI_PRELU_BWD = 8
+EPI_UNSHUFFLE = 16
+EPI_POOL = 32
+EPI_LAST = 64
+
+
+class ConvDesc(Structure):
+    _fields_ = [
+        ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
+        ("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("epi", c_int), ("alpha", c_void_p),
+        ("y", c_void_p), ("y_pre", c_void_p), ("res", c_void_p * 3), ("pre_in", c_void_p),
+        ("part", c_void_p), ("lr", c_void_p), ("scale", c_int), ("clamp", c_int), ("hr", c_void_p),
+        ("dout", c_void_p), ("l1_scale", c_float), ("loss_part", c_void_p),
+    ]
+
+
+class WgradDesc(Structure):
+    _fields_ = [
+        ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
+        ("cout_valid", c_int), ("x", c_void_p), ("dy", c_void_p), ("dw", c_void_p), ("db", c_void_p),
+        ("accumulate", c_int), ("work", c_void_p),
+    ]
+
+
+_SIGS = {
+    "fen_conv3x3": (c_int, [POINTER(ConvDesc), c_void_p]),
+    "fen_wgrad_work_floats": (c_size_t, [POINTER(WgradDesc)]),
+    "fen_wgrad3x3": (c_int, [POINTER(WgradDesc), c_void_p]),
+    "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
+    "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),
+    "fen_conv_first_wgrad": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_int, c_void_p, c_void_p]),
+    "fen_conv_last_dgrad_part_rows": (c_size_t, [c_int] * 3),
+    "fen_conv_last_dgrad": (c_int, [c_int] * 6 + [c_void_p] * 6 + [c_void_p]),
+    "fen_se_fwd": (c_int, [c_int, c_int, c_int, c_int, c_float] + [c_void_p] * 6 + [c_void_p]),
+    "fen_se_apply": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
+    "fen_pool_parts": (c_size_t, [c_int]),
+    "fen_pool_dot": (c_int, [c_int] * 4 + [c_void_p] * 3 + [c_void_p]),
+    "fen_se_bwd": (c_int, [c_int] * 4 + [c_float, c_float] + [c_void_p] * 9 + [c_void_p]),
+    "fen_se_bwd_apply": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
+    "fen_bicubic_down4": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_void_p]),
+    "fen_colsum": (c_int, [c_int, c_int, c_void_p, c_float, c_void_p, c_int, c_void_p]),
+    "fen_pack_conv_w": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_void_p]),
+    "fen_packed_elems": (c_size_t, [c_int] * 3),
+    "fen_nchw_to_nhwc": (c_int, [c_int] * 5 + [c_void_p, c_void_p, c_void_p]),
+    "fen_nhwc_to_nchw": (c_int, [c_int] * 5 + [c_void_p, c_void_p, c_void_p]),
+    "fen_sumsq_parts": (c_int, [c_size_t]),
+    "fen_sumsq": (c_int, [c_size_t, c_void_p, c_void_p, c_void_p]),
+    "fen_optim_prepare": (c_int, [c_int, c_void_p, c_float, c_float, c_float, c_float, c_void_p, c_void_p]),
+    "fen_adamw": (c_int, [c_size_t] + [c_void_p] * 5 + [c_float, c_float, c_float, c_void_p]),
+    "fen_scale": (c_int, [c_size_t, c_void_p, c_float, c_void_p]),
+    "fen_status_string": (ctypes.c_char_p, [c_int]),
+    "fen_build_info": (ctypes.c_char_p, []),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+class FenError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes handle; raises FenError if the library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FenError(
+            f"libfen_hip.so not found at {LIB_PATH}: build it with `make -C face-super-resolution_amd/csrc` "
+            "or __graft_entry__.build(); the HIP backend has no fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(code: int, what: str = "") -> None:
+    if code != 0:
+        msg = load().fen_status_string(code).decode()
+        raise FenError(f"{what}: {msg} (status {code})")
+
+
+def dtype_code(torch_dtype) -> int:
+    import torch
+    if torch_dtype == torch.float32:
+        return F32
+    if torch_dtype == torch.bfloat16:
+        return BF16
+    raise FenError(f"unsupported compute dtype {torch_dtype}")

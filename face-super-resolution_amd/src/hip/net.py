@@ -1,0 +1,320 @@
+"""FaceEnhanceNet forward / backward as sequences of C-ABI launches.
+
+One builder, used two ways (program.Ctx): eagerly by the nn.Module autograd Functions
+(src/models) and recorded once into static programs by the training/inference engine
+(engine.py).  Activations are NHWC tensors of the compute dtype; parameters and their
+gradients are the reference's fp32 OIHW tensors, addressed by state_dict key.
+
+Reference structure followed (tomasz-pres/face-super-resolution):
+  FaceEnhanceNet.forward   src/models/custom.py:147-190
+  ResidualGroup.forward    src/models/blocks.py:185-189
+  RCAB.forward             src/models/blocks.py:135-153
+  ChannelAttention.forward src/models/blocks.py:75-92
+  PixelShuffleUpsample     src/models/blocks.py:223-227
+and their autograd backward (trainer.py:482-485).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import lib as L
+from .program import Ctx, byref, ptr
+
+
+@dataclass(frozen=True)
+class NetSpec:
+    C: int = 64
+    G: int = 3
+    NB: int = 4
+    Cr: int = 16
+    scale: int = 4
+    res_scale: float = 0.2
+    in_ch: int = 3
+    out_ch: int = 3
+
+    @property
+    def n_stages(self) -> int:
+        return int(round(math.log2(self.scale)))
+
+    @staticmethod
+    def from_config(cfg) -> "NetSpec":
+        # reduced channels rule of blocks.py:62
+        return NetSpec(C=cfg.num_channels, G=cfg.num_groups, NB=cfg.blocks_per_group,
+                       Cr=max(cfg.num_channels // cfg.reduction_ratio, 8), scale=cfg.scale_factor,
+                       res_scale=float(cfg.res_scale), in_ch=cfg.in_channels, out_ch=cfg.out_channels)
+
+
+def tiles(H: int, W: int) -> int:
+    return ((H + 15) // 16) * ((W + 15) // 16)
+
+
+class Weights:
+    """fp32 parameters (by state_dict key) + their packed kernel-layout copies."""
+
+    def __init__(self, params: Dict[str, torch.Tensor], dtype: torch.dtype, device):
+        self.p = params
+        self.dtype = dtype
+        self.device = device
+        self.packs: Dict[tuple, torch.Tensor] = {}
+        self.pack_ctx = Ctx(dtype, device, record=True)
+
+    def packed(self, key: str, mode: int) -> torch.Tensor:
+        k = (key, mode)
+        if k not in self.packs:
+            w = self.p[key + ".weight"]
+            cout, cin = int(w.shape[0]), int(w.shape[1])
+            lib = self.pack_ctx.lib
+            n = lib.fen_packed_elems(mode, cout, cin)
+            buf = torch.empty(n, dtype=self.dtype, device=self.device)
+            args = (L.dtype_code(self.dtype), mode, cout, cin, ptr(w), ptr(buf))
+            self.pack_ctx.emit("pack_conv_w", lib.fen_pack_conv_w, *args)
+            # pack now too, so a buffer is valid from the moment a builder sees it
+            L.check(lib.fen_pack_conv_w(*args, torch.cuda.current_stream().cuda_stream), "pack_conv_w")
+            self.packs[k] = buf
+        return self.packs[k]
+
+    def pack(self) -> None:
+        self.pack_ctx.run()
+
+
+# --------------------------------------------------------------------------------------
+# primitive emitters
+# --------------------------------------------------------------------------------------
+def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, y=None, y_pre=None,
+         res: Sequence = (), pre_in=None, part=None, lr=None, scale=0, clamp=0, hr=None, dout=None,
+         l1_scale=0.0, loss_part=None) -> None:
+    d = L.ConvDesc()
+    d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = ctx.code, B, H, W, Cin, Cout
+    d.x, d.w, d.bias = ptr(x), ptr(wpk), ptr(bias)
+    d.epi = epi | (L.EPI_BIAS if bias is not None else 0)
+    d.alpha, d.y, d.y_pre = ptr(alpha), ptr(y), ptr(y_pre)
+    for i, r in enumerate(res):
+        d.res[i] = ptr(r)
+    d.pre_in, d.part = ptr(pre_in), ptr(part)
+    d.lr, d.scale, d.clamp, d.hr, d.dout = ptr(lr), scale, clamp, ptr(hr), ptr(dout)
+    d.l1_scale, d.loss_part = float(l1_scale), ptr(loss_part)
+    ctx.emit("conv3x3", ctx.lib.fen_conv3x3, byref(d))
+
+
+def wgrad(ctx: Ctx, x, dy, B, H, W, Cin, Cout, dw, db, cout_valid=None) -> None:
+    d = L.WgradDesc()
+    d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = ctx.code, B, H, W, Cin, Cout
+    d.cout_valid = Cout if cout_valid is None else cout_valid
+    d.x, d.dy, d.dw, d.db, d.accumulate = ptr(x), ptr(dy), ptr(dw), ptr(db), 0
+    nwork = ctx.lib.fen_wgrad_work_floats(byref(d))
+    work = ctx.scratch("wgrad_work", (nwork,), torch.float32)
+    d.work = ptr(work)
+    ctx.emit("wgrad3x3", ctx.lib.fen_wgrad3x3, byref(d))
+
+
+def colsum(ctx: Ctx, part, rows, cols, out, scale=1.0) -> None:
+    ctx.emit("colsum", ctx.lib.fen_colsum, rows, cols, ptr(part), float(scale), ptr(out), 0)
+
+
+# --------------------------------------------------------------------------------------
+# forward
+# --------------------------------------------------------------------------------------
+class Forward:
+    """Builds the forward of FaceEnhanceNet; with `save=True` keeps what backward needs."""
+
+    def __init__(self, spec: NetSpec, ctx: Ctx, Wt: Weights, save: bool):
+        self.s, self.ctx, self.Wt, self.save = spec, ctx, Wt, save
+
+    def head(self, x: torch.Tensor) -> torch.Tensor:
+        """conv_first on the NCHW fp32 LR input (custom.py:164)."""
+        B, _, H, W = x.shape
+        s, ctx, p = self.s, self.ctx, self.Wt.p
+        feat = ctx.alloc((B, H, W, s.C))
+        ctx.emit("conv_first_fwd", ctx.lib.fen_conv_first_fwd, ctx.code, B, s.in_ch, H, W, s.C, ptr(x),
+                 ptr(p["conv_first.weight"]), ptr(p["conv_first.bias"]), ptr(feat))
+        return feat
+
+    def rcab(self, x: torch.Tensor, pre: str, out: Optional[torch.Tensor] = None):
+        """RCAB (blocks.py:135-153) -> (y, saved)."""
+        s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
+        B, H, W, C = x.shape
+        a1 = ctx.alloc(x.shape) if self.save else ctx.scratch("rcab_a1", x.shape)
+        z1 = ctx.alloc(x.shape) if self.save else None
+        conv(ctx, x, Wt.packed(pre + "conv1", 0), B, H, W, C, C, bias=p[pre + "conv1.bias"],
+             epi=L.EPI_PRELU, alpha=p[pre + "prelu.weight"], y=a1, y_pre=z1)
+        t = ctx.alloc(x.shape) if self.save else ctx.scratch("rcab_t", x.shape)
+        T = tiles(H, W)
+        part = ctx.scratch("pool_part", (B * T, C), torch.float32)
+        conv(ctx, a1, Wt.packed(pre + "conv2", 0), B, H, W, C, C, bias=p[pre + "conv2.bias"],
+             epi=L.EPI_POOL, y=t, part=part)
+        if self.save:
+            mean = ctx.alloc((B, C), torch.float32)
+            hid = ctx.alloc((B, s.Cr), torch.float32)
+            sg = ctx.alloc((B, C), torch.float32)
+        else:
+            mean = hid = None
+            sg = ctx.scratch("se_s", (B, C), torch.float32)
+        ca = pre + "channel_attention.fc."
+        ctx.emit("se_fwd", ctx.lib.fen_se_fwd, B, C, s.Cr, T, 1.0 / (H * W), ptr(part), ptr(p[ca + "0.weight"]),
+                 ptr(p[ca + "2.weight"]), ptr(mean), ptr(hid), ptr(sg))
+        y = out if out is not None else ctx.alloc(x.shape)
+        ctx.emit("se_apply", ctx.lib.fen_se_apply, ctx.code, B, H * W, C, ptr(t), ptr(sg), s.res_scale, ptr(x),
+                 ptr(y))
+        saved = dict(x=x, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg) if self.save else dict(s=sg)
+        return y, saved
+
+    def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None):
+        """ResidualGroup (blocks.py:185-189) -> (y, saved)."""
+        s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
+        B, H, W, C = x.shape
+        pre = f"residual_groups.{g}."
+        blocks = []
+        h = x
+        for b in range(s.NB):
+            if self.save:
+                h, sv = self.rcab(h, f"{pre}blocks.{b}.")
+            else:  # ping-pong two scratch buffers between blocks
+                h, sv = self.rcab(h, f"{pre}blocks.{b}.", out=ctx.scratch(f"rg_pp{b & 1}", x.shape))
+            blocks.append(sv)
+        y = out if out is not None else ctx.alloc(x.shape)
+        conv(ctx, h, Wt.packed(pre + "conv", 0), B, H, W, C, C, bias=p[pre + "conv.bias"], y=y, res=(x,))
+        return y, dict(blocks=blocks, x=x, x_last=h)
+
+    def tail(self, feat: torch.Tensor, feat0: torch.Tensor, x_lr: torch.Tensor, training: bool,
+             out: Optional[torch.Tensor] = None, hr: Optional[torch.Tensor] = None, l1_scale: float = 0.0):
+        """conv_after_body + skip, upsampler, conv_last + bicubic skip (+ clamp / + L1 grad)."""
+        s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
+        B, H, W, C = feat.shape
+        fb = ctx.alloc(feat.shape) if self.save else ctx.scratch("tail_fb", feat.shape)
+        conv(ctx, feat, Wt.packed("conv_after_body", 0), B, H, W, C, C, bias=p["conv_after_body.bias"], y=fb,
+             res=(feat0,))
+        h, hh, ww = fb, H, W
+        stages = []
+        for st in range(s.n_stages):
+            key = f"upsample.stages.{st}."
+            a = ctx.alloc((B, 2 * hh, 2 * ww, C)) if self.save else ctx.scratch(f"up_a{st & 1}", (B, 2 * hh, 2 * ww, C))
+            v = ctx.alloc((B, 2 * hh, 2 * ww, C)) if self.save else None
+            conv(ctx, h, Wt.packed(key + "conv", 1), B, hh, ww, C, 4 * C, bias=p[key + "conv.bias"],
+                 epi=L.EPI_PRELU | L.EPI_SHUFFLE, alpha=p[key + "prelu.weight"], y=a, y_pre=v)
+            stages.append(dict(x=h, v=v, a=a, H=hh, W=ww))
+            h, hh, ww = a, 2 * hh, 2 * ww
+        if out is None:
+            out = ctx.alloc((B, s.out_ch, hh, ww), torch.float32)
+        dout = loss_part = None
+        if hr is not None:
+            dout = ctx.alloc((B, hh, ww, 16)) if self.save else ctx.scratch("dout", (B, hh, ww, 16))
+            loss_part = ctx.scratch("loss_part", (B * tiles(hh, ww), 1), torch.float32)
+        conv(ctx, h, Wt.packed("conv_last", 0), B, hh, ww, C, s.out_ch, bias=p["conv_last.bias"],
+             epi=L.EPI_LAST, y=out, lr=x_lr, scale=s.scale, clamp=0 if training else 1, hr=hr, dout=dout,
+             l1_scale=l1_scale, loss_part=loss_part)
+        saved = dict(feat=feat, fb=fb, stages=stages, a_last=h, dout=dout, loss_part=loss_part, Ho=hh, Wo=ww)
+        return out, saved
+
+
+# --------------------------------------------------------------------------------------
+# backward
+# --------------------------------------------------------------------------------------
+class Backward:
+    """Builds the backward; writes fp32 parameter gradients into G[state_dict key]."""
+
+    def __init__(self, spec: NetSpec, ctx: Ctx, Wt: Weights, G: Dict[str, torch.Tensor]):
+        self.s, self.ctx, self.Wt, self.G = spec, ctx, Wt, G
+
+    def _wg(self, key, x, dy, B, H, W, Cin, Cout, cout_valid=None):
+        wgrad(self.ctx, x, dy, B, H, W, Cin, Cout, self.G[key + ".weight"], self.G.get(key + ".bias"), cout_valid)
+
+    def rcab(self, sv: dict, dy: torch.Tensor, pre: str, extra_res: Sequence = (), dx_out=None) -> torch.Tensor:
+        s, ctx, Wt, p, G = self.s, self.ctx, self.Wt, self.Wt.p, self.G
+        B, H, W, C = dy.shape
+        HW = H * W
+        npart = ctx.lib.fen_pool_parts(HW)
+        part = ctx.scratch("bw_pool", (B * npart, C), torch.float32)
+        ctx.emit("pool_dot", ctx.lib.fen_pool_dot, ctx.code, B, HW, C, ptr(dy), ptr(sv["t"]), ptr(part))
+        g = ctx.scratch("bw_g", (B, C), torch.float32)
+        dw1p = ctx.scratch("bw_dw1p", (B, s.Cr * C), torch.float32)
+        dw2p = ctx.scratch("bw_dw2p", (B, s.Cr * C), torch.float32)
+        ca = pre + "channel_attention.fc."
+        ctx.emit("se_bwd", ctx.lib.fen_se_bwd, B, C, s.Cr, npart, 1.0 / HW, s.res_scale, ptr(part), ptr(sv["mean"]),
+                 ptr(sv["hid"]), ptr(sv["s"]), ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]), ptr(g), ptr(dw1p),
+                 ptr(dw2p))
+        colsum(ctx, dw1p, B, s.Cr * C, G[ca + "0.weight"])
+        colsum(ctx, dw2p, B, s.Cr * C, G[ca + "2.weight"])
+        dt = ctx.scratch("bw_dt", dy.shape)
+        ctx.emit("se_bwd_apply", ctx.lib.fen_se_bwd_apply, ctx.code, B, HW, C, ptr(dy), ptr(sv["s"]), s.res_scale,
+                 ptr(g), ptr(dt))
+        self._wg(pre + "conv2", sv["a1"], dt, B, H, W, C, C)
+        dz1 = ctx.scratch("bw_dz1", dy.shape)
+        T = tiles(H, W)
+        dal = ctx.scratch("bw_dal", (B * T, C), torch.float32)
+        conv(ctx, dt, Wt.packed(pre + "conv2", 2), B, H, W, C, C, epi=L.EPI_PRELU_BWD, alpha=p[pre + "prelu.weight"],
+             pre_in=sv["z1"], y=dz1, part=dal)
+        colsum(ctx, dal, B * T, C, G[pre + "prelu.weight"])
+        self._wg(pre + "conv1", sv["x"], dz1, B, H, W, C, C)
+        dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
+        conv(ctx, dz1, Wt.packed(pre + "conv1", 2), B, H, W, C, C, y=dx, res=(dy,) + tuple(extra_res))
+        return dx
+
+    def group(self, sv: dict, dy: torch.Tensor, g: int, extra_res: Sequence = (), dx_out=None) -> torch.Tensor:
+        s, ctx, Wt = self.s, self.ctx, self.Wt
+        B, H, W, C = dy.shape
+        pre = f"residual_groups.{g}."
+        self._wg(pre + "conv", sv["x_last"], dy, B, H, W, C, C)
+        d = ctx.scratch("bw_rg_in", dy.shape)
+        conv(ctx, dy, Wt.packed(pre + "conv", 2), B, H, W, C, C, y=d)
+        for b in reversed(range(s.NB)):
+            if b == 0:
+                d = self.rcab(sv["blocks"][b], d, f"{pre}blocks.{b}.", extra_res=(dy,) + tuple(extra_res),
+                              dx_out=dx_out)
+            else:
+                d = self.rcab(sv["blocks"][b], d, f"{pre}blocks.{b}.",
+                              dx_out=ctx.scratch(f"bw_rg_pp{b & 1}", dy.shape))
+        return d
+
+    def tail(self, sv: dict) -> torch.Tensor:
+        """Backward of conv_last, the upsampler and conv_after_body; returns d(body output).
+        sv['dout'] holds dL/dsr (written by the conv_last epilogue); stores d(fb) in sv['d_fb']."""
+        s, ctx, Wt, p, G = self.s, self.ctx, self.Wt, self.Wt.p, self.G
+        C = s.C
+        B, Ho, Wo = sv["dout"].shape[0], sv["Ho"], sv["Wo"]
+        stages = sv["stages"]
+        # conv_last: weight grad (dy = zero-padded 16-channel dout), data grad fused with the
+        # last stage's PReLU backward and PixelShuffle inverse
+        self._wg("conv_last", sv["a_last"], sv["dout"], B, Ho, Wo, C, 16, cout_valid=s.out_ch)
+        last = stages[-1]
+        rows = ctx.lib.fen_conv_last_dgrad_part_rows(B, Ho, Wo)
+        dal = ctx.scratch("bw_dal_up", (rows, C), torch.float32)
+        du = ctx.scratch(f"bw_du{(len(stages) - 1) & 1}", (B, last["H"], last["W"], 4 * C))
+        ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, Ho, Wo, C, s.out_ch, ptr(sv["dout"]),
+                 ptr(p["conv_last.weight"]), ptr(last["v"]), ptr(p[f"upsample.stages.{len(stages) - 1}.prelu.weight"]),
+                 ptr(du), ptr(dal))
+        colsum(ctx, dal, rows, C, G[f"upsample.stages.{len(stages) - 1}.prelu.weight"])
+        for st in reversed(range(len(stages))):
+            info = stages[st]
+            key = f"upsample.stages.{st}."
+            hh, ww = info["H"], info["W"]
+            self._wg(key + "conv", info["x"], du, B, hh, ww, C, 4 * C)
+            if st > 0:
+                prev = stages[st - 1]
+                du_prev = ctx.scratch(f"bw_du{(st - 1) & 1}", (B, prev["H"], prev["W"], 4 * C))
+                T = tiles(hh, ww)
+                dal = ctx.scratch("bw_dal_up", (B * T, C), torch.float32)
+                conv(ctx, du, Wt.packed(key + "conv", 2), B, hh, ww, 4 * C, C, epi=L.EPI_PRELU_BWD | L.EPI_UNSHUFFLE,
+                     alpha=p[f"upsample.stages.{st - 1}.prelu.weight"], pre_in=prev["v"], y=du_prev, part=dal)
+                colsum(ctx, dal, B * T, C, G[f"upsample.stages.{st - 1}.prelu.weight"])
+                du = du_prev
+            else:
+                d_fb = ctx.scratch("bw_d_fb", (B, hh, ww, C))
+                conv(ctx, du, Wt.packed(key + "conv", 2), B, hh, ww, 4 * C, C, y=d_fb)
+        H, W = stages[0]["H"], stages[0]["W"]
+        self._wg("conv_after_body", sv["feat"], d_fb, B, H, W, C, C)
+        d_body = ctx.scratch("bw_d_body", (B, H, W, C))
+        conv(ctx, d_fb, Wt.packed("conv_after_body", 2), B, H, W, C, C, y=d_body)
+        sv["d_fb"] = d_fb
+        return d_body
+
+    def head(self, x_lr: torch.Tensor, d_feat0: torch.Tensor) -> None:
+        s, ctx, G = self.s, self.ctx, self.G
+        B, _, H, W = x_lr.shape
+        nwork = ctx.lib.fen_conv_first_work_floats(B, s.in_ch, H, W, s.C)
+        work = ctx.scratch("cf_work", (nwork,), torch.float32)
+        ctx.emit("conv_first_wgrad", ctx.lib.fen_conv_first_wgrad, ctx.code, B, s.in_ch, H, W, s.C, ptr(x_lr),
+                 ptr(d_feat0), ptr(G["conv_first.weight"]), ptr(G["conv_first.bias"]), 0, ptr(work))

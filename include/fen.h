@@ -1,0 +1,171 @@
+/*
+ * fen.h -- C-ABI of libfen_hip.so, the MI355X (gfx950) kernels behind the FaceEnhanceNet
+ * forward/backward hot path.
+ *
+ * Plain C: device pointers, sizes and an opaque hipStream_t (passed as void*).  No torch
+ * types.  Every entry point is asynchronous on `stream`, allocates nothing, never syncs,
+ * and returns 0 (FEN_OK) or a negative fen_status.  fen_status_string() names the code.
+ *
+ * Activations are NHWC (channels-last) in the compute dtype (FEN_F32 or FEN_BF16).
+ * Weights are the reference's OIHW fp32 tensors; fen_pack_conv_w() repacks them into the
+ * kernel layout [9 taps][Cout_pad][Cin] of the compute dtype.
+ *
+ * Each entry point replaces an aten op (or a fused chain of them) that the reference
+ * calls from src/models (reference file:line given per entry); see SURVEY.md §8a/§8b.
+ */
+#ifndef FEN_H
+#define FEN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    FEN_OK = 0,
+    FEN_EINVAL = -1,        /* bad pointer / shape / alignment                  */
+    FEN_EUNSUPPORTED = -2,  /* valid request outside what the kernels implement */
+    FEN_EHIP = -3           /* a HIP launch error                               */
+} fen_status;
+
+typedef enum { FEN_F32 = 0, FEN_BF16 = 1 } fen_dtype;
+
+/* conv3x3 epilogue flags (fen_conv_desc.epi) */
+enum {
+    FEN_EPI_BIAS = 1,       /* v += bias[co]                                                    */
+    FEN_EPI_PRELU = 2,      /* y_pre = v (if y_pre); y = v>0 ? v : alpha[c]*v                   */
+    FEN_EPI_SHUFFLE = 4,    /* PixelShuffle(2) store: packed rows are permuted (see pack mode 1)*/
+    FEN_EPI_PRELU_BWD = 8,  /* y = v*(pre>0?1:alpha[co]); part[blk][co] = sum v*pre*(pre<=0)     */
+    FEN_EPI_UNSHUFFLE = 16, /* inverse PixelShuffle(2) store: y is [B,H/2,W/2,4*Cout]           */
+    FEN_EPI_POOL = 32,      /* part[b][tile][co] = sum over the tile's pixels of the stored v   */
+    FEN_EPI_LAST = 64       /* conv_last: + bicubic skip, eval clamp, NCHW fp32 out, L1 grad    */
+};
+
+/* 3x3, stride 1, pad 1 convolution as an implicit GEMM on MFMA.
+ *   forward : RCAB conv1/conv2 (blocks.py:123-131,145-147), ResidualGroup conv (blocks.py:182-189),
+ *             conv_after_body (custom.py:109-112,172-175), PixelShuffleUpsample conv+shuffle+PReLU
+ *             (blocks.py:211-227), conv_last + bicubic skip + clamp (custom.py:121-124,158-161,181-188)
+ *   backward: the same kernel is the data-gradient (dgrad) of every 3x3 conv when given
+ *             fen_pack_conv_w(mode 2) weights; its epilogue fuses PReLU backward and the
+ *             PixelShuffle inverse (autograd of blocks.py:146,225-226).                        */
+typedef struct {
+    int dtype;                 /* fen_dtype of x, w, y, y_pre, res[], pre_in                    */
+    int B, H, W, Cin, Cout;    /* conv geometry (output = input spatial size)                   */
+    const void* x;             /* NHWC [B,H,W,Cin]                                              */
+    const void* w;             /* packed [9][Cout_pad][Cin], Cout_pad = Cout rounded up to 16    */
+    const float* bias;         /* [Cout] (FEN_EPI_BIAS)                                         */
+    int epi;                   /* FEN_EPI_* bitmask                                             */
+    const float* alpha;        /* PReLU slopes: [Cout/4] with SHUFFLE, else [Cout]              */
+    void* y;                   /* output: NHWC [B,H,W,Cout] | SHUFFLE [B,2H,2W,Cout/4] |
+                                  UNSHUFFLE [B,H/2,W/2,4*Cout] | LAST NCHW fp32 [B,Cout,H,W]     */
+    void* y_pre;               /* FEN_EPI_PRELU: pre-activation copy, same layout as y (or NULL) */
+    const void* res[3];        /* residual tensors NHWC [B,H,W,Cout] added to v (or NULL)       */
+    const void* pre_in;        /* FEN_EPI_PRELU_BWD: pre-activation NHWC [B,H,W,Cout]          */
+    float* part;               /* POOL / PRELU_BWD partial sums [B*tiles][Cout], tiles=ceil(H/16)*ceil(W/16) */
+    /* FEN_EPI_LAST only */
+    const float* lr;           /* LR input NCHW fp32 [B,Cout,H/scale,W/scale] for the bicubic skip */
+    int scale;                 /* skip scale factor (4 for 64->256)                             */
+    int clamp;                 /* 1 = eval-mode clamp to [0,1]                                  */
+    const float* hr;           /* target NCHW fp32 [B,Cout,H,W] or NULL (then no loss)          */
+    void* dout;                /* dL/dsr in NHWC16 dtype layout [B,H,W,16] (zero padded) or NULL */
+    float l1_scale;            /* dL/dsr = sign(sr-hr) * l1_scale   (weight / numel)             */
+    float* loss_part;          /* [B*tiles] partial sums of |sr-hr|                              */
+} fen_conv_desc;
+
+int fen_conv3x3(const fen_conv_desc* d, void* stream);
+
+/* Weight gradient of a 3x3 conv: dW[co][ci][kh][kw] = sum_px dy[px][co] * x[px+tap][ci],
+ * db[co] = sum_px dy[px][co].  Two launches: partial slabs then a deterministic reduction.
+ * (autograd of every nn.Conv2d on the hot path; trainer.py:482-485)                       */
+typedef struct {
+    int dtype;
+    int B, H, W, Cin, Cout;    /* Cout % 16 == 0 (the dy tensor's channel count)            */
+    int cout_valid;            /* rows of dW actually written (<= Cout; conv_last: 3)        */
+    const void* x;             /* NHWC [B,H,W,Cin]                                          */
+    const void* dy;            /* NHWC [B,H,W,Cout]                                         */
+    float* dw;                 /* OIHW fp32 [cout_valid][Cin][3][3]                         */
+    float* db;                 /* [cout_valid] or NULL                                      */
+    int accumulate;            /* 1: dw += ..., db += ...                                   */
+    float* work;               /* workspace, fen_wgrad_work_floats() floats                 */
+} fen_wgrad_desc;
+
+size_t fen_wgrad_work_floats(const fen_wgrad_desc* d);
+int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream);
+
+/* conv_first forward: NCHW fp32 [B,Ci,H,W] -> NHWC [B,H,W,C] (custom.py:91-94,164)          */
+int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x,
+                       const float* w, const float* bias, void* y, void* stream);
+/* conv_first weight gradient (no data gradient: x needs none) -> dw OIHW, db              */
+size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C);
+int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const float* x,
+                         const void* dy, float* dw, float* db, int accumulate, float* work,
+                         void* stream);
+
+/* conv_last data gradient fused with the previous stage's PReLU backward and the
+ * PixelShuffle inverse: dout NHWC16 [B,H,W,16] -> du NHWC [B,H/2,W/2,4C];
+ * pre = that stage's pre-activation NHWC [B,H,W,C]; part[B*tiles][C] dalpha partials.    */
+size_t fen_conv_last_dgrad_part_rows(int B, int H, int W);
+int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const void* dout,
+                        const float* w, const void* pre, const float* alpha, void* du,
+                        float* part, void* stream);
+
+/* Channel attention (blocks.py:44-92) forward: pool partials -> s = sigmoid(W2 relu(W1 mean)) */
+int fen_se_fwd(int B, int C, int Cr, int nparts, float inv_hw, const float* part,
+               const float* w1, const float* w2, float* mean, float* hid, float* s, void* stream);
+/* y = t * s[b,c] * res_scale + x   (blocks.py:92,153)                                       */
+int fen_se_apply(int dtype, int B, int HW, int C, const void* t, const float* s, float res_scale,
+                 const void* x, void* y, void* stream);
+/* part[b][chunk][c] = sum over the chunk's pixels of a*b_ (b_ may be NULL -> sum of a)     */
+size_t fen_pool_parts(int HW);
+int fen_pool_dot(int dtype, int B, int HW, int C, const void* a, const void* b_, float* part,
+                 void* stream);
+/* SE backward (per image): ds = rs*sum(dy*t) -> sigmoid/FC/ReLU/FC backward.
+ * g[b][c] = dL/dmean / HW; dw1p[b][Cr][C], dw2p[b][C][Cr] per-image weight-grad partials. */
+int fen_se_bwd(int B, int C, int Cr, int nparts, float inv_hw, float res_scale,
+               const float* part, const float* mean, const float* hid, const float* s,
+               const float* w1, const float* w2, float* g, float* dw1p, float* dw2p, void* stream);
+/* dt = dy * s[b,c] * res_scale + g[b,c]                                                    */
+int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy, const float* s,
+                     float res_scale, const float* g, void* dt, void* stream);
+
+/* trainer.py:416-421 LR synthesis: bicubic x0.25, align_corners=False, NCHW fp32          */
+int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, float* lr, void* stream);
+
+/* out[c] = (accumulate ? out[c] : 0) + scale * sum_r part[r][c]                            */
+int fen_colsum(int rows, int cols, const float* part, float scale, float* out, int accumulate,
+               void* stream);
+
+/* OIHW fp32 -> kernel layout of dtype.  mode 0: [9][Cout_pad][Cin] rows = co;
+ * mode 1: same with rows permuted for FEN_EPI_SHUFFLE (row t*Cout/4+c <- co = 4c+t);
+ * mode 2: dgrad weights [9][Cin_pad][Cout], flipped taps (row = ci).                        */
+int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const float* w, void* out, void* stream);
+size_t fen_packed_elems(int mode, int Cout, int Cin);
+
+/* fp32 <-> dtype layout conversions (NCHW fp32 <-> NHWC dtype)                              */
+int fen_nchw_to_nhwc(int dtype, int B, int C, int H, int W, const float* x, void* y, void* stream);
+int fen_nhwc_to_nchw(int dtype, int B, int C, int H, int W, const void* x, float* y, void* stream);
+
+/* clip_grad_norm_ + AdamW (trainer.py:490-503) over one flat fp32 arena.
+ * fen_sumsq: part[i] partial sums of g^2 (nparts = fen_sumsq_parts(n)).
+ * fen_optim_prepare: one block; reads part, writes scal[0..7]:
+ *   scal[0]=grad norm, scal[1]=clip coef, scal[2]=step (incremented), scal[3]=lr,
+ *   scal[4]=1-lr*wd, scal[5]=step_size=lr/bc1, scal[6]=1/sqrt(bc2)   (scal[3] is an input)
+ * fen_adamw: p,m,v updated in place with g*scal[1].                                         */
+int fen_sumsq_parts(size_t n);
+int fen_sumsq(size_t n, const float* g, float* part, void* stream);
+int fen_optim_prepare(int nparts, const float* part, float max_norm, float beta1, float beta2,
+                      float wd, float* scal, void* stream);
+int fen_adamw(size_t n, float* p, const float* g, float* m, float* v, const float* scal,
+              float beta1, float beta2, float eps, void* stream);
+/* y[i] *= s  (DP gradient averaging helper)                                                 */
+int fen_scale(size_t n, float* y, float s, void* stream);
+
+const char* fen_status_string(int code);
+const char* fen_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEN_H */

@@ -1,0 +1,209 @@
+"""CPU oracle for the FaceEnhanceNet hot path  --  TEST INFRASTRUCTURE ONLY.
+
+This module is the *checker*.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import it.  The product path (face-super-resolution_amd/src) never
+imports or calls it and fails loudly when the HIP library is missing.
+
+It is a functional restatement, in plain PyTorch-CPU ops, of the reference algorithm
+(tomasz-pres/face-super-resolution @ /root/reference), written from SURVEY.md §8a and
+the cited reference lines -- it shares no code with the reference.  Parity of this
+oracle is PINNED against golden vectors produced by importing the reference itself
+(tests/golden/make_golden.py -> tests/golden/*.npz; tests/test_oracle.py).
+
+Parameters are passed as a flat dict keyed exactly like the reference state_dict
+(SURVEY.md §8b), tensors in the reference OIHW fp32 layout.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+Params = Dict[str, torch.Tensor]
+
+
+@dataclass
+class NetShape:
+    """Architecture knobs used by the oracle (reference custom.py:22-43)."""
+    num_channels: int = 64
+    num_groups: int = 3
+    blocks_per_group: int = 4
+    reduction_ratio: int = 4
+    scale_factor: int = 4
+    res_scale: float = 0.2
+
+
+# ---------------------------------------------------------------------------------------
+# bicubic resampling, align_corners=False, A = -0.75, border-clamped taps
+# (used by custom.py:158-161 for the x4 skip and trainer.py:416-421 for the /4 LR synthesis)
+# ---------------------------------------------------------------------------------------
+def _cubic_weights(t: torch.Tensor, A: float = -0.75) -> torch.Tensor:
+    """Keys cubic convolution weights for the 4 taps at offsets -1,0,1,2 around floor(src)."""
+    def w_near(d):  # |d| <= 1
+        return ((A + 2) * d - (A + 3)) * d * d + 1
+
+    def w_far(d):  # 1 < |d| < 2
+        return ((A * d - 5 * A) * d + 8 * A) * d - 4 * A
+
+    return torch.stack([w_far(t + 1), w_near(t), w_near(1 - t), w_far(2 - t)], dim=-1)
+
+
+def _resize_axis(x: torch.Tensor, out_len: int, scale: float, dim: int) -> torch.Tensor:
+    in_len = x.shape[dim]
+    d = torch.arange(out_len, dtype=torch.float64)
+    src = (d + 0.5) / scale - 0.5
+    i0 = torch.floor(src)
+    t = src - i0
+    w = _cubic_weights(t)                                    # [out, 4]
+    idx = i0.long().unsqueeze(-1) + torch.arange(-1, 3)      # [out, 4]
+    idx = idx.clamp(0, in_len - 1)
+    xm = x.movedim(dim, -1)                                  # [..., in]
+    g = xm[..., idx]                                         # [..., out, 4]
+    y = (g * w.to(x.dtype)).sum(-1)
+    return y.movedim(-1, dim)
+
+
+def bicubic(x: torch.Tensor, scale: float) -> torch.Tensor:
+    """F.interpolate(x, scale_factor=scale, mode='bicubic', align_corners=False) restated."""
+    n, c, h, w = x.shape
+    oh, ow = int(math.floor(h * scale)), int(math.floor(w * scale))
+    y = _resize_axis(x, oh, scale, 2)
+    return _resize_axis(y, ow, scale, 3)
+
+
+def pixel_shuffle(x: torch.Tensor, r: int) -> torch.Tensor:
+    """out[b, c, r*h+i, r*w+j] = in[b, c*r*r + i*r + j, h, w]  (blocks.py:215,225)."""
+    b, c, h, w = x.shape
+    co = c // (r * r)
+    return x.reshape(b, co, r, r, h, w).permute(0, 1, 4, 2, 5, 3).reshape(b, co, h * r, w * r)
+
+
+def prelu(x: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+    return torch.where(x > 0, x, a.view(1, -1, 1, 1) * x)
+
+
+def conv3x3(x, w, b):
+    return F.conv2d(x, w, b, padding=1)
+
+
+# ---------------------------------------------------------------------------------------
+# network blocks (reference blocks.py / custom.py)
+# ---------------------------------------------------------------------------------------
+def channel_attention(t: torch.Tensor, p: Params, pre: str) -> torch.Tensor:
+    """blocks.py:83-92 -> the sigmoid gate s[b, c]."""
+    y = t.mean(dim=(2, 3))
+    y = torch.relu(y @ p[pre + "fc.0.weight"].t())
+    return torch.sigmoid(y @ p[pre + "fc.2.weight"].t())
+
+
+def rcab(x: torch.Tensor, p: Params, pre: str, res_scale: float, attn: Optional[dict] = None,
+         name: str = "") -> torch.Tensor:
+    """blocks.py:135-153: conv -> PReLU -> conv -> SE gate -> out*res_scale + x."""
+    t = conv3x3(x, p[pre + "conv1.weight"], p[pre + "conv1.bias"])
+    t = prelu(t, p[pre + "prelu.weight"])
+    t = conv3x3(t, p[pre + "conv2.weight"], p[pre + "conv2.bias"])
+    s = channel_attention(t, p, pre + "channel_attention.")
+    if attn is not None:
+        attn[name] = s.detach()
+    return t * s[:, :, None, None] * res_scale + x
+
+
+def residual_group(x, p, pre, nb, res_scale, attn=None, gi=0):
+    """blocks.py:185-189."""
+    out = x
+    for bi in range(nb):
+        out = rcab(out, p, f"{pre}blocks.{bi}.", res_scale, attn, f"group{gi}_rcab{bi}")
+    out = conv3x3(out, p[pre + "conv.weight"], p[pre + "conv.bias"])
+    return out + x
+
+
+def forward(p: Params, x: torch.Tensor, shape: NetShape, training: bool = True,
+            attn: Optional[dict] = None) -> torch.Tensor:
+    """FaceEnhanceNet.forward (custom.py:147-190)."""
+    bic = bicubic(x, shape.scale_factor)
+    feat = conv3x3(x, p["conv_first.weight"], p["conv_first.bias"])
+    res = feat
+    for g in range(shape.num_groups):
+        feat = residual_group(feat, p, f"residual_groups.{g}.", shape.blocks_per_group,
+                              shape.res_scale, attn, g)
+    feat = conv3x3(feat, p["conv_after_body.weight"], p["conv_after_body.bias"]) + res
+    n_stages = int(round(math.log2(shape.scale_factor)))
+    for s in range(n_stages):
+        pre = f"upsample.stages.{s}."
+        feat = conv3x3(feat, p[pre + "conv.weight"], p[pre + "conv.bias"])
+        feat = pixel_shuffle(feat, 2)
+        feat = prelu(feat, p[pre + "prelu.weight"])
+    out = conv3x3(feat, p["conv_last.weight"], p["conv_last.bias"]) + bic
+    if not training:
+        out = out.clamp(0.0, 1.0)
+    return out
+
+
+def lr_from_hr(hr: torch.Tensor) -> torch.Tensor:
+    """trainer.py:416-421: F.interpolate(hr, 0.25, 'bicubic', align_corners=False)."""
+    return bicubic(hr, 0.25)
+
+
+def psnr(pred: torch.Tensor, target: torch.Tensor) -> float:
+    """trainer.py:621-628 (batch-mean MSE), evaluated in fp64."""
+    mse = torch.mean((pred.double() - target.double()) ** 2)
+    return float(10.0 * torch.log10(1.0 / mse))
+
+
+# ---------------------------------------------------------------------------------------
+# one optimizer step: L1 loss, backward, clip_grad_norm_, AdamW (trainer.py:458-503)
+# ---------------------------------------------------------------------------------------
+def l1_grads(p: Params, hr: torch.Tensor, shape: NetShape) -> Tuple[float, Params]:
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+    lr = lr_from_hr(hr)
+    out = forward(leaves, lr, shape, training=True)
+    loss = (out - hr).abs().mean()
+    loss.backward()
+    return float(loss), {k: v.grad.detach() for k, v in leaves.items()}
+
+
+def clip_coef(grads: Params, max_norm: float) -> float:
+    """torch.nn.utils.clip_grad_norm_ semantics: coef = max_norm/(||g||+1e-6), capped at 1."""
+    norms = torch.stack([g.detach().float().norm(2) for g in grads.values()])
+    total = norms.norm(2)
+    return float(torch.clamp(max_norm / (total + 1e-6), max=1.0))
+
+
+def adamw_step(p: Params, g: Params, m: Params, v: Params, step: int, lr: float,
+               betas=(0.9, 0.999), eps=1e-8, wd=0.0) -> None:
+    """torch.optim.AdamW single-tensor update restated (in place on p, m, v)."""
+    b1, b2 = betas
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    for k in p:
+        p[k].mul_(1 - lr * wd)
+        m[k].lerp_(g[k], 1 - b1)
+        v[k].mul_(b2).addcmul_(g[k], g[k], value=1 - b2)
+        denom = (v[k].sqrt() / math.sqrt(bc2)).add_(eps)
+        p[k].addcdiv_(m[k], denom, value=-lr / bc1)
+
+
+def train_step(p: Params, hr: torch.Tensor, shape: NetShape, lr: float = 1e-4,
+               clip: float = 0.5, wd: float = 0.0) -> Tuple[float, Params]:
+    """One Trainer._train_epoch batch (fresh optimizer state): returns (loss, new params)."""
+    loss, g = l1_grads(p, hr, shape)
+    if clip > 0:
+        c = clip_coef(g, clip)
+        g = {k: t * c for k, t in g.items()}
+    newp = {k: t.detach().clone() for k, t in p.items()}
+    m = {k: torch.zeros_like(t) for k, t in newp.items()}
+    v = {k: torch.zeros_like(t) for k, t in newp.items()}
+    adamw_step(newp, g, m, v, 1, lr, wd=wd)
+    return loss, newp
+
+
+def rcab_with_grads(p: Params, x: torch.Tensor, r: torch.Tensor, res_scale: float = 0.2):
+    """G2 helper: out and the gradients of sum(out*r) w.r.t. x and every RCAB parameter."""
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+    xl = x.detach().clone().requires_grad_(True)
+    out = rcab(xl, leaves, "", res_scale)
+    (out * r).sum().backward()
+    return out.detach(), xl.grad.detach(), {k: v.grad.detach() for k, v in leaves.items()}

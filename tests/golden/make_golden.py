@@ -1,0 +1,173 @@
+"""Golden-vector generator (test infrastructure; runs ONLY in the survey container).
+
+Imports the reference implementation from /root/reference (read-only, no bytecode
+written) and records numeric input/output fixtures for the FaceEnhanceNet hot path
+into tests/golden/*.npz.  Nothing from the reference travels except these numbers.
+
+Fixtures:
+  g1_config1.npz  config 1 (C=64, 1 group x 2 RCAB, x4), B=2, HR 128x128 -> LR 32x32:
+                  seed-0 reference init (+ conv_last ~ N(0,1e-3) so the body is exercised),
+                  train/eval forward, attention maps, L1 grads of every parameter,
+                  parameters after one Trainer._train_epoch step (AdamW, clip 0.5).
+  g2_rcab.npz     one RCAB (C=64) B=2 16x16 with random weights; out and all grads
+                  of sum(out*R).
+  g3_kat.npz      bicubic x2/x4/x8 up, bicubic x0.25 down, PixelShuffle(2) KATs.
+  g4_full.npz     full 6x10 network, B=1, 32x32 input: init statistics + outputs.
+  g5_c128.npz     128-ch 10x20 x8 variant, B=1, 16x16 input: init statistics + output.
+  g6_lite.npz     FaceEnhanceNetLite (C=32, r=2), B=1, 16x16 input: output.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+sys.dont_write_bytecode = True
+REF = os.environ.get("FEN_REFERENCE", "/root/reference")
+sys.path.insert(0, REF)
+
+from src.models.custom import FaceEnhanceNet, FaceEnhanceNetLite  # noqa: E402  (reference)
+from src.models.blocks import RCAB  # noqa: E402  (reference)
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+torch.set_num_threads(8)
+
+
+def sd_np(model, prefix="p/"):
+    return {prefix + k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+
+
+def init_stats(model):
+    names, s1, s2 = [], [], []
+    for k, v in model.state_dict().items():
+        v64 = v.detach().double()
+        names.append(k)
+        s1.append(float(v64.sum()))
+        s2.append(float((v64 * v64).sum()))
+    return {"stat_names": np.array(names), "stat_sum": np.array(s1), "stat_sumsq": np.array(s2)}
+
+
+def perturb_conv_last(model, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        model.conv_last.weight.copy_(torch.randn(model.conv_last.weight.shape, generator=g) * 1e-3)
+
+
+class _L1(nn.Module):
+    """Loss module with the (loss, components) contract Trainer expects (trainer.py:465)."""
+
+    def forward(self, sr, hr):
+        loss = F.l1_loss(sr, hr)
+        return loss, {"l1": loss.detach()}
+
+
+def g1():
+    torch.manual_seed(0)
+    model = FaceEnhanceNet(num_channels=64, num_groups=1, blocks_per_group=2,
+                           reduction_ratio=4, scale_factor=4, res_scale=0.2)
+    d = {}
+    d.update(init_stats(model))
+    perturb_conv_last(model, 1)
+    d.update(sd_np(model, "p/"))
+    hr = torch.rand(2, 3, 128, 128, generator=torch.Generator().manual_seed(2))
+    lr = F.interpolate(hr, scale_factor=0.25, mode="bicubic", align_corners=False)
+    d["hr"] = hr.numpy()
+    d["lr"] = lr.numpy()
+    model.train()
+    with torch.no_grad():
+        d["out_train"] = model(lr).numpy()
+    model.eval()
+    with torch.no_grad():
+        d["out_eval"] = model(lr).numpy()
+    attn = model.get_attention_maps(lr)
+    for k, v in attn.items():
+        d["attn/" + k] = v.numpy()
+    # L1 gradients of every parameter (train mode, reference autograd)
+    model.train()
+    model.zero_grad()
+    out = model(lr)
+    loss = F.l1_loss(out, hr)
+    loss.backward()
+    d["l1_loss"] = np.array(float(loss))
+    for k, p in model.named_parameters():
+        d["g/" + k] = p.grad.detach().numpy().copy()
+    # one step of the reference Trainer (trainer.py:390-550): AdamW + clip 0.5, fp32
+    model.zero_grad()
+    import src.training.trainer as T  # reference
+    with tempfile.TemporaryDirectory() as tmp:
+        cfg = T.TrainerConfig(learning_rate=1e-4, weight_decay=0.0, gradient_clip=0.5,
+                              use_amp=False, use_wandb=False, device="cpu",
+                              checkpoint_dir=tmp)
+        tr = T.Trainer(model, [{"hr": hr}], [{"hr": hr}], _L1(), cfg)
+        m = tr._train_epoch()
+    d["step_loss"] = np.array(float(m["loss"]))
+    for k, v in model.state_dict().items():
+        d["s/" + k] = v.detach().numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "g1_config1.npz"), **d)
+
+
+def g2():
+    torch.manual_seed(3)
+    rcab = RCAB(64, 3, 4, True, 0.2)
+    with torch.no_grad():
+        rcab.prelu.weight.copy_(0.25 + 0.2 * torch.randn(64))
+        rcab.conv1.bias.copy_(0.05 * torch.randn(64))
+        rcab.conv2.bias.copy_(0.05 * torch.randn(64))
+    x = torch.randn(2, 64, 16, 16, requires_grad=True)
+    r = torch.randn(2, 64, 16, 16)
+    out = rcab(x)
+    (out * r).sum().backward()
+    d = {"x": x.detach().numpy(), "r": r.numpy(), "out": out.detach().numpy(), "dx": x.grad.numpy()}
+    for k, v in rcab.state_dict().items():
+        d["p/" + k] = v.numpy().copy()
+    for k, p in rcab.named_parameters():
+        d["g/" + k] = p.grad.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "g2_rcab.npz"), **d)
+
+
+def g3():
+    g = torch.Generator().manual_seed(5)
+    d = {}
+    x = torch.rand(2, 3, 8, 8, generator=g)
+    d["up_in"] = x.numpy()
+    for s in (2, 4, 8):
+        d[f"up_x{s}"] = F.interpolate(x, scale_factor=s, mode="bicubic", align_corners=False).numpy()
+    hr = torch.rand(2, 3, 32, 32, generator=g)
+    d["down_in"] = hr.numpy()
+    d["down_x4"] = F.interpolate(hr, scale_factor=0.25, mode="bicubic", align_corners=False).numpy()
+    ps = torch.arange(2 * 8 * 3 * 5, dtype=torch.float32).reshape(2, 8, 3, 5)
+    d["ps_in"] = ps.numpy()
+    d["ps_out"] = nn.PixelShuffle(2)(ps).numpy()
+    np.savez_compressed(os.path.join(OUT, "g3_kat.npz"), **d)
+
+
+def g_net(fname, ctor, x_shape, seed_x):
+    torch.manual_seed(0)
+    model = ctor()
+    d = init_stats(model)
+    perturb_conv_last(model, 1)
+    x = torch.rand(*x_shape, generator=torch.Generator().manual_seed(seed_x))
+    d["x"] = x.numpy()
+    with torch.no_grad():
+        model.eval()
+        d["out_eval"] = model(x).numpy()
+        model.train()
+        d["out_train"] = model(x).numpy()
+    np.savez_compressed(os.path.join(OUT, fname), **d)
+
+
+if __name__ == "__main__":
+    g1()
+    g2()
+    g3()
+    g_net("g4_full.npz", lambda: FaceEnhanceNet(num_channels=64, num_groups=6, blocks_per_group=10,
+                                                reduction_ratio=4, scale_factor=4), (1, 3, 32, 32), 4)
+    g_net("g5_c128.npz", lambda: FaceEnhanceNet(num_channels=128, num_groups=10, blocks_per_group=20,
+                                                reduction_ratio=4, scale_factor=8), (1, 3, 16, 16), 6)
+    g_net("g6_lite.npz", lambda: FaceEnhanceNetLite(), (1, 3, 16, 16), 7)
+    print("golden fixtures written to", OUT)

@@ -1,0 +1,47 @@
+"""The C-ABI library loads on CPU and exports every entry point include/fen.h declares."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "fen.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fen_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    from src.hip import lib as L
+    lib = L.load()
+    names = _declared()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(L.EXPORTED), set(names) ^ set(L.EXPORTED)
+
+
+def test_status_strings_and_pure_queries():
+    from src.hip import lib as L
+    lib = L.load()
+    assert lib.fen_status_string(-2).startswith(b"FEN_EUNSUPPORTED")
+    assert b"gfx950" in lib.fen_build_info()
+    assert lib.fen_packed_elems(0, 3, 64) == 9 * 16 * 64
+    assert lib.fen_packed_elems(2, 256, 64) == 9 * 64 * 256
+    assert lib.fen_pool_parts(4096) == 16
+    assert lib.fen_sumsq_parts(5115651) == 1024
+
+
+def test_bad_args_rejected_without_gpu():
+    """Argument validation happens before any launch, so it is testable on CPU."""
+    from src.hip import lib as L
+    lib = L.load()
+    d = L.ConvDesc()
+    assert lib.fen_conv3x3(None, None) == L.load().fen_conv3x3(None, None) == -1
+    d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = 1, 1, 8, 8, 48, 64  # Cin not a multiple of 64 (bf16 panel)
+    d.x = d.w = d.y = 16
+    assert lib.fen_conv3x3(d, None) == -2
+    with pytest.raises(L.FenError):
+        L.check(-2, "conv")

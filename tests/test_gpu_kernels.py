@@ -1,0 +1,282 @@
+"""Per-kernel GPU parity: each C-ABI entry point against the CPU oracle's restatement of
+the same op (fp32 exact-ish, bf16 within bf16 rounding)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import fen_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ctx(dtype):
+    from src.hip.program import Ctx
+    return Ctx(dtype, DEV)
+
+
+def nhwc(x_nchw, dtype):
+    return x_nchw.permute(0, 2, 3, 1).contiguous().to(DEV, dtype)
+
+
+def nchw(x_nhwc):
+    return x_nhwc.float().cpu().permute(0, 3, 1, 2).contiguous()
+
+
+def _tol(dtype, ref):
+    return (2e-5 if dtype == torch.float32 else 3e-2) * max(1.0, float(ref.abs().max()))
+
+
+def _pack(ctx, w, mode):
+    from src.hip.program import ptr
+    n = ctx.lib.fen_packed_elems(mode, w.shape[0], w.shape[1])
+    buf = torch.empty(n, dtype=ctx.tdtype, device=DEV)
+    wd = w.to(DEV).contiguous()
+    ctx.emit("pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, w.shape[0], w.shape[1], ptr(wd), ptr(buf))
+    return buf
+
+
+DT = [torch.float32, torch.bfloat16]
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 20, 36, 64, 64), (2, 32, 16, 128, 64),
+                                             (1, 16, 32, 64, 256), (1, 8, 8, 64, 16)])
+def test_conv3x3_plain(dtype, B, H, W, Cin, Cout):
+    from src.hip import net
+    torch.manual_seed(0)
+    x = torch.randn(B, Cin, H, W)
+    w = torch.randn(Cout, Cin, 3, 3) * 0.05
+    b = torch.randn(Cout) * 0.1
+    ref = F.conv2d(x, w, b, padding=1)
+    ctx = _ctx(dtype)
+    wp = _pack(ctx, w, 0)
+    y = ctx.alloc((B, H, W, Cout))
+    net.conv(ctx, nhwc(x, dtype), wp, B, H, W, Cin, Cout, bias=b.to(DEV), y=y)
+    torch.cuda.synchronize()
+    err = (nchw(y) - ref).abs().max()
+    assert err <= _tol(dtype, ref), float(err)
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_conv3x3_prelu_pool_res(dtype):
+    from src.hip import lib as L, net
+    torch.manual_seed(1)
+    B, H, W, C = 2, 24, 40, 64
+    x = torch.randn(B, C, H, W)
+    r = torch.randn(B, C, H, W)
+    w = torch.randn(C, C, 3, 3) * 0.05
+    b = torch.randn(C) * 0.1
+    a = torch.rand(C) * 0.5
+    z = F.conv2d(x, w, b, padding=1) + r
+    act = O.prelu(z, a)
+    ctx = _ctx(dtype)
+    wp = _pack(ctx, w, 0)
+    y = ctx.alloc((B, H, W, C))
+    ypre = ctx.alloc((B, H, W, C))
+    T = net.tiles(H, W)
+    net.conv(ctx, nhwc(x, dtype), wp, B, H, W, C, C, bias=b.to(DEV), epi=L.EPI_PRELU, alpha=a.to(DEV), y=y,
+             y_pre=ypre, res=(nhwc(r, dtype),))
+    part = ctx.alloc((B * T, C), torch.float32)
+    y2 = ctx.alloc((B, H, W, C))
+    net.conv(ctx, nhwc(x, dtype), wp, B, H, W, C, C, bias=b.to(DEV), epi=L.EPI_POOL, y=y2, part=part)
+    torch.cuda.synchronize()
+    assert (nchw(ypre) - z).abs().max() <= _tol(dtype, z)
+    assert (nchw(y) - act).abs().max() <= _tol(dtype, act)
+    pool = part.view(B, T, C).sum(1).cpu() / (H * W)
+    ref_pool = F.conv2d(x, w, b, padding=1).mean(dim=(2, 3))
+    assert (pool - ref_pool).abs().max() <= (1e-5 if dtype == torch.float32 else 2e-3)
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_upsample_conv_shuffle_prelu(dtype):
+    from src.hip import lib as L, net
+    torch.manual_seed(2)
+    B, H, W, C = 2, 16, 32, 64
+    x = torch.randn(B, C, H, W)
+    w = torch.randn(4 * C, C, 3, 3) * 0.05
+    b = torch.randn(4 * C) * 0.1
+    a = torch.rand(C) * 0.5
+    v = O.pixel_shuffle(F.conv2d(x, w, b, padding=1), 2)
+    ref = O.prelu(v, a)
+    ctx = _ctx(dtype)
+    wp = _pack(ctx, w, 1)
+    y = ctx.alloc((B, 2 * H, 2 * W, C))
+    ypre = ctx.alloc((B, 2 * H, 2 * W, C))
+    net.conv(ctx, nhwc(x, dtype), wp, B, H, W, C, 4 * C, bias=b.to(DEV), epi=L.EPI_PRELU | L.EPI_SHUFFLE,
+             alpha=a.to(DEV), y=y, y_pre=ypre)
+    torch.cuda.synchronize()
+    assert (nchw(ypre) - v).abs().max() <= _tol(dtype, v)
+    assert (nchw(y) - ref).abs().max() <= _tol(dtype, ref)
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_conv_first(dtype):
+    torch.manual_seed(3)
+    B, H, W, C = 2, 20, 24, 64
+    x = torch.rand(B, 3, H, W)
+    w = torch.randn(C, 3, 3, 3) * 0.2
+    b = torch.randn(C) * 0.1
+    ref = F.conv2d(x, w, b, padding=1)
+    ctx = _ctx(dtype)
+    from src.hip.program import ptr
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    y = ctx.alloc((B, H, W, C))
+    ctx.emit("cf", ctx.lib.fen_conv_first_fwd, ctx.code, B, 3, H, W, C, ptr(xd), ptr(wd), ptr(bd), ptr(y))
+    torch.cuda.synchronize()
+    assert (nchw(y) - ref).abs().max() <= _tol(dtype, ref)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("clamp", [0, 1])
+def test_conv_last_bicubic_l1(dtype, clamp):
+    from src.hip import lib as L, net
+    torch.manual_seed(4)
+    B, C, h, w_ = 2, 64, 8, 12
+    H, W = 4 * h, 4 * w_
+    feat = torch.randn(B, C, H, W)
+    lr = torch.rand(B, 3, h, w_)
+    hr = torch.rand(B, 3, H, W)
+    wl = torch.randn(3, C, 3, 3) * 0.01
+    bl = torch.randn(3) * 0.01
+    out_ref = F.conv2d(feat, wl, bl, padding=1) + O.bicubic(lr.double(), 4).float()
+    if clamp:
+        out_ref = out_ref.clamp(0, 1)
+    n = out_ref.numel()
+    ctx = _ctx(dtype)
+    wp = _pack(ctx, wl, 0)
+    out = ctx.alloc((B, 3, H, W), torch.float32)
+    dout = ctx.alloc((B, H, W, 16))
+    lp = ctx.alloc((B * net.tiles(H, W), 1), torch.float32)
+    net.conv(ctx, nhwc(feat, dtype), wp, B, H, W, C, 3, bias=bl.to(DEV), epi=L.EPI_LAST, y=out, lr=lr.to(DEV),
+             scale=4, clamp=clamp, hr=hr.to(DEV), dout=dout, l1_scale=1.0 / n, loss_part=lp)
+    torch.cuda.synchronize()
+    assert (out.cpu() - out_ref).abs().max() <= (1e-4 if dtype == torch.float32 else 3e-2)
+    loss = float(lp.sum()) / n
+    assert abs(loss - float((out.cpu() - hr).abs().mean())) < 1e-5
+    g = dout.float().cpu()
+    assert torch.all(g[..., 3:] == 0)
+    sgn = torch.sign(out.cpu() - hr).permute(0, 2, 3, 1) / n
+    assert torch.allclose(g[..., :3], sgn.to(g.dtype).float(), rtol=1e-2, atol=0)
+
+
+def test_bicubic_down4_and_layouts():
+    torch.manual_seed(5)
+    from src.hip.program import ptr
+    ctx = _ctx(torch.float32)
+    hr = torch.rand(2, 3, 64, 48)
+    lr = ctx.alloc((2, 3, 16, 12), torch.float32)
+    hd = hr.to(DEV)
+    ctx.emit("down", ctx.lib.fen_bicubic_down4, 2, 3, 64, 48, ptr(hd), ptr(lr))
+    torch.cuda.synchronize()
+    ref = O.lr_from_hr(hr.double()).float()
+    assert (lr.cpu() - ref).abs().max() < 2e-6
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_se_fwd_apply(dtype):
+    from src.hip.program import ptr
+    torch.manual_seed(6)
+    B, C, Cr, H, W = 3, 64, 16, 16, 16
+    t = torch.randn(B, C, H, W)
+    x = torch.randn(B, C, H, W)
+    w1 = torch.randn(Cr, C) * 0.2
+    w2 = torch.randn(C, Cr) * 0.2
+    p = {"fc.0.weight": w1, "fc.2.weight": w2}
+    s_ref = O.channel_attention(t, p, "")
+    y_ref = t * s_ref[:, :, None, None] * 0.2 + x
+    ctx = _ctx(dtype)
+    td, xd = nhwc(t, dtype), nhwc(x, dtype)
+    npart = ctx.lib.fen_pool_parts(H * W)
+    part = ctx.alloc((B * npart, C), torch.float32)
+    ctx.emit("pool", ctx.lib.fen_pool_dot, ctx.code, B, H * W, C, ptr(td), 0, ptr(part))
+    mean = ctx.alloc((B, C), torch.float32)
+    hid = ctx.alloc((B, Cr), torch.float32)
+    s = ctx.alloc((B, C), torch.float32)
+    w1d, w2d = w1.to(DEV), w2.to(DEV)
+    ctx.emit("se", ctx.lib.fen_se_fwd, B, C, Cr, npart, 1.0 / (H * W), ptr(part), ptr(w1d), ptr(w2d), ptr(mean),
+             ptr(hid), ptr(s))
+    y = ctx.alloc((B, H, W, C))
+    ctx.emit("apply", ctx.lib.fen_se_apply, ctx.code, B, H * W, C, ptr(td), ptr(s), 0.2, ptr(xd), ptr(y))
+    torch.cuda.synchronize()
+    tol_s = 1e-5 if dtype == torch.float32 else 3e-3
+    assert (s.cpu() - s_ref).abs().max() <= tol_s
+    assert (nchw(y) - y_ref).abs().max() <= _tol(dtype, y_ref)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 24, 40, 64, 64), (1, 16, 16, 64, 256),
+                                             (1, 32, 32, 64, 16)])
+def test_wgrad(dtype, B, H, W, Cin, Cout):
+    from src.hip import net
+    torch.manual_seed(7)
+    x = torch.randn(B, Cin, H, W)
+    dy = torch.randn(B, Cout, H, W)
+    w = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
+    bb = torch.zeros(Cout, requires_grad=True)
+    F.conv2d(x, w, bb, padding=1).mul(dy).sum().backward()
+    ctx = _ctx(dtype)
+    cv = Cout if Cout != 16 else 3
+    dw = ctx.alloc((cv, Cin, 3, 3), torch.float32)
+    db = ctx.alloc((cv,), torch.float32)
+    net.wgrad(ctx, nhwc(x, dtype), nhwc(dy, dtype), B, H, W, Cin, Cout, dw, db, cout_valid=cv)
+    torch.cuda.synchronize()
+    gw, gb = w.grad[:cv], bb.grad[:cv]
+    rel = float((dw.cpu() - gw).norm() / gw.norm())
+    relb = float((db.cpu() - gb).norm() / gb.norm())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel <= tol and relb <= tol, (rel, relb)
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_dgrad_prelu_bwd(dtype):
+    """dgrad (mode-2 weights) with the fused PReLU backward epilogue."""
+    from src.hip import lib as L, net
+    torch.manual_seed(8)
+    B, H, W, C = 2, 16, 24, 64
+    z = torch.randn(B, C, H, W)
+    dy = torch.randn(B, C, H, W)
+    w = torch.randn(C, C, 3, 3) * 0.05
+    a = (torch.rand(C) * 0.5).requires_grad_(True)
+    a1 = torch.randn(B, C, H, W, requires_grad=True)
+    zz = z.clone().requires_grad_(True)
+    # reference: y = conv(prelu(zz)); d/dzz and d/da of sum(y*dy)
+    F.conv2d(O.prelu(zz, a), w, None, padding=1).mul(dy).sum().backward()
+    ctx = _ctx(dtype)
+    wp = _pack(ctx, w, 2)
+    dz = ctx.alloc((B, H, W, C))
+    T = net.tiles(H, W)
+    part = ctx.alloc((B * T, C), torch.float32)
+    net.conv(ctx, nhwc(dy, dtype), wp, B, H, W, C, C, epi=L.EPI_PRELU_BWD, alpha=a.detach().to(DEV),
+             pre_in=nhwc(z, dtype), y=dz, part=part)
+    torch.cuda.synchronize()
+    assert (nchw(dz) - zz.grad).abs().max() <= _tol(dtype, zz.grad)
+    da = part.sum(0).cpu()
+    rel = float((da - a.grad).norm() / a.grad.norm())
+    assert rel <= (1e-5 if dtype == torch.float32 else 2e-2), rel
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_dgrad_unshuffle(dtype):
+    from src.hip import lib as L, net
+    torch.manual_seed(9)
+    B, H, W, C = 1, 32, 32, 64         # dgrad conv output space (2H' x 2W')
+    v = torch.randn(B, C, H, W)       # previous stage pre-activation
+    dy = torch.randn(B, 4 * C, H, W)  # grad at the next conv's output
+    w = torch.randn(4 * C, C, 3, 3) * 0.05
+    a = torch.rand(C) * 0.5
+    vv = v.clone().requires_grad_(True)
+    F.conv2d(O.prelu(vv, a), w, None, padding=1).mul(dy).sum().backward()
+    # du = unshuffle(dv): du[b, 4c+2i+j, h, w] = dv[b, c, 2h+i, 2w+j]
+    ref = vv.grad.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H // 2, W // 2)
+    ctx = _ctx(dtype)
+    wp = _pack(ctx, w, 2)
+    du = ctx.alloc((B, H // 2, W // 2, 4 * C))
+    part = ctx.alloc((B * net.tiles(H, W), C), torch.float32)
+    net.conv(ctx, nhwc(dy, dtype), wp, B, H, W, 4 * C, C, epi=L.EPI_PRELU_BWD | L.EPI_UNSHUFFLE, alpha=a.to(DEV),
+             pre_in=nhwc(v, dtype), y=du, part=part)
+    torch.cuda.synchronize()
+    assert (nchw(du) - ref).abs().max() <= _tol(dtype, ref)
