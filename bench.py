@@ -1,0 +1,200 @@
+#!/usr/bin/env python
+"""FaceEnhanceNet 64->256 (x4) super-resolution throughput on MI355X.
+
+Metric (BASELINE.json): images/sec at batch 32 per GPU on 1/2/4/8 GPUs.  The workload of
+`value` is BASELINE configs[1]: the full network (6 groups x 10 RCAB, 64 ch) in bf16,
+inference, batch 32 per GPU, synthetic 64x64x3 inputs resident in HBM, random-init
+weights of the reference architecture (seeded reference init + conv_last ~ N(0,1e-3)).
+One "step" = one forward of one 32-image batch, replayed from a hipGraph.  With N>1 each
+rank runs its own replica on its own shard (inference has no exchange step: weak scaling).
+
+Also reported (field "train"): the stage-1 generator training step (bicubic /4 LR
+synthesis, forward, L1, backward, RCCL gradient all-reduce over xGMI for N>1, clip,
+AdamW) at batch 32 per GPU -- the DP path of the north star.
+
+roofline: the dominant kernel is the RCAB 3x3 conv (64->64 ch, 64x64, B=32):
+  algorithmic FLOPs per launch = 2 * 32*64*64 px * 64 co * 576 (= 9 taps * 64 ci) = 9.664 GFLOP,
+  timed live here with HIP events on the launch stream; peak = 2500 TFLOP/s bf16 dense.
+cpu_baseline: the CPU oracle (oracle/fen_oracle.py, fp32 PyTorch-CPU restatement of the
+reference forward) on this node's host cores, rank 0, N=1 only, bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "face-super-resolution_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+PEAK_HBM_GBS = 8000.0
+RCAB_CONV_FLOP = 2.0 * 32 * 64 * 64 * 64 * 576
+
+
+def build_model(precision):
+    from src.models import FaceEnhanceNet
+    torch.manual_seed(42)  # stage1_psnr_config.yaml project.seed
+    m = FaceEnhanceNet(num_channels=64, num_groups=6, blocks_per_group=10, reduction_ratio=4, scale_factor=4,
+                       precision=precision)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        m.conv_last.weight.copy_(torch.randn(m.conv_last.weight.shape, generator=g) * 1e-3)
+    return m
+
+
+def timed(fn, steps, warmup, world):
+    for _ in range(warmup):
+        fn()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], device="cuda", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    return float(dt)
+
+
+def time_dominant_kernel(engine, reps=50):
+    """Average duration of the RCAB conv launch (first conv3x3 of the forward program)."""
+    from src.hip.program import current_stream_handle
+    name, fn, args = next(op for op in engine.ctx.ops if op[0] == "conv3x3" and op[1] is not None
+                          and args_is_rcab(op))
+    s = current_stream_handle()
+    for _ in range(5):
+        fn(*args, s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn(*args, s)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps  # ms
+
+
+def args_is_rcab(op):
+    d = op[2][0]._obj
+    return d.Cin == 64 and d.Cout == 64 and d.H == 64 and d.W == 64 and d.B == 32
+
+
+def cpu_baseline(model, seconds=10.0):
+    from oracle import fen_oracle as O
+    sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
+    shape = O.NetShape(64, 6, 10, 4, 4, 0.2)
+    x = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(1234))
+    threads = torch.get_num_threads()
+    with torch.no_grad():
+        O.forward(sd, x, shape, training=False)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            O.forward(sd, x, shape, training=False)
+            n += 1
+            el = time.perf_counter() - t0
+            if (el >= seconds and n >= 3) or n >= 200:
+                break
+    return {"value": round(2 * n / el, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 eval forward, full 6x10 net, batch 2 of 64x64, {n} passes in {el:.1f}s"}
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_rcab_conv.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from src.hip.engine import FENEngine
+
+    B = args.batch
+    model = build_model("bf16")
+    cpu_model_sd = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_model_sd = build_model("fp32")
+    eng = FENEngine(model, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=False, device="cuda")
+    x = torch.rand(B, 3, 64, 64, generator=torch.Generator().manual_seed(1234 + rank)).cuda()
+    eng.x.copy_(x)
+    eng.capture()
+    t = timed(eng.replay, args.steps, args.warmup, world)
+    value = B * world * args.steps / t
+    ms = 1000.0 * t / args.steps
+    kern_ms = time_dominant_kernel(eng)
+    achieved = RCAB_CONV_FLOP / (kern_ms * 1e-3) / 1e12
+    out = {
+        "metric": "images/sec (64->256 4x SR) at batch 32/GPU",
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic U[0,1) 64x64x3 batches resident in HBM; seeded random-init weights of the reference "
+                "architecture",
+        "config": {"workload": "FaceEnhanceNet full (6x10 RCAB, 64ch) inference 64->256, bf16", "global_batch": B * world,
+                   "per_gpu_batch": B, "parallelism": f"replicas x{world}" if world > 1 else "single"},
+        "roofline": {"bound": "mfma", "kernel": "k_conv3x3<bf16,64> (RCAB conv 64->64, 64x64, B=32)",
+                     "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "kernel_ms": round(kern_ms, 5),
+                     "flop_per_launch": RCAB_CONV_FLOP, "traffic": load_traffic()},
+    }
+    del eng
+    torch.cuda.empty_cache()
+    if not args.no_train:
+        tm = build_model("bf16")
+        teng = FENEngine(tm, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=True, device="cuda")
+        hr = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(4321 + rank)).cuda()
+        teng.hr.copy_(hr)
+        if world == 1:
+            teng.capture()
+            fn = teng.replay
+        else:
+            fn = teng.step
+        tt = timed(fn, args.train_steps, 3, world)
+        out["train"] = {"metric": "training images/sec (stage-1 L1 generator step) at batch 32/GPU",
+                        "value": round(B * world * args.train_steps / tt, 2),
+                        "ms_per_step": round(1000.0 * tt / args.train_steps, 3), "steps": args.train_steps,
+                        "loss": float(teng.loss), "allreduce": "RCCL (torch.distributed nccl backend), 8 buckets, "
+                                                               "overlapped with backward" if world > 1 else "none"}
+        del teng
+    if cpu_model_sd is not None:
+        out["cpu_baseline"] = cpu_baseline(cpu_model_sd, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

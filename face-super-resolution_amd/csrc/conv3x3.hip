@@ -4,16 +4,25 @@
 // 182-183, 211-214; custom.py:109-112, 121-124) and, given flipped/transposed weights
 // (fen_pack_conv_w mode 2), the data-gradient of each of them.
 //
-// Block = 256 threads (4 waves), output tile = 16x16 pixels x COT output channels.
-//   D[co][px] = sum_k W[co][k] * X[k][px],  k = (tap, ci):  A = weights, B = pixels.
-//   Each wave owns 4 output rows (4 x 16 px) x COT co -> MT*4 16x16 accumulators.
-// LDS: the 18x18-pixel input halo of one 128-B channel panel (41.5 KB, XOR-swizzled rows)
-//      + two 128-B-row weight tiles [COT][panel] (one per tap, double buffered, T14 split
-//      issue-early / write-late).  57.9 KB at COT=64 -> 2 blocks (8 waves) per CU.
-// Epilogue fuses bias, residual adds, PReLU (fwd) or PReLU-backward (dgrad), PixelShuffle /
-// inverse-PixelShuffle stores, SE global-average-pool partials, and for conv_last the
-// bicubic skip + eval clamp + L1-loss gradient.  bf16 tiles leave through LDS as full
-// 128-B rows (coalesced 16-B stores).
+// Output tile = 16x16 pixels x COT output channels, 4 waves; each wave owns 4 output rows:
+//   D[co][px] = sum_k W[co][k] * X[k][px],  k = (tap, ci):  A = weights, B = pixels,
+//   MT*4 accumulators of v_mfma_f32_16x16x32_bf16 (or 4x v_mfma_f32_16x16x4_f32 per 16 B).
+// Every LDS image has 128-B rows (64 bf16 / 32 f32 channels = one "panel") with the
+// 16-B chunks XOR-swizzled by (row>>1)&7 -> conflict-free ds_read_b128 fragment reads.
+//
+// Two kernels:
+//  * k_conv3x3_p (bf16, Cin == 64 -- every 64-channel conv of the network, forward and
+//    dgrad, the x2 upsampler and conv_last): PERSISTENT, one 256-thread block per CU.
+//    The block's whole filter (9 taps x COT x 64, 72 KB) stays resident in LDS; the
+//    18x18-pixel input halo of the next tile is streamed by LDS-DMA (buffer_load ... lds,
+//    zero padding via the buffer range check) into a second buffer while the MFMAs run
+//    on the current one: one barrier per tile, none per tap.  156.7 KB LDS.
+//  * k_conv3x3_s (any Cin multiple of the panel, bf16 and f32): weights streamed per tap
+//    through a double-buffered LDS tile, halo staged through registers; 2 blocks per CU.
+//    Used for f32 (the parity path) and for Cin > 64 (upsampler dgrad, 128-ch variant).
+// The epilogue fuses bias, residual adds, PReLU (fwd) or PReLU-backward (dgrad),
+// PixelShuffle / inverse-PixelShuffle stores, SE global-average-pool partials, and for
+// conv_last the bicubic skip + eval clamp + L1-loss gradient.
 #include "fen_common.h"
 
 namespace {
@@ -21,97 +30,121 @@ namespace {
 constexpr int HALO = 18;
 constexpr int HP = HALO * HALO;        // 324 halo pixels
 constexpr int HALO_BYTES = HP * 128;   // 41472
+constexpr int HALO_DMA = (HP * 8 + 63) / 64;   // 41 wave-wide 1-KiB LDS-DMA pieces per halo
+constexpr int HALO_SLOT = HALO_DMA * 1024;     // 41984: halo + slack for the last piece
 
-template <typename T, int COT>
-__global__ __launch_bounds__(256, 2) void k_conv3x3(const fen_conv_desc d) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* halo = smem;
-    char* wbuf = smem + HALO_BYTES;
-    constexpr int MT = COT / 16;
-    constexpr int CK = Tr<T>::CK;
-    constexpr int WCH = COT * 8;               // 16-B weight chunks per (tap, panel)
-    constexpr int WPT = (WCH + 255) / 256;     // per thread
+typedef __attribute__((address_space(3))) void lds_void;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q = lane >> 4, c16 = lane & 15;
-    const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
-    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
-    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
-    const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-    const int co0 = blockIdx.y * COT;
-    const int coutp = (Cout + 15) & ~15;
-    const char* xb = (const char*)d.x;
-    const char* wb = (const char*)d.w;
-    const size_t xrow = (size_t)Cin * sizeof(T);
-    const size_t wrow = (size_t)Cin * sizeof(T);
+// Halo images (18 x 18 pixels, 128-B rows): 16-B chunk c of pixel p sits at chunk c ^ (col & 7),
+// col = p % 18.  Fragment reads touch 16 consecutive columns of one halo row at the same
+// logical chunk -> 16 distinct 16-B bank slots (conflict-free ds_read_b128), and because the
+// key depends only on the column, every read of a lane is base(kw, kk) + row * 2304.
+__device__ __forceinline__ int hswz(int p, int chunk) {
+    return (p << 7) + ((chunk ^ ((p % HALO) & 7)) << 4);
+}
+__device__ __forceinline__ int hcol(int col, int chunk) {   // offset of (column col, chunk) in a row
+    return (col << 7) + ((chunk ^ (col & 7)) << 4);
+}
 
-    f32x4 acc[MT][4];
+// Buffer resource (V#) words for a raw byte buffer: base, stride 0, num_records = bytes.
+// Loads at voffset >= bytes return 0 -- used for the conv's zero padding.
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+    r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32) & 0xffff);
+    r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+
+// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds) written to lds_base + lane*16.
+// Issued from inline asm on purpose: hipcc then does not see an LDS write in flight, so it
+// does not drain vmcnt before every ds_read of the *other* halo buffer.  The caller waits
+// (s_waitcnt vmcnt(0)) and barriers before reading the destination.
+__device__ __forceinline__ void dma16(const i32x4& rsrc, unsigned lds_base, int voff) {
+    unsigned keep;  // M0 is compiler-reserved: save and restore it inside the statement
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(lds_base), "v"(voff), "s"(rsrc)
+        : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(size_t)(const lds_void*)p;
+}
+
+
+// s_waitcnt vmcnt(n) for a runtime n (the immediate must be a literal): waits until at
+// most n of this wave's vector-memory ops are outstanding.  Ops retire in issue order, so
+// with n = number of stores issued after the halo prefetch, the prefetch has landed while
+// the tile's output stores keep draining behind the next tile's MFMAs.
+__device__ __forceinline__ void wait_vm_upto(int n) {
+    switch (n) {
+#define FEN_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+        FEN_VMC(1) FEN_VMC(2) FEN_VMC(3) FEN_VMC(4) FEN_VMC(5) FEN_VMC(6) FEN_VMC(7) FEN_VMC(8)
+        FEN_VMC(9) FEN_VMC(10) FEN_VMC(11) FEN_VMC(12) FEN_VMC(13) FEN_VMC(14) FEN_VMC(15) FEN_VMC(16)
+        FEN_VMC(17) FEN_VMC(18) FEN_VMC(19) FEN_VMC(20) FEN_VMC(21) FEN_VMC(22) FEN_VMC(23) FEN_VMC(24)
+        FEN_VMC(25) FEN_VMC(26) FEN_VMC(27) FEN_VMC(28) FEN_VMC(29) FEN_VMC(30) FEN_VMC(31) FEN_VMC(32)
+#undef FEN_VMC
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// Output store instructions a wave is guaranteed to issue in conv_epilogue after the halo
+// prefetch (full interior tiles, plain/SHUFFLE stores); 0 = "wait for everything".
+__device__ __forceinline__ int epi_store_count(const fen_conv_desc& d, int h0, int w0, int mtnt) {
+    if ((d.epi & (FEN_EPI_LAST | FEN_EPI_UNSHUFFLE)) || h0 + 16 > d.H || w0 + 16 > d.W) return 0;
+    return mtnt * (((d.epi & FEN_EPI_PRELU) && d.y_pre) ? 2 : 1);
+}
+
+// Per-channel epilogue constants of one wave's output channels, loaded once per block
+// (bias[co] and the PReLU slope; for SHUFFLE the packed row cp maps to co = 4(cp%Cq)+cp/Cq
+// and the slope index to cp%Cq).
+template <int MT>
+struct EpiConst {
+    float bias[MT][4];
+    float alpha[MT][4];
+};
+template <int MT>
+__device__ __forceinline__ EpiConst<MT> epi_consts(const fen_conv_desc& d, int cob0) {
+    EpiConst<MT> e;
+    const int Cout = d.Cout, Cq = Cout >> 2;
+    const bool shuf = d.epi & FEN_EPI_SHUFFLE;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int npan = Cin / CK;
-    for (int pn = 0; pn < npan; ++pn) {
-        // ---- stage the input halo of panel pn (zero padding outside the image) ----
-        for (int i = tid; i < HP * 8; i += 256) {
-            const int p = i >> 3, ch = i & 7;
-            const int hr = p / HALO, hc = p - hr * HALO;
-            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
-                v = *(const uint4*)(xb + ((size_t)(b * H + gh) * W + gw) * xrow + pn * 128 + ch * 16);
-            *(uint4*)(halo + swz(p, ch)) = v;
+        for (int r = 0; r < 4; ++r) {
+            const int cp = cob0 + m * 16 + r;
+            const bool ok = cp < Cout;
+            const int co = shuf ? 4 * (cp % Cq) + cp / Cq : cp;
+            e.bias[m][r] = (ok && (d.epi & FEN_EPI_BIAS)) ? d.bias[co] : 0.f;
+            e.alpha[m][r] = (ok && (d.epi & (FEN_EPI_PRELU | FEN_EPI_PRELU_BWD))) ? d.alpha[shuf ? cp % Cq : cp] : 0.f;
         }
-        uint4 wr[WPT];
-        auto load_w = [&](int tap) {
-#pragma unroll
-            for (int j = 0; j < WPT; ++j) {
-                const int i = tid + j * 256;
-                if (i < WCH) {
-                    const int r = i >> 3, ch = i & 7;
-                    wr[j] = *(const uint4*)(wb + (size_t)(tap * coutp + co0 + r) * wrow + pn * 128 + ch * 16);
-                }
-            }
-        };
-        auto store_w = [&](char* dst) {
-#pragma unroll
-            for (int j = 0; j < WPT; ++j) {
-                const int i = tid + j * 256;
-                if (i < WCH) *(uint4*)(dst + swz(i >> 3, i & 7)) = wr[j];
-            }
-        };
-        load_w(0);
-        store_w(wbuf);
-        __syncthreads();
-        for (int tap = 0; tap < 9; ++tap) {
-            if (tap < 8) load_w(tap + 1);      // issue early, write after the MFMAs
-            const char* wt = wbuf + (tap & 1) * COT * 128;
-            const int kh = tap / 3, kw = tap - kh * 3;
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                const int chunk = kk * 4 + q;
-                uint4 A[MT], Bf[4];
-#pragma unroll
-                for (int m = 0; m < MT; ++m) A[m] = *(const uint4*)(wt + swz(m * 16 + c16, chunk));
-#pragma unroll
-                for (int n = 0; n < 4; ++n) {
-                    const int p = (wave * 4 + n + kh) * HALO + c16 + kw;
-                    Bf[n] = *(const uint4*)(halo + swz(p, chunk));
-                }
-#pragma unroll
-                for (int m = 0; m < MT; ++m)
-#pragma unroll
-                    for (int n = 0; n < 4; ++n) mma16<T>(acc[m][n], A[m], Bf[n]);
-            }
-            if (tap < 8) store_w(wbuf + ((tap + 1) & 1) * COT * 128);
-            __syncthreads();
-        }
-    }
+    return e;
+}
 
-    // ------------------------------- epilogue -------------------------------
+// ------------------------------------------------------------------------------------
+// epilogue (shared by both kernels).  acc[m][n][r] = D[co = co0 + m*16 + 4q + r][pixel
+// (h0 + wave*4 + n, w0 + c16)].  `stage` (>= 32 KB LDS) enables the bf16 LDS-staged
+// store path (COT == 64 only); `red` is >= 4*COT floats of LDS.  Contains barriers:
+// every thread of the block must call it.
+// ------------------------------------------------------------------------------------
+template <typename T, int COT, int WR, int WC>
+__device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&acc)[COT / 16 / WC][16 / WR], int b,
+                                              int tlin, int h0, int w0, int co0, char* stage, float* red,
+                                              const EpiConst<COT / 16 / WC>& ec) {
+    constexpr int MT = COT / 16 / WC, NT = 16 / WR, CW = COT / WC;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave % WR, wc = wave / WR;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int H = d.H, W = d.W, Cout = d.Cout;
     const int epi = d.epi;
-    float* red = (float*)wbuf;                 // [4 waves][COT] (LDS is free after the loop)
     const int w_ = w0 + c16;
 
     if (epi & FEN_EPI_LAST) {
@@ -121,8 +154,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3(const fen_conv_desc d) {
         const float inv = 1.0f / (float)d.scale;
         float lsum = 0.f;
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const int h = h0 + wave * 4 + n;
+        for (int n = 0; n < NT; ++n) {
+            const int h = h0 + wr * NT + n;
             const bool valid = h < H && w_ < W;
             float bic = 0.f;
             if (valid && q < Cout)
@@ -135,7 +168,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3(const fen_conv_desc d) {
             for (int r = 0; r < 4; ++r) {
                 const int co = q * 4 + r;
                 if (valid && co < Cout) {
-                    float v = acc[0][n][r] + ((epi & FEN_EPI_BIAS) ? d.bias[co] : 0.f) + bq[r];
+                    float v = acc[0][n][r] + ec.bias[0][r] + bq[r];
                     if (d.clamp) v = fminf(fmaxf(v, 0.f), 1.f);
                     const size_t oi = (((size_t)b * Cout + co) * H + h) * W + w_;
                     if (d.y) ((float*)d.y)[oi] = v;
@@ -151,9 +184,14 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3(const fen_conv_desc d) {
         }
         if (d.hr && d.loss_part) {
             lsum = wave_sum(lsum);
+            __syncthreads();
             if (lane == 0) red[wave] = lsum;
             __syncthreads();
-            if (tid == 0) d.loss_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+            if (tid == 0) {
+                float t = 0.f;
+                for (int w = 0; w < WR * WC; ++w) t += red[w];
+                d.loss_part[tlin] = t;
+            }
         }
         return;
     }
@@ -170,24 +208,12 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3(const fen_conv_desc d) {
     // pass 1: elementwise epilogue in registers (acc <- pre-activation value)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-        const int cob = co0 + m * 16 + q * 4;      // first of 4 consecutive (packed) channels
-        float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-        if (epi & FEN_EPI_BIAS) {
+        const int cob = co0 + wc * CW + m * 16 + q * 4;      // first of 4 consecutive (packed) channels
+        const float* bias4 = ec.bias[m];
+        const float* al4 = ec.alpha[m];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int cp = cob + r;
-                const int co = shuf ? 4 * (cp % Cq) + cp / Cq : cp;
-                bias4[r] = cob < Cout ? d.bias[co] : 0.f;
-            }
-        }
-        float al4[4] = {0.f, 0.f, 0.f, 0.f};
-        if ((epi & FEN_EPI_PRELU_BWD) && cob < Cout) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) al4[r] = d.alpha[cob + r];
-        }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const int h = h0 + wave * 4 + n;
+        for (int n = 0; n < NT; ++n) {
+            const int h = h0 + wr * NT + n;
             const bool valid = h < H && w_ < W && cob < Cout;
             const size_t oi = ((size_t)(b * H + h) * W + w_) * Cout + cob;
             float v[4];
@@ -230,126 +256,505 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3(const fen_conv_desc d) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float s = group16_sum(psum[m][r]);
-                if (c16 == 0) red[wave * COT + m * 16 + q * 4 + r] = s;
+                if (c16 == 0) red[wr * COT + wc * CW + m * 16 + q * 4 + r] = s;
             }
         __syncthreads();
-        if (tid < COT && co0 + tid < Cout)
-            d.part[(size_t)blockIdx.x * Cout + co0 + tid] =
-                red[tid] + red[COT + tid] + red[2 * COT + tid] + red[3 * COT + tid];
+        if (tid < COT && co0 + tid < Cout) {
+            float t = 0.f;
+#pragma unroll
+            for (int w = 0; w < WR; ++w) t += red[w * COT + tid];
+            d.part[(size_t)tlin * Cout + co0 + tid] = t;
+        }
     }
 
     const bool prelu = epi & FEN_EPI_PRELU;
-    // value actually stored for output k (0: y_pre, 1: y)
-    auto final_v = [&](float v, int cp, int k) -> float {
-        if (k == 1 && prelu) {
-            const float a = d.alpha[shuf ? (cp % Cq) : cp];
-            return v > 0.f ? v : a * v;
-        }
+    auto final_v = [&](float v, int m, int r, int k) -> float {   // value stored for output k (0: y_pre, 1: y)
+        if (k == 1 && prelu) return v > 0.f ? v : ec.alpha[m][r] * v;
         return v;
     };
 
-    if constexpr (sizeof(T) == 2 && COT == 64) {
-        // ---- bf16: stage the 256 x 64 tile in LDS, leave as full 128-B rows ----
-        char* st = halo;
-        for (int k = 0; k < 2; ++k) {
-            void* dst = k == 0 ? d.y_pre : d.y;
-            if (k == 0 && (!prelu || !dst)) continue;
-            __syncthreads();
+    if (stage != nullptr) {
+        if constexpr (sizeof(T) == 2 && COT == 64) {
+            // ---- bf16: stage the 256 x 64 tile in LDS, leave as full 128-B rows ----
+            for (int k = 0; k < 2; ++k) {
+                void* dst = k == 0 ? d.y_pre : d.y;
+                if (k == 0 && (!prelu || !dst)) continue;
+                __syncthreads();
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const int cl = m * 16 + q * 4;
+                for (int m = 0; m < MT; ++m) {
+                    const int cl = wc * CW + m * 16 + q * 4;
 #pragma unroll
-                for (int n = 0; n < 4; ++n) {
-                    const int px = (wave * 4 + n) * 16 + c16;
-                    float v[4];
+                    for (int n = 0; n < NT; ++n) {
+                        const int px = (wr * NT + n) * 16 + c16;
+                        float v[4];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = final_v(acc[m][n][r], co0 + cl + r, k);
-                    st4<bf16>(st + swz(px, cl >> 3) + (q & 1) * 8, v);
+                        for (int r = 0; r < 4; ++r) v[r] = final_v(acc[m][n][r], m, r, k);
+                        st4<bf16>(stage + swz(px, cl >> 3) + (q & 1) * 8, v);
+                    }
+                }
+                __syncthreads();
+                if (!unshuf) {
+                    for (int i = tid; i < 256 * 8; i += 256) {
+                        const int px = i >> 3, ch = i & 7;
+                        const int h = h0 + (px >> 4), w = w0 + (px & 15);
+                        if (h >= H || w >= W) continue;
+                        const uint4 v = *(const uint4*)(stage + swz(px, ch));
+                        size_t o;
+                        if (shuf) {
+                            const int cp = co0 + ch * 8, t = cp / Cq, c = cp % Cq;
+                            o = ((size_t)(b * 2 * H + 2 * h + (t >> 1)) * (2 * W) + 2 * w + (t & 1)) * Cq + c;
+                        } else {
+                            o = ((size_t)(b * H + h) * W + w) * Cout + co0 + ch * 8;
+                        }
+                        *(uint4*)((char*)dst + o * 2) = v;
+                    }
+                } else {
+                    // du[b][h/2][w/2][4*co + 2*(h&1) + (w&1)]: 8x8 du pixels x 4*COT channels
+                    const int Hh = H >> 1, Wh = W >> 1;
+                    for (int i = tid; i < 64 * 32; i += 256) {
+                        const int dp = i >> 5, kq = i & 31;
+                        const int hh = dp >> 3, ww = dp & 7;
+                        const int gh = (h0 >> 1) + hh, gw = (w0 >> 1) + ww;
+                        if (gh >= Hh || gw >= Wh) continue;
+                        unsigned short e[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int cl = 2 * kq + (j >> 2), t = j & 3;
+                            const int px = (2 * hh + (t >> 1)) * 16 + 2 * ww + (t & 1);
+                            e[j] = *(const unsigned short*)(stage + swz(px, cl >> 3) + (cl & 7) * 2);
+                        }
+                        uint4 u;
+                        u.x = e[0] | ((unsigned)e[1] << 16);
+                        u.y = e[2] | ((unsigned)e[3] << 16);
+                        u.z = e[4] | ((unsigned)e[5] << 16);
+                        u.w = e[6] | ((unsigned)e[7] << 16);
+                        const size_t o = ((size_t)(b * Hh + gh) * Wh + gw) * (4 * Cout) + 4 * co0 + 8 * kq;
+                        *(uint4*)((char*)dst + o * 2) = u;
+                    }
                 }
             }
-            __syncthreads();
-            if (!unshuf) {
-                for (int i = tid; i < 256 * 8; i += 256) {
-                    const int px = i >> 3, ch = i & 7;
-                    const int h = h0 + (px >> 4), w = w0 + (px & 15);
-                    if (h >= H || w >= W) continue;
-                    const uint4 v = *(const uint4*)(st + swz(px, ch));
-                    size_t o;
-                    if (shuf) {
-                        const int cp = co0 + ch * 8, t = cp / Cq, c = cp % Cq;
-                        o = ((size_t)(b * 2 * H + 2 * h + (t >> 1)) * (2 * W) + 2 * w + (t & 1)) * Cq + c;
-                    } else {
-                        o = ((size_t)(b * H + h) * W + w) * Cout + co0 + ch * 8;
-                    }
-                    *(uint4*)((char*)dst + o * 2) = v;
-                }
-            } else {
-                // du[b][h/2][w/2][4*co + 2*(h&1) + (w&1)]: 8x8 du pixels x 4*COT channels
-                const int Hh = H >> 1, Wh = W >> 1;
-                for (int i = tid; i < 64 * 32; i += 256) {
-                    const int dp = i >> 5, kq = i & 31;
-                    const int hh = dp >> 3, ww = dp & 7;
-                    const int gh = (h0 >> 1) + hh, gw = (w0 >> 1) + ww;
-                    if (gh >= Hh || gw >= Wh) continue;
-                    unsigned short e[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int cl = 2 * kq + (j >> 2), t = j & 3;
-                        const int px = (2 * hh + (t >> 1)) * 16 + 2 * ww + (t & 1);
-                        e[j] = *(const unsigned short*)(st + swz(px, cl >> 3) + (cl & 7) * 2);
-                    }
-                    uint4 u;
-                    u.x = e[0] | ((unsigned)e[1] << 16);
-                    u.y = e[2] | ((unsigned)e[3] << 16);
-                    u.z = e[4] | ((unsigned)e[5] << 16);
-                    u.w = e[6] | ((unsigned)e[7] << 16);
-                    const size_t o = ((size_t)(b * Hh + gh) * Wh + gw) * (4 * Cout) + 4 * co0 + 8 * kq;
-                    *(uint4*)((char*)dst + o * 2) = u;
-                }
-            }
+            return;
         }
-    } else {
-        // ---- direct stores from registers (f32, or bf16 with COT != 64) ----
-        for (int k = 0; k < 2; ++k) {
-            void* dst = k == 0 ? d.y_pre : d.y;
-            if (k == 0 && (!prelu || !dst)) continue;
+    }
+    // ---- direct stores from registers ----
+    for (int k = 0; k < 2; ++k) {
+        void* dst = k == 0 ? d.y_pre : d.y;
+        if (k == 0 && (!prelu || !dst)) continue;
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const int cob = co0 + m * 16 + q * 4;
-                if (cob >= Cout) continue;
+        for (int m = 0; m < MT; ++m) {
+            const int cob = co0 + wc * CW + m * 16 + q * 4;
+            if (cob >= Cout) continue;
 #pragma unroll
-                for (int n = 0; n < 4; ++n) {
-                    const int h = h0 + wave * 4 + n;
-                    if (h >= H || w_ >= W) continue;
-                    float v[4];
+            for (int n = 0; n < NT; ++n) {
+                const int h = h0 + wr * NT + n;
+                if (h >= H || w_ >= W) continue;
+                float v[4];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = final_v(acc[m][n][r], cob + r, k);
-                    if (shuf) {
-                        const int t = cob / Cq, c = cob % Cq;
-                        const size_t o = ((size_t)(b * 2 * H + 2 * h + (t >> 1)) * (2 * W) + 2 * w_ + (t & 1)) * Cq + c;
-                        st4<T>((char*)dst + o * sizeof(T), v);
-                    } else if (unshuf) {
-                        const int Hh = H >> 1, Wh = W >> 1, t = 2 * (h & 1) + (w_ & 1);
-                        const size_t o = ((size_t)(b * Hh + (h >> 1)) * Wh + (w_ >> 1)) * (4 * Cout) + t;
+                for (int r = 0; r < 4; ++r) v[r] = final_v(acc[m][n][r], m, r, k);
+                if (shuf) {
+                    const int t = cob / Cq, c = cob % Cq;
+                    const size_t o = ((size_t)(b * 2 * H + 2 * h + (t >> 1)) * (2 * W) + 2 * w_ + (t & 1)) * Cq + c;
+                    st4<T>((char*)dst + o * sizeof(T), v);
+                } else if (unshuf) {
+                    const int Hh = H >> 1, Wh = W >> 1, t = 2 * (h & 1) + (w_ & 1);
+                    const size_t o = ((size_t)(b * Hh + (h >> 1)) * Wh + (w_ >> 1)) * (4 * Cout) + t;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) ((T*)dst)[o + 4 * (cob + r)] = fromf<T>(v[r]);
-                    } else {
-                        const size_t o = ((size_t)(b * H + h) * W + w_) * Cout + cob;
-                        st4<T>((char*)dst + o * sizeof(T), v);
-                    }
+                    for (int r = 0; r < 4; ++r) ((T*)dst)[o + 4 * (cob + r)] = fromf<T>(v[r]);
+                } else {
+                    const size_t o = ((size_t)(b * H + h) * W + w_) * Cout + cob;
+                    st4<T>((char*)dst + o * sizeof(T), v);
                 }
             }
         }
     }
 }
 
+// MFMAs of one tap from a weight tile wt ([COT rows][128 B]) and a halo image
+// wave (wr, wc) reads weight rows wc*MT*16 + m*16 + c16 and halo rows wr*NT + n + kh
+template <typename T, int MT, int NT>
+__device__ __forceinline__ void conv_tap(f32x4 (&acc)[MT][NT], const char* wt, const char* halo, int tap, int wr,
+                                         int wc, int q, int c16) {
+    const int kh = tap / 3, kw = tap - kh * 3;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + q;
+        uint4 A[MT], Bf[NT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) A[m] = *(const uint4*)(wt + swz(wc * MT * 16 + m * 16 + c16, chunk));
+        const char* hb = halo + hcol(c16 + kw, chunk);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) Bf[n] = *(const uint4*)(hb + (wr * NT + n + kh) * (HALO * 128));
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A[m], Bf[n]);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv3x3_p: persistent, resident weights, LDS-DMA double-buffered halo (bf16, Cin=64)
+// ------------------------------------------------------------------------------------
+template <int COT, int WR, int WC>
+__global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_desc d) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int MT = COT / 16 / WC, NT = 16 / WR, NW = WR * WC;
+    constexpr int WBYTES = 9 * COT * 128;
+    char* wts = smem;
+    char* hbuf = smem + WBYTES;                              // 2 x HALO_SLOT
+    float* red = (float*)(smem + WBYTES + 2 * HALO_SLOT);    // WR * COT floats
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave % WR, wc = wave / WR;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int H = d.H, W = d.W, Cout = d.Cout;
+    const int coutp = (Cout + 15) & ~15;
+    const int ncot = coutp / COT;
+    const int cot = blockIdx.x % ncot, co0 = cot * COT;
+    const int nslot = gridDim.x / ncot, slot = blockIdx.x / ncot;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int ntiles = d.B * tpi;
+
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)d.w, (short)0, (int)((size_t)9 * coutp * 128), 0x00020000);
+
+    // resident filter: rows r = tap*COT + co_l; lane-linear LDS slots, swizzle on the source
+    for (int i = wave; i < WBYTES / 1024; i += NW) {
+        const int s = i * 64 + lane;
+        const int r = s >> 3, pc = s & 7;
+        const int c = pc ^ ((r >> 1) & 7);
+        const int tap = r / COT, col = r - tap * COT;
+        const int voff = ((tap * coutp + co0 + col) * 64 + c * 8) * 2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wts + i * 1024), 16, voff, 0, 0, 0);
+    }
+    const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * 128));
+    // lane-linear LDS slots s = i*64 + lane hold (pixel p = s>>3, chunk pc = s&7); the XOR
+    // swizzle is applied to the SOURCE address; slots past the halo read out of range (-> 0)
+    // and land in the slack after each buffer.
+    auto load_halo = [&](int t, char* buf) {
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const unsigned base = lds_addr(buf);
+        for (int i = wave; i < HALO_DMA; i += NW) {
+            const int s = i * 64 + lane;
+            const int p = s >> 3, pc = s & 7;
+            const int hr = p / HALO, hc = p - hr * HALO;
+            const int c = pc ^ (hc & 7);
+            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+            const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
+            dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
+        }
+    };
+
+    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * MT * 16 + q * 4);
+    int t = slot;
+    if (t < ntiles) load_halo(t, hbuf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int k = 0; t < ntiles; ++k, t += nslot) {
+        char* cur = hbuf + (k & 1) * HALO_SLOT;
+        const int tn = t + nslot;
+        if (tn < ntiles) load_halo(tn, hbuf + ((k + 1) & 1) * HALO_SLOT);
+        f32x4 acc[MT][NT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(d.debug & 2)) {
+#pragma unroll 1
+            for (int tap = 0; tap < 9; ++tap)
+                conv_tap<bf16, MT, NT>(acc, wts + tap * COT * 128, cur, tap, wr, wc, q, c16);
+        }
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        if (d.debug & 1) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int n = 0; n < NT; ++n) asm volatile("" ::"v"(acc[m][n]));
+        } else {
+            conv_epilogue<bf16, COT, WR, WC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
+        }
+        wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                        // ... for everyone; cur is free
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv3x3_r: register-resident filter (bf16, Cin == 64).  Each wave keeps its whole
+// share of the filter -- 9 taps x 64 ci x (16*MT) co = 36 KB at MT=2 -- in 144 VGPRs for
+// the life of the persistent block, so the tap loop reads only pixel fragments from LDS.
+// The halo image uses a 160-B pixel row (128 B data + 32 B pad): every ds_read_b128 of a
+// fragment is conflict-free AND is one base VGPR + an immediate offset.  The next tile's
+// halo streams in by LDS-DMA (inline-asm buffer_load ... lds, zero padding by the range
+// check) while the current tile's MFMAs run; one barrier per tile.
+// ------------------------------------------------------------------------------------
+constexpr int RSTRIDE = 160;
+constexpr int RHALO_DMA = (HP * 10 + 63) / 64;   // 51 one-KiB pieces per halo
+constexpr int RHALO_SLOT = RHALO_DMA * 1024;     // 52224 B
+
+template <int COT, int MT>
+__global__ __launch_bounds__(64 * 4 * (COT / 16 / MT), 1) void k_conv3x3_r(const fen_conv_desc d) {
+    constexpr int WC = COT / 16 / MT, WR = 4, NT = 4, NW = WR * WC;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* ring = smem;                                      // 3 x RHALO_SLOT
+    float* red = (float*)(smem + 3 * RHALO_SLOT);           // WR * COT floats
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave % WR, wc = wave / WR;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int H = d.H, W = d.W, Cout = d.Cout;
+    const int coutp = (Cout + 15) & ~15;
+    const int ncot = coutp / COT;
+    const int cot = blockIdx.x % ncot, co0 = cot * COT;
+    const int nslot = gridDim.x / ncot, slot = blockIdx.x / ncot;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int ntiles = d.B * tpi;
+    const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * 128));
+    const i32x4 wr4 = make_rsrc(d.w, (unsigned)((size_t)9 * coutp * 128));
+
+    auto load_halo = [&](int t, char* buf) {   // slot s -> pixel s/10, 16-B chunk s%10 (8, 9 = pad)
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const unsigned base = lds_addr(buf);
+        for (int i = wave; i < RHALO_DMA; i += NW) {
+            const int s = i * 64 + lane;
+            const int p = s / 10, c = s - p * 10;
+            const int hr = p / HALO, hc = p - hr * HALO;
+            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+            const bool in = c < 8 && p < HP && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
+            dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
+        }
+    };
+
+    // prologue: filter -> LDS (buffers 1-2), first halo -> buffer 0, then filter -> VGPRs
+    {
+        const unsigned wbase = lds_addr(ring + RHALO_SLOT);
+        for (int i = wave; i < 9 * COT * 8 / 64; i += NW) {
+            const int s = i * 64 + lane;
+            const int r = s >> 3, c = s & 7;
+            const int tap = r / COT, col = r - tap * COT;
+            dma16(wr4, __builtin_amdgcn_readfirstlane(wbase + i * 1024), ((tap * coutp + co0 + col) * 64 + c * 8) * 2);
+        }
+    }
+    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * MT * 16 + q * 4);
+    int t = slot;
+    if (t < ntiles) load_halo(t, ring);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint4 wreg[9][2][MT];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const int row = tap * COT + wc * MT * 16 + m * 16 + c16;
+                wreg[tap][kk][m] = *(const uint4*)(ring + RHALO_SLOT + row * 128 + (kk * 4 + q) * 16);
+            }
+    __syncthreads();   // filter staging area is reused as halo buffers below
+
+    const int lane_off = c16 * RSTRIDE + q * 16;
+    for (int k = 0; t < ntiles; ++k, t += nslot) {
+        char* cur = ring + (k % 3) * RHALO_SLOT;
+        const int tn = t + nslot;
+        if (tn < ntiles) load_halo(tn, ring + ((k + 1) % 3) * RHALO_SLOT);
+        f32x4 acc[MT][NT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* hb = cur + lane_off + wr * NT * HALO * RSTRIDE;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                uint4 Bf[NT];
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    Bf[n] = *(const uint4*)(hb + ((n + kh) * HALO + kw) * RSTRIDE + kk * 64);
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], wreg[tap][kk][m], Bf[n]);
+            }
+        }
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        conv_epilogue<bf16, COT, WR, WC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
+        wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                        // ... for everyone; cur is free
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv3x3_s: streamed per-tap weights, register-staged halo (f32 / bf16, any Cin panel)
+// ------------------------------------------------------------------------------------
 template <typename T, int COT>
-int launch_conv(const fen_conv_desc* d, hipStream_t s) {
+__global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* halo = smem;
+    char* wbuf = smem + HALO_BYTES;
+    constexpr int MT = COT / 16;
+    constexpr int CK = Tr<T>::CK;
+    constexpr int WCH = COT * 8;               // 16-B weight chunks per (tap, panel)
+    constexpr int WPT = (WCH + 255) / 256;     // per thread
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
+    const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+    const int co0 = blockIdx.y * COT;
+    const int coutp = (Cout + 15) & ~15;
+    const char* xb = (const char*)d.x;
+    const char* wb = (const char*)d.w;
+    const size_t xrow = (size_t)Cin * sizeof(T);
+
+    f32x4 acc[MT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + q * 4);   // latency hidden by the main loop
+
+    const int npan = Cin / CK;
+    for (int pn = 0; pn < npan; ++pn) {
+        // ---- stage the input halo of panel pn (zero padding outside the image) ----
+        constexpr int HPT = (HP * 8 + 255) / 256;   // 11 chunks per thread: loads first, then writes
+        uint4 hv[HPT];
+#pragma unroll
+        for (int j = 0; j < HPT; ++j) {
+            const int i = tid + j * 256;
+            hv[j] = make_uint4(0, 0, 0, 0);
+            if (i < HP * 8) {
+                const int p = i >> 3, ch = i & 7;
+                const int hr = p / HALO, hc = p - hr * HALO;
+                const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+                if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
+                    hv[j] = *(const uint4*)(xb + ((size_t)(b * H + gh) * W + gw) * xrow + pn * 128 + ch * 16);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < HPT; ++j) {
+            const int i = tid + j * 256;
+            if (i < HP * 8) *(uint4*)(halo + hswz(i >> 3, i & 7)) = hv[j];
+        }
+        uint4 wr[WPT];
+        // every thread loads WPT chunks (chunk index wrapped, duplicates are harmless): no
+        // per-load branch, so hipcc keeps the prefetch in flight across the tap's MFMAs
+        auto load_w = [&](int tap) {
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) {
+                const int i = (tid + j * 256) % WCH;
+                const int r = i >> 3, ch = i & 7;
+                wr[j] = *(const uint4*)(wb + (size_t)(tap * coutp + co0 + r) * xrow + pn * 128 + ch * 16);
+            }
+        };
+        auto store_w = [&](char* dst) {
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) {
+                const int i = (tid + j * 256) % WCH;
+                *(uint4*)(dst + swz(i >> 3, i & 7)) = wr[j];
+            }
+        };
+        load_w(0);
+        store_w(wbuf);
+        __syncthreads();
+        for (int tap = 0; tap < 9; ++tap) {
+            if (tap < 8) load_w(tap + 1);      // issue early, write after the MFMAs
+            conv_tap<T, MT, 4>(acc, wbuf + (tap & 1) * COT * 128, halo, tap, wave, 0, q, c16);
+            if (tap < 8) store_w(wbuf + ((tap + 1) & 1) * COT * 128);
+            __syncthreads();
+        }
+    }
+    float* red = (float*)wbuf;     // LDS is free after the loop
+    char* stage = (sizeof(T) == 2 && COT == 64) ? halo : nullptr;
+    conv_epilogue<T, COT, 4, 1>(d, acc, b, blockIdx.x, h0, w0, co0, stage, red, ec);
+}
+
+int g_num_cus = 0;
+
+// kernel-variant selector for tuning runs (FEN_CONV_VARIANT): 0 default (LDS-resident filter,
+// 4x2 waves for 64-channel tiles; streamed kernel for 16-channel tiles), 1 streamed everywhere,
+// 2/3/4/5 LDS-resident filter with 8x1 / 4x2 / 2x4 / 4x1 waves (rows x co-groups),
+// 6 register-resident filter (r<64,4>), 7 register-resident filter (r<64,2>)
+int conv_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("FEN_CONV_VARIANT");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
+template <int COT, int WR, int WC>
+int launch_p(const fen_conv_desc* d, hipStream_t s) {
+    const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
+    const int ntiles = d->B * tpi;
+    const int ncot = ((d->Cout + 15) & ~15) / COT;
+    if (g_num_cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int grid = g_num_cus;
+    grid -= grid % ncot;
+    const int maxg = ntiles * ncot;
+    if (grid > maxg) grid = maxg;
+    const size_t lds = 9 * COT * 128 + 2 * HALO_SLOT + WR * COT * 4 + 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_p<COT, WR, WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_conv3x3_p<COT, WR, WC>), dim3(grid), dim3(64 * WR * WC), lds, s, *d);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+template <int COT, int MT>
+int launch_r(const fen_conv_desc* d, hipStream_t s) {
+    const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
+    const int ntiles = d->B * tpi;
+    const int ncot = ((d->Cout + 15) & ~15) / COT;
+    if (g_num_cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int grid = g_num_cus;
+    grid -= grid % ncot;
+    const int maxg = ntiles * ncot;
+    if (grid > maxg) grid = maxg;
+    constexpr int NW = 4 * (COT / 16 / MT);
+    const size_t lds = 3 * RHALO_SLOT + 4 * COT * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_r<COT, MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_conv3x3_r<COT, MT>), dim3(grid), dim3(64 * NW), lds, s, *d);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+template <typename T, int COT>
+int launch_s(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int coutp = (d->Cout + 15) & ~15;
     dim3 grid(d->B * tpi, coutp / COT);
     const size_t lds = HALO_BYTES + 2 * COT * 128;
-    hipLaunchKernelGGL((k_conv3x3<T, COT>), grid, dim3(256), lds, s, *d);
+    hipLaunchKernelGGL((k_conv3x3_s<T, COT>), grid, dim3(256), lds, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
@@ -370,11 +775,17 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     if ((epi & FEN_EPI_POOL) && (epi & FEN_EPI_PRELU_BWD)) return FEN_EUNSUPPORTED;
     if ((epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE)) == (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE))
         return FEN_EUNSUPPORTED;
+    // the persistent kernel addresses the input with 32-bit buffer offsets
+    const bool small = (size_t)d->B * d->H * d->W * 128 < (size_t)0x7fff0000;
+    const bool persist = d->dtype == FEN_BF16 && d->Cin == 64 && small && !(epi & FEN_EPI_UNSHUFFLE) &&
+                         conv_variant() != 1;
     hipStream_t s = (hipStream_t)stream;
     if (epi & FEN_EPI_LAST) {
         if (d->Cout > 4 || !d->lr || d->scale <= 0 || d->H % d->scale || d->W % d->scale) return FEN_EINVAL;
         if (epi & ~(FEN_EPI_LAST | FEN_EPI_BIAS)) return FEN_EUNSUPPORTED;
-        return d->dtype == FEN_BF16 ? launch_conv<bf16, 16>(d, s) : launch_conv<float, 16>(d, s);
+        if (persist && conv_variant() == 5) return launch_p<16, 4, 1>(d, s);
+        if (persist && conv_variant() >= 6) return launch_r<16, 1>(d, s);
+        return d->dtype == FEN_BF16 ? launch_s<bf16, 16>(d, s) : launch_s<float, 16>(d, s);
     }
     if (!d->y) return FEN_EINVAL;
     if (epi & FEN_EPI_SHUFFLE) {
@@ -383,9 +794,24 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
             return FEN_EUNSUPPORTED;
     }
     if ((epi & FEN_EPI_UNSHUFFLE) && ((d->H | d->W) & 1)) return FEN_EINVAL;
-    if (d->Cout % 64 == 0)
-        return d->dtype == FEN_BF16 ? launch_conv<bf16, 64>(d, s) : launch_conv<float, 64>(d, s);
-    if (d->Cout % 16 == 0)
-        return d->dtype == FEN_BF16 ? launch_conv<bf16, 16>(d, s) : launch_conv<float, 16>(d, s);
+    if (d->Cout % 64 == 0) {
+        if (persist) {
+            switch (conv_variant()) {
+                case 7: return launch_r<64, 2>(d, s);
+                case 6: return launch_r<64, 4>(d, s);
+                case 5: return launch_p<64, 4, 1>(d, s);
+                case 2: return launch_p<64, 8, 1>(d, s);
+                case 3: return launch_p<64, 4, 2>(d, s);
+                case 4: return launch_p<64, 2, 4>(d, s);
+                default: return launch_p<64, 4, 2>(d, s);
+            }
+        }
+        return d->dtype == FEN_BF16 ? launch_s<bf16, 64>(d, s) : launch_s<float, 64>(d, s);
+    }
+    if (d->Cout % 16 == 0) {
+        if (persist && conv_variant() == 5) return launch_p<16, 4, 1>(d, s);
+        if (persist && conv_variant() >= 6) return launch_r<16, 1>(d, s);
+        return d->dtype == FEN_BF16 ? launch_s<bf16, 16>(d, s) : launch_s<float, 16>(d, s);
+    }
     return FEN_EUNSUPPORTED;
 }

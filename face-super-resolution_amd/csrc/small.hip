@@ -339,13 +339,61 @@ __global__ void k_bicubic_down4(int B, int C, int H, int W, const float* __restr
 }
 
 template <typename T>
-__global__ void k_nchw_to_nhwc(int B, int C, int H, int W, const float* __restrict__ x, T* __restrict__ y) {
+__global__ void k_nchw_to_nhwc(int B, int C, int H, int W, int Cpad, const float* __restrict__ x, T* __restrict__ y) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // NHWC order
-    if (i >= (size_t)B * C * H * W) return;
-    const int c = (int)(i % C);
-    const size_t px = i / C;
+    if (i >= (size_t)B * Cpad * H * W) return;
+    const int c = (int)(i % Cpad);
+    const size_t px = i / Cpad;
     const int w = (int)(px % W), h = (int)((px / W) % H), b = (int)(px / ((size_t)W * H));
-    y[i] = fromf<T>(x[(((size_t)b * C + c) * H + h) * W + w]);
+    y[i] = fromf<T>(c < C ? x[(((size_t)b * C + c) * H + h) * W + w] : 0.f);
+}
+
+// dv = dy * (pre>0 ? 1 : alpha[c]) -> du[b][h/2][w/2][4c + 2(h&1) + (w&1)]; block = 16x16 px tile
+template <typename T>
+__global__ __launch_bounds__(256) void k_prelu_bwd_unshuffle(int B, int H, int W, int C, const T* __restrict__ dy,
+                                                             const T* __restrict__ pre, const float* __restrict__ alpha,
+                                                             T* __restrict__ du, float* __restrict__ part) {
+    __shared__ float sdal[256 * 2];
+    const int tid = threadIdx.x;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
+    const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+    const int K2 = C / 2, k = tid % K2;
+    const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
+    float dal0 = 0.f, dal1 = 0.f;
+    const int Hh = H >> 1, Wh = W >> 1;
+    for (int i = tid; i < 64 * K2; i += 256) {
+        const int dp = i / K2, hh = dp >> 3, ww = dp & 7;
+        const int gh2 = (h0 >> 1) + hh, gw2 = (w0 >> 1) + ww;
+        if (gh2 >= Hh || gw2 >= Wh) continue;
+        float out[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const size_t pi = ((size_t)(b * H + 2 * gh2 + (t >> 1)) * W + 2 * gw2 + (t & 1)) * C + 2 * k;
+            const float d0 = tof<T>(dy[pi]), d1 = tof<T>(dy[pi + 1]);
+            const float p0 = tof<T>(pre[pi]), p1 = tof<T>(pre[pi + 1]);
+            dal0 += p0 > 0.f ? 0.f : d0 * p0;
+            dal1 += p1 > 0.f ? 0.f : d1 * p1;
+            out[t] = p0 > 0.f ? d0 : d0 * al0;
+            out[4 + t] = p1 > 0.f ? d1 : d1 * al1;
+        }
+        char* o = (char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 8 * k) * sizeof(T);
+        if constexpr (sizeof(T) == 2) {
+            *(uint4*)o = pack16<bf16>(out);
+        } else {
+            *(uint4*)o = pack16<float>(out);
+            *(uint4*)(o + 16) = pack16<float>(out + 4);
+        }
+    }
+    sdal[tid * 2] = dal0;
+    sdal[tid * 2 + 1] = dal1;
+    __syncthreads();
+    if (tid < C) {
+        const int kk = tid >> 1, e = tid & 1;
+        float s = 0.f;
+        for (int r = kk; r < 256; r += K2) s += sdal[r * 2 + e];
+        part[(size_t)blockIdx.x * C + tid] = s;
+    }
 }
 template <typename T>
 __global__ void k_nhwc_to_nchw(int B, int C, int H, int W, const T* __restrict__ x, float* __restrict__ y) {
@@ -630,13 +678,29 @@ extern "C" int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const flo
     return FEN_OK;
 }
 
-extern "C" int fen_nchw_to_nhwc(int dtype, int B, int C, int H, int W, const float* x, void* y, void* stream) {
-    if (!x || !y) return FEN_EINVAL;
-    const size_t n = (size_t)B * C * H * W;
+extern "C" int fen_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cpad, const float* x, void* y,
+                                void* stream) {
+    if (!x || !y || Cpad < C) return FEN_EINVAL;
+    const size_t n = (size_t)B * Cpad * H * W;
     if (dtype == FEN_BF16)
-        hipLaunchKernelGGL(k_nchw_to_nhwc<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, x, (bf16*)y);
+        hipLaunchKernelGGL(k_nchw_to_nhwc<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, Cpad, x, (bf16*)y);
     else
-        hipLaunchKernelGGL(k_nchw_to_nhwc<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, x, (float*)y);
+        hipLaunchKernelGGL(k_nchw_to_nhwc<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, Cpad, x, (float*)y);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_prelu_bwd_unshuffle(int dtype, int B, int H, int W, int C, const void* dy, const void* pre,
+                                       const float* alpha, void* du, float* part, void* stream) {
+    if (!dy || !pre || !alpha || !du || !part || C < 32 || C > 256 || 256 % (C / 2) || (H | W) & 1)
+        return FEN_EINVAL;
+    const int nb = B * ((H + 15) / 16) * ((W + 15) / 16);
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_prelu_bwd_unshuffle<bf16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, (const bf16*)dy,
+                           (const bf16*)pre, alpha, (bf16*)du, part);
+    else
+        hipLaunchKernelGGL(k_prelu_bwd_unshuffle<float>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C,
+                           (const float*)dy, (const float*)pre, alpha, (float*)du, part);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -166,25 +166,48 @@ __global__ __launch_bounds__(576, 1) void k_wgrad(const fen_wgrad_desc d, int tp
 }
 
 // dw[co][ci][kh][kw] (+)= sum_chunk slab[chunk][tap][co][ci];  db[co] (+)= sum_chunk dbpart
-__global__ void k_wgrad_finalize(int nchunk, int Cout, int Cin, int cout_valid, const float* part,
-                                 const float* dbpart, float* dw, float* db, int accumulate) {
+// block = 64 consecutive slab elements x 4 waves, each wave sums a quarter of the chunks
+// (independent loads in flight), fixed-order combine in LDS -> bitwise reproducible.
+__global__ __launch_bounds__(256) void k_wgrad_finalize(int nchunk, int Cout, int Cin, int cout_valid,
+                                                        const float* __restrict__ part,
+                                                        const float* __restrict__ dbpart, float* dw, float* db,
+                                                        int accumulate) {
+    __shared__ float red[4][64];
     const size_t per = (size_t)9 * Cout * Cin;
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const size_t i = (size_t)blockIdx.x * 64 + lane;
+    const int q0 = (nchunk * g) / 4, q1 = (nchunk * (g + 1)) / 4;
+    float s = 0.f;
     if (i < per) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int c = q0;
+        for (; c + 3 < q1; c += 4) {
+            s0 += part[(size_t)c * per + i];
+            s1 += part[(size_t)(c + 1) * per + i];
+            s2 += part[(size_t)(c + 2) * per + i];
+            s3 += part[(size_t)(c + 3) * per + i];
+        }
+        for (; c < q1; ++c) s0 += part[(size_t)c * per + i];
+        s = (s0 + s1) + (s2 + s3);
+    }
+    red[g][lane] = s;
+    __syncthreads();
+    if (g == 0 && i < per) {
+        const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
         const int ci = (int)(i % Cin);
         const int co = (int)((i / Cin) % Cout);
         const int tap = (int)(i / ((size_t)Cin * Cout));
         if (co < cout_valid) {
-            float s = 0.f;
-            for (int c = 0; c < nchunk; ++c) s += part[(size_t)c * per + i];
             float* o = dw + ((size_t)co * Cin + ci) * 9 + tap;
-            *o = accumulate ? *o + s : s;
+            *o = accumulate ? *o + t : t;
         }
     }
-    if (db && i < (size_t)cout_valid) {
-        float s = 0.f;
-        for (int c = 0; c < nchunk; ++c) s += dbpart[(size_t)c * Cout + i];
-        db[i] = accumulate ? db[i] + s : s;
+    if (db && blockIdx.x == 0 && g == 1) {
+        for (int co = lane; co < cout_valid; co += 64) {
+            float t = 0.f;
+            for (int c = 0; c < nchunk; ++c) t += dbpart[(size_t)c * Cout + co];
+            db[co] = accumulate ? db[co] + t : t;
+        }
     }
 }
 
@@ -233,7 +256,7 @@ extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
     }
     FEN_CHECK_LAUNCH();
     const size_t per = (size_t)9 * d->Cout * d->Cin;
-    const int nb = (int)((per + 255) / 256);
+    const int nb = (int)((per + 63) / 64);
     hipLaunchKernelGGL(k_wgrad_finalize, dim3(nb), dim3(256), 0, s, nchunk, d->Cout, d->Cin, d->cout_valid,
                        part, dbpart, d->dw, d->db, d->accumulate);
     FEN_CHECK_LAUNCH();

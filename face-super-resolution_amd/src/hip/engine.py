@@ -1,0 +1,209 @@
+"""Static-buffer execution engine for FaceEnhanceNet on one MI355X.
+
+The engine records the whole forward (and, for training, the backward, the gradient
+all-reduce hooks and the clip+AdamW update) once into C-ABI programs over persistent
+buffers, so one call = one replay of ~400-1100 launches with no allocation -- and the
+replay is capturable into a single hipGraph (`capture()`).
+
+Data parallelism: one process per GPU; the loss gradient is pre-scaled by
+1/world so a SUM all-reduce yields the global-batch mean.  Gradients live in one flat fp32
+arena laid out in parameter order, so each ResidualGroup's gradients are one contiguous
+bucket; the backward program issues `dist.all_reduce(bucket, async_op=True)` as soon as a
+bucket's last weight-gradient kernel is enqueued -- RCCL then runs on its own HIP stream
+beside the remaining backward kernels -- and the update waits for all buckets.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import lib as L
+from .net import Backward, Forward, NetSpec, Weights, colsum, tiles
+from .program import Ctx, ptr
+
+
+def flatten_params(model: torch.nn.Module, device) -> Dict[str, torch.Tensor]:
+    """Re-home every parameter of `model` into one flat fp32 arena (module order) and
+    return {name: view}.  Parameters keep their identity (state_dict / hooks unaffected)."""
+    named = list(model.named_parameters())
+    total = sum(p.numel() for _, p in named)
+    flat = torch.empty(total, dtype=torch.float32, device=device)
+    views, off = {}, 0
+    for name, p in named:
+        n = p.numel()
+        v = flat[off:off + n].view_as(p)
+        v.copy_(p.data.to(device=device, dtype=torch.float32))
+        p.data = v
+        views[name] = v
+        off += n
+    model._fen_flat = flat
+    return views
+
+
+class FENEngine:
+    def __init__(self, model, batch: int, lr_hw, dtype: torch.dtype = torch.bfloat16, train: bool = False,
+                 device="cuda", loss_weight: float = 1.0, clip: float = 0.5, lr: float = 1e-4,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, process_group=None):
+        self.spec = NetSpec.from_config(model.config)
+        self.dtype, self.device, self.train = dtype, torch.device(device), train
+        self.B, (self.h, self.w) = batch, lr_hw
+        s = self.spec
+        self.H, self.W = self.h * s.scale, self.w * s.scale
+        self.clip, self.betas, self.eps, self.wd = clip, betas, eps, weight_decay
+        self.pg = process_group
+        self.world = 1
+        if process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            self.world = torch.distributed.get_world_size(process_group)
+
+        model.to(self.device)
+        if getattr(model, "_fen_flat", None) is None:
+            self.params = flatten_params(model, self.device)
+        else:
+            self.params = {n: p.data for n, p in model.named_parameters()}
+        self.flat_p = model._fen_flat
+        self.Wt = Weights(self.params, dtype, self.device)
+
+        B, h, w = batch, self.h, self.w
+        self.x = torch.zeros(B, s.in_ch, h, w, device=self.device)
+        self.out = torch.zeros(B, s.out_ch, self.H, self.W, device=self.device)
+        self.ctx = Ctx(dtype, self.device, record=True)
+        ctx = self.ctx
+        self.works: List = []
+        if not train:
+            self._build_forward(training=False)
+        else:
+            self.hr = torch.zeros(B, s.out_ch, self.H, self.W, device=self.device)
+            n = self.flat_p.numel()
+            self.flat_g = torch.zeros(n, device=self.device)
+            self.flat_m = torch.zeros(n, device=self.device)
+            self.flat_v = torch.zeros(n, device=self.device)
+            self.grads, off = {}, 0
+            for name, p in model.named_parameters():
+                self.grads[name] = self.flat_g[off:off + p.numel()].view_as(p)
+                p.grad = self.grads[name]
+                off += p.numel()
+            self.scal = torch.zeros(8, device=self.device)
+            self.scal[3] = lr
+            self.loss = torch.zeros(1, device=self.device)
+            ctx.emit("bicubic_down4", ctx.lib.fen_bicubic_down4, B, s.out_ch, self.H, self.W, ptr(self.hr),
+                     ptr(self.x))
+            self.l1_scale = loss_weight / (B * s.out_ch * self.H * self.W * self.world)
+            self._build_forward(training=True)
+            self._build_backward()
+            self._build_update()
+
+    # ------------------------------------------------------------------ build
+    def _build_forward(self, training: bool):
+        s, ctx = self.spec, self.ctx
+        fw = Forward(s, ctx, self.Wt, save=self.train)
+        feat0 = fw.head(self.x)
+        h = feat0
+        self.saved = []
+        for g in range(s.G):
+            out = None if self.train else ctx.scratch(f"grp_pp{g & 1}", feat0.shape)
+            h, sv = fw.group(h, g, out=out)
+            self.saved.append(sv)
+        hr = self.hr if self.train else None
+        _, self.saved_tail = fw.tail(h, feat0, self.x, training, out=self.out, hr=hr,
+                                     l1_scale=self.l1_scale if self.train else 0.0)
+        if self.train:
+            lp = self.saved_tail["loss_part"]
+            colsum(ctx, lp, lp.shape[0], 1, self.loss, scale=1.0 / (self.B * s.out_ch * self.H * self.W))
+
+    def _bucket(self, prefixes) -> torch.Tensor:
+        lo, hi, off = None, None, 0
+        for name, v in self.grads.items():
+            n = v.numel()
+            if any(name.startswith(p) for p in prefixes):
+                lo = off if lo is None else lo
+                hi = off + n
+            off += n
+        return self.flat_g[lo:hi]
+
+    def _allreduce(self, bucket: torch.Tensor):
+        if self.world > 1:
+            self.works.append(torch.distributed.all_reduce(bucket, group=self.pg, async_op=True))
+
+    def _build_backward(self):
+        s, ctx = self.spec, self.ctx
+        bw = Backward(s, ctx, self.Wt, self.grads)
+        d = bw.tail(self.saved_tail)
+        tail_b = self._bucket(("conv_after_body.", "upsample.", "conv_last."))
+        ctx.mark("allreduce_tail", lambda b=tail_b: self._allreduce(b))
+        for g in reversed(range(s.G)):
+            extra = (self.saved_tail["d_fb"],) if g == 0 else ()
+            d = bw.group(self.saved[g], d, g, extra_res=extra, dx_out=ctx.scratch(f"bw_grp{g & 1}", d.shape))
+            bk = self._bucket((f"residual_groups.{g}.",))
+            ctx.mark(f"allreduce_rg{g}", lambda b=bk: self._allreduce(b))
+        bw.head(self.x, d)
+        head_b = self._bucket(("conv_first.",))
+        ctx.mark("allreduce_head", lambda b=head_b: self._allreduce(b))
+
+    def _build_update(self):
+        self.upd = Ctx(self.dtype, self.device, record=True)
+        u, lib = self.upd, self.upd.lib
+        n = self.flat_g.numel()
+        nparts = lib.fen_sumsq_parts(n)
+        self.sq_part = torch.zeros(nparts, device=self.device)
+        b1, b2 = self.betas
+        u.emit("sumsq", lib.fen_sumsq, n, ptr(self.flat_g), ptr(self.sq_part))
+        u.emit("optim_prepare", lib.fen_optim_prepare, nparts, ptr(self.sq_part), float(self.clip), b1, b2,
+               float(self.wd), ptr(self.scal))
+        u.emit("adamw", lib.fen_adamw, n, ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
+               ptr(self.scal), b1, b2, float(self.eps))
+
+    # ------------------------------------------------------------------ run
+    def pack(self):
+        self.Wt.pack()
+
+    def forward(self, x: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Inference: x NCHW fp32 [B,3,h,w] -> out NCHW fp32 [B,3,H,W] (eval: clamped)."""
+        if x is not None:
+            self.x.copy_(x)
+        self.ctx.run()
+        return self.out
+
+    def step(self, hr: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One training step on HR [B,3,H,W]: LR synthesis, fwd, L1, bwd, all-reduce, clip, AdamW.
+        Returns the (device) loss of this rank's shard."""
+        if hr is not None:
+            self.hr.copy_(hr)
+        self.works = []
+        self.ctx.run()
+        for wk in self.works:
+            wk.wait()
+        self.upd.run()
+        self.Wt.pack()
+        return self.loss
+
+    def set_lr(self, lr: float):
+        self.scal[3] = lr
+
+    @property
+    def grad_norm(self) -> torch.Tensor:
+        return self.scal[0]
+
+    def capture(self):
+        """Capture one forward (inference) or one full step (single-GPU training) in a hipGraph."""
+        if self.train and self.world > 1:
+            raise RuntimeError("graph capture of the DP step is not supported (RCCL hooks run on the host)")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):  # warm-up on the side stream (allocator + lazy init)
+            self._replay_body()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._replay_body()
+        self.graph = g
+        return g
+
+    def _replay_body(self):
+        self.ctx.run()
+        if self.train:
+            self.upd.run()
+            self.Wt.pack()
+
+    def replay(self):
+        self.graph.replay()

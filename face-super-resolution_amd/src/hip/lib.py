@@ -30,7 +30,7 @@ class ConvDesc(Structure):
         ("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("epi", c_int), ("alpha", c_void_p),
         ("y", c_void_p), ("y_pre", c_void_p), ("res", c_void_p * 3), ("pre_in", c_void_p),
         ("part", c_void_p), ("lr", c_void_p), ("scale", c_int), ("clamp", c_int), ("hr", c_void_p),
-        ("dout", c_void_p), ("l1_scale", c_float), ("loss_part", c_void_p),
+        ("dout", c_void_p), ("l1_scale", c_float), ("loss_part", c_void_p), ("debug", c_int),
     ]
 
 
@@ -61,7 +61,8 @@ _SIGS = {
     "fen_colsum": (c_int, [c_int, c_int, c_void_p, c_float, c_void_p, c_int, c_void_p]),
     "fen_pack_conv_w": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_void_p]),
     "fen_packed_elems": (c_size_t, [c_int] * 3),
-    "fen_nchw_to_nhwc": (c_int, [c_int] * 5 + [c_void_p, c_void_p, c_void_p]),
+    "fen_nchw_to_nhwc": (c_int, [c_int] * 6 + [c_void_p, c_void_p, c_void_p]),
+    "fen_prelu_bwd_unshuffle": (c_int, [c_int] * 5 + [c_void_p] * 5 + [c_void_p]),
     "fen_nhwc_to_nchw": (c_int, [c_int] * 5 + [c_void_p, c_void_p, c_void_p]),
     "fen_sumsq_parts": (c_int, [c_size_t]),
     "fen_sumsq": (c_int, [c_size_t, c_void_p, c_void_p, c_void_p]),

@@ -121,8 +121,9 @@ def colsum(ctx: Ctx, part, rows, cols, out, scale=1.0) -> None:
 class Forward:
     """Builds the forward of FaceEnhanceNet; with `save=True` keeps what backward needs."""
 
-    def __init__(self, spec: NetSpec, ctx: Ctx, Wt: Weights, save: bool):
+    def __init__(self, spec: NetSpec, ctx: Ctx, Wt: Weights, save: bool, attn: Optional[dict] = None):
         self.s, self.ctx, self.Wt, self.save = spec, ctx, Wt, save
+        self.attn = attn  # optional {name: s[B,C]} capture (get_attention_maps, custom.py:192-230)
 
     def head(self, x: torch.Tensor) -> torch.Tensor:
         """conv_first on the NCHW fp32 LR input (custom.py:164)."""
@@ -133,7 +134,7 @@ class Forward:
                  ptr(p["conv_first.weight"]), ptr(p["conv_first.bias"]), ptr(feat))
         return feat
 
-    def rcab(self, x: torch.Tensor, pre: str, out: Optional[torch.Tensor] = None):
+    def rcab(self, x: torch.Tensor, pre: str, out: Optional[torch.Tensor] = None, name: Optional[str] = None):
         """RCAB (blocks.py:135-153) -> (y, saved)."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
@@ -156,24 +157,27 @@ class Forward:
         ca = pre + "channel_attention.fc."
         ctx.emit("se_fwd", ctx.lib.fen_se_fwd, B, C, s.Cr, T, 1.0 / (H * W), ptr(part), ptr(p[ca + "0.weight"]),
                  ptr(p[ca + "2.weight"]), ptr(mean), ptr(hid), ptr(sg))
+        if self.attn is not None and name is not None:
+            self.attn[name] = sg
         y = out if out is not None else ctx.alloc(x.shape)
         ctx.emit("se_apply", ctx.lib.fen_se_apply, ctx.code, B, H * W, C, ptr(t), ptr(sg), s.res_scale, ptr(x),
                  ptr(y))
         saved = dict(x=x, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg) if self.save else dict(s=sg)
         return y, saved
 
-    def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None):
+    def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None, pre: Optional[str] = None):
         """ResidualGroup (blocks.py:185-189) -> (y, saved)."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
-        pre = f"residual_groups.{g}."
+        pre = f"residual_groups.{g}." if pre is None else pre
         blocks = []
         h = x
         for b in range(s.NB):
+            nm = f"group{g}_rcab{b}"
             if self.save:
-                h, sv = self.rcab(h, f"{pre}blocks.{b}.")
+                h, sv = self.rcab(h, f"{pre}blocks.{b}.", name=nm)
             else:  # ping-pong two scratch buffers between blocks
-                h, sv = self.rcab(h, f"{pre}blocks.{b}.", out=ctx.scratch(f"rg_pp{b & 1}", x.shape))
+                h, sv = self.rcab(h, f"{pre}blocks.{b}.", out=ctx.scratch(f"rg_pp{b & 1}", x.shape), name=nm)
             blocks.append(sv)
         y = out if out is not None else ctx.alloc(x.shape)
         conv(ctx, h, Wt.packed(pre + "conv", 0), B, H, W, C, C, bias=p[pre + "conv.bias"], y=y, res=(x,))
@@ -253,10 +257,11 @@ class Backward:
         conv(ctx, dz1, Wt.packed(pre + "conv1", 2), B, H, W, C, C, y=dx, res=(dy,) + tuple(extra_res))
         return dx
 
-    def group(self, sv: dict, dy: torch.Tensor, g: int, extra_res: Sequence = (), dx_out=None) -> torch.Tensor:
+    def group(self, sv: dict, dy: torch.Tensor, g: int, extra_res: Sequence = (), dx_out=None,
+              pre: Optional[str] = None) -> torch.Tensor:
         s, ctx, Wt = self.s, self.ctx, self.Wt
         B, H, W, C = dy.shape
-        pre = f"residual_groups.{g}."
+        pre = f"residual_groups.{g}." if pre is None else pre
         self._wg(pre + "conv", sv["x_last"], dy, B, H, W, C, C)
         d = ctx.scratch("bw_rg_in", dy.shape)
         conv(ctx, dy, Wt.packed(pre + "conv", 2), B, H, W, C, C, y=d)

@@ -1,0 +1,75 @@
+"""Loss surface of the reference (src/losses/combined.py:16-302) restricted to the hot path.
+
+The stage-1 generator step's content loss is L1 (combined.py:38-47), which this build fuses
+into the conv_last epilogue (sign(sr-hr)/N written by the kernel, fen_conv_desc.hr).  The
+VGG19 perceptual and SSIM terms are the next rows of SURVEY.md §8f and are not built yet:
+asking for them raises instead of silently training something else.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class LossConfig:
+    l1_weight: float = 1.0
+    l2_weight: float = 0.0
+    perceptual_weight: float = 0.01
+    ssim_weight: float = 0.1
+    ms_ssim_weight: float = 0.0
+    use_charbonnier: bool = False
+    charbonnier_eps: float = 1e-3
+    perceptual_layers: list = field(default_factory=lambda: ["conv3_4", "conv4_4"])
+    ssim_window_size: int = 11
+
+
+class L1Loss(nn.Module):
+    """mean |pred - target| (combined.py:38-47)."""
+
+    def __init__(self, reduction: str = "mean"):
+        super().__init__()
+        self.reduction = reduction
+
+    def forward(self, pred, target):
+        return F.l1_loss(pred, target, reduction=self.reduction)
+
+
+class CombinedLoss(nn.Module):
+    """Weighted loss with component tracking (combined.py:80-203); L1 term only here.
+    `fused_l1_weight` tells the Trainer it may use the fused HIP training step."""
+
+    def __init__(self, config: LossConfig):
+        super().__init__()
+        self.config = config
+        if config.perceptual_weight or config.ssim_weight or config.ms_ssim_weight or config.l2_weight \
+                or config.use_charbonnier:
+            raise NotImplementedError(
+                "only the L1 content term is built on the MI355X path (perceptual / SSIM / L2 / Charbonnier are "
+                "SURVEY.md §8f 'next' rows); set perceptual_weight=0 and ssim_weight=0")
+        self.l1 = L1Loss()
+
+    @property
+    def fused_l1_weight(self) -> float:
+        return float(self.config.l1_weight)
+
+    def forward(self, pred, target) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+        l1 = self.l1(pred, target) * self.config.l1_weight
+        return l1, {"l1": l1.detach()}
+
+
+def create_loss_function(l1_weight: float = 1.0, perceptual_weight: float = 0.01, ssim_weight: float = 0.1,
+                         use_charbonnier: bool = False, charbonnier_eps: float = 1e-3,
+                         perceptual_layers=None, **kwargs) -> CombinedLoss:
+    """Factory with the reference's signature (combined.py:278-302)."""
+    cfg = LossConfig(l1_weight=l1_weight, perceptual_weight=perceptual_weight, ssim_weight=ssim_weight,
+                     use_charbonnier=use_charbonnier, charbonnier_eps=charbonnier_eps,
+                     perceptual_layers=list(perceptual_layers or ["conv3_4", "conv4_4"]))
+    return CombinedLoss(cfg)
+
+
+__all__ = ["LossConfig", "L1Loss", "CombinedLoss", "create_loss_function"]

@@ -1,0 +1,85 @@
+"""clip_grad_norm_ + AdamW over one flat fp32 parameter/gradient arena, on the GPU
+(reference trainer.py:217-221 optimizer, 490-503 clip + step).
+
+Three launches per step (fen_sumsq -> fen_optim_prepare -> fen_adamw), no host sync: the
+global grad norm, the clip coefficient and the bias corrections are computed on the
+device.  `state_dict()` / `load_state_dict()` speak torch.optim.AdamW's format so
+checkpoints interchange with the reference's Trainer (trainer.py:701-760).
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import torch
+
+from ..hip import lib as L
+from ..hip.program import Ctx, ptr
+
+
+class FusedAdamW:
+    def __init__(self, params: List[torch.nn.Parameter], flat_p: torch.Tensor, flat_g: torch.Tensor, lr=1e-4,
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_norm=0.0):
+        self.params = list(params)
+        self.flat_p, self.flat_g = flat_p, flat_g
+        dev = flat_p.device
+        self.m = torch.zeros_like(flat_p)
+        self.v = torch.zeros_like(flat_p)
+        self.scal = torch.zeros(8, device=dev)
+        self.betas, self.eps, self.wd, self.max_norm = betas, eps, weight_decay, max_norm
+        self.set_lr(lr)
+        n = flat_p.numel()
+        self.ctx = Ctx(torch.float32, dev, record=True)
+        lib = self.ctx.lib
+        nparts = lib.fen_sumsq_parts(n)
+        self.part = torch.zeros(nparts, device=dev)
+        b1, b2 = betas
+        self.ctx.emit("sumsq", lib.fen_sumsq, n, ptr(flat_g), ptr(self.part))
+        self.ctx.emit("optim_prepare", lib.fen_optim_prepare, nparts, ptr(self.part), float(max_norm), b1, b2,
+                      float(weight_decay), ptr(self.scal))
+        self.ctx.emit("adamw", lib.fen_adamw, n, ptr(flat_p), ptr(flat_g), ptr(self.m), ptr(self.v), ptr(self.scal),
+                      b1, b2, float(eps))
+
+    def set_lr(self, lr: float):
+        self.lr = float(lr)
+        self.scal[3] = self.lr
+
+    def step(self):
+        self.ctx.run()
+
+    @property
+    def grad_norm(self) -> torch.Tensor:
+        return self.scal[0]
+
+    @property
+    def steps(self) -> int:
+        return int(self.scal[2])
+
+    # ---- torch.optim.AdamW-compatible state ----
+    def _views(self, flat):
+        out, off = [], 0
+        for p in self.params:
+            out.append(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        return out
+
+    def state_dict(self) -> Dict:
+        step = torch.tensor(float(self.scal[2]))
+        ms, vs = self._views(self.m), self._views(self.v)
+        state = {i: {"step": step.clone(), "exp_avg": ms[i].detach().cpu().clone(),
+                     "exp_avg_sq": vs[i].detach().cpu().clone()} for i in range(len(self.params))}
+        group = {"lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.wd, "amsgrad": False,
+                 "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                 "params": list(range(len(self.params)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_state_dict(self, sd: Dict) -> None:
+        ms, vs = self._views(self.m), self._views(self.v)
+        step = 0.0
+        for i, st in sd.get("state", {}).items():
+            i = int(i)
+            ms[i].copy_(st["exp_avg"])
+            vs[i].copy_(st["exp_avg_sq"])
+            step = float(st["step"])
+        self.scal[2] = step
+        if sd.get("param_groups"):
+            self.set_lr(sd["param_groups"][0]["lr"])

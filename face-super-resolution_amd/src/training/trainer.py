@@ -1,0 +1,380 @@
+"""Training loop with the reference's API (src/training/trainer.py), data-parallel on MI355X.
+
+Same TrainerConfig fields/defaults, EarlyStopping, Trainer(model, train_loader, val_loader,
+loss_fn, config) with train / _train_epoch / _validate_epoch / _save_checkpoint /
+load_checkpoint, and overfit_test.  What changes (trainer row):
+  * the G step: with an L1 content loss the whole step -- on-device LR synthesis
+    (trainer.py:416-421), forward, L1, backward, clip_grad_norm_, AdamW (458-503) -- is the
+    fused HIP program of src.hip.engine.FENEngine (one hipGraph-able replay);
+  * data parallel: one process per GPU (torchrun), each rank steps on its shard of the
+    batch stream (DistributedSampler or `shard=rank::world`), gradients are summed by RCCL
+    all-reduce buckets issued from inside the backward and overlapped with it; clip and
+    AdamW run after the reduce so every rank stays identical; rank 0 logs/checkpoints;
+  * checkpoints keep the reference's dict layout (model/optimizer/scheduler state dicts,
+    torch.optim.AdamW-format optimizer state).
+Out of scope here: GAN discriminator steps, perceptual/SSIM losses, W&B.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..hip.engine import FENEngine, flatten_params
+from ..hip.program import Ctx, ptr
+from .optim import FusedAdamW
+
+
+@dataclass
+class TrainerConfig:
+    """Configuration for trainer (reference trainer.py:85-131)."""
+    epochs: int = 50
+    learning_rate: float = 1e-4
+    weight_decay: float = 1e-4
+    gradient_clip: float = 1.0
+    accumulation_steps: int = 1
+    use_amp: bool = True
+    scheduler_type: str = "cosine"
+    scheduler_T_max: int = 50
+    scheduler_eta_min: float = 1e-7
+    scheduler_step_size: int = 10
+    scheduler_gamma: float = 0.5
+    early_stopping_patience: int = 10
+    early_stopping_metric: str = "val_psnr"
+    early_stopping_mode: str = "max"
+    checkpoint_dir: str = "checkpoints"
+    save_every: int = 10
+    save_best: bool = True
+    log_every: int = 100
+    log_images_every: int = 5
+    use_wandb: bool = True
+    wandb_project: str = "face-super-resolution"
+    device: str = "cuda"
+    gan_weight: float = 0.0
+    gan_type: str = "vanilla"
+    d_learning_rate: float = 1e-4
+    d_weight_decay: float = 0.0
+    d_updates_per_g: int = 1
+    gan_start_epoch: int = 0
+
+
+class EarlyStopping:
+    """Patience-based early stopping (reference trainer.py:134-164)."""
+
+    def __init__(self, patience: int = 10, mode: str = "max", min_delta: float = 0.0):
+        self.patience, self.mode, self.min_delta = patience, mode, min_delta
+        self.counter = 0
+        self.best_score = None
+        self.should_stop = False
+
+    def __call__(self, score: float) -> bool:
+        if self.best_score is None:
+            self.best_score = score
+            return False
+        better = score > self.best_score + self.min_delta if self.mode == "max" else \
+            score < self.best_score - self.min_delta
+        if better:
+            self.best_score, self.counter = score, 0
+        else:
+            self.counter += 1
+            if self.counter >= self.patience:
+                self.should_stop = True
+        return self.should_stop
+
+
+def dist_info():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def bicubic_down4(hr: torch.Tensor) -> torch.Tensor:
+    """trainer.py:416-421 LR synthesis on the GPU (fen_bicubic_down4)."""
+    B, C, H, W = hr.shape
+    hr = hr.contiguous().float()
+    lr = torch.empty(B, C, H // 4, W // 4, device=hr.device)
+    c = Ctx(torch.float32, hr.device)
+    c.emit("bicubic_down4", c.lib.fen_bicubic_down4, B, C, H, W, ptr(hr), ptr(lr))
+    return lr
+
+
+class Trainer:
+    """Single-node, multi-GPU training manager for FaceEnhanceNet (reference trainer.py:167-760)."""
+
+    def __init__(self, model: nn.Module, train_loader, val_loader, loss_fn: nn.Module,
+                 config: Optional[TrainerConfig] = None, discriminator: Optional[nn.Module] = None,
+                 gan_loss: Optional[nn.Module] = None):
+        self.config = config or TrainerConfig()
+        if discriminator is not None and self.config.gan_weight > 0:
+            raise NotImplementedError("GAN (stage 3) training is SURVEY.md §8f 'next' #2; not built yet")
+        self.rank, self.world = dist_info()
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if not torch.cuda.is_available():
+            raise RuntimeError("the MI355X trainer needs a ROCm GPU (there is no CPU path)")
+        self.device = torch.device("cuda", local)
+        torch.cuda.set_device(self.device)
+        self.model = model.to(self.device)
+        if self.world > 1:  # identical start on every rank (RCCL broadcast of the flat arena)
+            flatten_params(self.model, self.device)
+            dist.broadcast(self.model._fen_flat, src=0)
+        elif getattr(self.model, "_fen_flat", None) is None:
+            flatten_params(self.model, self.device)
+        self.train_loader, self.val_loader = train_loader, val_loader
+        self.loss_fn = loss_fn.to(self.device) if loss_fn is not None else None
+        self.fused_l1 = getattr(loss_fn, "fused_l1_weight", None)
+        if self.fused_l1 is None and isinstance(loss_fn, nn.L1Loss):
+            self.fused_l1 = 1.0
+        # torch AdamW object = param_groups/lr holder for the schedulers and the checkpoint
+        # format; the update itself is the fused HIP kernel
+        self.optimizer = torch.optim.AdamW(self.model.parameters(), lr=self.config.learning_rate,
+                                           weight_decay=self.config.weight_decay)
+        self.scheduler = self._create_scheduler()
+        self._engines: Dict[tuple, FENEngine] = {}
+        self._generic_opt: Optional[FusedAdamW] = None
+        self.early_stopping = EarlyStopping(self.config.early_stopping_patience, self.config.early_stopping_mode)
+        self.checkpoint_dir = Path(self.config.checkpoint_dir)
+        if self.rank == 0:
+            self.checkpoint_dir.mkdir(parents=True, exist_ok=True)
+        self.best_metric = None
+        self.current_epoch = 0
+        self.global_step = 0
+        self.training_history: Dict[str, List] = {"train_loss": [], "val_loss": [], "val_psnr": [], "val_ssim": [],
+                                                  "learning_rate": []}
+        self.use_wandb = False
+
+    # ------------------------------------------------------------------ pieces
+    def _create_scheduler(self):
+        c = self.config
+        if c.scheduler_type == "cosine":
+            return torch.optim.lr_scheduler.CosineAnnealingLR(self.optimizer, T_max=c.scheduler_T_max,
+                                                              eta_min=c.scheduler_eta_min)
+        if c.scheduler_type == "step":
+            return torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=c.scheduler_step_size,
+                                                   gamma=c.scheduler_gamma)
+        if c.scheduler_type == "plateau":
+            return torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="max", factor=0.5, patience=5)
+        return None
+
+    @property
+    def lr(self) -> float:
+        return self.optimizer.param_groups[0]["lr"]
+
+    def engine(self, B: int, H: int, W: int) -> FENEngine:
+        key = (B, H, W)
+        if key not in self._engines:
+            dtype = self.model.compute_dtype
+            eng = FENEngine(self.model, batch=B, lr_hw=(H // self.model.scale_factor, W // self.model.scale_factor),
+                            dtype=dtype, train=True, device=self.device, loss_weight=self.fused_l1,
+                            clip=self.config.gradient_clip, lr=self.lr, weight_decay=self.config.weight_decay)
+            if self._engines:  # share optimizer moments/step between batch-size variants
+                first = next(iter(self._engines.values()))
+                eng.flat_m, eng.flat_v, eng.scal = first.flat_m, first.flat_v, first.scal
+                eng._build_update()
+            elif getattr(self, "_pending_opt_state", None):
+                self._load_opt_into(eng, self._pending_opt_state)
+            self._engines[key] = eng
+        return self._engines[key]
+
+    def _shard(self, hr: torch.Tensor) -> torch.Tensor:
+        """If the loader hands every rank the global batch, keep this rank's slice."""
+        if self.world > 1 and getattr(self.train_loader, "_fen_global_batches", False):
+            return hr.chunk(self.world)[self.rank]
+        return hr
+
+    def _generic_step(self, hr: torch.Tensor) -> torch.Tensor:
+        """Any other content loss: module autograd path + RCCL grad all-reduce + fused AdamW."""
+        lr = bicubic_down4(hr)
+        sr = self.model(lr)
+        loss, _ = self.loss_fn(sr, hr)
+        for p in self.model.parameters():
+            p.grad = None
+        (loss / self.world).backward()
+        if self._generic_opt is None:
+            flat = self.model._fen_flat
+            self._flat_g = torch.zeros_like(flat)
+            self._generic_opt = FusedAdamW(list(self.model.parameters()), flat, self._flat_g, lr=self.lr,
+                                           weight_decay=self.config.weight_decay, max_norm=self.config.gradient_clip)
+        off = 0
+        for p in self.model.parameters():
+            n = p.numel()
+            self._flat_g[off:off + n].copy_(p.grad.reshape(-1))
+            off += n
+        if self.world > 1:
+            dist.all_reduce(self._flat_g)
+        self._generic_opt.set_lr(self.lr)
+        self._generic_opt.step()
+        return loss.detach()
+
+    # ------------------------------------------------------------------ loops
+    def _train_epoch(self) -> Dict[str, float]:
+        self.model.train()
+        total, n = 0.0, 0
+        for batch in self.train_loader:
+            hr = self._shard(batch["hr"]).to(self.device, non_blocking=True)
+            if self.fused_l1 is not None:
+                B, _, H, W = hr.shape
+                eng = self.engine(B, H, W)
+                eng.set_lr(self.lr)
+                loss = eng.step(hr)
+            else:
+                loss = self._generic_step(hr)
+            self.global_step += 1
+            total += float(loss)  # per-step host sync, as trainer.py:508
+            n += 1
+        if self.world > 1:
+            t = torch.tensor([total, n], device=self.device, dtype=torch.float64)
+            dist.all_reduce(t)
+            total, n = float(t[0]), int(t[1])
+        return {"loss": total / max(n, 1), "l1": total / max(n, 1)}
+
+    @torch.no_grad()
+    def _validate_epoch(self) -> Dict[str, float]:
+        self.model.eval()
+        tl, tp, n = 0.0, 0.0, 0
+        for batch in self.val_loader:
+            hr = batch["hr"].to(self.device)
+            sr = self.model(bicubic_down4(hr))
+            loss = F.l1_loss(sr, hr) if self.loss_fn is None else self.loss_fn(sr, hr)[0]
+            tl += float(loss)
+            tp += self._compute_psnr(sr, hr)
+            n += 1
+        n = max(n, 1)
+        return {"loss": tl / n, "psnr": tp / n, "ssim": float("nan")}  # SSIM: SURVEY.md §8f next #4
+
+    def _compute_psnr(self, pred: torch.Tensor, target: torch.Tensor) -> float:
+        """10 log10(1/MSE) over the batch (trainer.py:621-628)."""
+        mse = torch.mean((pred - target) ** 2)
+        if mse == 0:
+            return float("inf")
+        return float(10 * torch.log10(1.0 / mse))
+
+    def train(self) -> Dict[str, Any]:
+        for epoch in range(self.current_epoch, self.config.epochs):
+            self.current_epoch = epoch
+            tm = self._train_epoch()
+            vm = self._validate_epoch() if self.val_loader is not None else {"loss": tm["loss"], "psnr": 0.0,
+                                                                             "ssim": float("nan")}
+            if self.scheduler is not None:
+                if self.config.scheduler_type == "plateau":
+                    self.scheduler.step(vm["psnr"])
+                else:
+                    self.scheduler.step()
+            self._log_epoch_metrics(epoch, tm, vm, self.lr)
+            if (epoch + 1) % self.config.save_every == 0:
+                self._save_checkpoint(f"epoch_{epoch + 1}.pth")
+            metric = vm.get(self.config.early_stopping_metric.replace("val_", ""), vm.get("psnr", 0))
+            if self.config.save_best and self._is_best(metric):
+                self._save_checkpoint("best_model.pth", is_best=True)
+            if self.early_stopping(metric):
+                if self.rank == 0:
+                    print(f"\nEarly stopping triggered at epoch {epoch + 1}")
+                break
+        self._save_checkpoint("final_model.pth")
+        return self.training_history
+
+    def _log_epoch_metrics(self, epoch, tm, vm, lr):
+        h = self.training_history
+        h["train_loss"].append(tm["loss"])
+        h["val_loss"].append(vm["loss"])
+        h["val_psnr"].append(vm["psnr"])
+        h["val_ssim"].append(vm["ssim"])
+        h["learning_rate"].append(lr)
+        if self.rank == 0:
+            print(f"\nEpoch {epoch + 1}/{self.config.epochs}\n  Train Loss: {tm['loss']:.4f}\n"
+                  f"  Val Loss:   {vm['loss']:.4f}\n  Val PSNR:   {vm['psnr']:.2f} dB\n  LR:         {lr:.2e}")
+
+    def _is_best(self, value: float) -> bool:
+        if self.best_metric is None:
+            self.best_metric = value
+            return True
+        better = value > self.best_metric if self.config.early_stopping_mode == "max" else value < self.best_metric
+        if better:
+            self.best_metric = value
+        return better
+
+    # ------------------------------------------------------------------ checkpoints
+    def _optimizer_state(self) -> Dict:
+        if self._engines:
+            eng = next(iter(self._engines.values()))
+            opt = FusedAdamW.__new__(FusedAdamW)
+            opt.params, opt.m, opt.v, opt.scal = list(self.model.parameters()), eng.flat_m, eng.flat_v, eng.scal
+            opt.lr, opt.betas, opt.eps, opt.wd = self.lr, eng.betas, eng.eps, eng.wd
+            return opt.state_dict()
+        if self._generic_opt is not None:
+            return self._generic_opt.state_dict()
+        return self.optimizer.state_dict()
+
+    def _save_checkpoint(self, filename: str, is_best: bool = False) -> None:
+        """Reference checkpoint layout (trainer.py:701-723); rank 0 only."""
+        if self.rank != 0:
+            return
+        sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+        ckpt = {
+            "epoch": self.current_epoch,
+            "global_step": self.global_step,
+            "model_state_dict": sd,
+            "optimizer_state_dict": self._optimizer_state(),
+            "scheduler_state_dict": self.scheduler.state_dict() if self.scheduler else None,
+            "best_metric": self.best_metric,
+            "training_history": self.training_history,
+            "config": dict(self.config.__dict__),
+        }
+        torch.save(ckpt, self.checkpoint_dir / filename)
+        if is_best:
+            print(f"  New best model saved: {self.best_metric:.4f}")
+
+    def load_checkpoint(self, path: str, weights_only: bool = False) -> None:
+        """Full resume or fine-tune (weights only) from a reference-format checkpoint
+        (trainer.py:725-760).  Loaded with torch.load(weights_only=True)."""
+        ckpt = torch.load(path, map_location="cpu", weights_only=True)
+        self.model.load_state_dict(ckpt["model_state_dict"])
+        if weights_only:
+            return
+        osd = ckpt.get("optimizer_state_dict")
+        if osd:
+            self.optimizer.load_state_dict(osd)
+            self._pending_opt_state = osd
+            for eng in self._engines.values():
+                self._load_opt_into(eng, osd)
+        if self.scheduler and ckpt.get("scheduler_state_dict"):
+            self.scheduler.load_state_dict(ckpt["scheduler_state_dict"])
+        self.current_epoch = ckpt["epoch"] + 1
+        self.global_step = ckpt["global_step"]
+        self.best_metric = ckpt["best_metric"]
+        self.training_history = ckpt["training_history"]
+
+    def _load_opt_into(self, eng: FENEngine, osd: Dict):
+        opt = FusedAdamW.__new__(FusedAdamW)
+        opt.params, opt.m, opt.v, opt.scal = list(self.model.parameters()), eng.flat_m, eng.flat_v, eng.scal
+        opt.lr = self.lr
+        opt.load_state_dict(osd)
+
+
+def overfit_test(model: nn.Module, dataloader, loss_fn: nn.Module, num_images: int = 10,
+                 num_iterations: int = 1000, device: str = "cuda") -> Dict[str, Any]:
+    """Overfit a few images with MSE on clamped output, Adam lr 2e-4 (reference trainer.py:763-848)."""
+    dev = torch.device(device)
+    model = model.to(dev).train()
+    hr = next(iter(dataloader))["hr"][:num_images].to(dev)
+    lr = bicubic_down4(hr)
+    opt = torch.optim.Adam(model.parameters(), lr=2e-4)
+    losses, psnrs = [], []
+    for _ in range(num_iterations):
+        opt.zero_grad()
+        sr = torch.clamp(model(lr), 0.0, 1.0)
+        loss = F.mse_loss(sr, hr)
+        loss.backward()
+        opt.step()
+        with torch.no_grad():
+            psnrs.append(float(10 * torch.log10(1.0 / torch.mean((sr - hr) ** 2))))
+        losses.append(float(loss))
+    return {"final_loss": losses[-1], "final_psnr": psnrs[-1], "loss_history": losses, "psnr_history": psnrs,
+            "converged": psnrs[-1] > 35}

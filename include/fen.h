@@ -72,6 +72,7 @@ typedef struct {
     void* dout;                /* dL/dsr in NHWC16 dtype layout [B,H,W,16] (zero padded) or NULL */
     float l1_scale;            /* dL/dsr = sign(sr-hr) * l1_scale   (weight / numel)             */
     float* loss_part;          /* [B*tiles] partial sums of |sr-hr|                              */
+    int debug;                 /* 0; tuning ablations only (1: skip epilogue, 2: skip MFMA loop)  */
 } fen_conv_desc;
 
 int fen_conv3x3(const fen_conv_desc* d, void* stream);
@@ -143,9 +144,16 @@ int fen_colsum(int rows, int cols, const float* part, float scale, float* out, i
 int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const float* w, void* out, void* stream);
 size_t fen_packed_elems(int mode, int Cout, int Cin);
 
-/* fp32 <-> dtype layout conversions (NCHW fp32 <-> NHWC dtype)                              */
-int fen_nchw_to_nhwc(int dtype, int B, int C, int H, int W, const float* x, void* y, void* stream);
+/* fp32 <-> dtype layout conversions (NCHW fp32 <-> NHWC dtype).  nchw_to_nhwc writes
+ * Cpad >= C channels per pixel, zero-filling c >= C (Cpad = 16 builds conv_last's dout).    */
+int fen_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cpad, const float* x, void* y, void* stream);
 int fen_nhwc_to_nchw(int dtype, int B, int C, int H, int W, const void* x, float* y, void* stream);
+
+/* Standalone PReLU backward + PixelShuffle inverse (UpsampleModule used on its own,
+ * blocks.py:223-227): dy, pre NHWC [B,H,W,C] -> du NHWC [B,H/2,W/2,4C];
+ * part[B*tiles(H,W)][C] dalpha partials.                                                    */
+int fen_prelu_bwd_unshuffle(int dtype, int B, int H, int W, int C, const void* dy, const void* pre,
+                            const float* alpha, void* du, float* part, void* stream);
 
 /* clip_grad_norm_ + AdamW (trainer.py:490-503) over one flat fp32 arena.
  * fen_sumsq: part[i] partial sums of g^2 (nparts = fen_sumsq_parts(n)).

@@ -12,7 +12,8 @@ Fixtures:
   g2_rcab.npz     one RCAB (C=64) B=2 16x16 with random weights; out and all grads
                   of sum(out*R).
   g3_kat.npz      bicubic x2/x4/x8 up, bicubic x0.25 down, PixelShuffle(2) KATs.
-  g4_full.npz     full 6x10 network, B=1, 32x32 input: init statistics + outputs.
+  g4_full.npz     full 6x10 network, B=1, 32x32 input: init statistics + outputs
+                  (fp32, and the eval output of the reference run in float64).
   g5_c128.npz     128-ch 10x20 x8 variant, B=1, 16x16 input: init statistics + output.
   g6_lite.npz     FaceEnhanceNetLite (C=32, r=2), B=1, 16x16 input: output.
 
@@ -158,6 +159,10 @@ def g_net(fname, ctor, x_shape, seed_x):
         d["out_eval"] = model(x).numpy()
         model.train()
         d["out_train"] = model(x).numpy()
+        # the reference evaluated in float64: the accuracy yardstick for deep variants whose
+        # fp32 rounding alone exceeds 1e-3 (e.g. 128 ch x 200 RCAB)
+        model.double().eval()
+        d["out_eval_f64"] = model(x.double()).numpy()
     np.savez_compressed(os.path.join(OUT, fname), **d)
 
 
