@@ -164,7 +164,7 @@ def main():
                 "architecture",
         "config": {"workload": "FaceEnhanceNet full (6x10 RCAB, 64ch) inference 64->256, bf16", "global_batch": B * world,
                    "per_gpu_batch": B, "parallelism": f"replicas x{world}" if world > 1 else "single"},
-        "roofline": {"bound": "mfma", "kernel": "k_conv3x3<bf16,64> (RCAB conv 64->64, 64x64, B=32)",
+        "roofline": {"bound": "mfma", "kernel": "k_conv3x3_p<64,4,2> (RCAB conv1 64->64 + bias + PReLU, 64x64, B=32)",
                      "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "kernel_ms": round(kern_ms, 5),
                      "flop_per_launch": RCAB_CONV_FLOP, "traffic": load_traffic()},

@@ -79,6 +79,28 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
     return (unsigned)(size_t)(const lds_void*)p;
 }
 
+// Diagnostic build only (-DFEN_STAMPS, tools/stamp_conv.py): per-block s_memrealtime /
+// s_memtime stamps of the persistent kernel's phases into d.loss_part (unused by the
+// forward epilogues), 16 x 2 u64 per block.  In the real build no stamp executes.
+#ifdef FEN_STAMPS
+#define FEN_STAMP(i)                                                                          \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        unsigned long long _rt, _mt;                                                          \
+        asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"                 \
+                     : "=s"(_rt), "=s"(_mt)::"memory");                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        if (threadIdx.x == 0 && (i) < 16) {                                                   \
+            unsigned long long* _p = (unsigned long long*)d.loss_part + (size_t)blockIdx.x * 32; \
+            _p[2 * (i)] = _rt;                                                                \
+            _p[2 * (i) + 1] = _mt;                                                            \
+        }                                                                                     \
+    } while (0)
+#else
+#define FEN_STAMP(i) \
+    do {             \
+    } while (0)
+#endif
 
 // s_waitcnt vmcnt(n) for a runtime n (the immediate must be a literal): waits until at
 // most n of this wave's vector-memory ops are outstanding.  Ops retire in issue order, so
@@ -135,17 +157,22 @@ __device__ __forceinline__ EpiConst<MT> epi_consts(const fen_conv_desc& d, int c
 // store path (COT == 64 only); `red` is >= 4*COT floats of LDS.  Contains barriers:
 // every thread of the block must call it.
 // ------------------------------------------------------------------------------------
-template <typename T, int COT, int WR, int WC>
+template <typename T, int COT, int WR, int WC, int EPIC = -1>
 __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&acc)[COT / 16 / WC][16 / WR], int b,
                                               int tlin, int h0, int w0, int co0, char* stage, float* red,
                                               const EpiConst<COT / 16 / WC>& ec) {
     constexpr int MT = COT / 16 / WC, NT = 16 / WR, CW = COT / WC;
+    // EPIC >= 0: the epilogue mode is a compile-time constant (flags | residual count << 8),
+    // so every branch on it folds away; -1: read it from the descriptor.
+    constexpr bool CT = EPIC >= 0;
+    constexpr int NRES = CT ? (EPIC >> 8) : 3;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave % WR, wc = wave / WR;
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, Cout = d.Cout;
-    const int epi = d.epi;
+    const int epi = CT ? (EPIC & 0xff) : d.epi;
     const int w_ = w0 + c16;
+    const bool full = h0 + 16 <= H && w0 + 16 <= W;
 
     if (epi & FEN_EPI_LAST) {
         // conv_last: rows co = 4q + r; only co < Cout (3) are real.  One bicubic sample per
@@ -214,15 +241,15 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int h = h0 + wr * NT + n;
-            const bool valid = h < H && w_ < W && cob < Cout;
+            const bool valid = (full || (h < H && w_ < W)) && cob < Cout;
             const size_t oi = ((size_t)(b * H + h) * W + w_) * Cout + cob;
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = acc[m][n][r] + bias4[r];
             if (valid) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    if (d.res[k]) {
+                for (int k = 0; k < NRES; ++k) {
+                    if (CT || d.res[k]) {
                         float rv[4];
                         ld4<T>((const char*)d.res[k] + oi * sizeof(T), rv);
 #pragma unroll
@@ -347,7 +374,7 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
                 const int h = h0 + wr * NT + n;
-                if (h >= H || w_ >= W) continue;
+                if (!full && (h >= H || w_ >= W)) continue;
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = final_v(acc[m][n][r], m, r, k);
@@ -391,10 +418,43 @@ __device__ __forceinline__ void conv_tap(f32x4 (&acc)[MT][NT], const char* wt, c
     }
 }
 
+// All 9 taps x 2 k-halves of one tile from an LDS-resident filter, software-pipelined:
+// the fragments of step s+1 are read while the MFMAs of step s run (two register sets).
+template <int COT, int MT, int NT>
+__device__ __forceinline__ void conv_tile_resident(f32x4 (&acc)[MT][NT], const char* wts, const char* halo, int wr,
+                                                   int wc, int q, int c16) {
+    uint4 A0[MT], B0[NT], A1[MT], B1[NT];
+    const int arow = wc * MT * 16 + c16;
+    auto load = [&](int tap, int kk, uint4 (&A)[MT], uint4 (&Bf)[NT]) {
+        const int kh = tap / 3, kw = tap - kh * 3;
+        const int chunk = kk * 4 + q;
+        const char* wt = wts + tap * COT * 128;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) A[m] = *(const uint4*)(wt + swz(arow + m * 16, chunk));
+        const char* hb = halo + hcol(c16 + kw, chunk) + (wr * NT + kh) * (HALO * 128);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) Bf[n] = *(const uint4*)(hb + n * (HALO * 128));
+    };
+    auto mma = [&](const uint4 (&A)[MT], const uint4 (&Bf)[NT]) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], A[m], Bf[n]);
+    };
+    load(0, 0, A0, B0);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+        load(tap, 1, A1, B1);
+        mma(A0, B0);
+        if (tap < 8) load(tap + 1, 0, A0, B0);
+        mma(A1, B1);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // k_conv3x3_p: persistent, resident weights, LDS-DMA double-buffered halo (bf16, Cin=64)
 // ------------------------------------------------------------------------------------
-template <int COT, int WR, int WC>
+template <int COT, int WR, int WC, int EPIC>
 __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MT = COT / 16 / WC, NT = 16 / WR, NW = WR * WC;
@@ -446,11 +506,13 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
         }
     };
 
+    FEN_STAMP(0);
     const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * MT * 16 + q * 4);
     int t = slot;
     if (t < ntiles) load_halo(t, hbuf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    FEN_STAMP(1);
     for (int k = 0; t < ntiles; ++k, t += nslot) {
         char* cur = hbuf + (k & 1) * HALO_SLOT;
         const int tn = t + nslot;
@@ -460,11 +522,8 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
         for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!(d.debug & 2)) {
-#pragma unroll 1
-            for (int tap = 0; tap < 9; ++tap)
-                conv_tap<bf16, MT, NT>(acc, wts + tap * COT * 128, cur, tap, wr, wc, q, c16);
-        }
+        if (!(d.debug & 2)) conv_tile_resident<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16);
+        FEN_STAMP(2 + 3 * k);
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         if (d.debug & 1) {
@@ -473,121 +532,13 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
 #pragma unroll
                 for (int n = 0; n < NT; ++n) asm volatile("" ::"v"(acc[m][n]));
         } else {
-            conv_epilogue<bf16, COT, WR, WC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
+            conv_epilogue<bf16, COT, WR, WC, EPIC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
         }
+        FEN_STAMP(3 + 3 * k);
         wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                        // ... for everyone; cur is free
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// k_conv3x3_r: register-resident filter (bf16, Cin == 64).  Each wave keeps its whole
-// share of the filter -- 9 taps x 64 ci x (16*MT) co = 36 KB at MT=2 -- in 144 VGPRs for
-// the life of the persistent block, so the tap loop reads only pixel fragments from LDS.
-// The halo image uses a 160-B pixel row (128 B data + 32 B pad): every ds_read_b128 of a
-// fragment is conflict-free AND is one base VGPR + an immediate offset.  The next tile's
-// halo streams in by LDS-DMA (inline-asm buffer_load ... lds, zero padding by the range
-// check) while the current tile's MFMAs run; one barrier per tile.
-// ------------------------------------------------------------------------------------
-constexpr int RSTRIDE = 160;
-constexpr int RHALO_DMA = (HP * 10 + 63) / 64;   // 51 one-KiB pieces per halo
-constexpr int RHALO_SLOT = RHALO_DMA * 1024;     // 52224 B
-
-template <int COT, int MT>
-__global__ __launch_bounds__(64 * 4 * (COT / 16 / MT), 1) void k_conv3x3_r(const fen_conv_desc d) {
-    constexpr int WC = COT / 16 / MT, WR = 4, NT = 4, NW = WR * WC;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* ring = smem;                                      // 3 x RHALO_SLOT
-    float* red = (float*)(smem + 3 * RHALO_SLOT);           // WR * COT floats
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave % WR, wc = wave / WR;
-    const int q = lane >> 4, c16 = lane & 15;
-    const int H = d.H, W = d.W, Cout = d.Cout;
-    const int coutp = (Cout + 15) & ~15;
-    const int ncot = coutp / COT;
-    const int cot = blockIdx.x % ncot, co0 = cot * COT;
-    const int nslot = gridDim.x / ncot, slot = blockIdx.x / ncot;
-    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
-    const int ntiles = d.B * tpi;
-    const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * 128));
-    const i32x4 wr4 = make_rsrc(d.w, (unsigned)((size_t)9 * coutp * 128));
-
-    auto load_halo = [&](int t, char* buf) {   // slot s -> pixel s/10, 16-B chunk s%10 (8, 9 = pad)
-        const int b = t / tpi, tile = t - b * tpi;
-        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        const unsigned base = lds_addr(buf);
-        for (int i = wave; i < RHALO_DMA; i += NW) {
-            const int s = i * 64 + lane;
-            const int p = s / 10, c = s - p * 10;
-            const int hr = p / HALO, hc = p - hr * HALO;
-            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-            const bool in = c < 8 && p < HP && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-            const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
-            dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
-        }
-    };
-
-    // prologue: filter -> LDS (buffers 1-2), first halo -> buffer 0, then filter -> VGPRs
-    {
-        const unsigned wbase = lds_addr(ring + RHALO_SLOT);
-        for (int i = wave; i < 9 * COT * 8 / 64; i += NW) {
-            const int s = i * 64 + lane;
-            const int r = s >> 3, c = s & 7;
-            const int tap = r / COT, col = r - tap * COT;
-            dma16(wr4, __builtin_amdgcn_readfirstlane(wbase + i * 1024), ((tap * coutp + co0 + col) * 64 + c * 8) * 2);
-        }
-    }
-    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * MT * 16 + q * 4);
-    int t = slot;
-    if (t < ntiles) load_halo(t, ring);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    uint4 wreg[9][2][MT];
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const int row = tap * COT + wc * MT * 16 + m * 16 + c16;
-                wreg[tap][kk][m] = *(const uint4*)(ring + RHALO_SLOT + row * 128 + (kk * 4 + q) * 16);
-            }
-    __syncthreads();   // filter staging area is reused as halo buffers below
-
-    const int lane_off = c16 * RSTRIDE + q * 16;
-    for (int k = 0; t < ntiles; ++k, t += nslot) {
-        char* cur = ring + (k % 3) * RHALO_SLOT;
-        const int tn = t + nslot;
-        if (tn < ntiles) load_halo(tn, ring + ((k + 1) % 3) * RHALO_SLOT);
-        f32x4 acc[MT][NT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const char* hb = cur + lane_off + wr * NT * HALO * RSTRIDE;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int kh = tap / 3, kw = tap % 3;
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                uint4 Bf[NT];
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    Bf[n] = *(const uint4*)(hb + ((n + kh) * HALO + kw) * RSTRIDE + kk * 64);
-#pragma unroll
-                for (int m = 0; m < MT; ++m)
-#pragma unroll
-                    for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], wreg[tap][kk][m], Bf[n]);
-            }
-        }
-        const int b = t / tpi, tile = t - b * tpi;
-        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        conv_epilogue<bf16, COT, WR, WC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
-        wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                        // ... for everyone; cur is free
+        FEN_STAMP(4 + 3 * k);
     }
 }
 
@@ -680,10 +631,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
 
 int g_num_cus = 0;
 
-// kernel-variant selector for tuning runs (FEN_CONV_VARIANT): 0 default (LDS-resident filter,
-// 4x2 waves for 64-channel tiles; streamed kernel for 16-channel tiles), 1 streamed everywhere,
-// 2/3/4/5 LDS-resident filter with 8x1 / 4x2 / 2x4 / 4x1 waves (rows x co-groups),
-// 6 register-resident filter (r<64,4>), 7 register-resident filter (r<64,2>)
+// kernel-variant selector for A/B runs (FEN_CONV_VARIANT): 0 default (persistent LDS-resident
+// filter for bf16 64-channel inputs, epilogue specialised per mode), 1 streamed kernel
+// everywhere, 2 persistent kernel with the generic (runtime-mode) epilogue
 int conv_variant() {
     static int v = -1;
     if (v < 0) {
@@ -693,7 +643,7 @@ int conv_variant() {
     return v;
 }
 
-template <int COT, int WR, int WC>
+template <int COT, int WR, int WC, int EPIC>
 int launch_p(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int ntiles = d->B * tpi;
@@ -711,39 +661,11 @@ int launch_p(const fen_conv_desc* d, hipStream_t s) {
     const size_t lds = 9 * COT * 128 + 2 * HALO_SLOT + WR * COT * 4 + 64;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_conv3x3_p<COT, WR, WC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_p<COT, WR, WC, EPIC>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_conv3x3_p<COT, WR, WC>), dim3(grid), dim3(64 * WR * WC), lds, s, *d);
-    FEN_CHECK_LAUNCH();
-    return FEN_OK;
-}
-
-template <int COT, int MT>
-int launch_r(const fen_conv_desc* d, hipStream_t s) {
-    const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
-    const int ntiles = d->B * tpi;
-    const int ncot = ((d->Cout + 15) & ~15) / COT;
-    if (g_num_cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (g_num_cus <= 0) g_num_cus = 256;
-    }
-    int grid = g_num_cus;
-    grid -= grid % ncot;
-    const int maxg = ntiles * ncot;
-    if (grid > maxg) grid = maxg;
-    constexpr int NW = 4 * (COT / 16 / MT);
-    const size_t lds = 3 * RHALO_SLOT + 4 * COT * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_conv3x3_r<COT, MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        attr_set = true;
-    }
-    hipLaunchKernelGGL((k_conv3x3_r<COT, MT>), dim3(grid), dim3(64 * NW), lds, s, *d);
+    hipLaunchKernelGGL((k_conv3x3_p<COT, WR, WC, EPIC>), dim3(grid), dim3(64 * WR * WC), lds, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
@@ -783,8 +705,6 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     if (epi & FEN_EPI_LAST) {
         if (d->Cout > 4 || !d->lr || d->scale <= 0 || d->H % d->scale || d->W % d->scale) return FEN_EINVAL;
         if (epi & ~(FEN_EPI_LAST | FEN_EPI_BIAS)) return FEN_EUNSUPPORTED;
-        if (persist && conv_variant() == 5) return launch_p<16, 4, 1>(d, s);
-        if (persist && conv_variant() >= 6) return launch_r<16, 1>(d, s);
         return d->dtype == FEN_BF16 ? launch_s<bf16, 16>(d, s) : launch_s<float, 16>(d, s);
     }
     if (!d->y) return FEN_EINVAL;
@@ -796,21 +716,29 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     if ((epi & FEN_EPI_UNSHUFFLE) && ((d->H | d->W) & 1)) return FEN_EINVAL;
     if (d->Cout % 64 == 0) {
         if (persist) {
-            switch (conv_variant()) {
-                case 7: return launch_r<64, 2>(d, s);
-                case 6: return launch_r<64, 4>(d, s);
-                case 5: return launch_p<64, 4, 1>(d, s);
-                case 2: return launch_p<64, 8, 1>(d, s);
-                case 3: return launch_p<64, 4, 2>(d, s);
-                case 4: return launch_p<64, 2, 4>(d, s);
-                default: return launch_p<64, 4, 2>(d, s);
+            // the network's epilogue modes get their own instantiation (mode | #residuals << 8)
+            const int nres = d->res[0] ? (d->res[1] ? (d->res[2] ? 3 : 2) : 1) : 0;
+            bool dense = true;   // residual pointers packed at the front
+            for (int k = nres; k < 3; ++k) dense = dense && !d->res[k];
+            const int key = dense && conv_variant() != 2 ? (epi | (nres << 8)) : -1;
+            constexpr int B_ = FEN_EPI_BIAS;
+            switch (key) {
+                case B_ | FEN_EPI_PRELU: return launch_p<64, 4, 2, B_ | FEN_EPI_PRELU>(d, s);
+                case B_ | FEN_EPI_POOL: return launch_p<64, 4, 2, B_ | FEN_EPI_POOL>(d, s);
+                case B_ | (1 << 8): return launch_p<64, 4, 2, B_ | (1 << 8)>(d, s);
+                case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE:
+                    return launch_p<64, 4, 2, B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
+                case FEN_EPI_PRELU_BWD: return launch_p<64, 4, 2, FEN_EPI_PRELU_BWD>(d, s);
+                case 0: return launch_p<64, 4, 2, 0>(d, s);
+                case 1 << 8: return launch_p<64, 4, 2, 1 << 8>(d, s);
+                case 2 << 8: return launch_p<64, 4, 2, 2 << 8>(d, s);
+                case 3 << 8: return launch_p<64, 4, 2, 3 << 8>(d, s);
+                default: return launch_p<64, 4, 2, -1>(d, s);
             }
         }
         return d->dtype == FEN_BF16 ? launch_s<bf16, 64>(d, s) : launch_s<float, 64>(d, s);
     }
     if (d->Cout % 16 == 0) {
-        if (persist && conv_variant() == 5) return launch_p<16, 4, 1>(d, s);
-        if (persist && conv_variant() >= 6) return launch_r<16, 1>(d, s);
         return d->dtype == FEN_BF16 ? launch_s<bf16, 16>(d, s) : launch_s<float, 16>(d, s);
     }
     return FEN_EUNSUPPORTED;

@@ -14,7 +14,7 @@ beside the remaining backward kernels -- and the update waits for all buckets.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional
+from typing import Dict, Optional
 
 import torch
 
@@ -69,7 +69,6 @@ class FENEngine:
         self.out = torch.zeros(B, s.out_ch, self.H, self.W, device=self.device)
         self.ctx = Ctx(dtype, self.device, record=True)
         ctx = self.ctx
-        self.works: List = []
         if not train:
             self._build_forward(training=False)
         else:
@@ -83,6 +82,8 @@ class FENEngine:
                 self.grads[name] = self.flat_g[off:off + p.numel()].view_as(p)
                 p.grad = self.grads[name]
                 off += p.numel()
+            from ..training.dp import BucketExchange, model_bucket_plan
+            self.exchange = BucketExchange(self.flat_g, model_bucket_plan(model), process_group)
             self.scal = torch.zeros(8, device=self.device)
             self.scal[3] = lr
             self.loss = torch.zeros(1, device=self.device)
@@ -111,34 +112,18 @@ class FENEngine:
             lp = self.saved_tail["loss_part"]
             colsum(ctx, lp, lp.shape[0], 1, self.loss, scale=1.0 / (self.B * s.out_ch * self.H * self.W))
 
-    def _bucket(self, prefixes) -> torch.Tensor:
-        lo, hi, off = None, None, 0
-        for name, v in self.grads.items():
-            n = v.numel()
-            if any(name.startswith(p) for p in prefixes):
-                lo = off if lo is None else lo
-                hi = off + n
-            off += n
-        return self.flat_g[lo:hi]
-
-    def _allreduce(self, bucket: torch.Tensor):
-        if self.world > 1:
-            self.works.append(torch.distributed.all_reduce(bucket, group=self.pg, async_op=True))
-
     def _build_backward(self):
         s, ctx = self.spec, self.ctx
         bw = Backward(s, ctx, self.Wt, self.grads)
+        ex = self.exchange
         d = bw.tail(self.saved_tail)
-        tail_b = self._bucket(("conv_after_body.", "upsample.", "conv_last."))
-        ctx.mark("allreduce_tail", lambda b=tail_b: self._allreduce(b))
+        ctx.mark("allreduce_tail", lambda: ex.launch("tail"))
         for g in reversed(range(s.G)):
             extra = (self.saved_tail["d_fb"],) if g == 0 else ()
             d = bw.group(self.saved[g], d, g, extra_res=extra, dx_out=ctx.scratch(f"bw_grp{g & 1}", d.shape))
-            bk = self._bucket((f"residual_groups.{g}.",))
-            ctx.mark(f"allreduce_rg{g}", lambda b=bk: self._allreduce(b))
+            ctx.mark(f"allreduce_rg{g}", lambda t=f"rg{g}": ex.launch(t))
         bw.head(self.x, d)
-        head_b = self._bucket(("conv_first.",))
-        ctx.mark("allreduce_head", lambda b=head_b: self._allreduce(b))
+        ctx.mark("allreduce_head", lambda: ex.launch("head"))
 
     def _build_update(self):
         self.upd = Ctx(self.dtype, self.device, record=True)
@@ -169,10 +154,8 @@ class FENEngine:
         Returns the (device) loss of this rank's shard."""
         if hr is not None:
             self.hr.copy_(hr)
-        self.works = []
         self.ctx.run()
-        for wk in self.works:
-            wk.wait()
+        self.exchange.wait()
         self.upd.run()
         self.Wt.pack()
         return self.loss

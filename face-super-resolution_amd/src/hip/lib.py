@@ -52,6 +52,7 @@ _SIGS = {
     "fen_conv_last_dgrad_part_rows": (c_size_t, [c_int] * 3),
     "fen_conv_last_dgrad": (c_int, [c_int] * 6 + [c_void_p] * 6 + [c_void_p]),
     "fen_se_fwd": (c_int, [c_int, c_int, c_int, c_int, c_float] + [c_void_p] * 6 + [c_void_p]),
+    "fen_se_fused": (c_int, [c_int] * 6 + [c_float] + [c_void_p] * 7 + [c_float, c_void_p, c_void_p, c_void_p]),
     "fen_se_apply": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
     "fen_pool_parts": (c_size_t, [c_int]),
     "fen_pool_dot": (c_int, [c_int] * 4 + [c_void_p] * 3 + [c_void_p]),

@@ -155,13 +155,12 @@ class Forward:
             mean = hid = None
             sg = ctx.scratch("se_s", (B, C), torch.float32)
         ca = pre + "channel_attention.fc."
-        ctx.emit("se_fwd", ctx.lib.fen_se_fwd, B, C, s.Cr, T, 1.0 / (H * W), ptr(part), ptr(p[ca + "0.weight"]),
-                 ptr(p[ca + "2.weight"]), ptr(mean), ptr(hid), ptr(sg))
         if self.attn is not None and name is not None:
             self.attn[name] = sg
         y = out if out is not None else ctx.alloc(x.shape)
-        ctx.emit("se_apply", ctx.lib.fen_se_apply, ctx.code, B, H * W, C, ptr(t), ptr(sg), s.res_scale, ptr(x),
-                 ptr(y))
+        ctx.emit("se_fused", ctx.lib.fen_se_fused, ctx.code, B, H * W, C, s.Cr, T, 1.0 / (H * W), ptr(part),
+                 ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]), ptr(mean), ptr(hid), ptr(sg), ptr(t), s.res_scale,
+                 ptr(x), ptr(y))
         saved = dict(x=x, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg) if self.save else dict(s=sg)
         return y, saved
 

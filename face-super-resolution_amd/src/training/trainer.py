@@ -30,6 +30,7 @@ import torch.nn.functional as F
 
 from ..hip.engine import FENEngine, flatten_params
 from ..hip.program import Ctx, ptr
+from .dp import broadcast_arena
 from .optim import FusedAdamW
 
 
@@ -124,7 +125,7 @@ class Trainer:
         self.model = model.to(self.device)
         if self.world > 1:  # identical start on every rank (RCCL broadcast of the flat arena)
             flatten_params(self.model, self.device)
-            dist.broadcast(self.model._fen_flat, src=0)
+            broadcast_arena(self.model._fen_flat, src=0)
         elif getattr(self.model, "_fen_flat", None) is None:
             flatten_params(self.model, self.device)
         self.train_loader, self.val_loader = train_loader, val_loader

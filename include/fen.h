@@ -115,6 +115,13 @@ int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const voi
 /* Channel attention (blocks.py:44-92) forward: pool partials -> s = sigmoid(W2 relu(W1 mean)) */
 int fen_se_fwd(int B, int C, int Cr, int nparts, float inv_hw, const float* part,
                const float* w1, const float* w2, float* mean, float* hid, float* s, void* stream);
+/* SE gate and apply in one launch (replaces fen_se_fwd + fen_se_apply on the forward path;
+ * ChannelAttention.forward blocks.py:83-92 and RCAB's `out * res_scale + x`, blocks.py:149-153):
+ * y = t * s[b,c] * res_scale + x with s computed from the pool partials as in fen_se_fwd.
+ * mean / hid / s (optional, may be NULL) receive the gate's intermediates.                   */
+int fen_se_fused(int dtype, int B, int HW, int C, int Cr, int nparts, float inv_hw, const float* part,
+                 const float* w1, const float* w2, float* mean, float* hid, float* s, const void* t,
+                 float res_scale, const void* x, void* y, void* stream);
 /* y = t * s[b,c] * res_scale + x   (blocks.py:92,153)                                       */
 int fen_se_apply(int dtype, int B, int HW, int C, const void* t, const float* s, float res_scale,
                  const void* x, void* y, void* stream);

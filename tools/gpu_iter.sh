@@ -1,0 +1,10 @@
+# quick iteration: kernel parity, phase stamps, conv microbench, end-to-end bench
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/iter_pytest.log 2>&1 || { tail -30 gpurun_out/iter_pytest.log; exit 1; }
+tail -2 gpurun_out/iter_pytest.log
+FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_stamp.so B=32 timeout -k 10 120 python tools/stamp_conv.py
+FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_stamp.so B=128 timeout -k 10 120 python tools/stamp_conv.py
+timeout -k 10 300 python tools/bench_conv.py
+timeout -k 10 300 python bench.py --no-cpu-baseline
