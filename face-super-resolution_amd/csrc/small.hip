@@ -305,6 +305,289 @@ __global__ __launch_bounds__(256) void k_se_fused(int HW, int C, int Cr, int npa
     }
 }
 
+// y = t * s[b,c] * rs + x   or (bwd)  dt = dy * s[b,c] * rs + g[b,c]
+template <typename T, bool BWD>
+__global__ void k_se_apply(size_t nvec, int HW, int C, const T* __restrict__ t, const float* __restrict__ s,
+                           float rs, const void* __restrict__ x, T* __restrict__ y) {
+    constexpr int V = 16 / sizeof(T);
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nvec) return;
+    const size_t e0 = i * V;
+    const int c0 = (int)(e0 % C);
+    const size_t b = e0 / ((size_t)HW * C);
+    float tv[V], o[V];
+    unpack16<T>(*(const uint4*)(t + e0), tv);
+    const float* sp = s + b * C + c0;
+    if constexpr (!BWD) {
+        float xv[V];
+        unpack16<T>(*(const uint4*)((const T*)x + e0), xv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = tv[j] * sp[j] * rs + xv[j];
+    } else {
+        const float* gp = (const float*)x + b * C + c0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = tv[j] * rs * sp[j] + gp[j];
+    }
+    *(uint4*)(y + e0) = pack16<T>(o);
+}
+
+// part[b][chunk][c] = sum over the chunk's pixels of a*b_ (or a)
+template <typename T>
+__global__ __launch_bounds__(256) void k_pool_dot(int HW, int C, int nchunk, const T* __restrict__ a,
+                                                  const T* __restrict__ bb, float* __restrict__ part) {
+    constexpr int V = 16 / sizeof(T);
+    __shared__ float red[256][V];
+    const int TP = C / V;                    // threads per pixel
+    const int R = 256 / TP;                  // pixels per iteration
+    const int tid = threadIdx.x, cv = tid % TP, pr = tid / TP;
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int per = (HW + nchunk - 1) / nchunk;
+    const int p0 = ch * per, p1 = min(p0 + per, HW);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+    if (pr < R) {
+        for (int p = p0 + pr; p < p1; p += R) {
+            const size_t e = ((size_t)b * HW + p) * C + cv * V;
+            float av[V];
+            unpack16<T>(*(const uint4*)(a + e), av);
+            if (bb) {
+                float bv[V];
+                unpack16<T>(*(const uint4*)(bb + e), bv);
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] += av[j] * bv[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] += av[j];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[tid][j] = acc[j];
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        const int cvv = c / V, j = c % V;
+        float sum = 0.f;
+        for (int r = 0; r < R; ++r) sum += red[r * TP + cvv][j];
+        part[((size_t)b * nchunk + ch) * C + c] = sum;
+    }
+}
+
+// SE backward for one image (block per b)
+__global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, const float* __restrict__ part,
+                         const float* __restrict__ mean, const float* __restrict__ hid, const float* __restrict__ s,
+                         const float* __restrict__ w1, const float* __restrict__ w2, float* g, float* dw1p,
+                         float* dw2p) {
+    __shared__ float dz[512], dh[128];
+    const int b = blockIdx.x, t = threadIdx.x;
+    for (int c = t; c < C; c += blockDim.x) {
+        float a = 0.f;
+        for (int p = 0; p < nparts; ++p) a += part[((size_t)b * nparts + p) * C + c];
+        const float sv = s[(size_t)b * C + c];
+        dz[c] = a * rs * sv * (1.f - sv);                 // through sigmoid
+    }
+    __syncthreads();
+    for (int j = t; j < Cr; j += blockDim.x) {
+        float a = 0.f;
+        for (int c = 0; c < C; ++c) a += w2[(size_t)c * Cr + j] * dz[c];
+        const float h = hid[(size_t)b * Cr + j];
+        dh[j] = h > 0.f ? a : 0.f;                         // through ReLU
+    }
+    __syncthreads();
+    for (int i = t; i < C * Cr; i += blockDim.x) {
+        const int c = i / Cr, j = i % Cr;
+        dw2p[(size_t)b * C * Cr + i] = dz[c] * hid[(size_t)b * Cr + j];          // [C][Cr]
+        const int jj = i / C, cc = i % C;
+        dw1p[(size_t)b * C * Cr + i] = dh[jj] * mean[(size_t)b * C + cc];        // [Cr][C]
+    }
+    for (int c = t; c < C; c += blockDim.x) {
+        float a = 0.f;
+        for (int j = 0; j < Cr; ++j) a += w1[(size_t)j * C + c] * dh[j];
+        g[(size_t)b * C + c] = a * inv_hw;
+    }
+}
+
+// ------------------------------ resampling / layout ------------------------------
+__global__ void k_bicubic_down4(int B, int C, int H, int W, const float* __restrict__ hr, float* __restrict__ lr) {
+    const int Ho = H / 4, Wo = W / 4;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)B * C * Ho * Wo) return;
+    const int ox = (int)(i % Wo), oy = (int)((i / Wo) % Ho);
+    const size_t plane = i / ((size_t)Wo * Ho);
+    lr[i] = bicubic_sample(hr + plane * H * W, H, W, oy, ox, 4.0f);
+}
+
+template <typename T>
+__global__ void k_nchw_to_nhwc(int B, int C, int H, int W, int Cpad, const float* __restrict__ x, T* __restrict__ y) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // NHWC order
+    if (i >= (size_t)B * Cpad * H * W) return;
+    const int c = (int)(i % Cpad);
+    const size_t px = i / Cpad;
+    const int w = (int)(px % W), h = (int)((px / W) % H), b = (int)(px / ((size_t)W * H));
+    y[i] = fromf<T>(c < C ? x[(((size_t)b * C + c) * H + h) * W + w] : 0.f);
+}
+
+// dv = dy * (pre>0 ? 1 : alpha[c]) -> du[b][h/2][w/2][4c + 2(h&1) + (w&1)]; block = 16x16 px tile
+template <typename T>
+__global__ __launch_bounds__(256) void k_prelu_bwd_unshuffle(int B, int H, int W, int C, const T* __restrict__ dy,
+                                                             const T* __restrict__ pre, const float* __restrict__ alpha,
+                                                             T* __restrict__ du, float* __restrict__ part) {
+    __shared__ float sdal[256 * 2];
+    const int tid = threadIdx.x;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
+    const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+    const int K2 = C / 2, k = tid % K2;
+    const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
+    float dal0 = 0.f, dal1 = 0.f;
+    const int Hh = H >> 1, Wh = W >> 1;
+    for (int i = tid; i < 64 * K2; i += 256) {
+        const int dp = i / K2, hh = dp >> 3, ww = dp & 7;
+        const int gh2 = (h0 >> 1) + hh, gw2 = (w0 >> 1) + ww;
+        if (gh2 >= Hh || gw2 >= Wh) continue;
+        float out[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const size_t pi = ((size_t)(b * H + 2 * gh2 + (t >> 1)) * W + 2 * gw2 + (t & 1)) * C + 2 * k;
+            const float d0 = tof<T>(dy[pi]), d1 = tof<T>(dy[pi + 1]);
+            const float p0 = tof<T>(pre[pi]), p1 = tof<T>(pre[pi + 1]);
+            dal0 += p0 > 0.f ? 0.f : d0 * p0;
+            dal1 += p1 > 0.f ? 0.f : d1 * p1;
+            out[t] = p0 > 0.f ? d0 : d0 * al0;
+            out[4 + t] = p1 > 0.f ? d1 : d1 * al1;
+        }
+        char* o = (char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 8 * k) * sizeof(T);
+        if constexpr (sizeof(T) == 2) {
+            *(uint4*)o = pack16<bf16>(out);
+        } else {
+            *(uint4*)o = pack16<float>(out);
+            *(uint4*)(o + 16) = pack16<float>(out + 4);
+        }
+    }
+    sdal[tid * 2] = dal0;
+    sdal[tid * 2 + 1] = dal1;
+    __syncthreads();
+    if (tid < C) {
+        const int kk = tid >> 1, e = tid & 1;
+        float s = 0.f;
+        for (int r = kk; r < 256; r += K2) s += sdal[r * 2 + e];
+        part[(size_t)blockIdx.x * C + tid] = s;
+    }
+}
+template <typename T>
+__global__ void k_nhwc_to_nchw(int B, int C, int H, int W, const T* __restrict__ x, float* __restrict__ y) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // NCHW order
+    if (i >= (size_t)B * C * H * W) return;
+    const int w = (int)(i % W), h = (int)((i / W) % H), c = (int)((i / ((size_t)W * H)) % C);
+    const size_t b = i / ((size_t)W * H * C);
+    y[i] = tof<T>(x[((b * H + h) * W + w) * C + c]);
+}
+
+template <typename T>
+__global__ void k_pack(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mode == 2) {  // [9][Cin_pad][Cout], row = ci, taps flipped
+        const int co = (int)(i % Cout);
+        const int ci = (int)((i / Cout) % ((Cin + 15) & ~15));
+        const int tap = (int)(i / ((size_t)Cout * ((Cin + 15) & ~15)));
+        const int kh = 2 - tap / 3, kw = 2 - tap % 3;
+        out[i] = fromf<T>(ci < Cin ? w[(((size_t)co * Cin + ci) * 3 + kh) * 3 + kw] : 0.f);
+    } else {          // [9][Cout_pad][Cin], row = co (mode 1: shuffle-permuted rows)
+        const int coutp = (Cout + 15) & ~15;
+        const int ci = (int)(i % Cin);
+        const int cp = (int)((i / Cin) % coutp);
+        const int tap = (int)(i / ((size_t)Cin * coutp));
+        int co = cp;
+        if (mode == 1) { const int Cq = Cout / 4; co = 4 * (cp % Cq) + cp / Cq; }
+        out[i] = fromf<T>(cp < Cout ? w[(((size_t)co * Cin + ci) * 3 + tap / 3) * 3 + tap % 3] : 0.f);
+    }
+}
+
+// ------------------------------ reductions / optimizer ------------------------------
+// stage 1: block (cb, rb) sums rows [rb*RB, rb*RB+RB) of 64 columns into row rb*RB (in place)
+constexpr int COLSUM_RB = 256;
+__global__ void k_colsum1(int rows, int cols, float* part) {
+    __shared__ float red[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    const int r0 = blockIdx.y * COLSUM_RB, r1 = min(r0 + COLSUM_RB, rows);
+    float s = 0.f;
+    if (c < cols)
+        for (int r = r0 + g; r < r1; r += 4) s += part[(size_t)r * cols + c];
+    red[g][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (g == 0 && c < cols) part[(size_t)r0 * cols + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void k_colsum2(int rows, int cols, const float* part, float scale, float* out, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    float s = 0.f;
+    for (int r = 0; r < rows; r += COLSUM_RB) s += part[(size_t)r * cols + c];
+    s *= scale;
+    out[c] = accumulate ? out[c] + s : s;
+}
+
+constexpr int SUMSQ_BLOCKS_MAX = 1024;
+__global__ void k_sumsq(size_t n, const float* __restrict__ g, float* part) {
+    __shared__ float red[4];
+    float s = 0.f;
+    const size_t n4 = n / 4;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 v = ((const float4*)g)[i];
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    if (blockIdx.x == 0)
+        for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += g[i] * g[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ void k_optim_prepare(int nparts, const float* part, float max_norm, float b1, float b2, float wd,
+                                float* scal) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += part[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+        float coef = 1.f;
+        if (max_norm > 0.f) coef = fminf(max_norm / (norm + 1e-6f), 1.f);
+        const float step = scal[2] + 1.f;
+        const float lr = scal[3];
+        scal[0] = norm;
+        scal[1] = coef;
+        scal[2] = step;
+        scal[4] = 1.f - lr * wd;
+        scal[5] = lr / (1.f - powf(b1, step));
+        scal[6] = 1.f / sqrtf(1.f - powf(b2, step));
+    }
+}
+__global__ void k_adamw(size_t n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                        float* __restrict__ v, const float* __restrict__ scal, float b1, float b2, float eps) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float coef = scal[1], decay = scal[4], step_size = scal[5], rbc2 = scal[6];
+    const float gi = g[i] * coef;
+    float pi = p[i] * decay;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);    // lerp
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    const float denom = sqrtf(vi) * rbc2 + eps;
+    pi = pi - step_size * mi / denom;
+    p[i] = pi; m[i] = mi; v[i] = vi;
+}
+__global__ void k_scale(size_t n, float* y, float s) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] *= s;
+}
+
+}  // namespace
+
+// =================================== C-ABI ===================================
+#define STREAM ((hipStream_t)stream)
+
 extern "C" int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x, const float* w,
                                   const float* bias, void* y, void* stream) {
     if (!x || !w || !bias || !y || B <= 0 || Ci <= 0 || Ci > 3 || C % 8 || C > 128) return FEN_EINVAL;
