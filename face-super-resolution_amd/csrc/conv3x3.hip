@@ -81,7 +81,7 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 
 // Diagnostic build only (-DFEN_STAMPS, tools/stamp_conv.py): per-block s_memrealtime /
 // s_memtime stamps of the persistent kernel's phases into d.loss_part (unused by the
-// forward epilogues), 16 x 2 u64 per block.  In the real build no stamp executes.
+// forward epilogues), [block][wave][16 stamps][realtime, memtime] u64.  In the real build no stamp executes.
 #ifdef FEN_STAMPS
 #define FEN_STAMP(i)                                                                          \
     do {                                                                                      \
@@ -90,8 +90,9 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
         asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"                 \
                      : "=s"(_rt), "=s"(_mt)::"memory");                                       \
         __builtin_amdgcn_sched_barrier(0);                                                    \
-        if (threadIdx.x == 0 && (i) < 16) {                                                   \
-            unsigned long long* _p = (unsigned long long*)d.loss_part + (size_t)blockIdx.x * 32; \
+        if ((threadIdx.x & 63) == 0 && (i) < 16) {                                            \
+            unsigned long long* _p =                                                          \
+                (unsigned long long*)d.loss_part + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 32; \
             _p[2 * (i)] = _rt;                                                                \
             _p[2 * (i) + 1] = _mt;                                                            \
         }                                                                                     \
@@ -277,7 +278,7 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
 
     // per-channel partial sums (SE pool or PReLU dalpha): 16-lane butterfly, then across waves
     if (epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD)) {
-        __syncthreads();
+        // red[] was last read before the previous tile's closing barrier: no barrier needed here
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -420,9 +421,10 @@ __device__ __forceinline__ void conv_tap(f32x4 (&acc)[MT][NT], const char* wt, c
 
 // All 9 taps x 2 k-halves of one tile from an LDS-resident filter, software-pipelined:
 // the fragments of step s+1 are read while the MFMAs of step s run (two register sets).
-template <int COT, int MT, int NT>
+// per_tap(tap) runs once per tap between the MFMA groups (the next tile's halo DMA).
+template <int COT, int MT, int NT, typename F>
 __device__ __forceinline__ void conv_tile_resident(f32x4 (&acc)[MT][NT], const char* wts, const char* halo, int wr,
-                                                   int wc, int q, int c16) {
+                                                   int wc, int q, int c16, F&& per_tap) {
     uint4 A0[MT], B0[NT], A1[MT], B1[NT];
     const int arow = wc * MT * 16 + c16;
     auto load = [&](int tap, int kk, uint4 (&A)[MT], uint4 (&Bf)[NT]) {
@@ -441,13 +443,21 @@ __device__ __forceinline__ void conv_tile_resident(f32x4 (&acc)[MT][NT], const c
 #pragma unroll
             for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], A[m], Bf[n]);
     };
+    // sched_barriers pin the order: each fragment set is read one MFMA group ahead of its use
     load(0, 0, A0, B0);
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
         load(tap, 1, A1, B1);
+        per_tap(tap);
+        __builtin_amdgcn_sched_barrier(0);
         mma(A0, B0);
-        if (tap < 8) load(tap + 1, 0, A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        // unconditional (the last tap re-reads tap 0, unused): a conditional load here makes
+        // the waitcnt pass merge both paths and drain the prefetch before the next MFMAs
+        load(tap == 8 ? 0 : tap + 1, 0, A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
         mma(A1, B1);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -487,42 +497,52 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wts + i * 1024), 16, voff, 0, 0, 0);
     }
     const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * 128));
-    // lane-linear LDS slots s = i*64 + lane hold (pixel p = s>>3, chunk pc = s&7); the XOR
-    // swizzle is applied to the SOURCE address; slots past the halo read out of range (-> 0)
-    // and land in the slack after each buffer.
-    auto load_halo = [&](int t, char* buf) {
+    // Halo piece i (of HALO_DMA 1-KiB pieces) of tile t into buf: lane-linear LDS slots
+    // s = i*64 + lane hold (pixel p = s>>3, chunk pc = s&7); the XOR swizzle is applied to the
+    // SOURCE address; slots past the halo read out of range (-> 0) into the slack.
+    auto halo_piece = [&](int t, unsigned base, int i) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        const unsigned base = lds_addr(buf);
-        for (int i = wave; i < HALO_DMA; i += NW) {
-            const int s = i * 64 + lane;
-            const int p = s >> 3, pc = s & 7;
-            const int hr = p / HALO, hc = p - hr * HALO;
-            const int c = pc ^ (hc & 7);
-            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-            const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-            const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
-            dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
-        }
+        const int s = i * 64 + lane;
+        const int p = s >> 3, pc = s & 7;
+        const int hr = p / HALO, hc = p - hr * HALO;
+        const int c = pc ^ (hc & 7);
+        const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+        const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+        const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
+        dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
     };
 
     FEN_STAMP(0);
     const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * MT * 16 + q * 4);
     int t = slot;
-    if (t < ntiles) load_halo(t, hbuf);
+    if (t < ntiles)
+        for (int i = wave; i < HALO_DMA; i += NW) halo_piece(t, lds_addr(hbuf), i);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     FEN_STAMP(1);
     for (int k = 0; t < ntiles; ++k, t += nslot) {
         char* cur = hbuf + (k & 1) * HALO_SLOT;
         const int tn = t + nslot;
-        if (tn < ntiles) load_halo(tn, hbuf + ((k + 1) & 1) * HALO_SLOT);
+        const unsigned nbase = lds_addr(hbuf + ((k + 1) & 1) * HALO_SLOT);
+        // the next tile's halo: all pieces up front, or (debug & 4) one piece per wave per tap
+        const bool ilv = d.debug & 4;
+        if (!ilv && tn < ntiles)
+            for (int i = wave; i < HALO_DMA; i += NW) halo_piece(tn, nbase, i);
+        auto next_halo = [&](int tap) {
+            const int i = wave + tap * NW;
+            if (ilv && tn < ntiles && i < HALO_DMA) halo_piece(tn, nbase, i);
+        };
         f32x4 acc[MT][NT];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!(d.debug & 2)) conv_tile_resident<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16);
+        if (!(d.debug & 2)) {
+            conv_tile_resident<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16, next_halo);
+        } else {
+            for (int tap = 0; tap < 9; ++tap) next_halo(tap);
+        }
         FEN_STAMP(2 + 3 * k);
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
@@ -534,6 +554,137 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
         } else {
             conv_epilogue<bf16, COT, WR, WC, EPIC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
         }
+        FEN_STAMP(3 + 3 * k);
+        wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                        // ... for everyone; cur is free
+        FEN_STAMP(4 + 3 * k);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv3x3_q: persistent, filter resident in VGPRs (bf16, Cin == 64, Cout tile 64).
+// 8 waves = 4 pixel-row groups x 2 output-channel halves; each wave keeps its 32 output
+// channels x 576 (tap, ci) weights -- 36 x 16 B = 144 VGPRs -- for the life of the block,
+// so the tap loop reads only pixel fragments from LDS (0.5 ds_read_b128 per MFMA; the
+// LDS-resident-filter loop needs 0.75 and measured 1.4x slower in isolation,
+// tools/mfma_loop.hip).  LDS: 3 halo slots; slots 1-2 stage the filter at start-up while the
+// first halo lands in slot 0; afterwards tiles ping-pong between slots 0 and 1, the next
+// tile's halo streaming in by LDS-DMA under the current tile's MFMAs.
+// ------------------------------------------------------------------------------------
+template <int EPIC>
+__global__ __launch_bounds__(512, 1) void k_conv3x3_q(const fen_conv_desc d) {
+    constexpr int COT = 64, WR = 4, WC = 2, MT = 2, NT = 4, NW = 8;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* hbuf = smem;                                      // 3 x HALO_SLOT
+    float* red = (float*)(smem + 3 * HALO_SLOT);            // WR * COT floats
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave % WR, wc = wave / WR;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int H = d.H, W = d.W, Cout = d.Cout;
+    const int ncot = Cout / COT;
+    const int cot = blockIdx.x % ncot, co0 = cot * COT;
+    const int nslot = gridDim.x / ncot, slot = blockIdx.x / ncot;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int ntiles = d.B * tpi;
+    const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * 128));
+
+    auto halo_piece = [&](int t, unsigned base, int i) {
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const int s = i * 64 + lane;
+        const int p = s >> 3, pc = s & 7;
+        const int hr = p / HALO, hc = p - hr * HALO;
+        const int c = pc ^ (hc & 7);
+        const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+        const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+        const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
+        dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
+    };
+
+    FEN_STAMP(0);
+    // start-up: filter rows r = tap*64 + co_l (72 KB, swizzled 128-B rows: the VGPR fill
+    // below reads 16 rows at one chunk, conflict-free only with the XOR key) -> slots 1..2,
+    // first halo -> slot 0
+    {
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)d.w, (short)0, (int)((size_t)9 * Cout * 128), 0x00020000);
+        char* wst = hbuf + HALO_SLOT;
+        for (int i = wave; i < 9 * COT * 8 / 64; i += NW) {
+            const int s = i * 64 + lane;
+            const int r = s >> 3, pc = s & 7;
+            const int c = pc ^ ((r >> 1) & 7);
+            const int tap = r / COT, col = r - tap * COT;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wst + i * 1024), 16,
+                                                     ((tap * Cout + co0 + col) * 64 + c * 8) * 2, 0, 0, 0);
+        }
+    }
+    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * MT * 16 + q * 4);
+    int t = slot;
+    if (t < ntiles)
+        for (int i = wave; i < HALO_DMA; i += NW) halo_piece(t, lds_addr(hbuf), i);
+    FEN_STAMP(13);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    FEN_STAMP(14);
+    uint4 wreg[9][2][MT];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const int row = tap * COT + wc * MT * 16 + m * 16 + c16;
+                wreg[tap][kk][m] = *(const uint4*)(hbuf + HALO_SLOT + swz(row, kk * 4 + q));
+            }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();   // staging slots free again
+    FEN_STAMP(1);
+
+    for (int k = 0; t < ntiles; ++k, t += nslot) {
+        const char* cur = hbuf + (k & 1) * HALO_SLOT;
+        const int tn = t + nslot;
+        if (tn < ntiles) {
+            const unsigned nbase = lds_addr(hbuf + ((k + 1) & 1) * HALO_SLOT);
+            for (int i = wave; i < HALO_DMA; i += NW) halo_piece(tn, nbase, i);
+        }
+        f32x4 acc[MT][NT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        {
+            uint4 B0[NT], B1[NT];
+            auto load = [&](int tap, int kk, uint4 (&Bf)[NT]) {
+                const int kh = tap / 3, kw = tap - kh * 3;
+                const char* hb = cur + hcol(c16 + kw, kk * 4 + q) + (wr * NT + kh) * (HALO * 128);
+#pragma unroll
+                for (int n = 0; n < NT; ++n) Bf[n] = *(const uint4*)(hb + n * (HALO * 128));
+            };
+            auto mma = [&](int tap, int kk, const uint4 (&Bf)[NT]) {
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], wreg[tap][kk][m], Bf[n]);
+            };
+            load(0, 0, B0);
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                load(tap, 1, B1);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(tap, 0, B0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (tap < 8) load(tap + 1, 0, B0);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(tap, 1, B1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        FEN_STAMP(2 + 3 * k);
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        conv_epilogue<bf16, COT, WR, WC, EPIC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
         FEN_STAMP(3 + 3 * k);
         wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -670,6 +821,32 @@ int launch_p(const fen_conv_desc* d, hipStream_t s) {
     return FEN_OK;
 }
 
+template <int EPIC>
+int launch_q(const fen_conv_desc* d, hipStream_t s) {
+    const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
+    const int ntiles = d->B * tpi;
+    const int ncot = d->Cout / 64;
+    if (g_num_cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int grid = g_num_cus;
+    grid -= grid % ncot;
+    const int maxg = ntiles * ncot;
+    if (grid > maxg) grid = maxg;
+    const size_t lds = 3 * HALO_SLOT + 4 * 64 * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_q<EPIC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_conv3x3_q<EPIC>), dim3(grid), dim3(512), lds, s, *d);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
 template <typename T, int COT>
 int launch_s(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
@@ -722,6 +899,21 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
             for (int k = nres; k < 3; ++k) dense = dense && !d->res[k];
             const int key = dense && conv_variant() != 2 ? (epi | (nres << 8)) : -1;
             constexpr int B_ = FEN_EPI_BIAS;
+            if (conv_variant() == 3 && key == (B_ | FEN_EPI_PRELU)) return launch_p<64, 4, 1, B_ | FEN_EPI_PRELU>(d, s);
+            if (conv_variant() == 4) {
+                switch (key) {
+                    case B_ | FEN_EPI_PRELU: return launch_q<B_ | FEN_EPI_PRELU>(d, s);
+                    case B_ | FEN_EPI_POOL: return launch_q<B_ | FEN_EPI_POOL>(d, s);
+                    case B_ | (1 << 8): return launch_q<B_ | (1 << 8)>(d, s);
+                    case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE: return launch_q<B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
+                    case FEN_EPI_PRELU_BWD: return launch_q<FEN_EPI_PRELU_BWD>(d, s);
+                    case 0: return launch_q<0>(d, s);
+                    case 1 << 8: return launch_q<1 << 8>(d, s);
+                    case 2 << 8: return launch_q<2 << 8>(d, s);
+                    case 3 << 8: return launch_q<3 << 8>(d, s);
+                    default: break;
+                }
+            }
             switch (key) {
                 case B_ | FEN_EPI_PRELU: return launch_p<64, 4, 2, B_ | FEN_EPI_PRELU>(d, s);
                 case B_ | FEN_EPI_POOL: return launch_p<64, 4, 2, B_ | FEN_EPI_POOL>(d, s);

@@ -263,9 +263,11 @@ __global__ __launch_bounds__(256) void k_se_fwd(int C, int Cr, int nparts, float
 }
 
 // SE gate + apply in one launch: grid (splits, B); every block recomputes its image's gate
-// (a few KB of L2 reads), block 0 of each image stores mean/hid/s.  Each thread issues the
-// loads of its NPT t / x vectors BEFORE the gate, so the gate's latency hides under them,
-// then writes y = t * s[c] * rs + x.
+// and block 0 of each image stores mean/hid/s.  Latency layout: the gate's operands (pool
+// partials, both FC weights) are loaded first -- head of the memory queue -- then each
+// thread's NPT t / x vectors, so the streaming loads are in flight while the gate is
+// computed from LDS; then y = t * s[c] * rs + x.  Needs C * Cr <= 4096 and nparts <= 8*(256/C)
+// for the single-round-trip path (larger nparts take a slower tail loop).
 template <typename T, int NPT>
 __global__ __launch_bounds__(256) void k_se_fused(int HW, int C, int Cr, int nparts, float inv_hw,
                                                   const float* __restrict__ part, const float* __restrict__ w1,
@@ -273,11 +275,34 @@ __global__ __launch_bounds__(256) void k_se_fused(int HW, int C, int Cr, int npa
                                                   const T* __restrict__ t, float rs, const T* __restrict__ x,
                                                   T* __restrict__ y) {
     __shared__ float sm[256], sh[64], sg[256], red[256];
+    __shared__ __attribute__((aligned(16))) float w1s[4096], w2s[4096];
     constexpr int V = 16 / sizeof(T);
-    const int b = blockIdx.y;
+    const int tid = threadIdx.x, b = blockIdx.y;
+    // ---- 1. gate operands
+    const int G = C >= 256 ? 1 : 256 / C;
+    const int c = tid % C, g = tid / C;
+    const bool act = tid < G * C;
+    const float* pp = part + (size_t)b * nparts * C + c;
+    float pv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int p = g + i * G;
+        pv[i] = (act && p < nparts) ? pp[(size_t)p * C] : 0.f;
+    }
+    const int nw4 = C * Cr / 4;
+    float4 w1v[4], w2v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = tid + j * 256;
+        if (i < nw4) {
+            w1v[j] = ((const float4*)w1)[i];
+            w2v[j] = ((const float4*)w2)[i];
+        }
+    }
+    // ---- 2. streaming operands
     const size_t nv = (size_t)HW * C / V;
     const size_t base = (size_t)b * nv;
-    const size_t v0 = (size_t)blockIdx.x * (256 * NPT) + threadIdx.x;
+    const size_t v0 = (size_t)blockIdx.x * (256 * NPT) + tid;
     uint4 tv[NPT], xv[NPT];
 #pragma unroll
     for (int j = 0; j < NPT; ++j) {
@@ -287,19 +312,70 @@ __global__ __launch_bounds__(256) void k_se_fused(int HW, int C, int Cr, int npa
             xv[j] = *(const uint4*)(x + (base + v) * V);
         }
     }
+    // ---- 3. gate
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += pv[i];
+    for (int p = g + 8 * G; act && p < nparts; p += G) a += pp[(size_t)p * C];
+    if (act) red[g * C + c] = a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = tid + j * 256;
+        if (i < nw4) {
+            ((float4*)w1s)[i] = w1v[j];
+            ((float4*)w2s)[i] = w2v[j];
+        }
+    }
+    __syncthreads();
     const bool first = blockIdx.x == 0;
-    se_gate(b, C, Cr, nparts, inv_hw, part, w1, w2, sm, sh, sg, red, first ? mean : nullptr,
-            first ? hid : nullptr, first ? s : nullptr);
+    for (int cc = tid; cc < C; cc += 256) {
+        float m = 0.f;
+        for (int k = 0; k < G; ++k) m += red[k * C + cc];
+        m *= inv_hw;
+        sm[cc] = m;
+        if (first && mean) mean[(size_t)b * C + cc] = m;
+    }
+    __syncthreads();
+    const int k1 = C / 16;
+    for (int idx = tid; idx < Cr * 16; idx += 256) {
+        const int j = idx >> 4, seg = idx & 15;
+        const float* wr = w1s + j * C + seg * k1;
+        float h = 0.f;
+        for (int k = 0; k < k1; ++k) h += wr[k] * sm[seg * k1 + k];
+        h = group16_sum(h);
+        if (seg == 0) {
+            h = fmaxf(h, 0.f);
+            sh[j] = h;
+            if (first && hid) hid[(size_t)b * Cr + j] = h;
+        }
+    }
+    __syncthreads();
+    const int k2 = Cr / 4;
+    for (int idx = tid; idx < C * 4; idx += 256) {
+        const int cc = idx >> 2, seg = idx & 3;
+        const float* wr = w2s + cc * Cr + seg * k2;
+        float z = 0.f;
+        for (int k = 0; k < k2; ++k) z += wr[k] * sh[seg * k2 + k];
+        z += __shfl_xor(z, 1, 64);
+        z += __shfl_xor(z, 2, 64);
+        if (seg == 0) {
+            const float v = 1.f / (1.f + expf(-z));
+            sg[cc] = v;
+            if (first && s) s[(size_t)b * C + cc] = v;
+        }
+    }
+    __syncthreads();
+    // ---- 4. apply
 #pragma unroll
     for (int j = 0; j < NPT; ++j) {
         const size_t v = v0 + (size_t)j * 256;
         if (v < nv) {
             const int c0 = (int)((v * V) % C);
-            float a[V], bb[V], o[V];
-            unpack16<T>(tv[j], a);
-            unpack16<T>(xv[j], bb);
+            float av[V], bv[V], o[V];
+            unpack16<T>(tv[j], av);
+            unpack16<T>(xv[j], bv);
 #pragma unroll
-            for (int k = 0; k < V; ++k) o[k] = a[k] * sg[c0 + k] * rs + bb[k];
+            for (int k = 0; k < V; ++k) o[k] = av[k] * sg[c0 + k] * rs + bv[k];
             *(uint4*)(y + (base + v) * V) = pack16<T>(o);
         }
     }
@@ -677,7 +753,7 @@ extern "C" int fen_se_fused(int dtype, int B, int HW, int C, int Cr, int nparts,
                             const float* w1, const float* w2, float* mean, float* hid, float* s, const void* t,
                             float res_scale, const void* x, void* y, void* stream) {
     if (!part || !w1 || !w2 || !t || !x || !y || B <= 0 || HW <= 0 || nparts <= 0) return FEN_EINVAL;
-    if (!se_shape_ok(C, Cr)) return FEN_EUNSUPPORTED;
+    if (!se_shape_ok(C, Cr) || C * Cr > 4096) return FEN_EUNSUPPORTED;
     const int V = dtype == FEN_BF16 ? 8 : 4;
     const size_t nv = (size_t)HW * C / V;
     // 8 vectors per thread: 16 blocks per 64x64x64 bf16 image -> 512 blocks at B = 32

@@ -86,7 +86,7 @@ class Weights:
 # --------------------------------------------------------------------------------------
 def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, y=None, y_pre=None,
          res: Sequence = (), pre_in=None, part=None, lr=None, scale=0, clamp=0, hr=None, dout=None,
-         l1_scale=0.0, loss_part=None) -> None:
+         l1_scale=0.0, loss_part=None, debug=0) -> None:
     d = L.ConvDesc()
     d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = ctx.code, B, H, W, Cin, Cout
     d.x, d.w, d.bias = ptr(x), ptr(wpk), ptr(bias)
@@ -97,6 +97,7 @@ def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, 
     d.pre_in, d.part = ptr(pre_in), ptr(part)
     d.lr, d.scale, d.clamp, d.hr, d.dout = ptr(lr), scale, clamp, ptr(hr), ptr(dout)
     d.l1_scale, d.loss_part = float(l1_scale), ptr(loss_part)
+    d.debug = debug
     ctx.emit("conv3x3", ctx.lib.fen_conv3x3, byref(d))
 
 

@@ -30,29 +30,37 @@ ctx.emit("pack", ctx.lib.fen_pack_conv_w, ctx.code, 0, C, C, ptr(w), ptr(wp))
 bias = torch.zeros(C, device="cuda")
 alpha = torch.full((C,), 0.25, device="cuda")
 y = torch.empty_like(x)
-nblk = 4096
-st = torch.zeros(nblk * 32, dtype=torch.int64, device="cuda")
+nblk = 1024
+st = torch.zeros(nblk * 8 * 32, dtype=torch.int64, device="cuda")
 epi = int(os.environ.get("EPI", str(L.EPI_PRELU)))
 for _ in range(int(os.environ.get("REPS", "30"))):
     st.zero_()
-    net.conv(ctx, x, wp, B, H, W, C, C, bias=bias, epi=epi, alpha=alpha, y=y, loss_part=st)
+    net.conv(ctx, x, wp, B, H, W, C, C, bias=bias, epi=epi, alpha=alpha, y=y, loss_part=st,
+             debug=int(os.environ.get("DEBUG", "0")))
 torch.cuda.synchronize()
-a = st.view(nblk, 16, 2).cpu().numpy().astype(np.int64)
-used = a[:, 0, 0] != 0
-a = a[used]
-rt, mt = a[:, :, 0], a[:, :, 1]
-t0 = rt[:, 0].min()
-out = {"blocks": int(used.sum())}
-names = ["start", "prologue"] + [f"t{k}_{p}" for k in range(5) for p in ("mfma", "epi", "bar")]
-for i, nm in enumerate(names[:16]):
-    valid = rt[:, i] != 0
+a = st.view(nblk, 8, 16, 2).cpu().numpy().astype(np.int64)
+used = a[:, 0, 0, 0] != 0
+a = a[used]                      # [blk, wave, stamp, (rt, mt)]
+nw = int((a[0, :, 0, 0] != 0).sum())
+a = a[:, :nw]
+rt = a[..., 0]
+t0 = rt[:, :, 0].min()
+# slot -> label: 0 start, 1 end of start-up, 2+3k / 3+3k / 4+3k: tile k after MFMAs / after
+# epilogue / after the closing barrier; 13, 14: q-kernel start-up (DMA issued, DMA landed)
+labels = {0: "start", 1: "startup", 13: "dma_issued", 14: "dma_landed"}
+for k in range(4):
+    labels.update({2 + 3 * k: f"t{k}_mfma", 3 + 3 * k: f"t{k}_epi", 4 + 3 * k: f"t{k}_bar"})
+out = {"blocks": int(used.sum()), "waves": nw}
+for i in sorted(labels):
+    valid = (rt[:, :, i] != 0).all(axis=1)
     if not valid.any():
         continue
-    out[nm + "_us"] = round(float(np.median(rt[valid, i] - t0)) / 100.0, 2)
-    if i:
-        prev = i - 1
-        v2 = valid & (mt[:, prev] != 0)
-        out[nm + "_cyc"] = int(np.median(mt[v2, i] - mt[v2, prev]))
+    r = (rt[valid, :, i] - t0) / 100.0          # us since the first start, per wave
+    out[labels[i]] = [round(float(np.median(r.min(1))), 2), round(float(np.median(r.max(1))), 2)]
+mt = a[..., 1]
+valid = (rt[:, :, 1] != 0).all(axis=1) & (rt[:, :, 2] != 0).all(axis=1)
+dm = (mt[valid, :, 2] - mt[valid, :, 1]).astype(np.float64)
+dr = (rt[valid, :, 2] - rt[valid, :, 1]).astype(np.float64)
+out["t0_mfma_GHz"] = round(float(np.median(dm / np.maximum(dr, 1))) * 0.1, 3)
 out["end_max_us"] = round(float((rt.max() - t0)) / 100.0, 2)
-out["start_spread_us"] = round(float(rt[:, 0].max() - t0) / 100.0, 2)
 print(json.dumps(out))
