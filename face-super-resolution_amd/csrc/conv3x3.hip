@@ -27,58 +27,6 @@
 
 namespace {
 
-constexpr int HALO = 18;
-constexpr int HP = HALO * HALO;        // 324 halo pixels
-constexpr int HALO_BYTES = HP * 128;   // 41472
-constexpr int HALO_DMA = (HP * 8 + 63) / 64;   // 41 wave-wide 1-KiB LDS-DMA pieces per halo
-constexpr int HALO_SLOT = HALO_DMA * 1024;     // 41984: halo + slack for the last piece
-
-typedef __attribute__((address_space(3))) void lds_void;
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-// Halo images (18 x 18 pixels, 128-B rows): 16-B chunk c of pixel p sits at chunk c ^ (col & 7),
-// col = p % 18.  Fragment reads touch 16 consecutive columns of one halo row at the same
-// logical chunk -> 16 distinct 16-B bank slots (conflict-free ds_read_b128), and because the
-// key depends only on the column, every read of a lane is base(kw, kk) + row * 2304.
-__device__ __forceinline__ int hswz(int p, int chunk) {
-    return (p << 7) + ((chunk ^ ((p % HALO) & 7)) << 4);
-}
-__device__ __forceinline__ int hcol(int col, int chunk) {   // offset of (column col, chunk) in a row
-    return (col << 7) + ((chunk ^ (col & 7)) << 4);
-}
-
-// Buffer resource (V#) words for a raw byte buffer: base, stride 0, num_records = bytes.
-// Loads at voffset >= bytes return 0 -- used for the conv's zero padding.
-__device__ __forceinline__ i32x4 make_rsrc(const void* base, unsigned bytes) {
-    const unsigned long long a = (unsigned long long)base;
-    i32x4 r;
-    r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
-    r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32) & 0xffff);
-    r.z = __builtin_amdgcn_readfirstlane((int)bytes);
-    r.w = 0x00020000;
-    return r;
-}
-
-// 16 B per lane global -> LDS (buffer_load_dwordx4 ... lds) written to lds_base + lane*16.
-// Issued from inline asm on purpose: hipcc then does not see an LDS write in flight, so it
-// does not drain vmcnt before every ds_read of the *other* halo buffer.  The caller waits
-// (s_waitcnt vmcnt(0)) and barriers before reading the destination.
-__device__ __forceinline__ void dma16(const i32x4& rsrc, unsigned lds_base, int voff) {
-    unsigned keep;  // M0 is compiler-reserved: save and restore it inside the statement
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(lds_base), "v"(voff), "s"(rsrc)
-        : "memory");
-}
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-    return (unsigned)(size_t)(const lds_void*)p;
-}
-
 // Diagnostic build only (-DFEN_STAMPS, tools/stamp_conv.py): per-block s_memrealtime /
 // s_memtime stamps of the persistent kernel's phases into d.loss_part (unused by the
 // forward epilogues), [block][wave][16 stamps][realtime, memtime] u64.  In the real build no stamp executes.

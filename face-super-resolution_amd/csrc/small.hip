@@ -560,9 +560,85 @@ __global__ void k_nhwc_to_nchw(int B, int C, int H, int W, const T* __restrict__
 }
 
 template <typename T>
-__global__ void k_pack(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out, size_t n) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__global__ void k_pack(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out, size_t n);
+
+// Column sums out[c] (+)= scale * sum_r part[r][c], several independent jobs per launch
+// (the per-block PReLU dalpha / SE weight-gradient partials of a whole residual group).
+// Block = 1024 threads = 16 row-waves x 64 columns, 4 independent accumulators per lane,
+// fixed-order combine in LDS (bitwise reproducible).  cols == 1 (the loss) sums rows across
+// all 1024 threads instead.
+struct ColJobK {
+    const float* part;
+    float* out;
+    int rows, cols;
+    float scale;
+    int accumulate;
+    int blk0;   // first block of this job
+};
+constexpr int COLSUM_MAXJ = 40;
+struct ColJobs {
+    int n;
+    ColJobK j[COLSUM_MAXJ];
+};
+
+__global__ __launch_bounds__(1024) void k_colsum_multi(const ColJobs jobs) {
+    __shared__ float red[16][64];
+    int ji = 0;
+    while (ji + 1 < jobs.n && (int)blockIdx.x >= jobs.j[ji + 1].blk0) ++ji;
+    const ColJobK& jb = jobs.j[ji];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rows = jb.rows, cols = jb.cols;
+    if (cols == 1) {
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int r = tid;
+        for (; r + 3 * 1024 < rows; r += 4 * 1024) {
+            a0 += jb.part[r]; a1 += jb.part[r + 1024]; a2 += jb.part[r + 2048]; a3 += jb.part[r + 3072];
+        }
+        for (; r < rows; r += 1024) a0 += jb.part[r];
+        const float v = wave_sum((a0 + a1) + (a2 + a3));
+        if (lane == 0) red[0][w] = v;
+        __syncthreads();
+        if (tid == 0) {
+            float t = 0.f;
+            for (int k = 0; k < 16; ++k) t += red[0][k];
+            t *= jb.scale;
+            jb.out[0] = jb.accumulate ? jb.out[0] + t : t;
+        }
+        return;
+    }
+    const int c = ((int)blockIdx.x - jb.blk0) * 64 + lane;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (c < cols) {
+        const float* p = jb.part + c;
+        int r = w;
+        for (; r + 48 < rows; r += 64) {
+            a0 += p[(size_t)r * cols];
+            a1 += p[(size_t)(r + 16) * cols];
+            a2 += p[(size_t)(r + 32) * cols];
+            a3 += p[(size_t)(r + 48) * cols];
+        }
+        for (; r < rows; r += 16) a0 += p[(size_t)r * cols];
+    }
+    red[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (w == 0 && c < cols) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t += red[k][lane];
+        t *= jb.scale;
+        jb.out[c] = jb.accumulate ? jb.out[c] + t : t;
+    }
+}
+
+// Pack many conv weights in one launch: job k covers packed elements [e0[k], e0[k+1]).
+struct PackJobK {
+    const float* w;
+    void* out;
+    int mode, Cout, Cin;
+};
+template <typename T>
+__device__ __forceinline__ void pack_one(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out,
+                                         size_t i) {
     if (mode == 2) {  // [9][Cin_pad][Cout], row = ci, taps flipped
         const int co = (int)(i % Cout);
         const int ci = (int)((i / Cout) % ((Cin + 15) & ~15));
@@ -579,28 +655,23 @@ __global__ void k_pack(int mode, int Cout, int Cin, const float* __restrict__ w,
         out[i] = fromf<T>(cp < Cout ? w[(((size_t)co * Cin + ci) * 3 + tap / 3) * 3 + tap % 3] : 0.f);
     }
 }
-
-// ------------------------------ reductions / optimizer ------------------------------
-// stage 1: block (cb, rb) sums rows [rb*RB, rb*RB+RB) of 64 columns into row rb*RB (in place)
-constexpr int COLSUM_RB = 256;
-__global__ void k_colsum1(int rows, int cols, float* part) {
-    __shared__ float red[4][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
-    const int r0 = blockIdx.y * COLSUM_RB, r1 = min(r0 + COLSUM_RB, rows);
-    float s = 0.f;
-    if (c < cols)
-        for (int r = r0 + g; r < r1; r += 4) s += part[(size_t)r * cols + c];
-    red[g][threadIdx.x & 63] = s;
-    __syncthreads();
-    if (g == 0 && c < cols) part[(size_t)r0 * cols + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+template <typename T>
+__global__ void k_pack(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) pack_one<T>(mode, Cout, Cin, w, out, i);
 }
-__global__ void k_colsum2(int rows, int cols, const float* part, float scale, float* out, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= cols) return;
-    float s = 0.f;
-    for (int r = 0; r < rows; r += COLSUM_RB) s += part[(size_t)r * cols + c];
-    s *= scale;
-    out[c] = accumulate ? out[c] + s : s;
+template <typename T>
+__global__ void k_pack_multi(int njobs, const PackJobK* __restrict__ jobs, const unsigned long long* __restrict__ e0,
+                             unsigned long long total) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int lo = 0, hi = njobs - 1;   // last job with e0 <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (e0[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const PackJobK jb = jobs[lo];
+    pack_one<T>(jb.mode, jb.Cout, jb.Cin, jb.w, (T*)jb.out, (size_t)(i - e0[lo]));
 }
 
 constexpr int SUMSQ_BLOCKS_MAX = 1024;
@@ -827,17 +898,26 @@ extern "C" int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, fl
     return FEN_OK;
 }
 
-extern "C" int fen_colsum(int rows, int cols, const float* part, float scale, float* out, int accumulate,
-                          void* stream) {
-    if (!part || !out || rows <= 0 || cols <= 0) return FEN_EINVAL;
-    float* p = const_cast<float*>(part);  // stage 1 reduces in place (documented: part is clobbered)
-    hipLaunchKernelGGL(k_colsum1, dim3((cols + 63) / 64, (rows + COLSUM_RB - 1) / COLSUM_RB), dim3(256), 0, STREAM,
-                       rows, cols, p);
-    FEN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_colsum2, dim3(nblk(cols)), dim3(256), 0, STREAM, rows, cols, (const float*)p, scale, out,
-                       accumulate);
+extern "C" int fen_colsum_multi(int njobs, const fen_colsum_job* jobs, void* stream) {
+    if (njobs <= 0 || njobs > COLSUM_MAXJ || !jobs) return FEN_EINVAL;
+    ColJobs k;
+    k.n = njobs;
+    int blk = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const fen_colsum_job& j = jobs[i];
+        if (!j.part || !j.out || j.rows <= 0 || j.cols <= 0) return FEN_EINVAL;
+        k.j[i] = ColJobK{j.part, j.out, j.rows, j.cols, j.scale, j.accumulate, blk};
+        blk += j.cols == 1 ? 1 : (j.cols + 63) / 64;
+    }
+    hipLaunchKernelGGL(k_colsum_multi, dim3(blk), dim3(1024), 0, STREAM, k);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
+}
+
+extern "C" int fen_colsum(int rows, int cols, const float* part, float scale, float* out, int accumulate,
+                          void* stream) {
+    const fen_colsum_job j{part, out, rows, cols, scale, accumulate};
+    return fen_colsum_multi(1, &j, stream);
 }
 
 extern "C" size_t fen_packed_elems(int mode, int Cout, int Cin) {
@@ -852,6 +932,42 @@ extern "C" int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const flo
         hipLaunchKernelGGL(k_pack<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, mode, Cout, Cin, w, (bf16*)out, n);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_pack<float>, dim3(nblk(n)), dim3(256), 0, STREAM, mode, Cout, Cin, w, (float*)out, n);
+    else
+        return FEN_EINVAL;
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" size_t fen_pack_table_bytes(int njobs) {
+    return (size_t)njobs * (sizeof(PackJobK) + sizeof(unsigned long long)) + sizeof(unsigned long long);
+}
+
+extern "C" int fen_pack_table(int dtype, int njobs, const fen_pack_job* jobs, void* table_host, size_t* total) {
+    if (njobs <= 0 || !jobs || !table_host || !total || (dtype != FEN_BF16 && dtype != FEN_F32)) return FEN_EINVAL;
+    PackJobK* pj = (PackJobK*)table_host;
+    unsigned long long* e0 = (unsigned long long*)(pj + njobs);
+    unsigned long long acc = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const fen_pack_job& j = jobs[i];
+        if (!j.w || !j.out || j.mode < 0 || j.mode > 2 || (j.mode == 1 && j.Cout % 4)) return FEN_EINVAL;
+        pj[i] = PackJobK{j.w, j.out, j.mode, j.Cout, j.Cin};
+        e0[i] = acc;
+        acc += fen_packed_elems(j.mode, j.Cout, j.Cin);
+    }
+    e0[njobs] = acc;
+    *total = (size_t)acc;
+    return FEN_OK;
+}
+
+extern "C" int fen_pack_multi(int dtype, int njobs, const void* table_dev, size_t total, void* stream) {
+    if (njobs <= 0 || !table_dev || total == 0) return FEN_EINVAL;
+    const PackJobK* pj = (const PackJobK*)table_dev;
+    const unsigned long long* e0 = (const unsigned long long*)(pj + njobs);
+    const unsigned nb = (unsigned)((total + 255) / 256);
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_pack_multi<bf16>, dim3(nb), dim3(256), 0, STREAM, njobs, pj, e0, (unsigned long long)total);
+    else if (dtype == FEN_F32)
+        hipLaunchKernelGGL(k_pack_multi<float>, dim3(nb), dim3(256), 0, STREAM, njobs, pj, e0, (unsigned long long)total);
     else
         return FEN_EINVAL;
     FEN_CHECK_LAUNCH();

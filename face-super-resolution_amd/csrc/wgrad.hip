@@ -16,8 +16,6 @@
 
 namespace {
 
-constexpr int HALO = 18;
-constexpr int HP = HALO * HALO;
 constexpr int PANEL_HALO = HP * 128;   // 41472 B
 constexpr int PANEL_TILE = 256 * 128;  // 32768 B
 
@@ -211,6 +209,228 @@ __global__ __launch_bounds__(256) void k_wgrad_finalize(int nchunk, int Cout, in
     }
 }
 
+
+// ------------------------------------------------------------------------------------
+// k_wgrad_p: bf16, Cout % 64 == 0, Cin % 64 == 0 -- the network's 64-channel wgrads.
+// One 512-thread block per CU walks a contiguous chunk of 16x16-pixel tiles.  Per tile the
+// 18x18 input halo (64 ci from ci0) and the 16x16 dy tile (64 co from co0) are streamed by
+// LDS-DMA into one of two slots while the MFMAs run on the other.  8 waves = 2 co halves x
+// 4 ci quarters; every wave accumulates 32 co x (9 taps x 16 ci) in registers (18 16x16
+// accumulators), K = pixels, fragments read with ds_read_b64_tr_b16.  Both LDS images key
+// their 16-B chunk positions by bits 1 and 3 of the pixel column (wkey), which makes every
+// transposed fragment read bank-conflict free.  The bias gradient rides along as MFMAs
+// against a ones fragment, spread over the 4 ci-quarter waves (2 of the 8 k-steps each).
+// One fp32 slab per block in OIHW order [Cout][Cin][3][3] + [Cout] (bias); a second
+// launch sums the slabs in fixed order (bitwise reproducible).
+// ------------------------------------------------------------------------------------
+constexpr int WG_TILE = 256 * 128;             // dy tile image, 32 KB
+constexpr int WG_TILE_DMA = WG_TILE / 1024;    // 32 pieces
+constexpr int WG_SLOT = HALO_SLOT + WG_TILE;   // 74752 B per slot, 2 slots
+
+__device__ __forceinline__ int wkey(int col) { return (((col >> 1) & 1) << 1) | (((col >> 3) & 1) << 2); }
+
+__global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int tpc, float* part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ch = wave & 1, cq = wave >> 1;
+    const int q = lane >> 4, c16 = lane & 15, qq = c16 >> 2, pp = c16 & 3;
+    const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int ntiles = d.B * tpi;
+    const int co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64;
+    const int t_begin = blockIdx.x * tpc, t_end = min(t_begin + tpc, ntiles);
+    const i32x4 xr = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * Cin * 2));
+    const i32x4 yr = make_rsrc(d.dy, (unsigned)((size_t)d.B * H * W * Cout * 2));
+
+    // every wave issues its share of the tile's 41 halo + 32 dy pieces
+    auto issue = [&](int t, const char* slot) {
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const unsigned hbase = lds_addr(slot), ybase = lds_addr(slot + HALO_SLOT);
+        for (int i = wave; i < HALO_DMA + WG_TILE_DMA; i += 8) {
+            if (i < HALO_DMA) {
+                const int s = i * 64 + lane, p = s >> 3, pos = s & 7;
+                const int hr = p / HALO, hc = p - hr * HALO;
+                const int c = pos ^ wkey(hc);
+                const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+                const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+                const int voff = in ? (((b * H + gh) * W + gw) * Cin + ci0 + c * 8) * 2 : 0x7ffffff0;
+                dma16(xr, __builtin_amdgcn_readfirstlane(hbase + i * 1024), voff);
+            } else {
+                const int j = i - HALO_DMA;
+                const int s = j * 64 + lane, p = s >> 3, pos = s & 7;
+                const int c = pos ^ wkey(p & 15);
+                const int gh = h0 + (p >> 4), gw = w0 + (p & 15);
+                const bool in = gh < H && gw < W;
+                const int voff = in ? (((b * H + gh) * W + gw) * Cout + co0 + c * 8) * 2 : 0x7ffffff0;
+                dma16(yr, __builtin_amdgcn_readfirstlane(ybase + j * 1024), voff);
+            }
+        }
+    };
+
+    // per-lane fragment offsets (see k_wgrad for the transposed-read lane mapping): lane
+    // (q, qq, pp) of half h reads pixel k = 8q + 4h + qq of the 32-pixel k-step, 4 channels
+    // from 4*pp.  A (dy): + s*4096; B (halo, tap kh,kw): + (2s + kh) * 2304.
+    int offA[2][2], offB[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int k = 8 * q + 4 * h + qq, r = k >> 4, pc = k & 15;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const int c = ch * 32 + m * 16 + 4 * pp;
+            offA[h][m] = (r * 16 + pc) * 128 + (((c >> 3) ^ wkey(pc)) << 4) + (c & 7) * 2;
+        }
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const int c = cq * 16 + 4 * pp, hc = pc + kw;
+            offB[h][kw] = (r * HALO + hc) * 128 + (((c >> 3) ^ wkey(hc)) << 4) + (c & 7) * 2;
+        }
+    }
+
+    f32x4 acc[2][9], accb[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        accb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+
+    if (t_begin < t_end) issue(t_begin, smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int k = 0, t = t_begin; t < t_end; ++k, ++t) {
+        const char* cur = smem + (k & 1) * WG_SLOT;
+        if (t + 1 < t_end) issue(t + 1, smem + ((k + 1) & 1) * WG_SLOT);
+        const char* hx = cur;
+        const char* ty = cur + HALO_SLOT;
+        uint4 A0[2], B0[9], A1[2], B1[9];
+        auto load = [&](int s, uint4 (&A)[2], uint4 (&Bf)[9]) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(ty + offA[h][m] + s * 4096));
+                    const uint2 u = __builtin_bit_cast(uint2, v);
+                    if (h == 0) { A[m].x = u.x; A[m].y = u.y; } else { A[m].z = u.x; A[m].w = u.y; }
+                }
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    const int kh = tap / 3, kw = tap % 3;
+                    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(hx + offB[h][kw] + (2 * s + kh) * (HALO * 128)));
+                    const uint2 u = __builtin_bit_cast(uint2, v);
+                    if (h == 0) { Bf[tap].x = u.x; Bf[tap].y = u.y; } else { Bf[tap].z = u.x; Bf[tap].w = u.y; }
+                }
+            }
+        };
+        auto mma = [&](int s, const uint4 (&A)[2], const uint4 (&Bf)[9]) {
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+                for (int m = 0; m < 2; ++m) mma16<bf16>(acc[m][tap], A[m], Bf[tap]);
+            if ((s & 3) == cq) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) mma16<bf16>(accb[m], A[m], ones);
+            }
+        };
+        load(0, A0, B0);
+#pragma unroll
+        for (int s = 0; s < 8; s += 2) {
+            load(s + 1, A1, B1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(s, A0, B0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (s + 2 < 8) load(s + 2, A0, B0);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(s + 1, A1, B1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile's pieces landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                         // ... for everyone; cur is free
+    }
+
+    // slab: OIHW [Cout][Cin][9] then [Cout] bias partials (ci0 == 0 blocks only)
+    float* slab = part + (size_t)blockIdx.x * ((size_t)Cout * Cin * 9 + Cout);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = co0 + ch * 32 + m * 16 + 4 * q + r, ci = ci0 + cq * 16 + c16;
+            float* o = slab + ((size_t)co * Cin + ci) * 9;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) o[tap] = acc[m][tap][r];
+        }
+    if (ci0 == 0) {
+        float* red = (float*)smem;   // [4 cq][64 co]; no DMA in flight, last barrier passed
+        if (c16 == 0) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[cq * 64 + ch * 32 + m * 16 + 4 * q + r] = accb[m][r];
+        }
+        __syncthreads();
+        if (tid < 64)
+            slab[(size_t)Cout * Cin * 9 + co0 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+    }
+}
+
+// dw (+)= sum_chunk slab[chunk][0 .. cout_valid*Cin*9), db (+)= sum_chunk slab[chunk][Cout*Cin*9 + co]:
+// column j (float4) per lane, the 8 waves split the chunks, fixed-order combine in LDS.
+__global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int nw4, int nb, int boff4,
+                                                   const float4* __restrict__ part, float* dw, float* db,
+                                                   int accumulate) {
+    __shared__ float4 red[8][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + lane;
+    const int nb4 = (nb + 3) / 4;
+    const bool isw = j < nw4, isb = !isw && j < nw4 + nb4;
+    const int col = isw ? j : boff4 + (j - nw4);
+    const int c0 = (nchunk * w) / 8, c1 = (nchunk * (w + 1)) / 8;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+    if (isw || isb) {
+        const float4* p = part + col;
+        int c = c0;
+        for (; c + 3 < c1; c += 4) {
+            const float4 a = p[(size_t)c * stride4], b = p[(size_t)(c + 1) * stride4];
+            const float4 e = p[(size_t)(c + 2) * stride4], f = p[(size_t)(c + 3) * stride4];
+            s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+            s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+            s2.x += e.x; s2.y += e.y; s2.z += e.z; s2.w += e.w;
+            s3.x += f.x; s3.y += f.y; s3.z += f.z; s3.w += f.w;
+        }
+        for (; c < c1; ++c) {
+            const float4 a = p[(size_t)c * stride4];
+            s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+        }
+    }
+    red[w][lane] = make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
+                               (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w));
+    __syncthreads();
+    if (w == 0 && (isw || isb)) {
+        float4 t = red[0][lane];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            const float4 a = red[k][lane];
+            t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+        }
+        const float v[4] = {t.x, t.y, t.z, t.w};
+        if (isw) {
+            float* o = dw + (size_t)j * 4;   // scalar stores: dw views need not be 16-B aligned
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = accumulate ? o[e] + v[e] : v[e];
+        } else if (db) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int co = (j - nw4) * 4 + e;
+                if (co < nb) db[co] = accumulate ? db[co] + v[e] : v[e];
+            }
+        }
+    }
+}
+
 int wgrad_geom(const fen_wgrad_desc* d, int* nchunk, int* tpc, int* cot) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int ntiles = d->B * tpi;
@@ -223,12 +443,20 @@ int wgrad_geom(const fen_wgrad_desc* d, int* nchunk, int* tpc, int* cot) {
     return FEN_OK;
 }
 
+// the persistent kernel: bf16, 64-multiple channel counts, 32-bit buffer offsets
+bool wgrad_use_p(const fen_wgrad_desc* d) {
+    const size_t xb = (size_t)d->B * d->H * d->W * d->Cin * 2, yb = (size_t)d->B * d->H * d->W * d->Cout * 2;
+    return d->dtype == FEN_BF16 && d->Cout % 64 == 0 && d->Cin % 64 == 0 && xb < 0x7fff0000u &&
+           yb < 0x7fff0000u && getenv("FEN_WGRAD_OLD") == nullptr;
+}
+
 }  // namespace
 
 extern "C" size_t fen_wgrad_work_floats(const fen_wgrad_desc* d) {
     if (!d || d->B <= 0 || d->Cin <= 0 || d->Cout <= 0) return 0;
     int nchunk, tpc, cot;
     wgrad_geom(d, &nchunk, &tpc, &cot);
+    if (wgrad_use_p(d)) return (size_t)nchunk * ((size_t)d->Cout * d->Cin * 9 + d->Cout);
     return (size_t)nchunk * 9 * d->Cout * d->Cin + (size_t)nchunk * d->Cout;
 }
 
@@ -241,6 +469,24 @@ extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
     int nchunk, tpc, cot;
     wgrad_geom(d, &nchunk, &tpc, &cot);
     hipStream_t s = (hipStream_t)stream;
+    if (wgrad_use_p(d)) {
+        static bool attr = false;
+        const size_t lds = 2 * WG_SLOT;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)k_wgrad_p, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_wgrad_p, dim3(nchunk, d->Cout / 64, d->Cin / 64), dim3(512), lds, s, *d, tpc, d->work);
+        FEN_CHECK_LAUNCH();
+        const int stride4 = (d->Cout * d->Cin * 9 + d->Cout) / 4;
+        const int nw4 = d->cout_valid * d->Cin * 9 / 4;
+        const int boff4 = d->Cout * d->Cin * 9 / 4;
+        const int ncol = nw4 + (d->cout_valid + 3) / 4;
+        hipLaunchKernelGGL(k_wgrad_fin, dim3((ncol + 63) / 64), dim3(512), 0, s, nchunk, stride4, nw4, d->cout_valid,
+                           boff4, (const float4*)d->work, d->dw, d->db, d->accumulate);
+        FEN_CHECK_LAUNCH();
+        return FEN_OK;
+    }
     float* part = d->work;
     float* dbpart = d->work + (size_t)nchunk * 9 * d->Cout * d->Cin;
     dim3 grid(nchunk, d->Cout / cot, d->Cin / 64);

@@ -46,8 +46,7 @@ class LiveWeights(Weights):
         stamp = (w.data_ptr(), w._version)
         k = (key, mode)
         if k in self.packs and self._stamp.get(k) != stamp:
-            del self.packs[k]
-            self.pack_ctx = Ctx(self.dtype, self.device, record=True)  # stale program; rebuilt lazily
+            del self.packs[k]   # stale copy: re-packed (and the multi-pack table rebuilt) below
         buf = super().packed(key, mode)
         self._stamp[k] = stamp
         return buf

@@ -34,6 +34,15 @@ class ConvDesc(Structure):
     ]
 
 
+class ColsumJob(Structure):
+    _fields_ = [("part", c_void_p), ("out", c_void_p), ("rows", c_int), ("cols", c_int), ("scale", c_float),
+                ("accumulate", c_int)]
+
+
+class PackJob(Structure):
+    _fields_ = [("w", c_void_p), ("out", c_void_p), ("mode", c_int), ("Cout", c_int), ("Cin", c_int)]
+
+
 class WgradDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
@@ -60,7 +69,11 @@ _SIGS = {
     "fen_se_bwd_apply": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
     "fen_bicubic_down4": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_void_p]),
     "fen_colsum": (c_int, [c_int, c_int, c_void_p, c_float, c_void_p, c_int, c_void_p]),
+    "fen_colsum_multi": (c_int, [c_int, c_void_p, c_void_p]),
     "fen_pack_conv_w": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_void_p]),
+    "fen_pack_table_bytes": (c_size_t, [c_int]),
+    "fen_pack_table": (c_int, [c_int, c_int, c_void_p, c_void_p, POINTER(c_size_t)]),
+    "fen_pack_multi": (c_int, [c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "fen_packed_elems": (c_size_t, [c_int] * 3),
     "fen_nchw_to_nhwc": (c_int, [c_int] * 6 + [c_void_p, c_void_p, c_void_p]),
     "fen_prelu_bwd_unshuffle": (c_int, [c_int] * 5 + [c_void_p] * 5 + [c_void_p]),

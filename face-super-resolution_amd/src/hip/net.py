@@ -15,6 +15,7 @@ and their autograd backward (trainer.py:482-485).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
@@ -53,7 +54,8 @@ def tiles(H: int, W: int) -> int:
 
 
 class Weights:
-    """fp32 parameters (by state_dict key) + their packed kernel-layout copies."""
+    """fp32 parameters (by state_dict key) + their packed kernel-layout copies.  `pack()`
+    refreshes every packed copy in ONE launch (fen_pack_multi over a device job table)."""
 
     def __init__(self, params: Dict[str, torch.Tensor], dtype: torch.dtype, device):
         self.p = params
@@ -61,6 +63,9 @@ class Weights:
         self.device = device
         self.packs: Dict[tuple, torch.Tensor] = {}
         self.pack_ctx = Ctx(dtype, device, record=True)
+        self._src: Dict[tuple, torch.Tensor] = {}
+        self._table = None        # (device job table, njobs, total elements)
+        self._dirty = True
 
     def packed(self, key: str, mode: int) -> torch.Tensor:
         k = (key, mode)
@@ -71,14 +76,38 @@ class Weights:
             n = lib.fen_packed_elems(mode, cout, cin)
             buf = torch.empty(n, dtype=self.dtype, device=self.device)
             args = (L.dtype_code(self.dtype), mode, cout, cin, ptr(w), ptr(buf))
-            self.pack_ctx.emit("pack_conv_w", lib.fen_pack_conv_w, *args)
-            # pack now too, so a buffer is valid from the moment a builder sees it
+            # pack now, so a buffer is valid from the moment a builder sees it
             L.check(lib.fen_pack_conv_w(*args, torch.cuda.current_stream().cuda_stream), "pack_conv_w")
             self.packs[k] = buf
+            self._src[k] = w
+            self._dirty = True
         return self.packs[k]
 
+    def _build_table(self) -> None:
+        lib = self.pack_ctx.lib
+        keys = list(self.packs)
+        jobs = (L.PackJob * len(keys))()
+        for i, k in enumerate(keys):
+            w = self._src[k]
+            jobs[i].w, jobs[i].out = ptr(w), ptr(self.packs[k])
+            jobs[i].mode, jobs[i].Cout, jobs[i].Cin = k[1], int(w.shape[0]), int(w.shape[1])
+        nbytes = lib.fen_pack_table_bytes(len(keys))
+        host = (ctypes.c_uint8 * nbytes)()
+        total = ctypes.c_size_t(0)
+        L.check(lib.fen_pack_table(L.dtype_code(self.dtype), len(keys), ctypes.cast(jobs, ctypes.c_void_p),
+                                   ctypes.cast(host, ctypes.c_void_p), ctypes.byref(total)), "pack_table")
+        dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(self.device)
+        self._table = (dev, len(keys), int(total.value))
+        self._dirty = False
+
     def pack(self) -> None:
-        self.pack_ctx.run()
+        if not self.packs:
+            return
+        if self._dirty:
+            self._build_table()
+        dev, nj, total = self._table
+        L.check(self.pack_ctx.lib.fen_pack_multi(L.dtype_code(self.dtype), nj, dev.data_ptr(), total,
+                                                 torch.cuda.current_stream().cuda_stream), "pack_multi")
 
 
 # --------------------------------------------------------------------------------------
@@ -114,6 +143,33 @@ def wgrad(ctx: Ctx, x, dy, B, H, W, Cin, Cout, dw, db, cout_valid=None) -> None:
 
 def colsum(ctx: Ctx, part, rows, cols, out, scale=1.0) -> None:
     ctx.emit("colsum", ctx.lib.fen_colsum, rows, cols, ptr(part), float(scale), ptr(out), 0)
+
+
+class ColsumBatch:
+    """Column sums queued by a backward builder and issued as ONE fen_colsum_multi launch
+    (each job keeps its own partial buffer until the flush)."""
+
+    MAX = 40
+
+    def __init__(self, ctx: Ctx):
+        self.ctx = ctx
+        self.jobs: List[tuple] = []
+
+    def add(self, part, rows, cols, out, scale=1.0) -> None:
+        self.jobs.append((part, int(rows), int(cols), out, float(scale)))
+        if len(self.jobs) == self.MAX:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.jobs:
+            return
+        arr = (L.ColsumJob * len(self.jobs))()
+        for i, (part, rows, cols, out, scale) in enumerate(self.jobs):
+            arr[i].part, arr[i].out, arr[i].rows, arr[i].cols = ptr(part), ptr(out), rows, cols
+            arr[i].scale, arr[i].accumulate = scale, 0
+        self.ctx.emit("colsum_multi", self.ctx.lib.fen_colsum_multi, len(self.jobs), ctypes.cast(arr, ctypes.c_void_p))
+        self.ctx.keep(arr)
+        self.jobs = []
 
 
 # --------------------------------------------------------------------------------------
@@ -222,11 +278,15 @@ class Backward:
 
     def __init__(self, spec: NetSpec, ctx: Ctx, Wt: Weights, G: Dict[str, torch.Tensor]):
         self.s, self.ctx, self.Wt, self.G = spec, ctx, Wt, G
+        self.cs = ColsumBatch(ctx)   # flushed at the end of every group / the tail
 
     def _wg(self, key, x, dy, B, H, W, Cin, Cout, cout_valid=None):
         wgrad(self.ctx, x, dy, B, H, W, Cin, Cout, self.G[key + ".weight"], self.G.get(key + ".bias"), cout_valid)
 
-    def rcab(self, sv: dict, dy: torch.Tensor, pre: str, extra_res: Sequence = (), dx_out=None) -> torch.Tensor:
+    def rcab(self, sv: dict, dy: torch.Tensor, pre: str, extra_res: Sequence = (), dx_out=None,
+             flush: bool = True) -> torch.Tensor:
+        """RCAB backward; its PReLU / SE weight-gradient column sums are queued on self.cs and
+        issued at the end (flush=True) or by the caller (group() batches a whole group)."""
         s, ctx, Wt, p, G = self.s, self.ctx, self.Wt, self.Wt.p, self.G
         B, H, W, C = dy.shape
         HW = H * W
@@ -234,27 +294,29 @@ class Backward:
         part = ctx.scratch("bw_pool", (B * npart, C), torch.float32)
         ctx.emit("pool_dot", ctx.lib.fen_pool_dot, ctx.code, B, HW, C, ptr(dy), ptr(sv["t"]), ptr(part))
         g = ctx.scratch("bw_g", (B, C), torch.float32)
-        dw1p = ctx.scratch("bw_dw1p", (B, s.Cr * C), torch.float32)
-        dw2p = ctx.scratch("bw_dw2p", (B, s.Cr * C), torch.float32)
+        dw1p = ctx.scratch("bw_dw1p" + pre, (B, s.Cr * C), torch.float32)
+        dw2p = ctx.scratch("bw_dw2p" + pre, (B, s.Cr * C), torch.float32)
         ca = pre + "channel_attention.fc."
         ctx.emit("se_bwd", ctx.lib.fen_se_bwd, B, C, s.Cr, npart, 1.0 / HW, s.res_scale, ptr(part), ptr(sv["mean"]),
                  ptr(sv["hid"]), ptr(sv["s"]), ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]), ptr(g), ptr(dw1p),
                  ptr(dw2p))
-        colsum(ctx, dw1p, B, s.Cr * C, G[ca + "0.weight"])
-        colsum(ctx, dw2p, B, s.Cr * C, G[ca + "2.weight"])
+        self.cs.add(dw1p, B, s.Cr * C, G[ca + "0.weight"])
+        self.cs.add(dw2p, B, s.Cr * C, G[ca + "2.weight"])
         dt = ctx.scratch("bw_dt", dy.shape)
         ctx.emit("se_bwd_apply", ctx.lib.fen_se_bwd_apply, ctx.code, B, HW, C, ptr(dy), ptr(sv["s"]), s.res_scale,
                  ptr(g), ptr(dt))
         self._wg(pre + "conv2", sv["a1"], dt, B, H, W, C, C)
         dz1 = ctx.scratch("bw_dz1", dy.shape)
         T = tiles(H, W)
-        dal = ctx.scratch("bw_dal", (B * T, C), torch.float32)
+        dal = ctx.scratch("bw_dal" + pre, (B * T, C), torch.float32)
         conv(ctx, dt, Wt.packed(pre + "conv2", 2), B, H, W, C, C, epi=L.EPI_PRELU_BWD, alpha=p[pre + "prelu.weight"],
              pre_in=sv["z1"], y=dz1, part=dal)
-        colsum(ctx, dal, B * T, C, G[pre + "prelu.weight"])
+        self.cs.add(dal, B * T, C, G[pre + "prelu.weight"])
         self._wg(pre + "conv1", sv["x"], dz1, B, H, W, C, C)
         dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
         conv(ctx, dz1, Wt.packed(pre + "conv1", 2), B, H, W, C, C, y=dx, res=(dy,) + tuple(extra_res))
+        if flush:
+            self.cs.flush()
         return dx
 
     def group(self, sv: dict, dy: torch.Tensor, g: int, extra_res: Sequence = (), dx_out=None,
@@ -268,10 +330,11 @@ class Backward:
         for b in reversed(range(s.NB)):
             if b == 0:
                 d = self.rcab(sv["blocks"][b], d, f"{pre}blocks.{b}.", extra_res=(dy,) + tuple(extra_res),
-                              dx_out=dx_out)
+                              dx_out=dx_out, flush=False)
             else:
                 d = self.rcab(sv["blocks"][b], d, f"{pre}blocks.{b}.",
-                              dx_out=ctx.scratch(f"bw_rg_pp{b & 1}", dy.shape))
+                              dx_out=ctx.scratch(f"bw_rg_pp{b & 1}", dy.shape), flush=False)
+        self.cs.flush()
         return d
 
     def tail(self, sv: dict) -> torch.Tensor:
@@ -286,12 +349,12 @@ class Backward:
         self._wg("conv_last", sv["a_last"], sv["dout"], B, Ho, Wo, C, 16, cout_valid=s.out_ch)
         last = stages[-1]
         rows = ctx.lib.fen_conv_last_dgrad_part_rows(B, Ho, Wo)
-        dal = ctx.scratch("bw_dal_up", (rows, C), torch.float32)
+        dal = ctx.scratch(f"bw_dal_up{len(stages) - 1}", (rows, C), torch.float32)
         du = ctx.scratch(f"bw_du{(len(stages) - 1) & 1}", (B, last["H"], last["W"], 4 * C))
         ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, Ho, Wo, C, s.out_ch, ptr(sv["dout"]),
                  ptr(p["conv_last.weight"]), ptr(last["v"]), ptr(p[f"upsample.stages.{len(stages) - 1}.prelu.weight"]),
                  ptr(du), ptr(dal))
-        colsum(ctx, dal, rows, C, G[f"upsample.stages.{len(stages) - 1}.prelu.weight"])
+        self.cs.add(dal, rows, C, G[f"upsample.stages.{len(stages) - 1}.prelu.weight"])
         for st in reversed(range(len(stages))):
             info = stages[st]
             key = f"upsample.stages.{st}."
@@ -301,10 +364,10 @@ class Backward:
                 prev = stages[st - 1]
                 du_prev = ctx.scratch(f"bw_du{(st - 1) & 1}", (B, prev["H"], prev["W"], 4 * C))
                 T = tiles(hh, ww)
-                dal = ctx.scratch("bw_dal_up", (B * T, C), torch.float32)
+                dal = ctx.scratch(f"bw_dal_up{st - 1}", (B * T, C), torch.float32)
                 conv(ctx, du, Wt.packed(key + "conv", 2), B, hh, ww, 4 * C, C, epi=L.EPI_PRELU_BWD | L.EPI_UNSHUFFLE,
                      alpha=p[f"upsample.stages.{st - 1}.prelu.weight"], pre_in=prev["v"], y=du_prev, part=dal)
-                colsum(ctx, dal, B * T, C, G[f"upsample.stages.{st - 1}.prelu.weight"])
+                self.cs.add(dal, B * T, C, G[f"upsample.stages.{st - 1}.prelu.weight"])
                 du = du_prev
             else:
                 d_fb = ctx.scratch("bw_d_fb", (B, hh, ww, C))
@@ -314,6 +377,7 @@ class Backward:
         d_body = ctx.scratch("bw_d_body", (B, H, W, C))
         conv(ctx, d_fb, Wt.packed("conv_after_body", 2), B, H, W, C, C, y=d_body)
         sv["d_fb"] = d_fb
+        self.cs.flush()
         return d_body
 
     def head(self, x_lr: torch.Tensor, d_feat0: torch.Tensor) -> None:

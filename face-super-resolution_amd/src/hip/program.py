@@ -55,6 +55,10 @@ class Ctx:
             self._scratch[key] = buf
         return buf[:n].view(tuple(shape))
 
+    def keep(self, obj) -> None:
+        """Keep a host object (e.g. a ctypes job table) alive as long as the program."""
+        self._hold.append(obj)
+
     # ---- launches ----
     def emit(self, name: str, fn: Callable, *args) -> None:
         if self.record:

@@ -141,15 +141,36 @@ int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy, const floa
 /* trainer.py:416-421 LR synthesis: bicubic x0.25, align_corners=False, NCHW fp32          */
 int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, float* lr, void* stream);
 
-/* out[c] = (accumulate ? out[c] : 0) + scale * sum_r part[r][c]                            */
+/* out[c] = (accumulate ? out[c] : 0) + scale * sum_r part[r][c]   (fixed-order, deterministic;
+ * the per-channel reductions behind PReLU / SE-FC weight gradients and the L1 loss value)   */
 int fen_colsum(int rows, int cols, const float* part, float scale, float* out, int accumulate,
                void* stream);
+typedef struct {
+    const float* part;
+    float* out;
+    int rows, cols;
+    float scale;
+    int accumulate;
+} fen_colsum_job;
+/* up to 40 independent column sums in one launch                                            */
+int fen_colsum_multi(int njobs, const fen_colsum_job* jobs, void* stream);
 
 /* OIHW fp32 -> kernel layout of dtype.  mode 0: [9][Cout_pad][Cin] rows = co;
  * mode 1: same with rows permuted for FEN_EPI_SHUFFLE (row t*Cout/4+c <- co = 4c+t);
  * mode 2: dgrad weights [9][Cin_pad][Cout], flipped taps (row = ci).                        */
 int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const float* w, void* out, void* stream);
 size_t fen_packed_elems(int mode, int Cout, int Cin);
+/* Many packs in one launch (the re-pack after every optimizer step).  fen_pack_table fills a
+ * host buffer of fen_pack_table_bytes(njobs) bytes (job table + element offsets, *total =
+ * packed elements); the caller copies it to device memory once and replays fen_pack_multi. */
+typedef struct {
+    const float* w;   /* OIHW fp32 source                                                     */
+    void* out;        /* packed destination of dtype                                          */
+    int mode, Cout, Cin;
+} fen_pack_job;
+size_t fen_pack_table_bytes(int njobs);
+int fen_pack_table(int dtype, int njobs, const fen_pack_job* jobs, void* table_host, size_t* total);
+int fen_pack_multi(int dtype, int njobs, const void* table_dev, size_t total, void* stream);
 
 /* fp32 <-> dtype layout conversions (NCHW fp32 <-> NHWC dtype).  nchw_to_nhwc writes
  * Cpad >= C channels per pixel, zero-filling c >= C (Cpad = 16 builds conv_last's dout).    */

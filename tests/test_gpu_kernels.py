@@ -277,15 +277,20 @@ def test_se_fused(dtype, B, C, Cr, H, W):
 
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 24, 40, 64, 64), (1, 16, 16, 64, 256),
-                                             (1, 32, 32, 64, 16)])
+                                             (1, 32, 32, 64, 16), (17, 64, 64, 64, 64), (2, 20, 36, 128, 64),
+                                             (3, 32, 48, 64, 256)])
 def test_wgrad(dtype, B, H, W, Cin, Cout):
+    """fen_wgrad3x3 vs autograd of conv2d.  The reference runs in float64 on the operands
+    rounded to the compute dtype, so bf16 is held to fp32-accumulation accuracy (rel 1e-5):
+    a wrong fragment mapping or a dropped tile shows as O(1).  (17, 64, 64) puts 2 tiles per
+    block; Cout 256 / Cin 128 exercise the co-group / ci-group grid."""
     from src.hip import net
     torch.manual_seed(7)
-    x = torch.randn(B, Cin, H, W)
-    dy = torch.randn(B, Cout, H, W)
-    w = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
-    bb = torch.zeros(Cout, requires_grad=True)
-    F.conv2d(x, w, bb, padding=1).mul(dy).sum().backward()
+    x = torch.randn(B, Cin, H, W).to(dtype).float()
+    dy = torch.randn(B, Cout, H, W).to(dtype).float()
+    w = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    bb = torch.zeros(Cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.double(), w, bb, padding=1).mul(dy.double()).sum().backward()
     ctx = _ctx(dtype)
     cv = Cout if Cout != 16 else 3
     dw = ctx.alloc((cv, Cin, 3, 3), torch.float32)
@@ -293,10 +298,9 @@ def test_wgrad(dtype, B, H, W, Cin, Cout):
     net.wgrad(ctx, nhwc(x, dtype), nhwc(dy, dtype), B, H, W, Cin, Cout, dw, db, cout_valid=cv)
     torch.cuda.synchronize()
     gw, gb = w.grad[:cv], bb.grad[:cv]
-    rel = float((dw.cpu() - gw).norm() / gw.norm())
-    relb = float((db.cpu() - gb).norm() / gb.norm())
-    tol = 1e-5 if dtype == torch.float32 else 1e-2
-    assert rel <= tol and relb <= tol, (rel, relb)
+    rel = float((dw.cpu().double() - gw).norm() / gw.norm())
+    relb = float((db.cpu().double() - gb).norm() / gb.norm())
+    assert rel <= 1e-5 and relb <= 1e-5, (rel, relb)
 
 
 @pytest.mark.parametrize("dtype", DT)

@@ -76,3 +76,10 @@ net.wgrad(rctx, x, x, B, 64, 64, 64, 64, dw, db)
 us = timeit(lambda: rctx.run())
 res["rcab_wgrad_us"] = round(us, 2); res["rcab_wgrad_tflops"] = round(flop / us / 1e6, 1)
 print(json.dumps(res))
+# wgrad upsample stage 1 (Cin 64, Cout 256 @128x128)
+dw1 = torch.empty(256, 64, 3, 3, device='cuda'); db1 = torch.empty(256, device='cuda')
+rctx1 = Ctx(dt, 'cuda', record=True)
+net.wgrad(rctx1, x1, du, B, 128, 128, 64, 256, dw1, db1)
+us = timeit(lambda: rctx1.run(), 10)
+res2 = {"up1_wgrad_us": round(us, 2), "up1_wgrad_tflops": round(2 * B * 128 * 128 * 256 * 576 / us / 1e6, 1)}
+print(json.dumps(res2))
