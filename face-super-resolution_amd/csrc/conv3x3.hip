@@ -106,11 +106,27 @@ __device__ __forceinline__ EpiConst<MT> epi_consts(const fen_conv_desc& d, int c
 // store path (COT == 64 only); `red` is >= 4*COT floats of LDS.  Contains barriers:
 // every thread of the block must call it.
 // ------------------------------------------------------------------------------------
-template <typename T, int COT, int WR, int WC, int EPIC = -1>
-__device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&acc)[COT / 16 / WC][16 / WR], int b,
-                                              int tlin, int h0, int w0, int co0, char* stage, float* red,
-                                              const EpiConst<COT / 16 / WC>& ec) {
+// Block barrier for LDS hand-offs only.  RAW (persistent kernel): lgkmcnt(0) + s_barrier,
+// no memory fence -- a __syncthreads() would also drain the next tile's in-flight halo
+// LDS-DMA (vmcnt(0)).  Returns the global store instructions this wave issued in its final
+// store phase when the tile is full and every lane stored in each of them (the caller then
+// waits vmcnt(that) for the older halo DMA), else 0 (= wait for everything).
+template <bool RAW>
+__device__ __forceinline__ void epi_barrier() {
+    if constexpr (RAW) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+
+template <typename T, int COT, int WR, int WC, int EPIC = -1, bool RAW = false>
+__device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc)[COT / 16 / WC][16 / WR], int b,
+                                             int tlin, int h0, int w0, int co0, char* stage, float* red,
+                                             const EpiConst<COT / 16 / WC>& ec) {
     constexpr int MT = COT / 16 / WC, NT = 16 / WR, CW = COT / WC;
+    constexpr int NTHR = 64 * WR * WC;
     // EPIC >= 0: the epilogue mode is a compile-time constant (flags | residual count << 8),
     // so every branch on it folds away; -1: read it from the descriptor.
     constexpr bool CT = EPIC >= 0;
@@ -169,7 +185,7 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
                 d.loss_part[tlin] = t;
             }
         }
-        return;
+        return 0;
     }
 
     const bool shuf = epi & FEN_EPI_SHUFFLE;
@@ -234,7 +250,7 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
                 const float s = group16_sum(psum[m][r]);
                 if (c16 == 0) red[wr * COT + wc * CW + m * 16 + q * 4 + r] = s;
             }
-        __syncthreads();
+        epi_barrier<RAW>();
         if (tid < COT && co0 + tid < Cout) {
             float t = 0.f;
 #pragma unroll
@@ -252,10 +268,11 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
     if (stage != nullptr) {
         if constexpr (sizeof(T) == 2 && COT == 64) {
             // ---- bf16: stage the 256 x 64 tile in LDS, leave as full 128-B rows ----
+            int nst = 0;
             for (int k = 0; k < 2; ++k) {
                 void* dst = k == 0 ? d.y_pre : d.y;
                 if (k == 0 && (!prelu || !dst)) continue;
-                __syncthreads();
+                epi_barrier<RAW>();   // every wave is done with the stage (its MFMAs / last reads)
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
                     const int cl = wc * CW + m * 16 + q * 4;
@@ -268,9 +285,10 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
                         st4<bf16>(stage + swz(px, cl >> 3) + (q & 1) * 8, v);
                     }
                 }
-                __syncthreads();
+                epi_barrier<RAW>();
                 if (!unshuf) {
-                    for (int i = tid; i < 256 * 8; i += 256) {
+                    nst += 256 * 8 / NTHR;
+                    for (int i = tid; i < 256 * 8; i += NTHR) {
                         const int px = i >> 3, ch = i & 7;
                         const int h = h0 + (px >> 4), w = w0 + (px & 15);
                         if (h >= H || w >= W) continue;
@@ -287,7 +305,8 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
                 } else {
                     // du[b][h/2][w/2][4*co + 2*(h&1) + (w&1)]: 8x8 du pixels x 4*COT channels
                     const int Hh = H >> 1, Wh = W >> 1;
-                    for (int i = tid; i < 64 * 32; i += 256) {
+                    nst += 64 * 32 / NTHR;
+                    for (int i = tid; i < 64 * 32; i += NTHR) {
                         const int dp = i >> 5, kq = i & 31;
                         const int hh = dp >> 3, ww = dp & 7;
                         const int gh = (h0 >> 1) + hh, gw = (w0 >> 1) + ww;
@@ -309,10 +328,11 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
                     }
                 }
             }
-            return;
+            return full ? nst : 0;
         }
     }
     // ---- direct stores from registers ----
+    int nst = 0;
     for (int k = 0; k < 2; ++k) {
         void* dst = k == 0 ? d.y_pre : d.y;
         if (k == 0 && (!prelu || !dst)) continue;
@@ -340,9 +360,11 @@ __device__ __forceinline__ void conv_epilogue(const fen_conv_desc& d, f32x4 (&ac
                     const size_t o = ((size_t)(b * H + h) * W + w_) * Cout + cob;
                     st4<T>((char*)dst + o * sizeof(T), v);
                 }
+                ++nst;
             }
         }
     }
+    return (full && !unshuf && co0 + COT <= Cout) ? nst : 0;
 }
 
 // MFMAs of one tap from a weight tile wt ([COT rows][128 B]) and a halo image
@@ -409,6 +431,103 @@ __device__ __forceinline__ void conv_tile_resident(f32x4 (&acc)[MT][NT], const c
     }
 }
 
+// Same tile, halo-row reuse order: for each (kw, k-half) the wave reads its NT+2 halo rows
+// once and applies them to all three kh taps (output row n uses halo row n + kh), so one
+// group = NT+2 pixel fragments + 3*MT filter fragments for 3*MT*NT MFMAs -- 0.5 LDS reads
+// per MFMA at MT=2, NT=4 (tap order: 0.75).  Double-buffered one group ahead.
+template <int COT, int MT, int NT>
+__device__ __forceinline__ void conv_tile_rows(f32x4 (&acc)[MT][NT], const char* wts, const char* halo, int wr,
+                                               int wc, int q, int c16) {
+    constexpr int NB = NT + 2;
+    uint4 A0[3][MT], B0[NB], A1[3][MT], B1[NB];
+    const int arow = wc * MT * 16 + c16;
+    auto load = [&](int g, uint4 (&A)[3][MT], uint4 (&Bf)[NB]) {
+        const int kw = g >> 1, kk = g & 1;
+        const int chunk = kk * 4 + q;
+        const char* hb = halo + hcol(c16 + kw, chunk) + (wr * NT) * (HALO * 128);
+#pragma unroll
+        for (int n = 0; n < NB; ++n) Bf[n] = *(const uint4*)(hb + n * (HALO * 128));
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const char* wt = wts + (kh * 3 + kw) * COT * 128;
+#pragma unroll
+            for (int m = 0; m < MT; ++m) A[kh][m] = *(const uint4*)(wt + swz(arow + m * 16, chunk));
+        }
+    };
+    auto mma = [&](const uint4 (&A)[3][MT], const uint4 (&Bf)[NB]) {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], A[kh][m], Bf[n + kh]);
+    };
+    load(0, A0, B0);
+#pragma unroll
+    for (int g = 0; g < 6; g += 2) {
+        load(g + 1, A1, B1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 2 < 6) load(g + 2, A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A1, B1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// The halo-row-reuse order at lower register cost: 18 steps (kw, k-half, kh); the filter
+// fragments of step s+1 and the halo rows of the next (kw, k-half) group are read while
+// step s's MFMAs run -- 2*MT + 2*(NT+2) fragment registers (64 at MT=NT=4) instead of
+// 6*MT + 2*(NT+2).
+template <int COT, int MT, int NT>
+__device__ __forceinline__ void conv_tile_rows2(f32x4 (&acc)[MT][NT], const char* wts, const char* halo, int wr,
+                                                int wc, int q, int c16) {
+    constexpr int NB = NT + 2;
+    uint4 A0[MT], A1[MT], B0[NB], B1[NB];
+    const int arow = wc * MT * 16 + c16;
+    auto loadB = [&](int g, uint4 (&Bf)[NB]) {
+        const int kw = g >> 1, kk = g & 1;
+        const char* hb = halo + hcol(c16 + kw, kk * 4 + q) + (wr * NT) * (HALO * 128);
+#pragma unroll
+        for (int n = 0; n < NB; ++n) Bf[n] = *(const uint4*)(hb + n * (HALO * 128));
+    };
+    auto loadA = [&](int st, uint4 (&A)[MT]) {
+        const int g = st / 3, kh = st % 3, kw = g >> 1, kk = g & 1;
+        const char* wt = wts + (kh * 3 + kw) * COT * 128;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) A[m] = *(const uint4*)(wt + swz(arow + m * 16, kk * 4 + q));
+    };
+    auto mma = [&](const uint4 (&A)[MT], const uint4 (&Bf)[NB], int kh) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], A[m], Bf[n + kh]);
+    };
+    loadB(0, B0);
+    loadA(0, A0);
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const int st = g * 3 + kh;
+            if (st + 1 < 18) {
+                if (st & 1) loadA(st + 1, A0); else loadA(st + 1, A1);
+            }
+            if (kh == 0 && g + 1 < 6) {
+                if (g & 1) loadB(g + 1, B0); else loadB(g + 1, B1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (st & 1) {
+                if (g & 1) mma(A1, B1, kh); else mma(A1, B0, kh);
+            } else {
+                if (g & 1) mma(A0, B1, kh); else mma(A0, B0, kh);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // k_conv3x3_p: persistent, resident weights, LDS-DMA double-buffered halo (bf16, Cin=64)
 // ------------------------------------------------------------------------------------
@@ -470,7 +589,7 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
     __syncthreads();
     FEN_STAMP(1);
     for (int k = 0; t < ntiles; ++k, t += nslot) {
-        char* cur = hbuf + (k & 1) * HALO_SLOT;
+        char* cur = hbuf + (k & 1) * HALO_SLOT;   // halo of tile t, then its output stage
         const int tn = t + nslot;
         const unsigned nbase = lds_addr(hbuf + ((k + 1) & 1) * HALO_SLOT);
         // the next tile's halo: all pieces up front, or (debug & 4) one piece per wave per tap
@@ -487,23 +606,26 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (!(d.debug & 2)) {
-            conv_tile_resident<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16, next_halo);
+            if (d.debug & 32) conv_tile_resident<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16, next_halo);
+            else conv_tile_rows<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16);
         } else {
             for (int tap = 0; tap < 9; ++tap) next_halo(tap);
         }
         FEN_STAMP(2 + 3 * k);
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        int nst = 0;
         if (d.debug & 1) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
 #pragma unroll
                 for (int n = 0; n < NT; ++n) asm volatile("" ::"v"(acc[m][n]));
         } else {
-            conv_epilogue<bf16, COT, WR, WC, EPIC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
+            nst = conv_epilogue<bf16, COT, WR, WC, EPIC, true>(d, acc, b, t, h0, w0, co0,
+                                                               (d.debug & 64) ? nullptr : cur, red, ec);
         }
         FEN_STAMP(3 + 3 * k);
-        wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
+        wait_vm_upto(nst);                                   // next halo landed (stores may drain)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                        // ... for everyone; cur is free
         FEN_STAMP(4 + 3 * k);
@@ -511,133 +633,248 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
 }
 
 // ------------------------------------------------------------------------------------
-// k_conv3x3_q: persistent, filter resident in VGPRs (bf16, Cin == 64, Cout tile 64).
-// 8 waves = 4 pixel-row groups x 2 output-channel halves; each wave keeps its 32 output
-// channels x 576 (tap, ci) weights -- 36 x 16 B = 144 VGPRs -- for the life of the block,
-// so the tap loop reads only pixel fragments from LDS (0.5 ds_read_b128 per MFMA; the
-// LDS-resident-filter loop needs 0.75 and measured 1.4x slower in isolation,
-// tools/mfma_loop.hip).  LDS: 3 halo slots; slots 1-2 stage the filter at start-up while the
-// first halo lands in slot 0; afterwards tiles ping-pong between slots 0 and 1, the next
-// tile's halo streaming in by LDS-DMA under the current tile's MFMAs.
+// k_conv3x3_g: persistent, two wave-groups in ping-pong (bf16, Cin == 64, Cout % 64 == 0).
+// 512 threads = group A (waves 0-3) + group B (waves 4-7); each wave owns 4 output rows x
+// 16 columns x all 64 output channels of a tile (16 accumulators, halo-row-reuse MFMA
+// order).  The block's tiles alternate between the groups, and the groups alternate
+// roles every phase: while one group runs the MFMAs of its tile (reading the shared,
+// LDS-resident filter and its own halo slot), the other group retires its previous tile
+// (epilogue + direct stores) and streams its next halo by LDS-DMA into its own slot.  One
+// s_barrier per phase; nothing else synchronises.  The per-channel partial sums of a tile
+// (SE pool / PReLU dalpha) are parked in LDS in the epilogue phase and folded into
+// part[tile][co] by the same group at the start of its next phase.
+//   LDS: filter 72 KB | halo slot A | halo slot B | red[2][4][64] | bias[64] alpha[64]
 // ------------------------------------------------------------------------------------
+constexpr int G_WBYTES = 9 * 64 * 128;
+constexpr int G_LDS = G_WBYTES + 2 * HALO_SLOT + 2 * 4 * 64 * 4 + 2 * 64 * 4;
+
 template <int EPIC>
-__global__ __launch_bounds__(512, 1) void k_conv3x3_q(const fen_conv_desc d) {
-    constexpr int COT = 64, WR = 4, WC = 2, MT = 2, NT = 4, NW = 8;
+__global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
+    constexpr int MT = 4, NT = 4;
+    constexpr int NRES = EPIC >> 8;
+    constexpr int EPI = EPIC & 0xff;
+    constexpr bool PRELU = EPI & FEN_EPI_PRELU, PBWD = EPI & FEN_EPI_PRELU_BWD, POOL = EPI & FEN_EPI_POOL;
+    constexpr bool SHUF = EPI & FEN_EPI_SHUFFLE;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* hbuf = smem;                                      // 3 x HALO_SLOT
-    float* red = (float*)(smem + 3 * HALO_SLOT);            // WR * COT floats
+    char* wts = smem;
+    float* red = (float*)(smem + G_WBYTES + 2 * HALO_SLOT);   // [grp][wr][64]
+    float* cst = red + 2 * 4 * 64;                            // bias[64], alpha[64]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave % WR, wc = wave / WR;
+    const int grp = wave >> 2, wr = wave & 3;
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, Cout = d.Cout;
-    const int ncot = Cout / COT;
-    const int cot = blockIdx.x % ncot, co0 = cot * COT;
+    const int ncot = Cout >> 6;
+    const int cot = blockIdx.x % ncot, co0 = cot * 64;
     const int nslot = gridDim.x / ncot, slot = blockIdx.x / ncot;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
     const int ntiles = d.B * tpi;
+    const int nmine = (ntiles - slot + nslot - 1) / nslot;    // tiles of this block (>= 1)
+    const int nj0 = (nmine + 1) >> 1, nj1 = nmine >> 1;      // per group
+    const int myn = grp ? nj1 : nj0;
+    char* hslot = smem + G_WBYTES + grp * HALO_SLOT;
     const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * 128));
 
-    auto halo_piece = [&](int t, unsigned base, int i) {
+    FEN_STAMP(0);
+    auto tile_of = [&](int g, int j) { return slot + (2 * j + g) * nslot; };
+    // this group's share of the 41 halo pieces of tile t into its slot
+    auto issue_halo = [&](int t) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        const int s = i * 64 + lane;
-        const int p = s >> 3, pc = s & 7;
-        const int hr = p / HALO, hc = p - hr * HALO;
-        const int c = pc ^ (hc & 7);
-        const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-        const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-        const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
-        dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
+        const unsigned base = lds_addr(hslot);
+        for (int i = wr; i < HALO_DMA; i += 4) {
+            const int s = i * 64 + lane;
+            const int p = s >> 3, pc = s & 7;
+            const int hr = p / HALO, hc = p - hr * HALO;
+            const int c = pc ^ (hc & 7);
+            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+            const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            const int voff = in ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
+            dma16(xr4, __builtin_amdgcn_readfirstlane(base + i * 1024), voff);
+        }
     };
 
-    FEN_STAMP(0);
-    // start-up: filter rows r = tap*64 + co_l (72 KB, swizzled 128-B rows: the VGPR fill
-    // below reads 16 rows at one chunk, conflict-free only with the XOR key) -> slots 1..2,
-    // first halo -> slot 0
+    // ---- start-up: filter slab of co-tile cot, bias/alpha, group A's first halo
     {
         const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)d.w, (short)0, (int)((size_t)9 * Cout * 128), 0x00020000);
-        char* wst = hbuf + HALO_SLOT;
-        for (int i = wave; i < 9 * COT * 8 / 64; i += NW) {
+        for (int i = wave; i < G_WBYTES / 1024; i += 8) {
             const int s = i * 64 + lane;
             const int r = s >> 3, pc = s & 7;
             const int c = pc ^ ((r >> 1) & 7);
-            const int tap = r / COT, col = r - tap * COT;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wst + i * 1024), 16,
+            const int tap = r >> 6, col = r & 63;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wts + i * 1024), 16,
                                                      ((tap * Cout + co0 + col) * 64 + c * 8) * 2, 0, 0, 0);
         }
+        if (tid < 64) {
+            const int cp = co0 + tid, Cq = Cout >> 2;
+            const int co = SHUF ? 4 * (cp % Cq) + cp / Cq : cp;
+            cst[tid] = (EPI & FEN_EPI_BIAS) ? d.bias[co] : 0.f;
+            cst[64 + tid] = (PRELU || PBWD) ? d.alpha[SHUF ? cp % Cq : cp] : 0.f;
+        }
+        if (grp == 0) issue_halo(tile_of(0, 0));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
-    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * MT * 16 + q * 4);
-    int t = slot;
-    if (t < ntiles)
-        for (int i = wave; i < HALO_DMA; i += NW) halo_piece(t, lds_addr(hbuf), i);
-    FEN_STAMP(13);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    FEN_STAMP(14);
-    uint4 wreg[9][2][MT];
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const int row = tap * COT + wc * MT * 16 + m * 16 + c16;
-                wreg[tap][kk][m] = *(const uint4*)(hbuf + HALO_SLOT + swz(row, kk * 4 + q));
-            }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();   // staging slots free again
     FEN_STAMP(1);
 
-    for (int k = 0; t < ntiles; ++k, t += nslot) {
-        const char* cur = hbuf + (k & 1) * HALO_SLOT;
-        const int tn = t + nslot;
-        if (tn < ntiles) {
-            const unsigned nbase = lds_addr(hbuf + ((k + 1) & 1) * HALO_SLOT);
-            for (int i = wave; i < HALO_DMA; i += NW) halo_piece(tn, nbase, i);
-        }
-        f32x4 acc[MT][NT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        {
-            uint4 B0[NT], B1[NT];
-            auto load = [&](int tap, int kk, uint4 (&Bf)[NT]) {
-                const int kh = tap / 3, kw = tap - kh * 3;
-                const char* hb = cur + hcol(c16 + kw, kk * 4 + q) + (wr * NT + kh) * (HALO * 128);
-#pragma unroll
-                for (int n = 0; n < NT; ++n) Bf[n] = *(const uint4*)(hb + n * (HALO * 128));
-            };
-            auto mma = [&](int tap, int kk, const uint4 (&Bf)[NT]) {
+    const int pend = max(2 * nj0 - 1, 2 * nj1);              // last phase (an epilogue)
+    f32x4 acc[MT][NT];
+    int pending_part = -1;                                   // tile whose partials sit in red[grp]
+    for (int ph = 0; ph <= pend; ++ph) {
+        int nst = 0;
+        if ((ph & 1) == grp) {
+            // ---------------- compute phase: tile j = (ph - grp) / 2 ----------------
+            if ((POOL || PBWD) && pending_part >= 0 && wr == 0) {
+                const float* rg = red + grp * 256;
+                d.part[(size_t)pending_part * Cout + co0 + lane] =
+                    (rg[lane] + rg[64 + lane]) + (rg[128 + lane] + rg[192 + lane]);
+            }
+            pending_part = -1;
+            const int j = (ph - grp) >> 1;
+            if (j < myn) {
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
 #pragma unroll
-                    for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], wreg[tap][kk][m], Bf[n]);
-            };
-            load(0, 0, B0);
+                    for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+                conv_tile_rows2<64, MT, NT>(acc, wts, hslot, wr, 0, q, c16);
+            }
+        } else {
+            // ---------------- service phase: retire tile jp, stream tile jp + 1 ----------------
+            // the next halo is issued first; the residual / pre-activation loads follow and
+            // one vmcnt(0) retires both (completion is in order), then the epilogue runs and
+            // its stores drain across the barrier
+            const int jp = (ph - grp - 1) >> 1;                  // -1 for group B at phase 0
+            const bool ret = ph > grp && jp >= 0 && jp < myn;
+            if (jp + 1 < myn) issue_halo(tile_of(grp, jp + 1));
+            uint2 rv[NRES > 0 ? NRES : 1][MT][NT];
+            uint2 pv[PBWD ? MT : 1][PBWD ? NT : 1];
+            int b = 0, h0 = 0, w0 = 0, t = 0;
+            bool full = true;
+            if (ret) {
+                t = tile_of(grp, jp);
+                b = t / tpi;
+                const int tile = t - b * tpi;
+                h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+                full = h0 + 16 <= H && w0 + 16 <= W;
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                load(tap, 1, B1);
-                __builtin_amdgcn_sched_barrier(0);
-                mma(tap, 0, B0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (tap < 8) load(tap + 1, 0, B0);
-                __builtin_amdgcn_sched_barrier(0);
-                mma(tap, 1, B1);
-                __builtin_amdgcn_sched_barrier(0);
+                for (int n = 0; n < NT; ++n) {
+                    const int h = h0 + wr * NT + n, w = w0 + c16;
+                    const bool ok = full || (h < H && w < W);
+                    const size_t oi = ((size_t)(b * H + (ok ? h : 0)) * W + (ok ? w : 0)) * Cout + co0 + 4 * q;
+#pragma unroll
+                    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+                        for (int k = 0; k < NRES; ++k) rv[k][m][n] = *(const uint2*)((const char*)d.res[k] + (oi + m * 16) * 2);
+                        if constexpr (PBWD) pv[m][n] = *(const uint2*)((const char*)d.pre_in + (oi + m * 16) * 2);
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (ret) {
+                float psum[MT][4];
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) psum[m][r] = 0.f;
+                const int Cq = Cout >> 2;
+                // pass 1 (in place): bias, residuals, PReLU backward, partial sums -- consumes
+                // the loaded operands right away so their registers die before the stores
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    const float4 bb = *(const float4*)(cst + m * 16 + 4 * q);
+                    const float4 aa = *(const float4*)(cst + 64 + m * 16 + 4 * q);
+                    const float bias4[4] = {bb.x, bb.y, bb.z, bb.w};
+                    const float al4[4] = {aa.x, aa.y, aa.z, aa.w};
+#pragma unroll
+                    for (int n = 0; n < NT; ++n) {
+                        const bool ok = full || (h0 + wr * NT + n < H && w0 + c16 < W);
+                        float rf[NRES > 0 ? NRES : 1][4], pf[4];
+#pragma unroll
+                        for (int k = 0; k < NRES; ++k) {
+                            rf[k][0] = __uint_as_float(rv[k][m][n].x << 16);
+                            rf[k][1] = __uint_as_float(rv[k][m][n].x & 0xffff0000u);
+                            rf[k][2] = __uint_as_float(rv[k][m][n].y << 16);
+                            rf[k][3] = __uint_as_float(rv[k][m][n].y & 0xffff0000u);
+                        }
+                        if constexpr (PBWD) {
+                            pf[0] = __uint_as_float(pv[m][n].x << 16);
+                            pf[1] = __uint_as_float(pv[m][n].x & 0xffff0000u);
+                            pf[2] = __uint_as_float(pv[m][n].y << 16);
+                            pf[3] = __uint_as_float(pv[m][n].y & 0xffff0000u);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float v = acc[m][n][r] + bias4[r];
+#pragma unroll
+                            for (int k = 0; k < NRES; ++k) v += rf[k][r];
+                            if constexpr (PBWD) {
+                                const float pr = pf[r];
+                                if (ok) psum[m][r] += pr > 0.f ? 0.f : v * pr;
+                                v = pr > 0.f ? v : v * al4[r];
+                            }
+                            if constexpr (POOL) {
+                                if (ok) psum[m][r] += v;
+                            }
+                            acc[m][n][r] = v;
+                        }
+                    }
+                }
+                // pass 2: activation + stores
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    const float4 aa = *(const float4*)(cst + 64 + m * 16 + 4 * q);
+                    const float al4[4] = {aa.x, aa.y, aa.z, aa.w};
+#pragma unroll
+                    for (int n = 0; n < NT; ++n) {
+                        const int h = h0 + wr * NT + n, w = w0 + c16;
+                        if (!(full || (h < H && w < W))) continue;
+                        float v[4], o[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            v[r] = acc[m][n][r];
+                            o[r] = PRELU ? (v[r] > 0.f ? v[r] : al4[r] * v[r]) : v[r];
+                        }
+                        const int cob = co0 + m * 16 + 4 * q;
+                        size_t off;
+                        if constexpr (SHUF) {
+                            const int tt = cob / Cq, c = cob % Cq;
+                            off = ((size_t)(b * 2 * H + 2 * h + (tt >> 1)) * (2 * W) + 2 * w + (tt & 1)) * Cq + c;
+                        } else {
+                            off = ((size_t)(b * H + h) * W + w) * Cout + cob;
+                        }
+                        if (PRELU && d.y_pre) {
+                            st4<bf16>((char*)d.y_pre + off * 2, v);
+                            ++nst;
+                        }
+                        st4<bf16>((char*)d.y + off * 2, o);
+                        ++nst;
+                    }
+                }
+                if constexpr (POOL || PBWD) {
+                    float* rg = red + grp * 256 + wr * 64;
+#pragma unroll
+                    for (int m = 0; m < MT; ++m)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float sv = group16_sum(psum[m][r]);
+                            if (c16 == 0) rg[m * 16 + 4 * q + r] = sv;
+                        }
+                    pending_part = t;
+                }
+                if (!full) nst = 0;
             }
         }
-        FEN_STAMP(2 + 3 * k);
-        const int b = t / tpi, tile = t - b * tpi;
-        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        conv_epilogue<bf16, COT, WR, WC, EPIC>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
-        FEN_STAMP(3 + 3 * k);
-        wait_vm_upto(epi_store_count(d, h0, w0, MT * NT));  // next halo landed (stores may drain)
+        FEN_STAMP(2 + 2 * ph);
+        wait_vm_upto(nst);                 // this wave's halo pieces landed (stores may drain)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                        // ... for everyone; cur is free
-        FEN_STAMP(4 + 3 * k);
+        __builtin_amdgcn_s_barrier();
+        FEN_STAMP(3 + 2 * ph);
+    }
+    if ((POOL || PBWD) && pending_part >= 0 && wr == 0) {
+        const float* rg = red + grp * 256;
+        d.part[(size_t)pending_part * Cout + co0 + lane] = (rg[lane] + rg[64 + lane]) + (rg[128 + lane] + rg[192 + lane]);
     }
 }
 
@@ -730,9 +967,10 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
 
 int g_num_cus = 0;
 
-// kernel-variant selector for A/B runs (FEN_CONV_VARIANT): 0 default (persistent LDS-resident
-// filter for bf16 64-channel inputs, epilogue specialised per mode), 1 streamed kernel
-// everywhere, 2 persistent kernel with the generic (runtime-mode) epilogue
+// kernel-variant selector for A/B runs (FEN_CONV_VARIANT): 0 default (ping-pong persistent
+// kernel k_conv3x3_g for the network's epilogue modes), 1 streamed kernel everywhere,
+// 2 single-group persistent kernel with the generic (runtime-mode) epilogue, 5 single-group
+// persistent kernel k_conv3x3_p with per-mode epilogues
 int conv_variant() {
     static int v = -1;
     if (v < 0) {
@@ -770,7 +1008,7 @@ int launch_p(const fen_conv_desc* d, hipStream_t s) {
 }
 
 template <int EPIC>
-int launch_q(const fen_conv_desc* d, hipStream_t s) {
+int launch_g(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int ntiles = d->B * tpi;
     const int ncot = d->Cout / 64;
@@ -784,13 +1022,12 @@ int launch_q(const fen_conv_desc* d, hipStream_t s) {
     grid -= grid % ncot;
     const int maxg = ntiles * ncot;
     if (grid > maxg) grid = maxg;
-    const size_t lds = 3 * HALO_SLOT + 4 * 64 * 4;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_conv3x3_q<EPIC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_g<EPIC>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_conv3x3_q<EPIC>), dim3(grid), dim3(512), lds, s, *d);
+    hipLaunchKernelGGL((k_conv3x3_g<EPIC>), dim3(grid), dim3(512), G_LDS, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
@@ -848,17 +1085,17 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
             const int key = dense && conv_variant() != 2 ? (epi | (nres << 8)) : -1;
             constexpr int B_ = FEN_EPI_BIAS;
             if (conv_variant() == 3 && key == (B_ | FEN_EPI_PRELU)) return launch_p<64, 4, 1, B_ | FEN_EPI_PRELU>(d, s);
-            if (conv_variant() == 4) {
+            if (conv_variant() != 5 && conv_variant() != 3) {   // default: ping-pong kernel
                 switch (key) {
-                    case B_ | FEN_EPI_PRELU: return launch_q<B_ | FEN_EPI_PRELU>(d, s);
-                    case B_ | FEN_EPI_POOL: return launch_q<B_ | FEN_EPI_POOL>(d, s);
-                    case B_ | (1 << 8): return launch_q<B_ | (1 << 8)>(d, s);
-                    case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE: return launch_q<B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
-                    case FEN_EPI_PRELU_BWD: return launch_q<FEN_EPI_PRELU_BWD>(d, s);
-                    case 0: return launch_q<0>(d, s);
-                    case 1 << 8: return launch_q<1 << 8>(d, s);
-                    case 2 << 8: return launch_q<2 << 8>(d, s);
-                    case 3 << 8: return launch_q<3 << 8>(d, s);
+                    case B_ | FEN_EPI_PRELU: return launch_g<B_ | FEN_EPI_PRELU>(d, s);
+                    case B_ | FEN_EPI_POOL: return launch_g<B_ | FEN_EPI_POOL>(d, s);
+                    case B_ | (1 << 8): return launch_g<B_ | (1 << 8)>(d, s);
+                    case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE: return launch_g<B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
+                    case FEN_EPI_PRELU_BWD: return launch_g<FEN_EPI_PRELU_BWD>(d, s);
+                    case 0: return launch_g<0>(d, s);
+                    case 1 << 8: return launch_g<1 << 8>(d, s);
+                    case 2 << 8: return launch_g<2 << 8>(d, s);
+                    case 3 << 8: return launch_g<3 << 8>(d, s);
                     default: break;
                 }
             }

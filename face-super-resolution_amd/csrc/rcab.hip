@@ -1,0 +1,615 @@
+// Fused RCAB forward (reference src/models/blocks.py:135-153 with ChannelAttention
+// blocks.py:83-92): one launch computes, per 16x16-pixel tile and all 64 channels,
+//
+//   z1 = conv1(x) + b1          (on the 18x18 region conv2 needs: halo recompute)
+//   a1 = PReLU(z1)              (zero outside the image = conv2's zero padding)
+//   t  = conv2(a1) + b2         (16x16)
+//   s  = sigmoid(W2 relu(W1 mean_hw(t)))   (per image: needs every tile of the image)
+//   y  = t * s * res_scale + x
+//
+// bf16 activations, fp32 MFMA accumulation, C = 64, Cr <= 16, H and W multiples of 16.
+//
+// Structure (one 512-thread block per CU, persistent; tiles walked in rounds that cover
+// whole images, so every tile an image needs is resident in the same round):
+//   * x halo of the tile (20x20 px) + a 4-column edge copy streamed by LDS-DMA, one tile
+//     ahead;
+//   * the two filters stream tap by tap from L2 through a 6-slot LDS ring (3 taps per
+//     phase, refilled one phase ahead) -- both filters (144 KB) do not fit next to the
+//     activation images;
+//   * conv1 (21 pixel fragments: 18 rows of 16 + 3 fragments of the 2 edge columns) ->
+//     bias + PReLU -> a1 image in LDS; conv2 reads it with the halo-row-reuse MFMA order;
+//   * t stays in registers.  The tile's pool partial goes to global memory, then the block
+//     arrives on its image's counter; the LAST arriver computes the gate (FC-ReLU-FC-
+//     sigmoid) and publishes it (agent-scope release/acquire, MI355X_MICROARCH.md
+//     'Workgroup dispatch ... inter-workgroup visibility').  Every tile applies
+//     y = t*s*rs + x one phase into its NEXT tile (the gate is ready by then), or right
+//     away for its last tile.  The counters clean themselves up, so a hipGraph can replay.
+#include "fen_common.h"
+
+namespace {
+
+constexpr int XW = 20;                       // conv1 input halo, 20x20 px
+constexpr int XH_BYTES = XW * XW * 128;      // 51200 = 50 DMA pieces
+constexpr int XH_DMA = XH_BYTES / 1024;
+constexpr int EH_BYTES = XW * 4 * 128;       // halo columns 16..19 again, row-keyed: 10 pieces
+constexpr int EH_DMA = EH_BYTES / 1024;
+constexpr int A1W = 18;                      // a1 image = conv2 halo, 18x18, hcol layout
+constexpr int A1_BYTES = A1W * A1W * 128;    // 41472
+constexpr int TAP_BYTES = 64 * 128;          // one filter tap [64 co][64 ci] bf16
+constexpr int O_XH = 0;
+constexpr int O_EH = O_XH + XH_BYTES;
+constexpr int O_A1 = O_EH + EH_BYTES;
+constexpr int O_RING = O_A1 + A1_BYTES;
+constexpr int O_RED = O_RING + 6 * TAP_BYTES;   // [4][64] f32 pool partials of the 4 row waves
+constexpr int O_CST = O_RED + 4 * 64 * 4;       // b1[64] alpha[64] b2[64]
+constexpr int O_FC = O_CST + 3 * 64 * 4;        // fc1 [16][64], fc2 [64][16] f32
+constexpr int O_FLAG = O_FC + 2 * 1024 * 4;     // block-wide scalars
+constexpr int RCAB_LDS = O_FLAG + 64;
+static_assert(RCAB_LDS <= 163840, "LDS budget");
+static_assert(O_RING % 16 == 0 && O_RED % 16 == 0 && O_FC % 16 == 0, "alignment");
+
+// diagnostic build (-DFEN_STAMPS): s_memrealtime per wave at phase points into d.stamps,
+// [block][wave][32]; the product build executes none of it
+#ifdef FEN_STAMPS
+#define RSTAMP(i)                                                                            \
+    do {                                                                                     \
+        unsigned long long _rt;                                                              \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt)::"memory");      \
+        if (d.stamps && lane == 0 && (i) < 32) d.stamps[((size_t)blockIdx.x * 8 + wave) * 32 + (i)] = _rt; \
+    } while (0)
+#else
+#define RSTAMP(i) \
+    do {          \
+    } while (0)
+#endif
+
+constexpr unsigned POLL_MAX = 1u << 22;      // ~0.5 s of s_sleep: a gate that never comes
+                                             // sets sync[3*B] and the kernel exits anyway
+
+// 16-B chunk position in the edge image: pixel e = row*4 + col', key = row & 7 (an edge
+// fragment's 16 lanes cover 8 rows x 2 columns: 16 distinct bank slots)
+__device__ __forceinline__ int ekey(int row, int chunk) { return (chunk ^ (row & 7)) << 4; }
+
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// agent-scope flag helpers (hipMalloc'd sync words)
+__device__ __forceinline__ int ld_acquire_poll(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------
+// conv1 MFMAs for one phase (3 taps, tap order), one wave, 32 output channels (MT = 2) x up
+// to 6 pixel fragments.  Slots 0..3 are output rows row0..row0+3 (columns 0..15); slot 4 is
+// row row0+4 (groups 0, 1) or an edge fragment (groups 2, 3: wave-uniform branch); slot 5
+// is a second edge fragment (group 3 only).  Fragments double-buffered one step ahead.
+//   main B: xh + mb[kw][kk] + (f + kh) * XW*128        (mb includes row0)
+//   edge B: eh + eb[kh][kk] + kw * 128
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void conv1_phase(f32x4 (&acc)[2][6], const char* xh, const char* eh,
+                                            const char* const (&tapp)[3], int kh, const int (&mb)[3][2],
+                                            const int (&e4)[2], const int (&e5)[2], bool main4, bool has5,
+                                            int arow, int q) {
+    // phase = kernel row kh: taps (kh, kw = 0..2); xh_k / e*_k fold the row offset in once
+    const char* xk = xh + kh * (XW * 128);
+    uint4 A0[2], B0[6], A1[2], B1[6];
+    auto load = [&](int st, uint4 (&A)[2], uint4 (&Bf)[6]) {
+        const int kw = st >> 1, kk = st & 1;
+        const char* wt = tapp[kw];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) A[m] = *(const uint4*)(wt + swz(arow + m * 16, kk * 4 + q));
+#pragma unroll
+        for (int f = 0; f < 4; ++f) Bf[f] = *(const uint4*)(xk + mb[kw][kk] + f * (XW * 128));
+        if (main4) Bf[4] = *(const uint4*)(xk + mb[kw][kk] + 4 * (XW * 128));
+        else Bf[4] = *(const uint4*)(eh + e4[kk] + kw * 128);
+        if (has5) Bf[5] = *(const uint4*)(eh + e5[kk] + kw * 128);
+    };
+    auto mma = [&](const uint4 (&A)[2], const uint4 (&Bf)[6]) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+#pragma unroll
+            for (int f = 0; f < 5; ++f) mma16<bf16>(acc[m][f], A[m], Bf[f]);
+            if (has5) mma16<bf16>(acc[m][5], A[m], Bf[5]);
+        }
+    };
+    load(0, A0, B0);
+#pragma unroll
+    for (int st = 0; st < 6; st += 2) {
+        load(st + 1, A1, B1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < 6) load(st + 2, A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A1, B1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// conv2 MFMAs for one phase (kernel column kw: taps (0,kw),(1,kw),(2,kw) in ring slots),
+// halo-row-reuse order on the a1 image; wave = 4 output rows x 32 channels.
+__device__ __forceinline__ void conv2_phase(f32x4 (&acc)[2][4], const char* a1, const char* const (&tapp)[3], int kw,
+                                            int wr, int arow, int q, int c16) {
+    uint4 A0[3][2], B0[6], A1[3][2], B1[6];
+    auto load = [&](int kk, uint4 (&A)[3][2], uint4 (&Bf)[6]) {
+        const int chunk = kk * 4 + q;
+        const char* hb = a1 + hcol(c16 + kw, chunk) + (wr * 4) * (A1W * 128);
+#pragma unroll
+        for (int n = 0; n < 6; ++n) Bf[n] = *(const uint4*)(hb + n * (A1W * 128));
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) A[kh][m] = *(const uint4*)(tapp[kh] + swz(arow + m * 16, chunk));
+    };
+    auto mma = [&](const uint4 (&A)[3][2], const uint4 (&Bf)[6]) {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) mma16<bf16>(acc[m][n], A[kh][m], Bf[n + kh]);
+    };
+    load(0, A0, B0);
+    load(1, A1, B1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(A0, B0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(A1, B1);
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// ------------------------------------------------------------------------------------
+// the kernel
+// ------------------------------------------------------------------------------------
+// edge fragment eidx: rows 8*eidx + lane/2 (clamped to 17 for the pad lanes of eidx 2),
+// column 16 + lane%2; base per (kh, k-half)
+__device__ __forceinline__ void edge_bases(int eidx, int c16, int q, int (&eb)[3][2]) {
+    int r = 8 * eidx + (c16 >> 1);
+    if (r > 17) r = 17;
+    const int b = c16 & 1;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) eb[kh][kk] = ((r + kh) * 4 + b) * 128 + ekey(r + kh, kk * 4 + q);
+}
+
+__global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* xh = smem + O_XH;
+    char* eh = smem + O_EH;
+    char* a1s = smem + O_A1;
+    char* ring = smem + O_RING;
+    float* red = (float*)(smem + O_RED);
+    float* cst = (float*)(smem + O_CST);
+    float* fcs = (float*)(smem + O_FC);
+    int* lflag = (int*)(smem + O_FLAG);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int ch = wave & 1, g = wave >> 1;          // conv1: channel half, fragment group
+    const int wr = wave >> 1, wc = wave & 1;         // conv2: row group, channel half
+    const int H = d.H, W = d.W, B = d.B, Cr = d.Cr;
+    const int twn = W >> 4, tpi = twn * (H >> 4);
+    const int ntiles = B * tpi;
+    const int nslot = gridDim.x;
+    const int nmine = (ntiles - (int)blockIdx.x + nslot - 1) / nslot;
+    // workspace (fen_rcab_workspace_alloc: uncached, so every access of the cross-block
+    // hand-off goes to memory -- the per-XCD L2s are not coherent): part [B*tpi][64] | gate
+    // [B][64] (unused) | cnt [B] | (unused) [B] | ack [B] | err
+    float* part = (float*)d.ws;
+    float* gate = part + (size_t)ntiles * 64;
+    int* cnt = (int*)(gate + (size_t)B * 64);         // [B] arrivals
+    int* ack = cnt + 2 * B;                           // [B] partials consumed
+    int* err = cnt + 3 * B;                           // [1] poll timeout
+
+    const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)B * H * W * 128));
+    const i32x4 w1r = make_rsrc(d.w1, 9u * 64u * 128u);
+    const i32x4 w2r = make_rsrc(d.w2, 9u * 64u * 128u);
+
+    // ring: phase P of the block's sequence (6 per tile) uses slots (P & 1) * 3 + i.
+    // phase p = 0..2: conv1 taps 3p..3p+2; p = 3..5: conv2 taps (kh, kw = p - 3), kh = 0..2
+    auto issue_taps = [&](int P) {
+        const int p = P % 6;
+        char* base = ring + (P & 1) * 3 * TAP_BYTES;
+        const int s = wave * 64 + lane, r = s >> 3, pc = s & 7;
+        const int c = pc ^ ((r >> 1) & 7);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int tap = p < 3 ? 3 * p + i : i * 3 + (p - 3);
+            const int voff = ((tap * 64 + r) * 64 + c * 8) * 2;
+            dma16(p < 3 ? w1r : w2r, __builtin_amdgcn_readfirstlane(lds_addr(base + i * TAP_BYTES + wave * 1024)),
+                  voff);
+        }
+    };
+    // x halo (20x20, hcol key) + edge copy (halo columns 16..19, row key) of tile t
+    auto issue_halo = [&](int t) {
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        for (int i = wave; i < XH_DMA + EH_DMA; i += 8) {
+            int voff = 0x7ffffff0;
+            unsigned base;
+            if (i < XH_DMA) {
+                const int s = i * 64 + lane, p = s >> 3, pc = s & 7;
+                const int hr = p / XW, hc = p - hr * XW;
+                const int c = pc ^ (hc & 7);
+                const int gh = h0 - 2 + hr, gw = w0 - 2 + hc;
+                if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) voff = (((b * H + gh) * W + gw) * 64 + c * 8) * 2;
+                base = lds_addr(xh + i * 1024);
+            } else {
+                const int s = (i - XH_DMA) * 64 + lane, e = s >> 3, pc = s & 7;
+                const int hr = e >> 2, hc = 16 + (e & 3);
+                const int c = pc ^ (hr & 7);
+                const int gh = h0 - 2 + hr, gw = w0 - 2 + hc;
+                if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) voff = (((b * H + gh) * W + gw) * 64 + c * 8) * 2;
+                base = lds_addr(eh + (i - XH_DMA) * 1024);
+            }
+            dma16(xr4, __builtin_amdgcn_readfirstlane(base), voff);
+        }
+    };
+
+    // ---- start-up: constants, SE weights, first taps, first halo
+    if (tid < 64) {
+        cst[tid] = d.b1[tid];
+        cst[64 + tid] = d.alpha[tid];
+        cst[128 + tid] = d.b2[tid];
+    }
+    for (int i = tid; i < 1024; i += 512) {
+        fcs[i] = i < Cr * 64 ? d.fc1[i] : 0.f;          // [Cr][64]
+        fcs[1024 + i] = i < Cr * 64 ? d.fc2[i] : 0.f;   // [64][Cr]
+    }
+    RSTAMP(0);
+    issue_taps(0);
+    issue_halo(blockIdx.x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    RSTAMP(1);
+
+    // conv1 per-lane addressing (group g: rows row0.., slot 4 main for g < 2, edges for g >= 2)
+    const int row0 = g == 0 ? 0 : g == 1 ? 5 : g == 2 ? 10 : 14;
+    const bool main4 = g < 2, has5 = g == 3;
+    int mbase[3][2], eb4[3][2], eb5[3][2];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) mbase[kw][kk] = hcol(c16 + kw, kk * 4 + q) + row0 * (XW * 128);
+    edge_bases(g == 2 ? 2 : 0, c16, q, eb4);
+    edge_bases(1, c16, q, eb5);
+    const int arow1 = ch * 32 + c16;                  // A row (co) of conv1's wave
+    const int arow2 = wc * 32 + c16;
+
+    uint2 tcar[2][4];                                 // t (bf16) of the tile awaiting its gate
+    int pend_t = -1;                                  // that tile (-1: none)
+
+    // y = t * s * rs + x for tile `pt` (t in tcar); wave-uniform poll of the image's gate
+    // The SE gate of image b, computed by every wave that needs it once all tpi partials of
+    // the image have arrived (poll the arrival counter, then read the partials; uncached
+    // workspace, so no fences): mean -> FC1 -> ReLU -> FC2 -> sigmoid.  Lane c ends with
+    // mean[c], hid (lane j < Cr), s[c].  Deterministic: fixed-order sums.
+    auto se_gate = [&](int b, float& mean, float& hid_mine) -> float {
+        if (lane == 0) {
+            unsigned it = 0;
+            while (ld_acquire_poll(cnt + b) < tpi && ++it < POLL_MAX) __builtin_amdgcn_s_sleep(1);
+            if (it >= POLL_MAX) atomicExch(err, 1);
+        }
+        float sm = 0.f;                       // 16 loads in flight per lane, fixed order
+        const float* pp = part + (size_t)b * tpi * 64 + lane;
+        int i = 0;
+        for (; i + 16 <= tpi; i += 16) {
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                v[j] = __hip_atomic_load(pp + (size_t)(i + j) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) sm += v[j];
+        }
+        for (; i < tpi; ++i) sm += __hip_atomic_load(pp + (size_t)i * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mean = sm * d.inv_hw;
+        hid_mine = 0.f;
+        for (int j = 0; j < Cr; ++j) {
+            const float v = wave_sum(fcs[j * 64 + lane] * mean);
+            if (lane == j) hid_mine = fmaxf(v, 0.f);
+        }
+        float z = 0.f;
+        for (int j = 0; j < Cr; ++j) z += fcs[1024 + lane * Cr + j] * __shfl(hid_mine, j, 64);
+        return 1.f / (1.f + expf(-z));
+    };
+
+    // y = t * s * rs + x for tile `pt` (t in tcar)
+    auto apply = [&](int pt) {
+        const int b = pt / tpi, tile = pt - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        float mean, hid_mine;
+        const float sg = se_gate(b, mean, hid_mine);
+        if (tile == 0 && wave == 0) {         // the user-visible copies, once per image
+            d.s[(size_t)b * 64 + lane] = sg;
+            if (d.mean) d.mean[(size_t)b * 64 + lane] = mean;
+            if (d.hid && lane < Cr) d.hid[(size_t)b * Cr + lane] = hid_mine;
+        }
+        const float rs = d.res_scale;
+        float sv[2][4];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sv[m][r] = __shfl(sg, wc * 32 + m * 16 + 4 * q + r, 64) * rs;
+        uint2 xv[2][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) xv[m][n] = *(const uint2*)((const char*)d.x + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2);
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                float o[4];
+                o[0] = __uint_as_float(tcar[m][n].x << 16) * sv[m][0] + __uint_as_float(xv[m][n].x << 16);
+                o[1] = __uint_as_float(tcar[m][n].x & 0xffff0000u) * sv[m][1] + __uint_as_float(xv[m][n].x & 0xffff0000u);
+                o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xv[m][n].y << 16);
+                o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xv[m][n].y & 0xffff0000u);
+                st4<bf16>((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
+            }
+        }
+    };
+    // after every wave of the block has read the image's partials: the last of its tiles
+    // resets the image's counters for the next launch
+    auto acknowledge = [&](int pt) {
+        if (tid == 0) {
+            const int b = pt / tpi;
+            if (atomicAdd(ack + b, 1) == tpi - 1) {
+                __hip_atomic_store(cnt + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ack + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
+
+#pragma unroll 1
+    for (int k = 0; k < nmine; ++k) {
+        const int t = (int)blockIdx.x + k * nslot;
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        f32x4 acc1[2][6];
+        // ================= conv1: phases 0..2 =================
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int f = 0; f < 6; ++f) acc1[m][f] = zero4();
+#pragma unroll 1
+        for (int p = 0; p < 3; ++p) {
+            const int P = k * 6 + p;
+            if (p > 0 || k > 0) {
+                if (k < 2) RSTAMP(2 + k * 14 + p * 2);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this phase's taps (+ halo) landed
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (k < 2) RSTAMP(3 + k * 14 + p * 2);
+            }
+            issue_taps(P + 1);
+            const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
+                                   ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
+            const int e4[2] = {p == 0 ? eb4[0][0] : p == 1 ? eb4[1][0] : eb4[2][0],
+                               p == 0 ? eb4[0][1] : p == 1 ? eb4[1][1] : eb4[2][1]};
+            const int e5[2] = {p == 0 ? eb5[0][0] : p == 1 ? eb5[1][0] : eb5[2][0],
+                               p == 0 ? eb5[0][1] : p == 1 ? eb5[1][1] : eb5[2][1]};
+            conv1_phase(acc1, xh, eh, tapp, p, mbase, e4, e5, main4, has5, arow1, q);
+        }
+        if (k == 0) RSTAMP(15);
+        // ---- conv1 epilogue: bias + PReLU -> a1 image (zero outside the image); training
+        //      copies of z1 / a1 for the backward (the 16x16 interior)
+        {
+            const int nf = has5 ? 6 : 5;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const float4 bb = *(const float4*)(cst + ch * 32 + m * 16 + 4 * q);
+                const float4 aa = *(const float4*)(cst + 64 + ch * 32 + m * 16 + 4 * q);
+                const float bia[4] = {bb.x, bb.y, bb.z, bb.w}, alp[4] = {aa.x, aa.y, aa.z, aa.w};
+                const int co = ch * 32 + m * 16 + 4 * q;
+#pragma unroll
+                for (int f = 0; f < 6; ++f) {
+                    if (f >= nf) continue;
+                    int ar, ac;
+                    const bool edge = f >= 4 && !main4;
+                    if (!edge) {
+                        ar = row0 + f;
+                        ac = c16;
+                    } else {
+                        const int eidx = g == 2 ? 2 : f - 4;
+                        ar = 8 * eidx + (c16 >> 1);
+                        ac = 16 + (c16 & 1);
+                        if (ar > 17) continue;
+                    }
+                    const int gh = h0 - 1 + ar, gw = w0 - 1 + ac;
+                    const bool in = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+                    float z[4], a[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        z[r] = acc1[m][f][r] + bia[r];
+                        a[r] = in ? (z[r] > 0.f ? z[r] : alp[r] * z[r]) : 0.f;
+                    }
+                    const int chunk = co >> 3;
+                    st4<bf16>(a1s + (ar * A1W + ac) * 128 + ((chunk ^ (ac & 7)) << 4) + (q & 1) * 8, a);
+                    if (d.z1 && ar >= 1 && ar <= 16 && ac >= 1 && ac <= 16) {
+                        const size_t o = ((size_t)(b * H + gh) * W + gw) * 64 + co;
+                        st4<bf16>((char*)d.z1 + o * 2, z);
+                        st4<bf16>((char*)d.a1 + o * 2, a);
+                    }
+                }
+            }
+        }
+        // previous tile: its gate is ready by now (its round ended a conv1 ago)
+        if (k < 2) RSTAMP(8 + k * 14);
+        __builtin_amdgcn_sched_barrier(0);
+        if (pend_t >= 0) apply(pend_t);
+        __builtin_amdgcn_sched_barrier(0);
+        if (k < 2) RSTAMP(9 + k * 14);
+        // ================= conv2: phases 3..5 =================
+        f32x4 acc2[2][4];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) acc2[m][n] = zero4();
+#pragma unroll 1
+        for (int p = 3; p < 6; ++p) {
+            const int P = k * 6 + p;
+            if (k < 2 && p == 3) RSTAMP(10 + k * 14);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (k < 2 && p == 3) RSTAMP(11 + k * 14);
+            if (p == 4 && pend_t >= 0) acknowledge(pend_t);   // every wave has applied it (barrier above)
+            if (!(k + 1 == nmine && p == 5)) issue_taps(P + 1);
+            if (p == 3 && k + 1 < nmine) issue_halo(t + nslot);   // conv1 is done with xh / eh
+            const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
+                                   ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
+            conv2_phase(acc2, a1s, tapp, p - 3, wr, arow2, q, c16);
+        }
+        if (k == 0) RSTAMP(29);
+        // ---- conv2 epilogue: t = acc + b2, pool partial, arrival; t stays in registers
+        float ps[2][4];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const float4 bb = *(const float4*)(cst + 128 + wc * 32 + m * 16 + 4 * q);
+            const float bia[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ps[m][r] = 0.f;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    acc2[m][n][r] += bia[r];
+                    ps[m][r] += acc2[m][n][r];
+                }
+                if (d.t) {
+                    const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
+                    float v[4] = {acc2[m][n][0], acc2[m][n][1], acc2[m][n][2], acc2[m][n][3]};
+                    st4<bf16>((char*)d.t + o * 2, v);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float s = group16_sum(ps[m][r]);
+                if (c16 == 0) red[wr * 64 + wc * 32 + m * 16 + 4 * q + r] = s;
+            }
+        if (k < 2) RSTAMP(12 + k * 14);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (k < 2) RSTAMP(13 + k * 14);
+        if (wave == 0) {
+            // tile partial -> uncached workspace, drained, then the arrival
+            __hip_atomic_store(part + (size_t)t * 64 + lane,
+                               (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) atomicAdd(cnt + b, 1);
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                tcar[m][n].x = (unsigned)f2bf(acc2[m][n][0]) | ((unsigned)f2bf(acc2[m][n][1]) << 16);
+                tcar[m][n].y = (unsigned)f2bf(acc2[m][n][2]) | ((unsigned)f2bf(acc2[m][n][3]) << 16);
+            }
+        pend_t = t;
+        if (k < 2) RSTAMP(14 + k * 14);
+    }
+    // the last tile: its gate comes from this round's other tiles
+    RSTAMP(30);
+    if (pend_t >= 0) {
+        apply(pend_t);
+        RSTAMP(31);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        acknowledge(pend_t);
+    }
+    (void)lflag;
+}
+
+}  // namespace
+
+extern "C" size_t fen_rcab_workspace_bytes(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    const size_t nt = (size_t)B * (H / 16) * (W / 16);
+    return (nt * 64 + (size_t)B * 64) * sizeof(float) + ((size_t)3 * B + 1) * sizeof(int);
+}
+
+// The one allocation the library makes: the fused RCAB's hand-off workspace must be uncached
+// (hipDeviceMallocUncached) so that pollers on other XCDs never read a stale L2 copy.  It is
+// zeroed here and the kernel leaves it zeroed.
+extern "C" int fen_rcab_workspace_alloc(int B, int H, int W, void** ws) {
+    if (!ws) return FEN_EINVAL;
+    const size_t n = fen_rcab_workspace_bytes(B, H, W);
+    if (n == 0) return FEN_EINVAL;
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached) != hipSuccess) return FEN_EHIP;
+    if (hipMemset(p, 0, n) != hipSuccess) {
+        (void)hipFree(p);
+        return FEN_EHIP;
+    }
+    *ws = p;
+    return FEN_OK;
+}
+// Diagnostic (synchronises the device): number of non-zero sync words left in the workspace
+// (0 after every completed launch; the last word is the poll-timeout flag), or < 0 on error.
+extern "C" int fen_rcab_workspace_status(const void* ws, int B, int H, int W) {
+    if (!ws || B <= 0) return FEN_EINVAL;
+    const size_t nt = (size_t)B * (H / 16) * (W / 16);
+    const size_t off = (nt * 64 + (size_t)B * 64) * sizeof(float);
+    const size_t n = (size_t)3 * B + 1;
+    int* h = (int*)malloc(n * sizeof(int));
+    if (!h) return FEN_EINVAL;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h, (const char*)ws + off, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
+        free(h);
+        return FEN_EHIP;
+    }
+    int c = 0;
+    for (size_t i = 0; i < n; ++i) c += h[i] != 0;
+    free(h);
+    return c;
+}
+extern "C" int fen_rcab_workspace_free(void* ws) {
+    if (ws && hipFree(ws) != hipSuccess) return FEN_EHIP;
+    return FEN_OK;
+}
+
+static int rcab_num_cus() {
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (ncu <= 0) ncu = 256;
+    }
+    return ncu;
+}
+
+extern "C" int fen_rcab_supported(int dtype, int B, int H, int W, int C, int Cr) {
+    if (dtype != FEN_BF16 || C != 64 || Cr <= 0 || Cr > 16 || B <= 0 || H <= 0 || W <= 0 || H % 16 || W % 16)
+        return 0;
+    if ((size_t)B * H * W * 128 >= (size_t)0x7fff0000) return 0;
+    return (H / 16) * (W / 16) <= rcab_num_cus() ? 1 : 0;
+}
+
+extern "C" int fen_rcab_fused(const fen_rcab_desc* d, void* stream) {
+    if (!d || !d->x || !d->y || !d->w1 || !d->w2 || !d->b1 || !d->b2 || !d->alpha || !d->fc1 || !d->fc2 || !d->s ||
+        !d->ws)
+        return FEN_EINVAL;
+    if (!fen_rcab_supported(d->dtype, d->B, d->H, d->W, d->C, d->Cr)) return FEN_EUNSUPPORTED;
+    if ((d->z1 != nullptr) != (d->a1 != nullptr)) return FEN_EINVAL;
+    const int ncu = rcab_num_cus();
+    const int tpi = (d->H / 16) * (d->W / 16);         // an image's tiles must be co-resident
+    const int ntiles = d->B * tpi;
+    int grid = (ncu / tpi) * tpi;                      // rounds of whole images
+    if (grid > ntiles) grid = ntiles;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_rcab, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_rcab, dim3(grid), dim3(512), RCAB_LDS, (hipStream_t)stream, *d);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -47,6 +48,11 @@ class NetSpec:
         return NetSpec(C=cfg.num_channels, G=cfg.num_groups, NB=cfg.blocks_per_group,
                        Cr=max(cfg.num_channels // cfg.reduction_ratio, 8), scale=cfg.scale_factor,
                        res_scale=float(cfg.res_scale), in_ch=cfg.in_channels, out_ch=cfg.out_channels)
+
+
+# fused RCAB forward (fen_rcab_fused) where supported (FEN_RCAB_FUSED=1); default: the per-op
+# launches until the fused kernel is the faster of the two on MI355X (tools/bench_rcab.py)
+FUSED_RCAB = os.environ.get("FEN_RCAB_FUSED", "0") != "0"
 
 
 def tiles(H: int, W: int) -> int:
@@ -192,9 +198,12 @@ class Forward:
         return feat
 
     def rcab(self, x: torch.Tensor, pre: str, out: Optional[torch.Tensor] = None, name: Optional[str] = None):
-        """RCAB (blocks.py:135-153) -> (y, saved)."""
+        """RCAB (blocks.py:135-153) -> (y, saved).  One fused launch (fen_rcab_fused) where the
+        shape allows it, else conv1(+PReLU) / conv2(+pool) / SE gate+apply launches."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
+        if FUSED_RCAB and ctx.lib.fen_rcab_supported(ctx.code, B, H, W, C, s.Cr):
+            return self._rcab_fused(x, pre, out, name)
         a1 = ctx.alloc(x.shape) if self.save else ctx.scratch("rcab_a1", x.shape)
         z1 = ctx.alloc(x.shape) if self.save else None
         conv(ctx, x, Wt.packed(pre + "conv1", 0), B, H, W, C, C, bias=p[pre + "conv1.bias"],
@@ -219,6 +228,37 @@ class Forward:
                  ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]), ptr(mean), ptr(hid), ptr(sg), ptr(t), s.res_scale,
                  ptr(x), ptr(y))
         saved = dict(x=x, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg) if self.save else dict(s=sg)
+        return y, saved
+
+    def _rcab_fused(self, x, pre, out, name):
+        s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
+        B, H, W, C = x.shape
+        d = L.RcabDesc()
+        d.dtype, d.B, d.H, d.W, d.C, d.Cr = ctx.code, B, H, W, C, s.Cr
+        ca = pre + "channel_attention.fc."
+        d.x, d.w1, d.b1 = ptr(x), ptr(Wt.packed(pre + "conv1", 0)), ptr(p[pre + "conv1.bias"])
+        d.alpha, d.w2, d.b2 = ptr(p[pre + "prelu.weight"]), ptr(Wt.packed(pre + "conv2", 0)), ptr(p[pre + "conv2.bias"])
+        d.fc1, d.fc2 = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
+        d.res_scale, d.inv_hw = float(s.res_scale), 1.0 / (H * W)
+        y = out if out is not None else ctx.alloc(x.shape)
+        d.y = ptr(y)
+        if self.save:
+            z1, a1, t = ctx.alloc(x.shape), ctx.alloc(x.shape), ctx.alloc(x.shape)
+            mean = ctx.alloc((B, C), torch.float32)
+            hid = ctx.alloc((B, s.Cr), torch.float32)
+            sg = ctx.alloc((B, C), torch.float32)
+            d.z1, d.a1, d.t, d.mean, d.hid = ptr(z1), ptr(a1), ptr(t), ptr(mean), ptr(hid)
+        else:
+            sg = ctx.scratch("se_s", (B, C), torch.float32)
+        d.s = ptr(sg)
+        d.ws = ctx.rcab_workspace(B, H, W).ptr
+        ctx.emit("rcab_fused", ctx.lib.fen_rcab_fused, byref(d))
+        if self.attn is not None and name is not None:
+            self.attn[name] = sg
+        if self.save:
+            saved = dict(x=x, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg)
+        else:
+            saved = dict(s=sg)
         return y, saved
 
     def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None, pre: Optional[str] = None):

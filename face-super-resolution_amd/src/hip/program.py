@@ -33,7 +33,10 @@ class Ctx:
 
     # ---- memory ----
     def alloc(self, shape, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-        return torch.empty(tuple(shape), dtype=dtype or self.tdtype, device=self.device)
+        t = torch.empty(tuple(shape), dtype=dtype or self.tdtype, device=self.device)
+        if self.record:   # a recorded program owns every buffer its launches touch
+            self._hold.append(t)
+        return t
 
     def zeros(self, shape, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
         return torch.zeros(tuple(shape), dtype=dtype or self.tdtype, device=self.device)
@@ -54,6 +57,33 @@ class Ctx:
             buf = torch.empty(n, dtype=dtype, device=self.device)
             self._scratch[key] = buf
         return buf[:n].view(tuple(shape))
+
+    def zero_scratch(self, tag: str, shape, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        """A persistent zero-initialised buffer (e.g. self-cleaning sync words), one per tag."""
+        dtype = dtype or self.tdtype
+        key = f"zero:{tag}/{dtype}"
+        buf = self._scratch.get(key)
+        n = 1
+        for s in shape:
+            n *= int(s)
+        if buf is None or buf.numel() < n:
+            if buf is not None:
+                self._hold.append(buf)
+            buf = torch.zeros(n, dtype=dtype, device=self.device)
+            self._scratch[key] = buf
+        return buf[:n].view(tuple(shape))
+
+    def rcab_workspace(self, B: int, H: int, W: int):
+        """The fused-RCAB hand-off workspace for this program (one per program, grown on
+        demand; launches in one program run one at a time on one stream)."""
+        ws = getattr(self, "_rcab_ws", None)
+        need = self.lib.fen_rcab_workspace_bytes(B, H, W)
+        if ws is None or ws.nbytes < need:
+            if ws is not None:
+                self._hold.append(ws)
+            ws = L.RcabWorkspace(B, H, W)
+            self._rcab_ws = ws
+        return ws
 
     def keep(self, obj) -> None:
         """Keep a host object (e.g. a ctypes job table) alive as long as the program."""

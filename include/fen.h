@@ -138,6 +138,46 @@ int fen_se_bwd(int B, int C, int Cr, int nparts, float inv_hw, float res_scale,
 int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy, const float* s,
                      float res_scale, const float* g, void* dt, void* stream);
 
+/* Fused RCAB forward (blocks.py:135-153, ChannelAttention blocks.py:83-92) in ONE launch:
+ *   z1 = conv1(x)+b1, a1 = PReLU(z1), t = conv2(a1)+b2, s = sigmoid(fc2 relu(fc1 mean_hw t)),
+ *   y = t*s*res_scale + x.
+ * bf16 NHWC, C = 64, Cr <= 16, H and W multiples of 16, (H/16)*(W/16) <= #CUs.  conv1 is
+ * recomputed on each tile's 18x18 halo; the per-image SE gate is published in-kernel by the
+ * last tile of the image to finish conv2.  Returns FEN_EUNSUPPORTED outside that envelope
+ * (callers then use the per-op kernels; fen_rcab_supported() asks in advance).
+ * ws: the hand-off workspace from fen_rcab_workspace_alloc (uncached device memory, zeroed,
+ * left zeroed by every launch, so a hipGraph replays it; reusable by any launch whose B,H,W
+ * fit its size, one launch at a time).                                                      */
+typedef struct {
+    int dtype;                 /* FEN_BF16                                                     */
+    int B, H, W, C, Cr;
+    const void* x;             /* NHWC [B,H,W,64]                                              */
+    const void* w1;            /* conv1 packed mode 0 [9][64][64]                              */
+    const float* b1;           /* [64]                                                         */
+    const float* alpha;        /* PReLU [64]                                                   */
+    const void* w2;            /* conv2 packed mode 0                                          */
+    const float* b2;
+    const float* fc1;          /* channel_attention.fc.0.weight [Cr][64]                       */
+    const float* fc2;          /* channel_attention.fc.2.weight [64][Cr]                       */
+    float res_scale;           /* 0.2                                                          */
+    float inv_hw;              /* 1/(H*W)                                                      */
+    void* y;                   /* out NHWC                                                     */
+    void* z1;                  /* training copies (or NULL): conv1 pre-activation,            */
+    void* a1;                  /*   its PReLU, conv2 output t (all NHWC)                      */
+    void* t;
+    float* s;                  /* [B][64] gate (always written)                                */
+    float* mean;               /* [B][64] or NULL                                              */
+    float* hid;                /* [B][Cr] or NULL                                              */
+    void* ws;                  /* fen_rcab_workspace_alloc()                                   */
+    unsigned long long* stamps;/* NULL; diagnostic build only (-DFEN_STAMPS): phase timestamps */
+} fen_rcab_desc;
+int fen_rcab_supported(int dtype, int B, int H, int W, int C, int Cr);  /* 1 if fen_rcab_fused runs this shape */
+size_t fen_rcab_workspace_bytes(int B, int H, int W);
+int fen_rcab_workspace_alloc(int B, int H, int W, void** ws);   /* the library's only allocation */
+int fen_rcab_workspace_free(void* ws);
+int fen_rcab_workspace_status(const void* ws, int B, int H, int W);  /* test aid: nonzero sync words, syncs */
+int fen_rcab_fused(const fen_rcab_desc* d, void* stream);
+
 /* trainer.py:416-421 LR synthesis: bicubic x0.25, align_corners=False, NCHW fp32          */
 int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, float* lr, void* stream);
 

@@ -181,6 +181,87 @@ void run3(const char* name, int ncu, float* out, int nblk_per_cu) {
     printf("%-28s %8.3f us/tile  %7.1f TFLOP/s\n", name, ms * 1e3 / N / reps / nblk_per_cu / GROUPS, flop / (ms * 1e-3) / 1e12);
 }
 
+
+// halo-row reuse order (the production loop): per (kw, k-half) group read NT+2 halo rows
+// once and use them for the 3 kh taps.  GROUPS independent wave-groups (own halo each),
+// each WR x WC waves, wave tile (64/WC) co x (16/WR rows).
+template <int WR, int WC, int GROUPS>
+__global__ __launch_bounds__(64 * WR * WC * GROUPS, 1) void k_rows(float* out, int reps) {
+    constexpr int COT = 64, MT = COT / 16 / WC, NT = 16 / WR, NB = NT + 2, NWG = WR * WC;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* wts = smem;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = wave / NWG, wig = wave % NWG;
+    char* halo = smem + 9 * COT * 128 + grp * HALO * HALO * 128;
+    const int wr = wig % WR, wc = wig / WR, q = lane >> 4, c16 = lane & 15;
+    for (int i = tid; i < (9 * COT * 128 + GROUPS * HALO * HALO * 128) / 4; i += blockDim.x)
+        ((unsigned*)smem)[i] = 0x3c003c00u ^ (i * 2654435761u & 0x00ff00ffu);
+    __syncthreads();
+    f32x4 acc[MT][NT];
+    for (int m = 0; m < MT; ++m)
+        for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0, 0, 0, 0};
+    const int arow = wc * MT * 16 + c16;
+    for (int r = 0; r < reps; ++r) {
+        uint4 A0[3][MT], B0[NB], A1[3][MT], B1[NB];
+        auto load = [&](int g, uint4 (&A)[3][MT], uint4 (&Bf)[NB]) {
+            const int kw = g >> 1, kk = g & 1, chunk = kk * 4 + q;
+            const char* hb = halo + hcol(c16 + kw, chunk) + (wr * NT) * (HALO * 128);
+#pragma unroll
+            for (int n = 0; n < NB; ++n) Bf[n] = *(const uint4*)(hb + n * (HALO * 128));
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    A[kh][m] = *(const uint4*)(wts + (kh * 3 + kw) * COT * 128 + swz(arow + m * 16, chunk));
+        };
+        auto run = [&](const uint4 (&A)[3][MT], const uint4 (&Bf)[NB]) {
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n) mma(acc[m][n], A[kh][m], Bf[n + kh]);
+        };
+        load(0, A0, B0);
+#pragma unroll
+        for (int g = 0; g < 6; g += 2) {
+            load(g + 1, A1, B1);
+            __builtin_amdgcn_sched_barrier(0);
+            run(A0, B0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g + 2 < 6) load(g + 2, A0, B0);
+            __builtin_amdgcn_sched_barrier(0);
+            run(A1, B1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    float s = 0;
+    for (int m = 0; m < MT; ++m)
+        for (int n = 0; n < NT; ++n) s += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
+    out[blockIdx.x * blockDim.x + tid] = s;
+}
+
+template <int WR, int WC, int GROUPS>
+void run_rows(const char* name, int ncu, float* out) {
+    const int reps = 200;
+    const size_t lds = 9 * 64 * 128 + GROUPS * HALO * HALO * 128;
+    (void)hipFuncSetAttribute((const void*)k_rows<WR, WC, GROUPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    const int T = 64 * WR * WC * GROUPS;
+    for (int it = 0; it < 3; ++it) hipLaunchKernelGGL((k_rows<WR, WC, GROUPS>), dim3(ncu), dim3(T), lds, 0, out, reps);
+    (void)hipEventRecord(e0);
+    const int N = 10;
+    for (int it = 0; it < N; ++it) hipLaunchKernelGGL((k_rows<WR, WC, GROUPS>), dim3(ncu), dim3(T), lds, 0, out, reps);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const double flop = 2.0 * 256 * 64 * 576 * reps * (double)ncu * GROUPS * N;
+    printf("%-28s %8.3f us/tile  %7.1f TFLOP/s\n", name, ms * 1e3 / N / reps / GROUPS, flop / (ms * 1e-3) / 1e12);
+}
+
 int main() {
     int dev = 0, ncu = 0;
     hipGetDevice(&dev);
@@ -195,6 +276,12 @@ int main() {
     run<4, 1, true>("4 waves MT4 NT4 regA", ncu, out);
     run3<1>("4 waves MT4 NT4 prefetch2", ncu, out, 1);
     run3<2>("2x4 waves MT4 NT4 prefetch2", ncu, out, 1);
+    run_rows<4, 2, 1>("rows 8 waves MT2 NT4", ncu, out);
+    run_rows<4, 1, 1>("rows 4 waves MT4 NT4", ncu, out);
+    run_rows<4, 1, 2>("rows 2x4 waves MT4 NT4", ncu, out);
+    run_rows<2, 2, 1>("rows 4 waves MT2 NT8", ncu, out);
+    run_rows<2, 2, 2>("rows 2x4 waves MT2 NT8", ncu, out);
+    run_rows<4, 2, 2>("rows 2x8 waves MT2 NT4", ncu, out);
     hipFree(out);
     return 0;
 }

@@ -47,16 +47,24 @@ rt = a[..., 0]
 t0 = rt[:, :, 0].min()
 # slot -> label: 0 start, 1 end of start-up, 2+3k / 3+3k / 4+3k: tile k after MFMAs / after
 # epilogue / after the closing barrier; 13, 14: q-kernel start-up (DMA issued, DMA landed)
-labels = {0: "start", 1: "startup", 13: "dma_issued", 14: "dma_landed"}
-for k in range(4):
-    labels.update({2 + 3 * k: f"t{k}_mfma", 3 + 3 * k: f"t{k}_epi", 4 + 3 * k: f"t{k}_bar"})
+labels = {0: "start", 1: "startup"}
+if os.environ.get("FEN_CONV_VARIANT", "0") == "5":   # single-group kernel: 3 stamps per tile
+    for k in range(4):
+        labels.update({2 + 3 * k: f"t{k}_mfma", 3 + 3 * k: f"t{k}_epi", 4 + 3 * k: f"t{k}_bar"})
+else:                                                # ping-pong kernel: 2 stamps per phase
+    for k in range(7):
+        labels.update({2 + 2 * k: f"ph{k}_work", 3 + 2 * k: f"ph{k}_bar"})
 out = {"blocks": int(used.sum()), "waves": nw}
 for i in sorted(labels):
     valid = (rt[:, :, i] != 0).all(axis=1)
     if not valid.any():
         continue
     r = (rt[valid, :, i] - t0) / 100.0          # us since the first start, per wave
-    out[labels[i]] = [round(float(np.median(r.min(1))), 2), round(float(np.median(r.max(1))), 2)]
+    if os.environ.get("FEN_CONV_VARIANT", "0") == "5" or nw < 8:
+        out[labels[i]] = [round(float(np.median(r.min(1))), 2), round(float(np.median(r.max(1))), 2)]
+    else:   # [group A min, max, group B min, max]
+        out[labels[i]] = [round(float(np.median(r[:, :4].min(1))), 2), round(float(np.median(r[:, :4].max(1))), 2),
+                          round(float(np.median(r[:, 4:].min(1))), 2), round(float(np.median(r[:, 4:].max(1))), 2)]
 mt = a[..., 1]
 valid = (rt[:, :, 1] != 0).all(axis=1) & (rt[:, :, 2] != 0).all(axis=1)
 dm = (mt[valid, :, 2] - mt[valid, :, 1]).astype(np.float64)

@@ -1,0 +1,51 @@
+"""Phase timeline of the fused RCAB kernel (diagnostic build with -DFEN_STAMPS).
+  make -C face-super-resolution_amd/csrc stamp
+  FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_stamp.so python tools/stamp_rcab.py
+Prints, per stamp slot, [median over blocks of the earliest wave, of the latest wave] in us
+since the kernel's first stamp."""
+import ctypes, json, os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'face-super-resolution_amd'))
+import numpy as np
+import torch
+from src.hip import lib as L
+from src.hip.net import Weights
+from src.hip.program import Ctx, ptr
+
+B = int(os.environ.get("B", "32")); H = W = 64
+torch.manual_seed(0)
+p = {"conv1.weight": torch.randn(64, 64, 3, 3) * 0.06, "conv1.bias": torch.zeros(64), "prelu.weight": torch.full((64,), .25),
+     "conv2.weight": torch.randn(64, 64, 3, 3) * 0.06, "conv2.bias": torch.zeros(64),
+     "fc1": torch.randn(16, 64) * .3, "fc2": torch.randn(64, 16) * .3}
+pd = {k: v.cuda() for k, v in p.items()}
+ctx = Ctx(torch.bfloat16, 'cuda')
+Wt = Weights(pd, torch.bfloat16, 'cuda')
+x = torch.randn(B, H, W, 64, device='cuda', dtype=torch.bfloat16)
+y = torch.empty_like(x)
+s = torch.empty(B, 64, device='cuda')
+lib = L.load()
+ws = L.RcabWorkspace(B, H, W)
+st = torch.zeros(256 * 8 * 32, dtype=torch.int64, device='cuda')
+d = L.RcabDesc()
+d.dtype, d.B, d.H, d.W, d.C, d.Cr = L.BF16, B, H, W, 64, 16
+d.x, d.w1, d.b1, d.alpha = ptr(x), ptr(Wt.packed("conv1", 0)), ptr(pd["conv1.bias"]), ptr(pd["prelu.weight"])
+d.w2, d.b2, d.fc1, d.fc2 = ptr(Wt.packed("conv2", 0)), ptr(pd["conv2.bias"]), ptr(pd["fc1"]), ptr(pd["fc2"])
+d.res_scale, d.inv_hw = 0.2, 1.0 / (H * W)
+d.y, d.s, d.ws, d.stamps = ptr(y), ptr(s), ws.ptr, ptr(st)
+for _ in range(int(os.environ.get("REPS", "20"))):
+    st.zero_()
+    L.check(lib.fen_rcab_fused(ctypes.byref(d), torch.cuda.current_stream().cuda_stream), "rcab")
+torch.cuda.synchronize()
+assert lib.fen_rcab_workspace_status(ws.ptr, B, H, W) == 0
+a = st.view(256, 8, 32).cpu().numpy().astype(np.int64)
+used = a[:, 0, 0] != 0
+a = a[used]
+t0 = a[:, :, 0][a[:, :, 0] > 0].min()
+out = {"blocks": int(used.sum())}
+for i in range(32):
+    v = a[:, :, i]
+    ok = (v > 0).all(axis=1)
+    if not ok.any():
+        continue
+    r = (v[ok] - t0) / 100.0
+    out[str(i)] = [round(float(np.median(r.min(1))), 2), round(float(np.median(r.max(1))), 2)]
+print(json.dumps(out))
