@@ -100,6 +100,20 @@ template <> __device__ __forceinline__ void mma16<float>(f32x4& acc, const uint4
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
 }
 
+// PReLU in arithmetic form (torch's own definition: max(0,v) + a*min(0,v)) and its backward
+// factor; written without a data-dependent select so hipcc never turns them into exec-masked
+// branches that sink an operand's pending LDS/global read into the branch (measured: a
+// 48-element epilogue became ~1000 instructions and ~2 us).
+__device__ __forceinline__ float prelu_f(float v, float a) { return fmaxf(v, 0.f) + a * fminf(v, 0.f); }
+__device__ __forceinline__ float pos_step(float v) { return v > 0.f ? 1.f : 0.f; }
+// dy * dPReLU(pre)/dpre = dy * (pre > 0 ? 1 : a)
+__device__ __forceinline__ float prelu_bwd_f(float dy, float pre, float a) {
+    const float s = pos_step(pre);
+    return dy * (s + (1.f - s) * a);
+}
+// contribution to dL/da: dy * pre where pre <= 0
+__device__ __forceinline__ float prelu_dalpha_f(float dy, float pre) { return dy * pre * (1.f - pos_step(pre)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

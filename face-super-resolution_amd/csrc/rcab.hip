@@ -18,12 +18,14 @@
 //     activation images;
 //   * conv1 (21 pixel fragments: 18 rows of 16 + 3 fragments of the 2 edge columns) ->
 //     bias + PReLU -> a1 image in LDS; conv2 reads it with the halo-row-reuse MFMA order;
-//   * t stays in registers.  The tile's pool partial goes to global memory, then the block
-//     arrives on its image's counter; the LAST arriver computes the gate (FC-ReLU-FC-
-//     sigmoid) and publishes it (agent-scope release/acquire, MI355X_MICROARCH.md
-//     'Workgroup dispatch ... inter-workgroup visibility').  Every tile applies
-//     y = t*s*rs + x one phase into its NEXT tile (the gate is ready by then), or right
-//     away for its last tile.  The counters clean themselves up, so a hipGraph can replay.
+//   * t stays in registers.  The tile's pool partial goes to an uncached workspace, then
+//     the block arrives on its image's counter (MI355X_MICROARCH.md 'inter-workgroup
+//     visibility': the per-XCD L2s are not coherent, so the hand-off bypasses them).
+//     One phase boundary into its NEXT tile, wave 0 polls the counter, sums the image's
+//     partials in a fixed order (deterministic), computes the gate (FC-ReLU-FC-sigmoid)
+//     into LDS, and after the next barrier every wave applies y = t*s*rs + x; the last
+//     tile does the same right away.  The counters clean themselves up (the last reader
+//     of an image resets them), so a hipGraph can replay the launch.
 #include "fen_common.h"
 
 namespace {
@@ -33,6 +35,7 @@ constexpr int XH_BYTES = XW * XW * 128;      // 51200 = 50 DMA pieces
 constexpr int XH_DMA = XH_BYTES / 1024;
 constexpr int EH_BYTES = XW * 4 * 128;       // halo columns 16..19 again, row-keyed: 10 pieces
 constexpr int EH_DMA = EH_BYTES / 1024;
+constexpr int HALO_W = (XH_DMA + EH_DMA) / 8;   // halo pieces per wave (+1 for the first waves)
 constexpr int A1W = 18;                      // a1 image = conv2 halo, 18x18, hcol layout
 constexpr int A1_BYTES = A1W * A1W * 128;    // 41472
 constexpr int TAP_BYTES = 64 * 128;          // one filter tap [64 co][64 ci] bf16
@@ -49,13 +52,13 @@ static_assert(RCAB_LDS <= 163840, "LDS budget");
 static_assert(O_RING % 16 == 0 && O_RED % 16 == 0 && O_FC % 16 == 0, "alignment");
 
 // diagnostic build (-DFEN_STAMPS): s_memrealtime per wave at phase points into d.stamps,
-// [block][wave][32]; the product build executes none of it
+// [block][wave][48]; the product build executes none of it
 #ifdef FEN_STAMPS
 #define RSTAMP(i)                                                                            \
     do {                                                                                     \
         unsigned long long _rt;                                                              \
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt)::"memory");      \
-        if (d.stamps && lane == 0 && (i) < 32) d.stamps[((size_t)blockIdx.x * 8 + wave) * 32 + (i)] = _rt; \
+        if (d.stamps && lane == 0 && (i) < 48) d.stamps[((size_t)blockIdx.x * 8 + wave) * 48 + (i)] = _rt; \
     } while (0)
 #else
 #define RSTAMP(i) \
@@ -63,7 +66,9 @@ static_assert(O_RING % 16 == 0 && O_RED % 16 == 0 && O_FC % 16 == 0, "alignment"
     } while (0)
 #endif
 
-constexpr unsigned POLL_MAX = 1u << 22;      // ~0.5 s of s_sleep: a gate that never comes
+constexpr int MAX_GRID = 1024;               // start-flag slots (grid <= CUs)
+constexpr int CP_SC = 17;                     // buffer cache policy sc0|sc1: straight to memory
+constexpr unsigned POLL_MAX = 1u << 20;      // ~0.5 s of s_sleep: a gate that never comes
                                              // sets sync[3*B] and the kernel exits anyway
 
 // 16-B chunk position in the edge image: pixel e = row*4 + col', key = row & 7 (an edge
@@ -72,9 +77,12 @@ __device__ __forceinline__ int ekey(int row, int chunk) { return (chunk ^ (row &
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// agent-scope flag helpers (hipMalloc'd sync words)
-__device__ __forceinline__ int ld_acquire_poll(const int* p) {
+// sync-word access (uncached workspace: every load / store goes to memory)
+__device__ __forceinline__ int ld_poll(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------
@@ -193,13 +201,21 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     const int nslot = gridDim.x;
     const int nmine = (ntiles - (int)blockIdx.x + nslot - 1) / nslot;
     // workspace (fen_rcab_workspace_alloc: uncached, so every access of the cross-block
-    // hand-off goes to memory -- the per-XCD L2s are not coherent): part [B*tpi][64] | gate
-    // [B][64] (unused) | cnt [B] | (unused) [B] | ack [B] | err
+    // hand-off goes to memory -- the per-XCD L2s are not coherent):
+    //   part  [tpi][B][64]  tile partial sums, image-interleaved so that one image's rows
+    //                       lie B*256 B apart (spread over many HBM channels, not one hot 16 KB)
+    //   tflag [tpi][B]      tile arrival flags (= launch epoch + 1 once the partial landed)
+    //   sflag [MAX_GRID]    block start flags (= epoch + 1 once the block has read the epoch)
+    //   epoch, err
+    // No atomics and no resets: flags only ever move to the current epoch + 1, and block 0
+    // advances the epoch at its end, once every block of the launch has read it.
     float* part = (float*)d.ws;
-    float* gate = part + (size_t)ntiles * 64;
-    int* cnt = (int*)(gate + (size_t)B * 64);         // [B] arrivals
-    int* ack = cnt + 2 * B;                           // [B] partials consumed
-    int* err = cnt + 3 * B;                           // [1] poll timeout
+    int* tflag = (int*)(part + (size_t)ntiles * 64);
+    int* sflag = tflag + ntiles;
+    int* epoch = sflag + MAX_GRID;
+    int* err = epoch + 1;
+    const __amdgpu_buffer_rsrc_t partr =
+        __builtin_amdgcn_make_buffer_rsrc(part, 0, (int)((size_t)ntiles * 256), 0x00020000);
 
     const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)B * H * W * 128));
     const i32x4 w1r = make_rsrc(d.w1, 9u * 64u * 128u);
@@ -252,10 +268,14 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         cst[64 + tid] = d.alpha[tid];
         cst[128 + tid] = d.b2[tid];
     }
-    for (int i = tid; i < 1024; i += 512) {
-        fcs[i] = i < Cr * 64 ? d.fc1[i] : 0.f;          // [Cr][64]
-        fcs[1024 + i] = i < Cr * 64 ? d.fc2[i] : 0.f;   // [64][Cr]
+    for (int i = tid; i < 1024; i += 512) {           // both zero-padded to 16 hidden units
+        fcs[i] = i < Cr * 64 ? d.fc1[i] : 0.f;          // [16][64]
+        const int c = i >> 4, j = i & 15;
+        fcs[1024 + i] = j < Cr ? d.fc2[c * Cr + j] : 0.f;   // [64][16]
     }
+    // this launch's epoch; announce that this block has read it
+    const int ep1 = __builtin_amdgcn_readfirstlane(ld_poll(epoch)) + 1;
+    if (tid == 0) st_flag(sflag + blockIdx.x, ep1);
     RSTAMP(0);
     issue_taps(0);
     issue_halo(blockIdx.x);
@@ -276,67 +296,121 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     edge_bases(1, c16, q, eb5);
     const int arow1 = ch * 32 + c16;                  // A row (co) of conv1's wave
     const int arow2 = wc * 32 + c16;
+    // conv1 epilogue addressing, fixed per lane: a1-image byte offsets of slot 0 (main rows:
+    // + f * 2304) and of slots 4, 5 (main row 4 or an edge fragment; edge pad lanes write a
+    // dummy word), and each slot's (row, column) in a1 coordinates
+    const int ar4 = main4 ? row0 + 4 : 8 * (g == 2 ? 2 : 0) + (c16 >> 1), ac4 = main4 ? c16 : 16 + (c16 & 1);
+    const int ar5 = 8 + (c16 >> 1), ac5 = 16 + (c16 & 1);
+    int a1m[2], a1o4[2], a1o5[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int chunk = ch * 4 + 2 * m + (q >> 1);
+        a1m[m] = (row0 * A1W + c16) * 128 + ((chunk ^ (c16 & 7)) << 4) + (q & 1) * 8;
+        a1o4[m] = ar4 <= 17 ? (ar4 * A1W + ac4) * 128 + ((chunk ^ (ac4 & 7)) << 4) + (q & 1) * 8 : O_FLAG - O_A1;
+        a1o5[m] = (ar5 * A1W + ac5) * 128 + ((chunk ^ (ac5 & 7)) << 4) + (q & 1) * 8;
+    }
 
     uint2 tcar[2][4];                                 // t (bf16) of the tile awaiting its gate
+    int arrive_f = -1;                                // tile flag still to be raised
+    auto arrive = [&]() {                             // after an s_waitcnt vmcnt(0) of wave 0
+        if (arrive_f >= 0 && tid == 0) st_flag(tflag + arrive_f, ep1);
+        arrive_f = -1;
+    };
     int pend_t = -1;                                  // that tile (-1: none)
 
-    // y = t * s * rs + x for tile `pt` (t in tcar); wave-uniform poll of the image's gate
-    // The SE gate of image b, computed by every wave that needs it once all tpi partials of
-    // the image have arrived (poll the arrival counter, then read the partials; uncached
-    // workspace, so no fences): mean -> FC1 -> ReLU -> FC2 -> sigmoid.  Lane c ends with
-    // mean[c], hid (lane j < Cr), s[c].  Deterministic: fixed-order sums.
-    auto se_gate = [&](int b, float& mean, float& hid_mine) -> float {
-        if (lane == 0) {
+    // The SE gate of image b, by wave 0 alone, into LDS (gsh[0..63] = s, read by every wave
+    // after the next barrier).  Poll the arrival counter, read the image's tpi partials with
+    // 16-B uncached loads (4 rows per instruction), fixed-order sums, mean -> FC1 -> ReLU ->
+    // FC2 -> sigmoid; `first` tiles write the user copies.
+    float* gsh = red;                                 // s of the pending tile (red is free then)
+    auto gate_to_lds = [&](int b, bool first, int sb) {
+        {   // every tile of the image has raised its flag (lane i watches tiles i, i+64, ..)
             unsigned it = 0;
-            while (ld_acquire_poll(cnt + b) < tpi && ++it < POLL_MAX) __builtin_amdgcn_s_sleep(1);
-            if (it >= POLL_MAX) atomicExch(err, 1);
+            for (;;) {
+                bool mine = true;
+                for (int i = lane; i < tpi; i += 64) mine &= ld_poll(tflag + i * B + b) == ep1;
+                if (__all(mine) || ++it >= POLL_MAX) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (it >= POLL_MAX && lane == 0) st_flag(err, 1);
         }
-        float sm = 0.f;                       // 16 loads in flight per lane, fixed order
-        const float* pp = part + (size_t)b * tpi * 64 + lane;
-        int i = 0;
-        for (; i + 16 <= tpi; i += 16) {
-            float v[16];
+        RSTAMP(sb);
+        const int rg = lane >> 4, c4 = (lane & 15) * 4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        asm volatile("" ::: "memory");                // the loads stay behind the poll
+        for (int r0 = 0; r0 < tpi; r0 += 16) {
+            unsigned __attribute__((ext_vector_type(4))) v[4];
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                v[j] = __hip_atomic_load(pp + (size_t)(i + j) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int j = 0; j < 4; ++j) {
+                const int r = min(r0 + 4 * j + rg, tpi - 1);
+                v[j] = __builtin_amdgcn_raw_buffer_load_b128(partr, ((r * B + b) * 64 + c4) * 4, 0, CP_SC);
+            }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) sm += v[j];
+            for (int j = 0; j < 4; ++j) {
+                if (r0 + 4 * j + rg < tpi) {
+                    acc.x += __uint_as_float(v[j][0]); acc.y += __uint_as_float(v[j][1]);
+                    acc.z += __uint_as_float(v[j][2]); acc.w += __uint_as_float(v[j][3]);
+                }
+            }
         }
-        for (; i < tpi; ++i) sm += __hip_atomic_load(pp + (size_t)i * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mean = sm * d.inv_hw;
-        hid_mine = 0.f;
-        for (int j = 0; j < Cr; ++j) {
-            const float v = wave_sum(fcs[j * 64 + lane] * mean);
-            if (lane == j) hid_mine = fmaxf(v, 0.f);
+        RSTAMP(sb + 1);
+        // fold the 4 row groups through LDS (red[4][64] -> mean in red[0..63]), then
+        // FC1: lane = (part, j) dots 16 channels of mean with fc1 row j, two xor folds;
+        // FC2: lane c dots the 16 (zero-padded) hidden units with fc2 row c.  A handful of
+        // dependent LDS round trips instead of a wave reduction per hidden unit.
+        *(float4*)(red + rg * 64 + c4) = acc;
+        const float mean = ((red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane])) * d.inv_hw;
+        red[lane] = mean;
+        const int j = lane & 15, part4 = lane >> 4;
+        float h = 0.f;
+#pragma unroll
+        for (int c = 0; c < 16; c += 4) {
+            const float4 w = *(const float4*)(fcs + j * 64 + part4 * 16 + c);
+            const float4 m = *(const float4*)(red + part4 * 16 + c);
+            h += w.x * m.x + w.y * m.y + w.z * m.z + w.w * m.w;
         }
+        h += __shfl_xor(h, 16, 64);
+        h += __shfl_xor(h, 32, 64);
+        const float hid_mine = fmaxf(h, 0.f);         // hidden unit j (0 for j >= Cr)
+        if (lane < 16) red[64 + lane] = hid_mine;
         float z = 0.f;
-        for (int j = 0; j < Cr; ++j) z += fcs[1024 + lane * Cr + j] * __shfl(hid_mine, j, 64);
-        return 1.f / (1.f + expf(-z));
-    };
-
-    // y = t * s * rs + x for tile `pt` (t in tcar)
-    auto apply = [&](int pt) {
-        const int b = pt / tpi, tile = pt - b * tpi;
-        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        float mean, hid_mine;
-        const float sg = se_gate(b, mean, hid_mine);
-        if (tile == 0 && wave == 0) {         // the user-visible copies, once per image
+#pragma unroll
+        for (int c = 0; c < 16; c += 4) {
+            const float4 w = *(const float4*)(fcs + 1024 + lane * 16 + c);
+            const float4 hv = *(const float4*)(red + 64 + c);
+            z += w.x * hv.x + w.y * hv.y + w.z * hv.z + w.w * hv.w;
+        }
+        const float sg = 1.f / (1.f + __expf(-z));
+        gsh[lane] = sg;
+        RSTAMP(sb + 2);
+        if (first) {                                  // the user-visible copies, once per image
             d.s[(size_t)b * 64 + lane] = sg;
             if (d.mean) d.mean[(size_t)b * 64 + lane] = mean;
             if (d.hid && lane < Cr) d.hid[(size_t)b * Cr + lane] = hid_mine;
         }
-        const float rs = d.res_scale;
-        float sv[2][4];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sv[m][r] = __shfl(sg, wc * 32 + m * 16 + 4 * q + r, 64) * rs;
-        uint2 xv[2][4];
+    };
+
+    // y = t * s * rs + x for tile `pt` (t in tcar, s in gsh)
+    uint2 xv[2][4];
+    auto load_x = [&](int pt) {
+        const int b = pt / tpi, tile = pt - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
             const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
 #pragma unroll
             for (int m = 0; m < 2; ++m) xv[m][n] = *(const uint2*)((const char*)d.x + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2);
+        }
+    };
+    auto apply = [&](int pt) {                        // after load_x(pt)
+        const int b = pt / tpi, tile = pt - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const float rs = d.res_scale;
+        float sv[2][4];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const float4 s4 = *(const float4*)(gsh + wc * 32 + m * 16 + 4 * q);
+            sv[m][0] = s4.x * rs; sv[m][1] = s4.y * rs; sv[m][2] = s4.z * rs; sv[m][3] = s4.w * rs;
         }
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
@@ -349,17 +423,6 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                 o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xv[m][n].y << 16);
                 o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xv[m][n].y & 0xffff0000u);
                 st4<bf16>((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
-            }
-        }
-    };
-    // after every wave of the block has read the image's partials: the last of its tiles
-    // resets the image's counters for the next launch
-    auto acknowledge = [&](int pt) {
-        if (tid == 0) {
-            const int b = pt / tpi;
-            if (atomicAdd(ack + b, 1) == tpi - 1) {
-                __hip_atomic_store(cnt + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(ack + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     };
@@ -381,6 +444,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             if (p > 0 || k > 0) {
                 if (k < 2) RSTAMP(2 + k * 14 + p * 2);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this phase's taps (+ halo) landed
+                arrive();                                          // ... and the last tile's partial
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 if (k < 2) RSTAMP(3 + k * 14 + p * 2);
@@ -395,54 +459,76 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             conv1_phase(acc1, xh, eh, tapp, p, mbase, e4, e5, main4, has5, arow1, q);
         }
         if (k == 0) RSTAMP(15);
-        // ---- conv1 epilogue: bias + PReLU -> a1 image (zero outside the image); training
-        //      copies of z1 / a1 for the backward (the 16x16 interior)
+        // ---- conv1 epilogue: bias + PReLU -> a1 image (zero outside the image; branch-free,
+        //      precomputed offsets); training copies of z1 / a1 for the backward (16x16 interior)
         {
-            const int nf = has5 ? 6 : 5;
+            const bool colok = (unsigned)(w0 - 1 + c16) < (unsigned)W;
+            const bool ok4 = (unsigned)(h0 - 1 + ar4) < (unsigned)H && (unsigned)(w0 - 1 + ac4) < (unsigned)W;
+            const bool ok5 = (unsigned)(h0 - 1 + ar5) < (unsigned)H && (unsigned)(w0 - 1 + ac5) < (unsigned)W;
+            float zs[2][6][4];
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 const float4 bb = *(const float4*)(cst + ch * 32 + m * 16 + 4 * q);
                 const float4 aa = *(const float4*)(cst + 64 + ch * 32 + m * 16 + 4 * q);
                 const float bia[4] = {bb.x, bb.y, bb.z, bb.w}, alp[4] = {aa.x, aa.y, aa.z, aa.w};
-                const int co = ch * 32 + m * 16 + 4 * q;
 #pragma unroll
                 for (int f = 0; f < 6; ++f) {
-                    if (f >= nf) continue;
-                    int ar, ac;
-                    const bool edge = f >= 4 && !main4;
-                    if (!edge) {
-                        ar = row0 + f;
-                        ac = c16;
-                    } else {
-                        const int eidx = g == 2 ? 2 : f - 4;
-                        ar = 8 * eidx + (c16 >> 1);
-                        ac = 16 + (c16 & 1);
-                        if (ar > 17) continue;
-                    }
-                    const int gh = h0 - 1 + ar, gw = w0 - 1 + ac;
-                    const bool in = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-                    float z[4], a[4];
+                    bool ok;
+                    if (f < 4) ok = colok && (unsigned)(h0 - 1 + row0 + f) < (unsigned)H;
+                    else ok = f == 4 ? ok4 : ok5;
+                    const float okf = ok ? 1.f : 0.f;
+                    float a[4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        z[r] = acc1[m][f][r] + bia[r];
-                        a[r] = in ? (z[r] > 0.f ? z[r] : alp[r] * z[r]) : 0.f;
+                        const float z = acc1[m][f][r] + bia[r];
+                        zs[m][f][r] = z;
+                        a[r] = okf * prelu_f(z, alp[r]);
                     }
-                    const int chunk = co >> 3;
-                    st4<bf16>(a1s + (ar * A1W + ac) * 128 + ((chunk ^ (ac & 7)) << 4) + (q & 1) * 8, a);
-                    if (d.z1 && ar >= 1 && ar <= 16 && ac >= 1 && ac <= 16) {
-                        const size_t o = ((size_t)(b * H + gh) * W + gw) * 64 + co;
-                        st4<bf16>((char*)d.z1 + o * 2, z);
+                    const int off = f < 4 ? a1m[m] + f * (A1W * 128) : f == 4 ? a1o4[m] : a1o5[m];
+                    if (f < 5 || has5) st4<bf16>(a1s + off, a);
+                }
+            }
+            if (d.z1) {
+                // interior pixels only (a1 rows / cols 1..16); exec-masked stores, training only
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const float4 aa = *(const float4*)(cst + 64 + ch * 32 + m * 16 + 4 * q);
+                    const float alp[4] = {aa.x, aa.y, aa.z, aa.w};
+#pragma unroll
+                    for (int f = 0; f < 6; ++f) {
+                        const int ar = f < 4 ? row0 + f : f == 4 ? ar4 : ar5;
+                        const int ac = f < 4 ? c16 : f == 4 ? ac4 : ac5;
+                        if (!(f < 5 || has5) || ar < 1 || ar > 16 || ac < 1 || ac > 16) continue;
+                        const size_t o = ((size_t)(b * H + h0 - 1 + ar) * W + w0 - 1 + ac) * 64 + ch * 32 + m * 16 + 4 * q;
+                        float a[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) a[r] = prelu_f(zs[m][f][r], alp[r]);
+                        st4<bf16>((char*)d.z1 + o * 2, zs[m][f]);
                         st4<bf16>((char*)d.a1 + o * 2, a);
                     }
                 }
             }
         }
-        // previous tile: its gate is ready by now (its round ended a conv1 ago)
+        // the pending tile's gate (its round ended a conv1 ago): wave 0 -> LDS
+        if (pend_t >= 0 && wave == 0) gate_to_lds(pend_t / tpi, pend_t % tpi == 0, 32);
         if (k < 2) RSTAMP(8 + k * 14);
-        __builtin_amdgcn_sched_barrier(0);
-        if (pend_t >= 0) apply(pend_t);
-        __builtin_amdgcn_sched_barrier(0);
+        // ---- phase-3 boundary: a1 image + gate published; apply the pending tile before the
+        //      conv2 accumulators come alive (keeps the register peak at the MFMA loops)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
         if (k < 2) RSTAMP(9 + k * 14);
+        // vmcnt counts in issue order: the apply's residual loads go out before the next
+        // tile's halo so that they do not wait for it, and phase 4 waits for its taps only
+        // (vmcnt = this wave's halo pieces), leaving the halo in flight until phase 5
+        issue_taps(k * 6 + 4);
+        if (pend_t >= 0) {
+            load_x(pend_t);
+            apply(pend_t);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bool halo_next = k + 1 < nmine;
+        if (halo_next) issue_halo(t + nslot);       // conv1 is done with xh / eh
         // ================= conv2: phases 3..5 =================
         f32x4 acc2[2][4];
 #pragma unroll
@@ -452,14 +538,19 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 #pragma unroll 1
         for (int p = 3; p < 6; ++p) {
             const int P = k * 6 + p;
-            if (k < 2 && p == 3) RSTAMP(10 + k * 14);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            if (k < 2 && p == 3) RSTAMP(11 + k * 14);
-            if (p == 4 && pend_t >= 0) acknowledge(pend_t);   // every wave has applied it (barrier above)
-            if (!(k + 1 == nmine && p == 5)) issue_taps(P + 1);
-            if (p == 3 && k + 1 < nmine) issue_halo(t + nslot);   // conv1 is done with xh / eh
+            if (p > 3) {
+                if (k < 2 && p == 4) RSTAMP(10 + k * 14);
+                if (p == 4 && halo_next) {
+                    if (wave < (XH_DMA + EH_DMA) % 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HALO_W + 1) : "memory");
+                    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HALO_W) : "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (k < 2 && p == 4) RSTAMP(11 + k * 14);
+                if (!(k + 1 == nmine && p == 5)) issue_taps(P + 1);
+            }
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
                                    ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
             conv2_phase(acc2, a1s, tapp, p - 3, wr, arow2, q, c16);
@@ -499,13 +590,13 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         __builtin_amdgcn_s_barrier();
         if (k < 2) RSTAMP(13 + k * 14);
         if (wave == 0) {
-            // tile partial -> uncached workspace, drained, then the arrival
-            __hip_atomic_store(part + (size_t)t * 64 + lane,
+            // tile partial -> uncached workspace; the arrival is counted after the next
+            // phase boundary's vmcnt(0) has drained this store (no stall here)
+            __hip_atomic_store(part + ((size_t)tile * B + b) * 64 + lane,
                                (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) atomicAdd(cnt + b, 1);
         }
+        arrive_f = tile * B + b;
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -517,13 +608,31 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         if (k < 2) RSTAMP(14 + k * 14);
     }
     // the last tile: its gate comes from this round's other tiles
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    arrive();
     RSTAMP(30);
     if (pend_t >= 0) {
-        apply(pend_t);
-        RSTAMP(31);
+        load_x(pend_t);                               // the residual is in flight during the gate
+        if (wave == 0) gate_to_lds(pend_t / tpi, pend_t % tpi == 0, 35);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        acknowledge(pend_t);
+        apply(pend_t);
+        RSTAMP(31);
+    }
+    // block 0 advances the epoch once every block has read it (the next launch on the stream
+    // cannot start before this block ends)
+    if (blockIdx.x == 0 && wave == 0) {
+        unsigned it = 0;
+        for (;;) {
+            bool mine = true;
+            for (int i = lane; i < nslot; i += 64) mine &= ld_poll(sflag + i) == ep1;
+            if (__all(mine) || ++it >= POLL_MAX) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (lane == 0) {
+            if (it >= POLL_MAX) st_flag(err, 1);
+            st_flag(epoch, ep1);
+        }
     }
     (void)lflag;
 }
@@ -533,7 +642,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 extern "C" size_t fen_rcab_workspace_bytes(int B, int H, int W) {
     if (B <= 0 || H <= 0 || W <= 0) return 0;
     const size_t nt = (size_t)B * (H / 16) * (W / 16);
-    return (nt * 64 + (size_t)B * 64) * sizeof(float) + ((size_t)3 * B + 1) * sizeof(int);
+    return nt * 64 * sizeof(float) + (nt + MAX_GRID + 2) * sizeof(int);
 }
 
 // The one allocation the library makes: the fused RCAB's hand-off workspace must be uncached
@@ -552,21 +661,24 @@ extern "C" int fen_rcab_workspace_alloc(int B, int H, int W, void** ws) {
     *ws = p;
     return FEN_OK;
 }
-// Diagnostic (synchronises the device): number of non-zero sync words left in the workspace
-// (0 after every completed launch; the last word is the poll-timeout flag), or < 0 on error.
+// Diagnostic (synchronises the device): after a completed launch of shape (B, H, W) every
+// tile flag equals the epoch and the poll-timeout word is 0; returns the number of words
+// that break this (0 = healthy), or < 0 on error.
 extern "C" int fen_rcab_workspace_status(const void* ws, int B, int H, int W) {
-    if (!ws || B <= 0) return FEN_EINVAL;
+    if (!ws || B <= 0 || H < 16 || W < 16) return FEN_EINVAL;
     const size_t nt = (size_t)B * (H / 16) * (W / 16);
-    const size_t off = (nt * 64 + (size_t)B * 64) * sizeof(float);
-    const size_t n = (size_t)3 * B + 1;
+    const size_t n = nt + MAX_GRID + 2;
     int* h = (int*)malloc(n * sizeof(int));
     if (!h) return FEN_EINVAL;
-    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h, (const char*)ws + off, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h, (const char*)ws + nt * 64 * sizeof(float), n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
         free(h);
         return FEN_EHIP;
     }
-    int c = 0;
-    for (size_t i = 0; i < n; ++i) c += h[i] != 0;
+    const int ep = h[nt + MAX_GRID];
+    int c = ep == 0 ? 1 : 0;
+    for (size_t i = 0; i < nt; ++i) c += h[i] != ep;
+    c += h[nt + MAX_GRID + 1] != 0;
     free(h);
     return c;
 }
@@ -604,6 +716,7 @@ extern "C" int fen_rcab_fused(const fen_rcab_desc* d, void* stream) {
     const int ntiles = d->B * tpi;
     int grid = (ncu / tpi) * tpi;                      // rounds of whole images
     if (grid > ntiles) grid = ntiles;
+    if (grid > MAX_GRID) grid = (MAX_GRID / tpi) * tpi;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_rcab, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);

@@ -172,10 +172,10 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
                 }
             const size_t pi = ((size_t)(b * H + h0 + sh) * W + w0 + sw) * C + 2 * k;
             const float p0 = tof<T>(pre[pi]), p1 = tof<T>(pre[pi + 1]);
-            dal0 += p0 > 0.f ? 0.f : da0 * p0;
-            dal1 += p1 > 0.f ? 0.f : da1 * p1;
-            out[t] = p0 > 0.f ? da0 : da0 * al0;
-            out[4 + t] = p1 > 0.f ? da1 : da1 * al1;
+            dal0 += prelu_dalpha_f(da0, p0);
+            dal1 += prelu_dalpha_f(da1, p1);
+            out[t] = prelu_bwd_f(da0, p0, al0);
+            out[4 + t] = prelu_bwd_f(da1, p1, al1);
         }
         char* o = (char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 8 * k) * sizeof(T);
         if constexpr (sizeof(T) == 2) {
@@ -527,10 +527,10 @@ __global__ __launch_bounds__(256) void k_prelu_bwd_unshuffle(int B, int H, int W
             const size_t pi = ((size_t)(b * H + 2 * gh2 + (t >> 1)) * W + 2 * gw2 + (t & 1)) * C + 2 * k;
             const float d0 = tof<T>(dy[pi]), d1 = tof<T>(dy[pi + 1]);
             const float p0 = tof<T>(pre[pi]), p1 = tof<T>(pre[pi + 1]);
-            dal0 += p0 > 0.f ? 0.f : d0 * p0;
-            dal1 += p1 > 0.f ? 0.f : d1 * p1;
-            out[t] = p0 > 0.f ? d0 : d0 * al0;
-            out[4 + t] = p1 > 0.f ? d1 : d1 * al1;
+            dal0 += prelu_dalpha_f(d0, p0);
+            dal1 += prelu_dalpha_f(d1, p1);
+            out[t] = prelu_bwd_f(d0, p0, al0);
+            out[4 + t] = prelu_bwd_f(d1, p1, al1);
         }
         char* o = (char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 8 * k) * sizeof(T);
         if constexpr (sizeof(T) == 2) {

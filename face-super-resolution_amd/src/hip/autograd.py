@@ -60,6 +60,7 @@ class Runtime:
         self.dtype = dtype
         self.module = module
         self.weights = None
+        self.shared: dict = {}            # eager contexts' long-lived state (fused-RCAB workspace)
 
     def wt(self, device) -> LiveWeights:
         if self.weights is None or self.weights.device != device:
@@ -68,7 +69,7 @@ class Runtime:
         return self.weights
 
     def ctx(self, device) -> Ctx:
-        return Ctx(self.dtype, device)
+        return Ctx(self.dtype, device, shared=self.shared)
 
 
 def _check_input(x: torch.Tensor):

@@ -50,9 +50,9 @@ class NetSpec:
                        res_scale=float(cfg.res_scale), in_ch=cfg.in_channels, out_ch=cfg.out_channels)
 
 
-# fused RCAB forward (fen_rcab_fused) where supported (FEN_RCAB_FUSED=1); default: the per-op
-# launches until the fused kernel is the faster of the two on MI355X (tools/bench_rcab.py)
-FUSED_RCAB = os.environ.get("FEN_RCAB_FUSED", "0") != "0"
+# fused RCAB forward (fen_rcab_fused, one launch per RCAB) where supported; FEN_RCAB_FUSED=0
+# selects the per-op launches (B=32 64x64: 46.7 vs 52.0 us per RCAB, tools/bench_rcab.py)
+FUSED_RCAB = os.environ.get("FEN_RCAB_FUSED", "1") != "0"
 
 
 def tiles(H: int, W: int) -> int:

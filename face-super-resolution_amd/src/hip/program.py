@@ -21,7 +21,7 @@ def current_stream_handle() -> int:
 
 
 class Ctx:
-    def __init__(self, dtype: torch.dtype, device, record: bool = False):
+    def __init__(self, dtype: torch.dtype, device, record: bool = False, shared: Optional[dict] = None):
         self.tdtype = dtype
         self.code = L.dtype_code(dtype)
         self.device = torch.device(device)
@@ -30,6 +30,8 @@ class Ctx:
         self._scratch: Dict[str, torch.Tensor] = {}
         self._hold: List[torch.Tensor] = []   # replaced scratch buffers still referenced by ops
         self.lib = L.load()
+        # long-lived state shared by short-lived eager contexts (the fused-RCAB workspace)
+        self._shared = {} if shared is None else shared
 
     # ---- memory ----
     def alloc(self, shape, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
@@ -74,15 +76,16 @@ class Ctx:
         return buf[:n].view(tuple(shape))
 
     def rcab_workspace(self, B: int, H: int, W: int):
-        """The fused-RCAB hand-off workspace for this program (one per program, grown on
-        demand; launches in one program run one at a time on one stream)."""
-        ws = getattr(self, "_rcab_ws", None)
+        """The fused-RCAB hand-off workspace (grown on demand).  One per program -- or per
+        owner of `shared` for eager contexts: launches that share one must run one at a time
+        (one stream), which a program's replay and a module's forward both do."""
+        ws = self._shared.get("rcab_ws")
         need = self.lib.fen_rcab_workspace_bytes(B, H, W)
         if ws is None or ws.nbytes < need:
             if ws is not None:
                 self._hold.append(ws)
             ws = L.RcabWorkspace(B, H, W)
-            self._rcab_ws = ws
+            self._shared["rcab_ws"] = ws
         return ws
 
     def keep(self, obj) -> None:

@@ -72,12 +72,11 @@ def test_fused_rcab(B, H, W, train):
                                 "channel_attention.")
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV, torch.bfloat16)
     y, sv, ctx = _run(p, xd, train, True, twice=True)
-    assert "rcab_fused" in [op[0] for op in ctx.ops] or not ctx.record
     out = y.float().cpu().permute(0, 3, 1, 2)
     assert _rel(out, ref) <= 5e-3
     assert float((sv["s"].cpu() - s_ref).abs().max()) <= 2e-3
     lib = L.load()
-    assert lib.fen_rcab_workspace_status(ctx._rcab_ws.ptr, B, H, W) == 0, \
+    assert lib.fen_rcab_workspace_status(ctx._shared["rcab_ws"].ptr, B, H, W) == 0, \
         "sync words must be left zeroed (self-cleaning, no poll timeout)"
     if train:
         yu, svu, _ = _run(p, xd, True, False)
@@ -104,8 +103,14 @@ def test_fused_rcab_graph_replay():
     ctx = Ctx(torch.bfloat16, DEV, record=True)
     fw = Forward(NetSpec(C=64, G=1, NB=1, Cr=16), ctx, Weights(p, torch.bfloat16, DEV), save=False)
     h = x
-    for i in range(10):
-        h, _ = fw.rcab(h, "", out=ctx.scratch(f"pp{i & 1}", x.shape))
+    old = net.FUSED_RCAB
+    net.FUSED_RCAB = True
+    try:
+        for i in range(10):
+            h, _ = fw.rcab(h, "", out=ctx.scratch(f"pp{i & 1}", x.shape))
+    finally:
+        net.FUSED_RCAB = old
+    assert sum(op[0] == "rcab_fused" for op in ctx.ops) == 10
     ctx.run()
     torch.cuda.synchronize()
     ref = h.clone()
@@ -129,4 +134,4 @@ def test_fused_rcab_graph_replay():
     finally:
         net.FUSED_RCAB = old
     assert _rel(ref.float(), h2.float()) <= 1e-2
-    assert L.load().fen_rcab_workspace_status(ctx._rcab_ws.ptr, B, H, W) == 0
+    assert L.load().fen_rcab_workspace_status(ctx._shared["rcab_ws"].ptr, B, H, W) == 0

@@ -63,6 +63,9 @@ res["last_us"] = round(us, 2); res["last_GBs"] = round(y1.numel() * 2 / us / 1e3
 wd = pack(w, 2); dz = torch.empty_like(x)
 us = timeit(lambda: net.conv(ctx, x, wd, B, 64, 64, 64, 64, epi=L.EPI_PRELU_BWD, alpha=al, pre_in=x, y=dz, part=part))
 res["rcab_dgrad_us"] = round(us, 2)
+# dgrad of conv1 + the identity-skip gradient (one residual, no bias)
+us = timeit(lambda: net.conv(ctx, x, wd, B, 64, 64, 64, 64, res=(dz,), y=y))
+res["rcab_dgrad_res_us"] = round(us, 2)
 # upsample dgrad 256->64 unshuffle (streamed kernel)
 du = torch.randn(B, 128, 128, 256, device='cuda', dtype=dt); wud = pack(w1, 2)
 dprev = torch.empty(B, 64, 64, 256, device='cuda', dtype=dt); v = torch.randn(B, 128, 128, 64, device='cuda', dtype=dt)

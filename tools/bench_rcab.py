@@ -40,5 +40,5 @@ for fused in (True, False):
         key = ("fused" if fused else "perop") + ("_train" if train else "")
         print(key, round(us, 2), flush=True)
         res[key + "_us"] = round(us, 2)
-        res[key + "_tflops"] = round(2 * 19.327e9 / 2 * B / 32 / us / 1e6 * 2, 1)
+        res[key + "_tflops"] = round(19.327e9 * B / 32 / us / 1e6, 1)
 print(json.dumps(res))

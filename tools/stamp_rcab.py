@@ -24,7 +24,7 @@ y = torch.empty_like(x)
 s = torch.empty(B, 64, device='cuda')
 lib = L.load()
 ws = L.RcabWorkspace(B, H, W)
-st = torch.zeros(256 * 8 * 32, dtype=torch.int64, device='cuda')
+st = torch.zeros(256 * 8 * 48, dtype=torch.int64, device='cuda')
 d = L.RcabDesc()
 d.dtype, d.B, d.H, d.W, d.C, d.Cr = L.BF16, B, H, W, 64, 16
 d.x, d.w1, d.b1, d.alpha = ptr(x), ptr(Wt.packed("conv1", 0)), ptr(pd["conv1.bias"]), ptr(pd["prelu.weight"])
@@ -36,16 +36,16 @@ for _ in range(int(os.environ.get("REPS", "20"))):
     L.check(lib.fen_rcab_fused(ctypes.byref(d), torch.cuda.current_stream().cuda_stream), "rcab")
 torch.cuda.synchronize()
 assert lib.fen_rcab_workspace_status(ws.ptr, B, H, W) == 0
-a = st.view(256, 8, 32).cpu().numpy().astype(np.int64)
+a = st.view(256, 8, 48).cpu().numpy().astype(np.int64)
 used = a[:, 0, 0] != 0
 a = a[used]
 t0 = a[:, :, 0][a[:, :, 0] > 0].min()
 out = {"blocks": int(used.sum())}
-for i in range(32):
-    v = a[:, :, i]
-    ok = (v > 0).all(axis=1)
+for i in range(48):
+    v = a[:, :, i].astype(np.float64)
+    ok = (v > 0).any(axis=1)              # slots only some waves stamp (e.g. wave 0's gate)
     if not ok.any():
         continue
-    r = (v[ok] - t0) / 100.0
-    out[str(i)] = [round(float(np.median(r.min(1))), 2), round(float(np.median(r.max(1))), 2)]
+    v = np.where(v > 0, (v - t0) / 100.0, np.nan)[ok]
+    out[str(i)] = [round(float(np.median(np.nanmin(v, 1))), 2), round(float(np.median(np.nanmax(v, 1))), 2)]
 print(json.dumps(out))
