@@ -119,9 +119,17 @@ __device__ __forceinline__ float wave_sum(float v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// sum over the 16 lanes of a DPP row (lanes 16r..16r+15), the same value in every lane:
+// quad xor 1, quad xor 2, half-row mirror, row mirror -- VALU-only (no LDS round trips)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float group16_sum(float v) {
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);    // row_half_mirror
+    v += dpp_f<0x140>(v);    // row_mirror
     return v;
 }
 

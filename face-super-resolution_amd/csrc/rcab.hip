@@ -180,6 +180,10 @@ __device__ __forceinline__ void edge_bases(int eidx, int c16, int q, int (&eb)[3
         for (int kk = 0; kk < 2; ++kk) eb[kh][kk] = ((r + kh) * 4 + b) * 128 + ekey(r + kh, kk * 4 + q);
 }
 
+// PARK (training, d.t given): t is parked in d.t (stored for the backward anyway) and the
+// apply re-reads it with coalesced 16-B loads; else t stays in 16 VGPRs (packed bf16) and the
+// apply uses the MFMA fragment layout (fewer HBM bytes, more registers).
+template <bool PARK>
 __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* xh = smem + O_XH;
@@ -273,6 +277,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         const int c = i >> 4, j = i & 15;
         fcs[1024 + i] = j < Cr ? d.fc2[c * Cr + j] : 0.f;   // [64][16]
     }
+#ifndef RCAB_NO_PRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);   // second-dispatched half: MI355X_MICROARCH.md 'Two waves per SIMD' 4
+#endif
     // this launch's epoch; announce that this block has read it
     const int ep1 = __builtin_amdgcn_readfirstlane(ld_poll(epoch)) + 1;
     if (tid == 0) st_flag(sflag + blockIdx.x, ep1);
@@ -310,7 +317,10 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         a1o5[m] = (ar5 * A1W + ac5) * 128 + ((chunk ^ (ac5 & 7)) << 4) + (q & 1) * 8;
     }
 
-    uint2 tcar[2][4];                                 // t (bf16) of the tile awaiting its gate
+    // t (bf16) of the tile awaiting its gate: parked in d.t (PARK) or carried in tcar
+    bf16* const tpark = (bf16*)d.t;
+    uint2 tcar[2][4];
+    (void)tcar;
     int arrive_f = -1;                                // tile flag still to be raised
     auto arrive = [&]() {                             // after an s_waitcnt vmcnt(0) of wave 0
         if (arrive_f >= 0 && tid == 0) st_flag(tflag + arrive_f, ep1);
@@ -390,19 +400,56 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         }
     };
 
-    // y = t * s * rs + x for tile `pt` (t in tcar, s in gsh)
-    uint2 xv[2][4];
+    // y = t * s * rs + x for tile `pt` (t parked, s in gsh), coalesced: wave w owns tile
+    // rows 2w, 2w+1 (4 KB); lane l moves 16-B chunks i*64 + l (8 full 128-B pixel rows
+    // per instruction) -- a quarter of the requests of the MFMA-fragment layout
+    uint4 xv[4], tv[4];   // PARK
     auto load_x = [&](int pt) {
+        const int b = pt / tpi, tile = pt - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int g = i * 64 + lane, p = g >> 3, c = g & 7;
+            const size_t o = ((size_t)(b * H + h0 + wave * 2 + (p >> 4)) * W + w0 + (p & 15)) * 128 + c * 16;
+            xv[i] = *(const uint4*)((const char*)d.x + o);
+            tv[i] = *(const uint4*)((const char*)tpark + o);
+        }
+    };
+    auto apply = [&](int pt) {                        // after load_x(pt)
+        const int b = pt / tpi, tile = pt - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const float rs = d.res_scale;
+        const int c = lane & 7;                       // the same chunk in every iteration
+        const float4 s0 = *(const float4*)(gsh + c * 8), s1 = *(const float4*)(gsh + c * 8 + 4);
+        const float sv[8] = {s0.x * rs, s0.y * rs, s0.z * rs, s0.w * rs, s1.x * rs, s1.y * rs, s1.z * rs, s1.w * rs};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int g = i * 64 + lane, p = g >> 3;
+            const size_t o = ((size_t)(b * H + h0 + wave * 2 + (p >> 4)) * W + w0 + (p & 15)) * 128 + c * 16;
+            const unsigned tw[4] = {tv[i].x, tv[i].y, tv[i].z, tv[i].w}, xw[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+            unsigned ow[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float lo = __uint_as_float(tw[e] << 16) * sv[2 * e] + __uint_as_float(xw[e] << 16);
+                const float hi = __uint_as_float(tw[e] & 0xffff0000u) * sv[2 * e + 1] + __uint_as_float(xw[e] & 0xffff0000u);
+                ow[e] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+            }
+            *(uint4*)((char*)d.y + o) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+    };
+    // (!PARK) y = t * s * rs + x in the MFMA fragment layout (t in tcar)
+    uint2 xf[2][4];
+    auto load_x_frag = [&](int pt) {
         const int b = pt / tpi, tile = pt - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
             const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
 #pragma unroll
-            for (int m = 0; m < 2; ++m) xv[m][n] = *(const uint2*)((const char*)d.x + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2);
+            for (int m = 0; m < 2; ++m) xf[m][n] = *(const uint2*)((const char*)d.x + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2);
         }
     };
-    auto apply = [&](int pt) {                        // after load_x(pt)
+    auto apply_frag = [&](int pt) {
         const int b = pt / tpi, tile = pt - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const float rs = d.res_scale;
@@ -418,10 +465,10 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 float o[4];
-                o[0] = __uint_as_float(tcar[m][n].x << 16) * sv[m][0] + __uint_as_float(xv[m][n].x << 16);
-                o[1] = __uint_as_float(tcar[m][n].x & 0xffff0000u) * sv[m][1] + __uint_as_float(xv[m][n].x & 0xffff0000u);
-                o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xv[m][n].y << 16);
-                o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xv[m][n].y & 0xffff0000u);
+                o[0] = __uint_as_float(tcar[m][n].x << 16) * sv[m][0] + __uint_as_float(xf[m][n].x << 16);
+                o[1] = __uint_as_float(tcar[m][n].x & 0xffff0000u) * sv[m][1] + __uint_as_float(xf[m][n].x & 0xffff0000u);
+                o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xf[m][n].y << 16);
+                o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xf[m][n].y & 0xffff0000u);
                 st4<bf16>((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
             }
         }
@@ -456,7 +503,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                                p == 0 ? eb4[0][1] : p == 1 ? eb4[1][1] : eb4[2][1]};
             const int e5[2] = {p == 0 ? eb5[0][0] : p == 1 ? eb5[1][0] : eb5[2][0],
                                p == 0 ? eb5[0][1] : p == 1 ? eb5[1][1] : eb5[2][1]};
+            if (k == 1 && p == 1) RSTAMP(45);
             conv1_phase(acc1, xh, eh, tapp, p, mbase, e4, e5, main4, has5, arow1, q);
+            if (k == 1 && p == 1) RSTAMP(46);
         }
         if (k == 0) RSTAMP(15);
         // ---- conv1 epilogue: bias + PReLU -> a1 image (zero outside the image; branch-free,
@@ -509,7 +558,14 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                 }
             }
         }
-        // the pending tile's gate (its round ended a conv1 ago): wave 0 -> LDS
+        // the pending tile's gate (its round ended a conv1 ago): wave 0 -> LDS (RCAB_XPRE:
+        // its residual loads go out first, in flight during the gate; costs registers)
+#ifdef RCAB_XPRE
+        if (pend_t >= 0) {
+            if constexpr (PARK) load_x(pend_t);
+            else load_x_frag(pend_t);
+        }
+#endif
         if (pend_t >= 0 && wave == 0) gate_to_lds(pend_t / tpi, pend_t % tpi == 0, 32);
         if (k < 2) RSTAMP(8 + k * 14);
         // ---- phase-3 boundary: a1 image + gate published; apply the pending tile before the
@@ -518,17 +574,35 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (k < 2) RSTAMP(9 + k * 14);
-        // vmcnt counts in issue order: the apply's residual loads go out before the next
-        // tile's halo so that they do not wait for it, and phase 4 waits for its taps only
-        // (vmcnt = this wave's halo pieces), leaving the halo in flight until phase 5
-        issue_taps(k * 6 + 4);
-        if (pend_t >= 0) {
-            load_x(pend_t);
-            apply(pend_t);
+        // vmcnt counts in issue order: the apply (its loads drained by the barrier above) runs
+        // before this phase's DMA, and phase 4 waits for its taps only (vmcnt = this wave's
+        // halo pieces), leaving the halo in flight until phase 5
+#ifdef RCAB_XPRE
+        if (pend_t >= 0) {                          // residual landed before the barrier
+            if constexpr (PARK) apply(pend_t);
+            else apply_frag(pend_t);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if (k == 1) RSTAMP(38);
+        issue_taps(k * 6 + 4);
+#else
+        issue_taps(k * 6 + 4);
+        if (k == 1) RSTAMP(38);
+        if (pend_t >= 0) {
+            if constexpr (PARK) {
+                load_x(pend_t);
+                apply(pend_t);
+            } else {
+                load_x_frag(pend_t);
+                apply_frag(pend_t);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        if (k == 1) RSTAMP(39);
         const bool halo_next = k + 1 < nmine;
         if (halo_next) issue_halo(t + nslot);       // conv1 is done with xh / eh
+        if (k == 1) RSTAMP(40);
         // ================= conv2: phases 3..5 =================
         f32x4 acc2[2][4];
 #pragma unroll
@@ -553,10 +627,12 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             }
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
                                    ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
+            if (k == 1 && p == 4) RSTAMP(41);
             conv2_phase(acc2, a1s, tapp, p - 3, wr, arow2, q, c16);
+            if (k == 1) RSTAMP(42 + (p - 3));
         }
         if (k == 0) RSTAMP(29);
-        // ---- conv2 epilogue: t = acc + b2, pool partial, arrival; t stays in registers
+        // ---- conv2 epilogue: t = acc + b2 (parked or carried), pool partial, arrival
         float ps[2][4];
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
@@ -571,10 +647,10 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                     acc2[m][n][r] += bia[r];
                     ps[m][r] += acc2[m][n][r];
                 }
-                if (d.t) {
+                if constexpr (PARK) {
                     const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
                     float v[4] = {acc2[m][n][0], acc2[m][n][1], acc2[m][n][2], acc2[m][n][3]};
-                    st4<bf16>((char*)d.t + o * 2, v);
+                    st4<bf16>((char*)tpark + o * 2, v);
                 }
             }
         }
@@ -597,13 +673,15 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         arrive_f = tile * B + b;
+        if constexpr (!PARK) {
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+            for (int m = 0; m < 2; ++m)
 #pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                tcar[m][n].x = (unsigned)f2bf(acc2[m][n][0]) | ((unsigned)f2bf(acc2[m][n][1]) << 16);
-                tcar[m][n].y = (unsigned)f2bf(acc2[m][n][2]) | ((unsigned)f2bf(acc2[m][n][3]) << 16);
-            }
+                for (int n = 0; n < 4; ++n) {
+                    tcar[m][n].x = (unsigned)f2bf(acc2[m][n][0]) | ((unsigned)f2bf(acc2[m][n][1]) << 16);
+                    tcar[m][n].y = (unsigned)f2bf(acc2[m][n][2]) | ((unsigned)f2bf(acc2[m][n][3]) << 16);
+                }
+        }
         pend_t = t;
         if (k < 2) RSTAMP(14 + k * 14);
     }
@@ -612,11 +690,13 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     arrive();
     RSTAMP(30);
     if (pend_t >= 0) {
-        load_x(pend_t);                               // the residual is in flight during the gate
+        if constexpr (PARK) load_x(pend_t);           // the residual is in flight during the gate
+        else load_x_frag(pend_t);
         if (wave == 0) gate_to_lds(pend_t / tpi, pend_t % tpi == 0, 35);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        apply(pend_t);
+        if constexpr (PARK) apply(pend_t);
+        else apply_frag(pend_t);
         RSTAMP(31);
     }
     // block 0 advances the epoch once every block has read it (the next launch on the stream
@@ -719,10 +799,12 @@ extern "C" int fen_rcab_fused(const fen_rcab_desc* d, void* stream) {
     if (grid > MAX_GRID) grid = (MAX_GRID / tpi) * tpi;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_rcab, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
+        (void)hipFuncSetAttribute((const void*)k_rcab<true>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
+        (void)hipFuncSetAttribute((const void*)k_rcab<false>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL(k_rcab, dim3(grid), dim3(512), RCAB_LDS, (hipStream_t)stream, *d);
+    if (d->t) hipLaunchKernelGGL(k_rcab<true>, dim3(grid), dim3(512), RCAB_LDS, (hipStream_t)stream, *d);
+    else hipLaunchKernelGGL(k_rcab<false>, dim3(grid), dim3(512), RCAB_LDS, (hipStream_t)stream, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
