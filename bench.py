@@ -118,11 +118,16 @@ def cpu_baseline(model, seconds=10.0):
             "sample": f"oracle fp32 eval forward, full 6x10 net, batch 2 of 64x64, {n} passes in {el:.1f}s"}
 
 
-def load_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_rcab_conv.json")
-    if os.path.exists(p):
+def load_traffic(label):
+    """HBM bytes per launch of the dominant kernel from its committed PMC summary
+    (profiles/pmc_*.json, tools/prof_summary.py pmc), or None when none matches it."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            js = json.load(f)
+        key = js.get("kernel_key")
+        if key and label.startswith(key):
+            return js.get("hbm_bytes_per_launch")
     return None
 
 
@@ -179,7 +184,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": kern_label,
                      "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "kernel_ms": round(kern_ms, 5),
-                     "flop_per_launch": kern_flop, "traffic": load_traffic()},
+                     "flop_per_launch": kern_flop, "traffic": load_traffic(kern_label)},
     }
     del eng
     torch.cuda.empty_cache()

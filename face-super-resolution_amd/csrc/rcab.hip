@@ -390,7 +390,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             const float4 hv = *(const float4*)(red + 64 + c);
             z += w.x * hv.x + w.y * hv.y + w.z * hv.z + w.w * hv.w;
         }
-        const float sg = 1.f / (1.f + __expf(-z));
+        const float sg = 1.f / (1.f + expf(-z));
         gsh[lane] = sg;
         RSTAMP(sb + 2);
         if (first) {                                  // the user-visible copies, once per image

@@ -51,65 +51,126 @@ __global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __
     }
 }
 
-// conv_first weight gradient: wave = one pixel at a time (uniform x loads), lane = co
+// conv_first weight gradient dw[co][ci][kh][kw] = sum_px dy[px][co] * x[ci][px + (kh-1, kw-1)]
+// (+ db = sum_px dy).  Persistent blocks walk 16x16-pixel tiles in a fixed order (deterministic
+// per-block partials): the tile's zero-padded 3 x 18 x 18 input halo is staged in LDS; wave w
+// takes rows 4w..4w+3, lane = output channel (+64 for the second set); along a row the 3x3
+// window of each input channel slides one column per pixel (9 LDS broadcast reads per pixel
+// instead of 27 global loads) and the row's 16 dy values are loaded ahead.
 constexpr int CF_BLOCKS = 512;
 template <typename T>
 __global__ __launch_bounds__(256) void k_conv_first_wgrad(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
                                    const T* __restrict__ dy, float* __restrict__ part) {
+    __shared__ float xs[3][18][19];
     __shared__ float red[4][28 * 2][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nc = (C + 63) / 64;
     float acc[2][28];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int k = 0; k < 28; ++k) acc[j][k] = 0.f;
-    const size_t npx = (size_t)B * H * W;
-    const int nc = (C + 63) / 64;
-    for (size_t px = (size_t)blockIdx.x * 4 + wave; px < npx; px += (size_t)gridDim.x * 4) {
-        const size_t pu = __builtin_amdgcn_readfirstlane((unsigned)px);
-        const int wq = (int)(pu % W), hq = (int)((pu / W) % H), b = (int)(pu / ((size_t)W * H));
-        float g[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int co = lane + 64 * j;
-            g[j] = (j < nc && co < C) ? tof<T>(dy[pu * C + co]) : 0.f;
+    const int th = (H + 15) >> 4, tw = (W + 15) >> 4;
+    const int ntiles = B * th * tw;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int b = t / (th * tw), tt = t - b * th * tw;
+        const int h0 = (tt / tw) << 4, w0 = (tt % tw) << 4;
+        __syncthreads();                              // previous tile's window reads are done
+        for (int i = threadIdx.x; i < 3 * 18 * 18; i += 256) {
+            const int ci = i / 324, r = (i / 18) % 18, c = i % 18;
+            const int hh = h0 - 1 + r, ww = w0 - 1 + c;
+            xs[ci][r][c] = (ci < Ci && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                               ? x[(((size_t)b * Ci + ci) * H + hh) * W + ww] : 0.f;
         }
-        for (int ci = 0; ci < Ci; ++ci) {
-            const float* xp = x + ((size_t)b * Ci + ci) * H * W;
+        __syncthreads();
+#pragma unroll 1
+        for (int rr = 0; rr < 4; ++rr) {
+            const int r = wave * 4 + rr, hq = h0 + r;
+            if (hq >= H) break;
+            float g[2][16];
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const int hh = hq + t / 3 - 1, ww = wq + t % 3 - 1;
-                const float v = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? xp[(size_t)hh * W + ww] : 0.f;
+            for (int c = 0; c < 16; ++c) {
+                const int wq = w0 + c;
+                const size_t px = ((size_t)b * H + hq) * W + wq;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[j][ci * 9 + t] += g[j] * v;
+                for (int j = 0; j < 2; ++j) {
+                    const int co = lane + 64 * j;
+                    g[j][c] = (j < nc && co < C && wq < W) ? tof<T>(dy[px * C + co]) : 0.f;
+                }
+            }
+            float win[3][3][3];                       // [ci][kh][kw]
+#pragma unroll
+            for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {
+                    win[ci][kh][1] = xs[ci][r + kh][0];
+                    win[ci][kh][2] = xs[ci][r + kh][1];
+                }
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+#pragma unroll
+                for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+                    for (int kh = 0; kh < 3; ++kh) {
+                        win[ci][kh][0] = win[ci][kh][1];
+                        win[ci][kh][1] = win[ci][kh][2];
+                        win[ci][kh][2] = xs[ci][r + kh][c + 2];
+                    }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (j >= nc) break;
+#pragma unroll
+                    for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+                        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                            for (int kw = 0; kw < 3; ++kw) acc[j][ci * 9 + kh * 3 + kw] += g[j][c] * win[ci][kh][kw];
+                    acc[j][27] += g[j][c];
+                }
             }
         }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[j][27] += g[j];
     }
-    for (int j = 0; j < nc; ++j)
-        for (int k = 0; k < 28; ++k) red[wave][j * 28 + k][lane] = acc[j][k];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        if (j < nc) {
+#pragma unroll
+            for (int k = 0; k < 28; ++k) red[wave][j * 28 + k][lane] = acc[j][k];
+        }
     __syncthreads();
     for (int i = threadIdx.x; i < nc * 28 * 64; i += 256) {
         const int lanei = i & 63, jk = i >> 6;
-        const float s = red[0][jk][lanei] + red[1][jk][lanei] + red[2][jk][lanei] + red[3][jk][lanei];
+        const float sum = red[0][jk][lanei] + red[1][jk][lanei] + red[2][jk][lanei] + red[3][jk][lanei];
         const int j = jk / 28, k = jk % 28, co = lanei + 64 * j;
-        if (co < C) part[((size_t)blockIdx.x * 28 + k) * C + co] = s;
+        if (co < C) part[((size_t)blockIdx.x * 28 + k) * C + co] = sum;
     }
 }
 
-__global__ void k_conv_first_finalize(int nb, int Ci, int C, const float* part, float* dw, float* db, int accum) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over 28*C
-    if (i >= 28 * C) return;
-    const int k = i / C, co = i % C;
+// block = one of the 28 rows k (27 weights + bias), 256 threads: thread (co, quarter) sums every
+// 4th partial block (coalesced over co), fixed-order LDS combine -- deterministic
+__global__ __launch_bounds__(256) void k_conv_first_finalize(int nb, int Ci, int C, const float* part, float* dw,
+                                                             float* db, int accum) {
+    __shared__ float red[4][128];
+    const int k = blockIdx.x;
     if (k >= Ci * 9 && k != 27) return;
-    float s = 0.f;
-    for (int r = 0; r < nb; ++r) s += part[((size_t)r * 28 + k) * C + co];
-    if (k == 27) {
-        if (db) db[co] = accum ? db[co] + s : s;
-    } else {
-        float* o = dw + (size_t)co * Ci * 9 + k;
-        *o = accum ? *o + s : s;
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        const int co = c0 + (threadIdx.x & 63), qr = threadIdx.x >> 6;
+        float a = 0.f;
+        if (co < C) {
+#pragma unroll 8
+            for (int r = qr; r < nb; r += 4) a += part[((size_t)r * 28 + k) * C + co];
+        }
+        red[qr][threadIdx.x & 63] = a;
+        __syncthreads();
+        if (threadIdx.x < 64 && co < C) {
+            const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+            if (k == 27) {
+                if (db) db[co] = accum ? db[co] + s : s;
+            } else {
+                float* o = dw + (size_t)co * Ci * 9 + k;
+                *o = accum ? *o + s : s;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -463,11 +524,14 @@ __global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, cons
         dz[c] = a * rs * sv * (1.f - sv);                 // through sigmoid
     }
     __syncthreads();
-    for (int j = t; j < Cr; j += blockDim.x) {
-        float a = 0.f;
-        for (int c = 0; c < C; ++c) a += w2[(size_t)c * Cr + j] * dz[c];
-        const float h = hid[(size_t)b * Cr + j];
-        dh[j] = h > 0.f ? a : 0.f;                         // through ReLU
+    {   // dh[j] = relu'(hid) * sum_c w2[c][j] dz[c]: one wave per hidden unit, lanes over c
+        const int lane = t & 63, nw = blockDim.x >> 6;
+        for (int j = t >> 6; j < Cr; j += nw) {
+            float a = 0.f;
+            for (int c = lane; c < C; c += 64) a += w2[(size_t)c * Cr + j] * dz[c];
+            a = wave_sum(a);
+            if (lane == 0) dh[j] = hid[(size_t)b * Cr + j] > 0.f ? a : 0.f;   // through ReLU
+        }
     }
     __syncthreads();
     for (int i = t; i < C * Cr; i += blockDim.x) {
@@ -766,8 +830,8 @@ extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int 
     else
         return FEN_EINVAL;
     FEN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_conv_first_finalize, dim3(nblk(28 * C)), dim3(256), 0, STREAM, CF_BLOCKS, Ci, C, work, dw,
-                       db, accumulate);
+    hipLaunchKernelGGL(k_conv_first_finalize, dim3(28), dim3(256), 0, STREAM, CF_BLOCKS, Ci, C, work, dw, db,
+                       accumulate);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

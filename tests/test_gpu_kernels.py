@@ -165,6 +165,33 @@ def test_conv_first(dtype):
 
 
 @pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("B,H,W,C", [(2, 20, 24, 64), (1, 16, 16, 64), (3, 37, 19, 64), (4, 64, 64, 64),
+                                     (1, 16, 32, 128)])
+def test_conv_first_wgrad(dtype, B, H, W, C):
+    """fen_conv_first_wgrad (3 -> C, fp32 NCHW input, NHWC dy) vs float64 autograd on the
+    same dy rounded to the compute dtype; ragged tiles (37 x 19), C = 128 (two lane sets)."""
+    torch.manual_seed(11)
+    x = torch.rand(B, 3, H, W)
+    dy = torch.randn(B, C, H, W).to(dtype).float()
+    w = torch.zeros(C, 3, 3, 3, dtype=torch.float64, requires_grad=True)
+    bb = torch.zeros(C, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.double(), w, bb, padding=1).mul(dy.double()).sum().backward()
+    ctx = _ctx(dtype)
+    from src.hip.program import ptr
+    xd = x.to(DEV)
+    dyd = nhwc(dy, dtype)
+    dw = ctx.alloc((C, 3, 3, 3), torch.float32)
+    db = ctx.alloc((C,), torch.float32)
+    work = ctx.alloc((ctx.lib.fen_conv_first_work_floats(B, 3, H, W, C),), torch.float32)
+    ctx.emit("cfw", ctx.lib.fen_conv_first_wgrad, ctx.code, B, 3, H, W, C, ptr(xd), ptr(dyd), ptr(dw), ptr(db), 0,
+             ptr(work))
+    torch.cuda.synchronize()
+    rel = float((dw.cpu().double() - w.grad).norm() / w.grad.norm())
+    relb = float((db.cpu().double() - bb.grad).norm() / bb.grad.norm())
+    assert rel <= 1e-5 and relb <= 1e-5, (rel, relb)
+
+
+@pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("clamp", [0, 1])
 def test_conv_last_bicubic_l1(dtype, clamp):
     from src.hip import lib as L, net
