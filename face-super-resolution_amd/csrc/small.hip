@@ -11,9 +11,12 @@ inline int nblk(size_t n, int t = 256) { return (int)((n + t - 1) / t); }
 
 // ------------------------------ conv_first (3 -> C) ------------------------------
 // reference custom.py:91-94,164; thread per (pixel, 8 output channels)
+// (also the VGG19 input conv, perceptual.py:67-72,84-95: in-bounds samples normalised by
+// (v - mean[ci]) * istd[ci] before the zero padding applies, output optionally ReLU'd)
 template <typename T>
 __global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
-                             const float* __restrict__ w, const float* __restrict__ bias, T* __restrict__ y) {
+                             const float* __restrict__ w, const float* __restrict__ bias, T* __restrict__ y,
+                             const float* __restrict__ in_mean, const float* __restrict__ in_istd, int relu) {
     extern __shared__ __attribute__((aligned(16))) float sw[];  // [Ci*9][C]
     const int K = Ci * 9;
     for (int i = threadIdx.x; i < K * C; i += blockDim.x) {
@@ -32,15 +35,21 @@ __global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __
     for (int j = 0; j < 8; ++j) acc[j] = bias[g * 8 + j];
     for (int ci = 0; ci < Ci; ++ci) {
         const float* xp = x + ((size_t)b * Ci + ci) * H * W;
+        const float mu = in_mean ? in_mean[ci] : 0.f, is = in_istd ? in_istd[ci] : 1.f;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int hh = hq + t / 3 - 1, ww = wq + t % 3 - 1;
-            const float v = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? xp[(size_t)hh * W + ww] : 0.f;
+            const float v = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? (xp[(size_t)hh * W + ww] - mu) * is
+                                                                                        : 0.f;
             const float4* wp = (const float4*)(sw + (ci * 9 + t) * C + g * 8);
             const float4 w0 = wp[0], w1 = wp[1];
             acc[0] += v * w0.x; acc[1] += v * w0.y; acc[2] += v * w0.z; acc[3] += v * w0.w;
             acc[4] += v * w1.x; acc[5] += v * w1.y; acc[6] += v * w1.z; acc[7] += v * w1.w;
         }
+    }
+    if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
     }
     char* o = (char*)y + (px * C + g * 8) * sizeof(T);
     if constexpr (sizeof(T) == 2) {
@@ -484,7 +493,8 @@ __global__ __launch_bounds__(256) void k_pool_dot(int HW, int C, int nchunk, con
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[j] = 0.f;
     if (pr < R) {
-        for (int p = p0 + pr; p < p1; p += R) {
+#pragma unroll 4
+        for (int p = p0 + pr; p < p1; p += R) {     // unrolled: 4 pixel rows of loads in flight
             const size_t e = ((size_t)b * HW + p) * C + cv * V;
             float av[V];
             unpack16<T>(*(const uint4*)(a + e), av);
@@ -515,11 +525,22 @@ __global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, cons
                          const float* __restrict__ mean, const float* __restrict__ hid, const float* __restrict__ s,
                          const float* __restrict__ w1, const float* __restrict__ w2, float* g, float* dw1p,
                          float* dw2p) {
-    __shared__ float dz[512], dh[128];
+    __shared__ float dz[512], dh[128], pr[4][256];
     const int b = blockIdx.x, t = threadIdx.x;
-    for (int c = t; c < C; c += blockDim.x) {
+    // pool partials: thread (c, quarter) sums every 4th part (independent loads in flight),
+    // fixed-order combine of the quarters (deterministic)
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        const int c = c0 + (t & 63), qr = t >> 6;
         float a = 0.f;
-        for (int p = 0; p < nparts; ++p) a += part[((size_t)b * nparts + p) * C + c];
+        if (c < C) {
+#pragma unroll 4
+            for (int p = qr; p < nparts; p += 4) a += part[((size_t)b * nparts + p) * C + c];
+        }
+        pr[qr][c & 255] = a;
+    }
+    __syncthreads();
+    for (int c = t; c < C; c += blockDim.x) {
+        const float a = (pr[0][c] + pr[1][c]) + (pr[2][c] + pr[3][c]);
         const float sv = s[(size_t)b * C + c];
         dz[c] = a * rs * sv * (1.f - sv);                 // through sigmoid
     }
@@ -799,19 +820,27 @@ __global__ void k_scale(size_t n, float* y, float s) {
 // =================================== C-ABI ===================================
 #define STREAM ((hipStream_t)stream)
 
-extern "C" int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x, const float* w,
-                                  const float* bias, void* y, void* stream) {
+extern "C" int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int C, const float* x, const float* w,
+                                     const float* bias, const float* in_mean, const float* in_istd, int relu, void* y,
+                                     void* stream) {
     if (!x || !w || !bias || !y || B <= 0 || Ci <= 0 || Ci > 3 || C % 8 || C > 128) return FEN_EINVAL;
     const size_t n = (size_t)B * H * W * (C / 8);
     const size_t lds = (size_t)Ci * 9 * C * sizeof(float);
     if (dtype == FEN_BF16)
-        hipLaunchKernelGGL(k_conv_first<bf16>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias, (bf16*)y);
+        hipLaunchKernelGGL(k_conv_first<bf16>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
+                           (bf16*)y, in_mean, in_istd, relu);
     else if (dtype == FEN_F32)
-        hipLaunchKernelGGL(k_conv_first<float>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias, (float*)y);
+        hipLaunchKernelGGL(k_conv_first<float>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
+                           (float*)y, in_mean, in_istd, relu);
     else
         return FEN_EINVAL;
     FEN_CHECK_LAUNCH();
     return FEN_OK;
+}
+
+extern "C" int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x, const float* w,
+                                  const float* bias, void* y, void* stream) {
+    return fen_conv_first_fwd_ex(dtype, B, Ci, H, W, C, x, w, bias, nullptr, nullptr, 0, y, stream);
 }
 
 extern "C" size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C) {

@@ -72,6 +72,7 @@ _SIGS = {
     "fen_rcab_workspace_status": (c_int, [c_void_p, c_int, c_int, c_int]),
     "fen_rcab_fused": (c_int, [POINTER(RcabDesc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
+    "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_int, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),
     "fen_conv_first_wgrad": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_int, c_void_p, c_void_p]),
     "fen_conv_last_dgrad_part_rows": (c_size_t, [c_int] * 3),
@@ -99,6 +100,10 @@ _SIGS = {
     "fen_optim_prepare": (c_int, [c_int, c_void_p, c_float, c_float, c_float, c_float, c_void_p, c_void_p]),
     "fen_adamw": (c_int, [c_size_t] + [c_void_p] * 5 + [c_float, c_float, c_float, c_void_p]),
     "fen_scale": (c_int, [c_size_t, c_void_p, c_float, c_void_p]),
+    "fen_maxpool2": (c_int, [c_int] * 5 + [c_void_p] * 3),
+    "fen_maxpool2_bwd_relu": (c_int, [c_int] * 5 + [c_void_p] * 4),
+    "fen_feat_loss_parts": (c_int, []),
+    "fen_feat_loss": (c_int, [c_int, c_size_t, c_void_p, c_int, c_float, c_void_p, c_int, c_void_p, c_void_p]),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
     "fen_build_info": (ctypes.c_char_p, []),
 }

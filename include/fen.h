@@ -98,6 +98,12 @@ int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream);
 /* conv_first forward: NCHW fp32 [B,Ci,H,W] -> NHWC [B,H,W,C] (custom.py:91-94,164)          */
 int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x,
                        const float* w, const float* bias, void* y, void* stream);
+/* ... with the VGG19 input stage (perceptual.py:67-72,84-95): in-bounds samples become
+ * (x - in_mean[ci]) * in_istd[ci] before the zero padding, relu != 0 applies ReLU to y;
+ * in_mean / in_istd may be NULL (identity).                                               */
+int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int C, const float* x,
+                          const float* w, const float* bias, const float* in_mean, const float* in_istd,
+                          int relu, void* y, void* stream);
 /* conv_first weight gradient (no data gradient: x needs none) -> dw OIHW, db              */
 size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C);
 int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const float* x,
@@ -237,6 +243,23 @@ int fen_adamw(size_t n, float* p, const float* g, float* m, float* v, const floa
               float beta1, float beta2, float eps, void* stream);
 /* y[i] *= s  (DP gradient averaging helper)                                                 */
 int fen_scale(size_t n, float* y, float s, void* stream);
+
+/* ---- VGG19 perceptual loss (src/losses/perceptual.py:13-169), frozen feature extractor ----
+ * The convs run on fen_conv3x3 (ReLU = FEN_EPI_PRELU with zero slopes; its backward =
+ * FEN_EPI_PRELU_BWD with zero slopes and pre_in = the ReLU output).  Below: the pool and the
+ * loss.  NHWC of dtype, C a multiple of 8, H and W even.                                   */
+/* y = max_pool2d(x, 2, 2) (torchvision vgg19.features 'M')                                  */
+int fen_maxpool2(int dtype, int B, int H, int W, int C, const void* x, void* y, void* stream);
+/* dx [B,H,W,C] = max-pool backward of dy [B,H/2,W/2,C] through a [B,H,W,C] (first maximum
+ * of each window, torch's choice) times the ReLU mask [a > 0]; every dx element written     */
+int fen_maxpool2_bwd_relu(int dtype, int B, int H, int W, int C, const void* dy, const void* a, void* dx,
+                          void* stream);
+/* f holds [pred; target] (n elements each): part[fen_feat_loss_parts()] = per-block sums of
+ * |p - t| (l2 = 0: nn.L1Loss) or (p - t)^2 (l2 = 1: nn.MSELoss); g (n elements) =
+ * (accumulate ? g : 0) + scale * d/dp (sign(p - t) or 2 (p - t)); scale = weight / n.       */
+int fen_feat_loss_parts(void);
+int fen_feat_loss(int dtype, size_t n, const void* f, int l2, float scale, void* g, int accumulate, float* part,
+                  void* stream);
 
 const char* fen_status_string(int code);
 const char* fen_build_info(void);

@@ -207,3 +207,78 @@ def rcab_with_grads(p: Params, x: torch.Tensor, r: torch.Tensor, res_scale: floa
     out = rcab(xl, leaves, "", res_scale)
     (out * r).sum().backward()
     return out.detach(), xl.grad.detach(), {k: v.grad.detach() for k, v in leaves.items()}
+
+
+# ---------------------------------------------------------------------------------------
+# VGG19 perceptual loss (reference src/losses/perceptual.py:13-169).  PARITY UNPINNED: the
+# reference builds torchvision.models.vgg19 with ImageNet weights (perceptual.py:48), and
+# neither torchvision nor the weights exist offline (SURVEY.md §8c/§8f).  This restates the
+# torchvision vgg19.features layer list (config 'E': 16 convs 3x3 pad 1 + ReLU, max pools
+# 2x2) and the loss as written in perceptual.py, for any weights given as a state dict
+# keyed like torchvision ('features.{i}.weight' / '.bias').
+VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M",
+             512, 512, 512, 512, "M"]
+VGG_MEAN = (0.485, 0.456, 0.406)     # perceptual.py:67-72
+VGG_STD = (0.229, 0.224, 0.225)
+
+
+def vgg19_layers():
+    """[(index, kind, cin, cout)] of torchvision vgg19.features; kind in conv/relu/pool."""
+    out, idx, cin = [], 0, 3
+    for v in VGG19_CFG:
+        if v == "M":
+            out.append((idx, "pool", cin, cin))
+            idx += 1
+        else:
+            out.append((idx, "conv", cin, v))
+            out.append((idx + 1, "relu", v, v))
+            idx += 2
+            cin = v
+    return out
+
+
+def vgg19_init(seed: int = 0) -> Params:
+    """Random weights in the torchvision layout (kaiming fan_out, zero bias), for tests."""
+    g = torch.Generator().manual_seed(seed)
+    p = {}
+    for idx, kind, cin, cout in vgg19_layers():
+        if kind == "conv":
+            std = math.sqrt(2.0 / (cout * 9))
+            p[f"features.{idx}.weight"] = torch.randn(cout, cin, 3, 3, generator=g) * std
+            p[f"features.{idx}.bias"] = torch.randn(cout, generator=g) * 0.01
+    return p
+
+
+def vgg_features(p: Params, x: torch.Tensor, layer_indices, normalize: bool = True) -> Dict[int, torch.Tensor]:
+    """perceptual.py:84-101: normalise, run features[:max+1], collect the listed indices."""
+    if normalize:
+        mean = torch.tensor(VGG_MEAN, dtype=x.dtype).view(1, 3, 1, 1)
+        std = torch.tensor(VGG_STD, dtype=x.dtype).view(1, 3, 1, 1)
+        x = (x - mean) / std
+    feats = {}
+    last = max(layer_indices)
+    for idx, kind, _, _ in vgg19_layers():
+        if idx > last:
+            break
+        if kind == "conv":
+            x = F.conv2d(x, p[f"features.{idx}.weight"].to(x.dtype), p[f"features.{idx}.bias"].to(x.dtype), padding=1)
+        elif kind == "relu":
+            x = F.relu(x)
+        else:
+            x = F.max_pool2d(x, 2, 2)
+        if idx in layer_indices:
+            feats[idx] = x
+    return feats
+
+
+def perceptual_loss(p: Params, pred: torch.Tensor, target: torch.Tensor, layer_indices, weights=None,
+                    criterion: str = "l1", normalize: bool = True) -> torch.Tensor:
+    """perceptual.py:144-169: sum over layers of weight * criterion(f_pred, f_target)."""
+    fp = vgg_features(p, pred, layer_indices, normalize)
+    ft = vgg_features(p, target, layer_indices, normalize)
+    loss = 0.0
+    for i in layer_indices:
+        w = 1.0 if weights is None else weights[i]
+        d = F.l1_loss(fp[i], ft[i]) if criterion == "l1" else F.mse_loss(fp[i], ft[i])
+        loss = loss + w * d
+    return loss
