@@ -139,6 +139,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--train-steps", type=int, default=10)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--no-perceptual", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -205,6 +206,31 @@ def main():
                         "loss": float(teng.loss), "allreduce": "RCCL (torch.distributed nccl backend), 8 buckets, "
                                                                "overlapped with backward" if world > 1 else "none"}
         del teng
+        torch.cuda.empty_cache()
+        if not args.no_perceptual:
+            # the stage-1 recipe proper (stage1_psnr_config.yaml:40-50): L1 x 1 + VGG19 conv3_4
+            # perceptual x 1; VGG19 randomly initialised (no ImageNet weights offline)
+            import warnings
+            from src.losses import PerceptualLoss
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                spec = PerceptualLoss(layers=["conv3_4"]).to("cuda").fused_spec(1.0)
+            pm = build_model("bf16")
+            peng = FENEngine(pm, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=True, device="cuda",
+                             perceptual=spec)
+            peng.hr.copy_(hr)
+            if world == 1:
+                peng.capture()
+                fn = peng.replay
+            else:
+                fn = peng.step
+            tp = timed(fn, args.train_steps, 3, world)
+            out["train_perceptual"] = {
+                "metric": "training images/sec (stage-1 step: L1 + VGG19 conv3_4 perceptual) at batch 32/GPU",
+                "value": round(B * world * args.train_steps / tp, 2),
+                "ms_per_step": round(1000.0 * tp / args.train_steps, 3), "steps": args.train_steps,
+                "loss": float(peng.total_loss()), "vgg": "random-init VGG19 (no ImageNet weights offline)"}
+            del peng
     if cpu_model_sd is not None:
         out["cpu_baseline"] = cpu_baseline(cpu_model_sd, args.cpu_seconds)
     if rank == 0:

@@ -44,7 +44,11 @@ def flatten_params(model: torch.nn.Module, device) -> Dict[str, torch.Tensor]:
 class FENEngine:
     def __init__(self, model, batch: int, lr_hw, dtype: torch.dtype = torch.bfloat16, train: bool = False,
                  device="cuda", loss_weight: float = 1.0, clip: float = 0.5, lr: float = 1e-4,
-                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, process_group=None):
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, process_group=None,
+                 perceptual: Optional[dict] = None):
+        """perceptual (training only): the stage configs' VGG19 term (perceptual.py:144-169) as
+        dict(weight=, layers=, criterion=, normalize=, params={'features.i.weight': ...},
+        layer_weights=None); its gradient joins the fused L1 gradient in dL/dsr."""
         self.spec = NetSpec.from_config(model.config)
         self.dtype, self.device, self.train = dtype, torch.device(device), train
         self.B, (self.h, self.w) = batch, lr_hw
@@ -72,7 +76,23 @@ class FENEngine:
         if not train:
             self._build_forward(training=False)
         else:
-            self.hr = torch.zeros(B, s.out_ch, self.H, self.W, device=self.device)
+            self.l1_weight = loss_weight
+            self.vgg = None
+            self.loss_perc = torch.zeros(1, device=self.device)
+            if perceptual:
+                # pred and target share one [2B,3,H,W] buffer: the frozen VGG runs once over both
+                self.x2 = torch.zeros(2 * B, s.out_ch, self.H, self.W, device=self.device)
+                self.out, self.hr = self.x2[:B], self.x2[B:]
+                from .vgg import VGGPerceptual
+                pw = float(perceptual.get("weight", 1.0))
+                layers = list(perceptual.get("layers", ["conv3_4"]))
+                lw = perceptual.get("layer_weights") or {}
+                self.vgg = VGGPerceptual(ctx, perceptual["params"], layers=layers,
+                                         weights={n: pw * float(lw.get(n, 1.0)) for n in layers},
+                                         criterion=perceptual.get("criterion", "l1"),
+                                         normalize=perceptual.get("normalize", True))
+            else:
+                self.hr = torch.zeros(B, s.out_ch, self.H, self.W, device=self.device)
             n = self.flat_p.numel()
             self.flat_g = torch.zeros(n, device=self.device)
             self.flat_m = torch.zeros(n, device=self.device)
@@ -111,6 +131,8 @@ class FENEngine:
         if self.train:
             lp = self.saved_tail["loss_part"]
             colsum(ctx, lp, lp.shape[0], 1, self.loss, scale=1.0 / (self.B * s.out_ch * self.H * self.W))
+            if self.vgg is not None:
+                self.vgg.build(self.x2, self.loss_perc, self.saved_tail["dout"], grad_scale=1.0 / self.world)
 
     def _build_backward(self):
         s, ctx = self.spec, self.ctx
@@ -150,15 +172,21 @@ class FENEngine:
         return self.out
 
     def step(self, hr: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """One training step on HR [B,3,H,W]: LR synthesis, fwd, L1, bwd, all-reduce, clip, AdamW.
-        Returns the (device) loss of this rank's shard."""
+        """One training step on HR [B,3,H,W]: LR synthesis, fwd, L1 (+ perceptual), bwd,
+        all-reduce, clip, AdamW.  Returns the (device) total loss of this rank's shard."""
         if hr is not None:
             self.hr.copy_(hr)
         self.ctx.run()
         self.exchange.wait()
         self.upd.run()
         self.Wt.pack()
-        return self.loss
+        return self.total_loss()
+
+    def total_loss(self) -> torch.Tensor:
+        """weight * L1 (+ the weighted perceptual term), on the device."""
+        if self.vgg is None:
+            return self.loss if self.l1_weight == 1.0 else self.loss * self.l1_weight
+        return self.loss * self.l1_weight + self.loss_perc
 
     def set_lr(self, lr: float):
         self.scal[3] = lr

@@ -129,22 +129,22 @@ class VGGPerceptual:
         return out
 
     # ------------------------------------------------------------------ program
-    def build(self, x2: torch.Tensor, loss: torch.Tensor, dpred: Optional[torch.Tensor]) -> Dict[int, torch.Tensor]:
-        """x2: NCHW fp32 [2B,3,H,W] = [pred; target]; loss: fp32 [1] the weighted perceptual
-        loss is ADDED to; dpred: NHWC [B,H,W,16] (dtype) dL/dpred the gradient is ADDED to
-        (None: forward + loss only).  Returns {feature index: NHWC [2B,h,w,C] feature}."""
-        ctx = self.ctx
-        N, _, H, W = x2.shape
-        B = N // 2
+    def forward(self, x: torch.Tensor, ctx: Optional[Ctx] = None, upto: Optional[int] = None):
+        """Record the extractor over NCHW fp32 x [N,3,H,W] up to conv index `upto` (default:
+        the deepest feature).  Returns (acts, feats): per conv its ReLU output and geometry,
+        and {feature index: NHWC [N,h,w,C] pre-ReLU conv output}."""
+        ctx = ctx or self.ctx
+        N, _, H, W = x.shape
+        last_idx = self.convs[-1]["idx"] if upto is None else upto
+        convs = [c for c in self.convs if c["idx"] <= last_idx]
         acts, feats = [], {}
         h, hh, ww = None, H, W
-        train = dpred is not None
-        for c in self.convs:
+        for c in convs:
             i, cin, cout = c["idx"], c["cin"], c["cout"]
-            is_feat, is_last = i in self.idx, i == self.convs[-1]["idx"]
+            is_feat, is_last = i in self.idx, i == last_idx
             if i == 0:
                 a = ctx.alloc((N, hh, ww, cout))
-                ctx.emit("vgg_conv1_1", ctx.lib.fen_conv_first_fwd_ex, ctx.code, N, 3, hh, ww, cout, ptr(x2),
+                ctx.emit("vgg_conv1_1", ctx.lib.fen_conv_first_fwd_ex, ctx.code, N, 3, hh, ww, cout, ptr(x),
                          ptr(self.p["features.0.weight"]), ptr(self.p["features.0.bias"]), ptr(self.mean),
                          ptr(self.istd), 1, ptr(a))
                 z = None
@@ -165,33 +165,45 @@ class VGGPerceptual:
                 pooled = ctx.alloc((N, hh // 2, ww // 2, cout))
                 ctx.emit("vgg_pool", ctx.lib.fen_maxpool2, ctx.code, N, hh, ww, cout, ptr(a), ptr(pooled))
                 h, hh, ww = pooled, hh // 2, ww // 2
-        # loss of every feature layer (+ its gradient into the pred half when training)
+        return acts, feats
+
+    def build(self, x2: torch.Tensor, loss: torch.Tensor, dpred: Optional[torch.Tensor], ctx: Optional[Ctx] = None,
+              grad_scale: float = 1.0) -> Dict[int, torch.Tensor]:
+        """x2: NCHW fp32 [2B,3,H,W] = [pred; target]; loss: fp32 [1], set to the weighted
+        perceptual loss; dpred: NHWC [B,H,W,16] (dtype) dL/dpred, which grad_scale x the
+        perceptual gradient is ADDED to (None: forward + loss only).  Returns the features."""
+        ctx = ctx or self.ctx
+        N = x2.shape[0]
+        B = N // 2
+        acts, feats = self.forward(x2, ctx)
+        train = dpred is not None
         nparts = ctx.lib.fen_feat_loss_parts()
-        grads = {}
-        for j, i in enumerate(sorted(self.idx, reverse=True)):
+        order = sorted(self.idx, reverse=True)
+        first = [True]
+
+        def feat_loss(i, d, j):
             f = feats[i]
             n = f.numel() // 2
-            g = ctx.alloc((B,) + tuple(f.shape[1:]))
+            g = d if d is not None else ctx.alloc((B,) + tuple(f.shape[1:]))
             part = ctx.scratch(f"vgg_lpart{j}", (nparts,), torch.float32)
-            grads[i] = (g, part, n)
+            ctx.emit("vgg_feat_loss", ctx.lib.fen_feat_loss, ctx.code, n, ptr(f), int(self.l2),
+                     self.wts[i] / n * grad_scale, ptr(g), int(d is not None), ptr(part))
+            ctx.emit("vgg_loss_sum", ctx.lib.fen_colsum, nparts, 1, ptr(part), self.wts[i] / n, ptr(loss),
+                     0 if first[0] else 1)
+            first[0] = False
+            return g
+
         if not train:
-            for i, (g, part, n) in grads.items():
-                ctx.emit("vgg_feat_loss", ctx.lib.fen_feat_loss, ctx.code, n, ptr(feats[i]), int(self.l2),
-                         self.wts[i] / n, ptr(g), 0, ptr(part))
-                ctx.emit("vgg_loss_sum", ctx.lib.fen_colsum, nparts, 1, ptr(part), self.wts[i] / n, ptr(loss), 1)
+            for j, i in enumerate(order):
+                feat_loss(i, None, j)
             return feats
         # backward on the pred half (first B images of every saved activation)
         d = None
         for k in range(len(acts) - 1, -1, -1):
             c = acts[k]["c"]
             i = c["idx"]
-            if i in grads:
-                g, part, n = grads[i]
-                ctx.emit("vgg_feat_loss", ctx.lib.fen_feat_loss, ctx.code, n, ptr(feats[i]), int(self.l2),
-                         self.wts[i] / n, ptr(d if d is not None else g), int(d is not None), ptr(part))
-                ctx.emit("vgg_loss_sum", ctx.lib.fen_colsum, nparts, 1, ptr(part), self.wts[i] / n, ptr(loss), 1)
-                if d is None:
-                    d = g
+            if i in self.idx:
+                d = feat_loss(i, d, order.index(i))
             hh, ww = acts[k]["H"], acts[k]["W"]
             if i == 0:
                 # d(pred) (NHWC, 3 valid of 16 channels) += dgrad of conv1_1 / std

@@ -1,14 +1,16 @@
 """Loss surface of the reference (src/losses/combined.py:16-302) restricted to the hot path.
 
-The stage-1 generator step's content loss is L1 (combined.py:38-47), which this build fuses
-into the conv_last epilogue (sign(sr-hr)/N written by the kernel, fen_conv_desc.hr).  The
-VGG19 perceptual and SSIM terms are the next rows of SURVEY.md §8f and are not built yet:
-asking for them raises instead of silently training something else.
+The stage-1 generator step's loss is L1 (combined.py:38-47) + the VGG19 perceptual term
+(perceptual.py, stage1_psnr_config.yaml:40-50).  L1 is fused into the conv_last epilogue
+(sign(sr-hr)/N written by the kernel, fen_conv_desc.hr); the perceptual term runs on the
+HIP VGG path (src/hip/vgg.py) and its gradient joins L1's in the same dL/dsr buffer.  SSIM
+/ MS-SSIM / L2 / Charbonnier are not built yet: asking for them raises
+instead of silently training something else.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -26,6 +28,7 @@ class LossConfig:
     charbonnier_eps: float = 1e-3
     perceptual_layers: list = field(default_factory=lambda: ["conv3_4", "conv4_4"])
     ssim_window_size: int = 11
+    vgg_weights: Optional[str] = None      # local torchvision VGG19 state dict (no download offline)
 
 
 class L1Loss(nn.Module):
@@ -40,26 +43,42 @@ class L1Loss(nn.Module):
 
 
 class CombinedLoss(nn.Module):
-    """Weighted loss with component tracking (combined.py:80-203); L1 term only here.
-    `fused_l1_weight` tells the Trainer it may use the fused HIP training step."""
+    """Weighted loss with component tracking (combined.py:80-203): L1 and perceptual terms.
+    `fused_l1_weight` / `fused_perceptual` tell the Trainer it may use the fused HIP step."""
 
     def __init__(self, config: LossConfig):
         super().__init__()
         self.config = config
-        if config.perceptual_weight or config.ssim_weight or config.ms_ssim_weight or config.l2_weight \
-                or config.use_charbonnier:
+        if config.ssim_weight or config.ms_ssim_weight or config.l2_weight or config.use_charbonnier:
             raise NotImplementedError(
-                "only the L1 content term is built on the MI355X path (perceptual / SSIM / L2 / Charbonnier are "
-                "SURVEY.md §8f 'next' rows); set perceptual_weight=0 and ssim_weight=0")
+                "only the L1 and perceptual terms are built on the MI355X path (SSIM / MS-SSIM / L2 / Charbonnier "
+                "are SURVEY.md §8f 'next' rows); set ssim_weight=0")
         self.l1 = L1Loss()
+        self.perceptual = None
+        if config.perceptual_weight > 0:
+            from .perceptual import PerceptualLoss
+            self.perceptual = PerceptualLoss(layers=list(config.perceptual_layers), vgg_weights=config.vgg_weights)
 
     @property
     def fused_l1_weight(self) -> float:
         return float(self.config.l1_weight)
 
+    @property
+    def fused_perceptual(self) -> Optional[dict]:
+        if self.perceptual is None:
+            return None
+        return self.perceptual.fused_spec(float(self.config.perceptual_weight))
+
     def forward(self, pred, target) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
-        l1 = self.l1(pred, target) * self.config.l1_weight
-        return l1, {"l1": l1.detach()}
+        l1 = self.l1(pred, target)
+        total = l1 * self.config.l1_weight
+        comps = {"l1": l1.detach()}
+        if self.perceptual is not None:
+            pl = self.perceptual(pred, target)
+            total = total + self.config.perceptual_weight * pl
+            comps["perceptual"] = pl.detach()
+        comps["total"] = total.detach()
+        return total, comps
 
 
 def create_loss_function(l1_weight: float = 1.0, perceptual_weight: float = 0.01, ssim_weight: float = 0.1,
@@ -72,4 +91,6 @@ def create_loss_function(l1_weight: float = 1.0, perceptual_weight: float = 0.01
     return CombinedLoss(cfg)
 
 
-__all__ = ["LossConfig", "L1Loss", "CombinedLoss", "create_loss_function"]
+from .perceptual import PerceptualLoss, VGGFeatureExtractor  # noqa: E402
+
+__all__ = ["LossConfig", "L1Loss", "CombinedLoss", "create_loss_function", "PerceptualLoss", "VGGFeatureExtractor"]

@@ -131,6 +131,7 @@ class Trainer:
         self.train_loader, self.val_loader = train_loader, val_loader
         self.loss_fn = loss_fn.to(self.device) if loss_fn is not None else None
         self.fused_l1 = getattr(loss_fn, "fused_l1_weight", None)
+        self.fused_perceptual = getattr(loss_fn, "fused_perceptual", None)
         if self.fused_l1 is None and isinstance(loss_fn, nn.L1Loss):
             self.fused_l1 = 1.0
         # torch AdamW object = param_groups/lr holder for the schedulers and the checkpoint
@@ -174,7 +175,8 @@ class Trainer:
             dtype = self.model.compute_dtype
             eng = FENEngine(self.model, batch=B, lr_hw=(H // self.model.scale_factor, W // self.model.scale_factor),
                             dtype=dtype, train=True, device=self.device, loss_weight=self.fused_l1,
-                            clip=self.config.gradient_clip, lr=self.lr, weight_decay=self.config.weight_decay)
+                            clip=self.config.gradient_clip, lr=self.lr, weight_decay=self.config.weight_decay,
+                            perceptual=self.fused_perceptual)
             if self._engines:  # share optimizer moments/step between batch-size variants
                 first = next(iter(self._engines.values()))
                 eng.flat_m, eng.flat_v, eng.scal = first.flat_m, first.flat_v, first.scal

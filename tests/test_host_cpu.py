@@ -108,11 +108,23 @@ def test_loss_factory():
     a, b = torch.rand(2, 3, 8, 8), torch.rand(2, 3, 8, 8)
     total, parts = loss(a, b)
     assert torch.allclose(total, 2.0 * (a - b).abs().mean())
-    assert set(parts) == {"l1"} and loss.fused_l1_weight == 2.0
-    for kw in (dict(perceptual_weight=0.01, ssim_weight=0.0), dict(perceptual_weight=0.0, ssim_weight=0.1),
+    assert set(parts) == {"l1", "total"} and loss.fused_l1_weight == 2.0 and loss.fused_perceptual is None
+    for kw in (dict(perceptual_weight=0.0, ssim_weight=0.1),
                dict(perceptual_weight=0.0, ssim_weight=0.0, use_charbonnier=True)):
         with pytest.raises(NotImplementedError):
             create_loss_function(**kw)
+    # the stage-1 recipe (stage1_psnr_config.yaml:40-50): L1 + perceptual on conv3_4
+    with pytest.warns(UserWarning, match="random"):
+        lp = create_loss_function(l1_weight=1.0, perceptual_weight=1.0, ssim_weight=0.0,
+                                  perceptual_layers=["conv3_4"])
+    spec = lp.fused_perceptual
+    assert spec["weight"] == 1.0 and spec["layers"] == ["conv3_4"] and spec["criterion"] == "l1"
+    assert sorted(spec["params"]) == sorted(f"features.{i}.{n}" for i in (0, 2, 5, 7, 10, 12, 14, 16)
+                                            for n in ("weight", "bias"))
+    fe = lp.perceptual.feature_extractor
+    assert len(fe.features) == 17 and not any(p.requires_grad for p in fe.parameters())
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        lp(a, b)
 
 
 def test_data_sources(tmp_path):
