@@ -45,10 +45,11 @@ class FENEngine:
     def __init__(self, model, batch: int, lr_hw, dtype: torch.dtype = torch.bfloat16, train: bool = False,
                  device="cuda", loss_weight: float = 1.0, clip: float = 0.5, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, process_group=None,
-                 perceptual: Optional[dict] = None):
+                 perceptual: Optional[dict] = None, ssim_weight: float = 0.0):
         """perceptual (training only): the stage configs' VGG19 term (perceptual.py:144-169) as
         dict(weight=, layers=, criterion=, normalize=, params={'features.i.weight': ...},
-        layer_weights=None); its gradient joins the fused L1 gradient in dL/dsr."""
+        layer_weights=None); its gradient joins the fused L1 gradient in dL/dsr.  ssim_weight
+        (training only): the stage-2 term weight * (1 - SSIM) (ssim_loss.py:174-226), likewise."""
         self.spec = NetSpec.from_config(model.config)
         self.dtype, self.device, self.train = dtype, torch.device(device), train
         self.B, (self.h, self.w) = batch, lr_hw
@@ -77,6 +78,8 @@ class FENEngine:
             self._build_forward(training=False)
         else:
             self.l1_weight = loss_weight
+            self.ssim_weight = float(ssim_weight)
+            self.ssim_val = torch.zeros(1, device=self.device)
             self.vgg = None
             self.loss_perc = torch.zeros(1, device=self.device)
             if perceptual:
@@ -133,6 +136,24 @@ class FENEngine:
             colsum(ctx, lp, lp.shape[0], 1, self.loss, scale=1.0 / (self.B * s.out_ch * self.H * self.W))
             if self.vgg is not None:
                 self.vgg.build(self.x2, self.loss_perc, self.saved_tail["dout"], grad_scale=1.0 / self.world)
+            if self.ssim_weight:
+                self._build_ssim()
+
+    def _build_ssim(self):
+        """weight * (1 - mean SSIM(sr, hr)): the SSIM map's tile sums and its gradient, added
+        to dL/dsr (NHWC16) in the same launch; then per-image and batch means."""
+        ctx, s = self.ctx, self.spec
+        B, C, H, W = self.B, s.out_ch, self.H, self.W
+        from ..losses.ssim import _window1d
+        self.ssim_win = _window1d(11, 1.5).to(self.device)
+        rows = ctx.lib.fen_ssim_parts(B, C, H, W)
+        part = ctx.scratch("ssim_part", (rows * B,), torch.float32)
+        per = ctx.scratch("ssim_img", (B,), torch.float32)
+        n = B * C * H * W
+        ctx.emit("ssim", ctx.lib.fen_ssim, ctx.code, B, C, H, W, ptr(self.out), ptr(self.hr), ptr(self.ssim_win), 11,
+                 0.01 ** 2, 0.03 ** 2, ptr(part), ptr(self.saved_tail["dout"]), -self.ssim_weight / (n * self.world), 2)
+        ctx.emit("ssim_img", ctx.lib.fen_colsum, rows, B, ptr(part), 1.0 / (C * H * W), ptr(per), 0)
+        ctx.emit("ssim_mean", ctx.lib.fen_colsum, B, 1, ptr(per), 1.0 / B, ptr(self.ssim_val), 0)
 
     def _build_backward(self):
         s, ctx = self.spec, self.ctx
@@ -184,9 +205,14 @@ class FENEngine:
 
     def total_loss(self) -> torch.Tensor:
         """weight * L1 (+ the weighted perceptual term), on the device."""
-        if self.vgg is None:
+        if self.vgg is None and not self.ssim_weight:
             return self.loss if self.l1_weight == 1.0 else self.loss * self.l1_weight
-        return self.loss * self.l1_weight + self.loss_perc
+        t = self.loss * self.l1_weight
+        if self.vgg is not None:
+            t = t + self.loss_perc
+        if self.ssim_weight:
+            t = t + self.ssim_weight * (1 - self.ssim_val)
+        return t
 
     def set_lr(self, lr: float):
         self.scal[3] = lr

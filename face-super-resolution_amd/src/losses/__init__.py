@@ -49,19 +49,27 @@ class CombinedLoss(nn.Module):
     def __init__(self, config: LossConfig):
         super().__init__()
         self.config = config
-        if config.ssim_weight or config.ms_ssim_weight or config.l2_weight or config.use_charbonnier:
+        if config.ms_ssim_weight or config.l2_weight or config.use_charbonnier:
             raise NotImplementedError(
-                "only the L1 and perceptual terms are built on the MI355X path (SSIM / MS-SSIM / L2 / Charbonnier "
-                "are SURVEY.md §8f 'next' rows); set ssim_weight=0")
+                "only the L1, perceptual and SSIM terms are built on the MI355X path (MS-SSIM / L2 / Charbonnier "
+                "are not); set ms_ssim_weight=0, l2_weight=0, use_charbonnier=False")
         self.l1 = L1Loss()
         self.perceptual = None
         if config.perceptual_weight > 0:
             from .perceptual import PerceptualLoss
             self.perceptual = PerceptualLoss(layers=list(config.perceptual_layers), vgg_weights=config.vgg_weights)
+        self.ssim = None
+        if config.ssim_weight > 0:
+            from .ssim import SSIMLoss
+            self.ssim = SSIMLoss(window_size=config.ssim_window_size)
 
     @property
     def fused_l1_weight(self) -> float:
         return float(self.config.l1_weight)
+
+    @property
+    def fused_ssim_weight(self) -> float:
+        return float(self.config.ssim_weight) if self.ssim is not None else 0.0
 
     @property
     def fused_perceptual(self) -> Optional[dict]:
@@ -77,6 +85,10 @@ class CombinedLoss(nn.Module):
             pl = self.perceptual(pred, target)
             total = total + self.config.perceptual_weight * pl
             comps["perceptual"] = pl.detach()
+        if self.ssim is not None:
+            sl = self.ssim(pred, target)
+            total = total + self.config.ssim_weight * sl
+            comps["ssim"] = sl.detach()
         comps["total"] = total.detach()
         return total, comps
 
@@ -92,5 +104,7 @@ def create_loss_function(l1_weight: float = 1.0, perceptual_weight: float = 0.01
 
 
 from .perceptual import PerceptualLoss, VGGFeatureExtractor  # noqa: E402
+from .ssim import MSSSIMLoss, SSIMLoss, ssim  # noqa: E402
 
-__all__ = ["LossConfig", "L1Loss", "CombinedLoss", "create_loss_function", "PerceptualLoss", "VGGFeatureExtractor"]
+__all__ = ["LossConfig", "L1Loss", "CombinedLoss", "create_loss_function", "PerceptualLoss", "VGGFeatureExtractor",
+           "SSIMLoss", "MSSSIMLoss", "ssim"]

@@ -132,6 +132,7 @@ class Trainer:
         self.loss_fn = loss_fn.to(self.device) if loss_fn is not None else None
         self.fused_l1 = getattr(loss_fn, "fused_l1_weight", None)
         self.fused_perceptual = getattr(loss_fn, "fused_perceptual", None)
+        self.fused_ssim = getattr(loss_fn, "fused_ssim_weight", 0.0)
         if self.fused_l1 is None and isinstance(loss_fn, nn.L1Loss):
             self.fused_l1 = 1.0
         # torch AdamW object = param_groups/lr holder for the schedulers and the checkpoint
@@ -176,7 +177,7 @@ class Trainer:
             eng = FENEngine(self.model, batch=B, lr_hw=(H // self.model.scale_factor, W // self.model.scale_factor),
                             dtype=dtype, train=True, device=self.device, loss_weight=self.fused_l1,
                             clip=self.config.gradient_clip, lr=self.lr, weight_decay=self.config.weight_decay,
-                            perceptual=self.fused_perceptual)
+                            perceptual=self.fused_perceptual, ssim_weight=self.fused_ssim)
             if self._engines:  # share optimizer moments/step between batch-size variants
                 first = next(iter(self._engines.values()))
                 eng.flat_m, eng.flat_v, eng.scal = first.flat_m, first.flat_v, first.scal
@@ -241,16 +242,22 @@ class Trainer:
     @torch.no_grad()
     def _validate_epoch(self) -> Dict[str, float]:
         self.model.eval()
-        tl, tp, n = 0.0, 0.0, 0
+        tl, tp, ts, n = 0.0, 0.0, 0.0, 0
         for batch in self.val_loader:
             hr = batch["hr"].to(self.device)
             sr = self.model(bicubic_down4(hr))
             loss = F.l1_loss(sr, hr) if self.loss_fn is None else self.loss_fn(sr, hr)[0]
             tl += float(loss)
             tp += self._compute_psnr(sr, hr)
+            ts += self._compute_ssim(sr, hr)
             n += 1
         n = max(n, 1)
-        return {"loss": tl / n, "psnr": tp / n, "ssim": float("nan")}  # SSIM: SURVEY.md §8f next #4
+        return {"loss": tl / n, "psnr": tp / n, "ssim": ts / n}
+
+    def _compute_ssim(self, pred: torch.Tensor, target: torch.Tensor) -> float:
+        """ssim(pred, target) with the reference defaults (trainer.py:630-634), on the HIP kernel."""
+        from ..losses.ssim import ssim
+        return float(ssim(pred, target))
 
     def _compute_psnr(self, pred: torch.Tensor, target: torch.Tensor) -> float:
         """10 log10(1/MSE) over the batch (trainer.py:621-628)."""

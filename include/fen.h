@@ -261,6 +261,18 @@ int fen_feat_loss_parts(void);
 int fen_feat_loss(int dtype, size_t n, const void* f, int l2, float scale, void* g, int accumulate, float* part,
                   void* stream);
 
+/* ---- SSIM (src/losses/ssim_loss.py:44-98, SSIMLoss 174-226; val metric trainer.py:630-634) ----
+ * pred / target NCHW fp32 [B,C,H,W]; window1d = the normalised 11-tap Gaussian (2-D window =
+ * its outer product, zero padding); C1 = (K1 range)^2, C2 = (K2 range)^2.
+ * part[fen_ssim_parts()] (rows = C x tiles, cols = B: part[(c*ntile + tile)*B + b]) = sums of
+ * the SSIM map per tile (fen_colsum over the rows gives per-image sums).  grad_mode 1: grad =
+ * NCHW fp32 grad_scale * d(sum S)/d(pred) (written); 2: grad = NHWC [B,H,W,16] of dtype,
+ * grad_scale * d(sum S)/d(pred) ADDED to channel c (the generator's dL/dsr buffer); 0: none. */
+size_t fen_ssim_parts(int B, int C, int H, int W);
+int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred, const float* target, const float* window1d,
+             int window_size, float C1, float C2, float* part, void* grad, float grad_scale, int grad_mode,
+             void* stream);
+
 const char* fen_status_string(int code);
 const char* fen_build_info(void);
 

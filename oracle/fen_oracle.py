@@ -282,3 +282,53 @@ def perceptual_loss(p: Params, pred: torch.Tensor, target: torch.Tensor, layer_i
         d = F.l1_loss(fp[i], ft[i]) if criterion == "l1" else F.mse_loss(fp[i], ft[i])
         loss = loss + w * d
     return loss
+
+
+# ---------------------------------------------------------------------------------------
+# SSIM (reference src/losses/ssim_loss.py:14-98,174-226); pinned by tests/golden/g7_ssim.npz
+# (made by importing the reference module, tests/golden/make_golden_ssim.py)
+def gaussian_window(window_size: int = 11, sigma: float = 1.5) -> torch.Tensor:
+    """ssim_loss.py:14-41: normalised 1-D Gaussian, 2-D window = outer product."""
+    c = torch.arange(window_size, dtype=torch.float32) - window_size // 2
+    g = torch.exp(-(c ** 2) / (2 * sigma ** 2))
+    g = g / g.sum()
+    return g[:, None] @ g[None, :]
+
+
+def _ssim_terms(pred, target, window_size, sigma, data_range):
+    C = pred.shape[1]
+    w = gaussian_window(window_size, sigma).to(pred.dtype).expand(C, 1, window_size, window_size)
+    pad = window_size // 2
+    f = lambda x: F.conv2d(x, w, padding=pad, groups=C)   # noqa: E731
+    mp, mt = f(pred), f(target)
+    spp = f(pred * pred) - mp * mp
+    stt = f(target * target) - mt * mt
+    spt = f(pred * target) - mp * mt
+    C1, C2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
+    lum = (2 * mp * mt + C1) / (mp * mp + mt * mt + C1)
+    cs = (2 * spt + C2) / (spp + stt + C2)
+    return lum, cs
+
+
+def ssim(pred, target, window_size=11, sigma=1.5, data_range=1.0, size_average=True):
+    """ssim_loss.py:44-98 (zero-padded depthwise Gaussian, K = (0.01, 0.03))."""
+    lum, cs = _ssim_terms(pred, target, window_size, sigma, data_range)
+    m = lum * cs
+    return m.mean() if size_average else m.mean(dim=[1, 2, 3])
+
+
+def ms_ssim(pred, target, window_size=11, sigma=1.5, data_range=1.0, weights=None):
+    """ssim_loss.py:101-171: 5 scales, 2x2 average pooling between them."""
+    if weights is None:
+        weights = torch.tensor([0.0448, 0.2856, 0.3001, 0.2363, 0.1333], dtype=pred.dtype)
+    mcs = []
+    for i in range(len(weights)):
+        lum, cs = _ssim_terms(pred, target, window_size, sigma, data_range)
+        if i == len(weights) - 1:
+            val = (lum * cs).mean()
+        else:
+            mcs.append(cs.mean())
+        pred, target = F.avg_pool2d(pred, 2, 2), F.avg_pool2d(target, 2, 2)
+    for i, m in enumerate(mcs):
+        val = val * (m ** weights[i])
+    return val

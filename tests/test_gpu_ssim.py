@@ -1,0 +1,106 @@
+"""SSIM on the HIP path (csrc/ssim.hip via src/losses/ssim.py) against the reference's own
+values (tests/golden/g7_ssim.npz, made by importing src/losses/ssim_loss.py) and the CPU
+oracle's restatement; the engine's stage-2 step (L1 + w (1 - SSIM)) against autograd."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fen_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_ssim_matches_reference_golden(golden):
+    from src.losses import SSIMLoss, ssim
+    g = golden("g7_ssim.npz")
+    p, t = torch.from_numpy(g["pred"]).to(DEV), torch.from_numpy(g["target"]).to(DEV)
+    assert abs(float(ssim(p, t)) - float(g["ssim_mean"])) <= 2e-6
+    assert np.allclose(ssim(p, t, size_average=False).cpu().numpy(), g["ssim_per_img"], atol=2e-6)
+    assert abs(float(ssim(p, p)) - 1.0) <= 1e-6
+    pr = p.clone().requires_grad_(True)
+    loss = SSIMLoss()(pr, t)
+    loss.backward()
+    assert abs(float(loss) - float(g["loss"])) <= 2e-6
+    ref = g["dpred"]
+    assert np.abs(pr.grad.cpu().numpy() - ref).max() <= 1e-4 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 3, 100, 70), (1, 1, 31, 33), (3, 3, 64, 64), (1, 3, 8, 5)])
+@pytest.mark.parametrize("size_average", [True, False])
+def test_ssim_loss_vs_oracle(B, C, H, W, size_average):
+    """Ragged tiles (100 x 70), images smaller than the window (8 x 5), one channel."""
+    from src.losses import SSIMLoss
+    torch.manual_seed(B * 1000 + H)
+    p = torch.rand(B, C, H, W)
+    t = (0.6 * p + 0.4 * torch.rand(B, C, H, W)).clamp(0, 1)
+    pr = p.clone().requires_grad_(True)
+    ref = 1 - O.ssim(pr, t, size_average=size_average)
+    ref.sum().backward()
+    pd = p.clone().to(DEV).requires_grad_(True)
+    out = SSIMLoss(size_average=size_average)(pd, t.to(DEV))
+    out.sum().backward()
+    assert torch.allclose(out.detach().cpu(), ref.detach(), atol=2e-6)
+    e = (pd.grad.cpu() - pr.grad).abs().max() / pr.grad.abs().max()
+    assert e <= 1e-4, float(e)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ssim_grad_accumulates_into_nhwc16(dtype):
+    """grad_mode 2: grad_scale * d(sum S)/dpred ADDED to channel c of an NHWC [B,H,W,16]
+    buffer (the generator's dL/dsr), padding channels untouched."""
+    from src.hip import lib as L
+    from src.hip.program import ptr
+    from src.losses.ssim import _window1d
+    torch.manual_seed(4)
+    B, C, H, W = 2, 3, 40, 36
+    p = torch.rand(B, C, H, W)
+    t = torch.rand(B, C, H, W)
+    pr = p.clone().requires_grad_(True)
+    O.ssim(pr, t).backward()                      # d(mean S)/dp
+    scale = -0.3 / (B * C * H * W)
+    expect = -0.3 * pr.grad                       # scale * d(sum S)/dp
+    lib = L.load()
+    base = 2e-4          # the order of the L1 gradient the buffer holds in the engine (w / N)
+    buf = torch.full((B, H, W, 16), base, device=DEV, dtype=dtype)
+    rows = lib.fen_ssim_parts(B, C, H, W)
+    part = torch.empty(rows * B, device=DEV)
+    win = _window1d(11, 1.5).to(DEV)
+    pd, td = p.to(DEV), t.to(DEV)
+    L.check(lib.fen_ssim(L.dtype_code(dtype), B, C, H, W, ptr(pd), ptr(td), ptr(win), 11, 1e-4, 9e-4, ptr(part),
+                         ptr(buf), scale, 2, torch.cuda.current_stream().cuda_stream), "ssim")
+    torch.cuda.synchronize()
+    base_q = torch.tensor(base, dtype=dtype).float()
+    got = buf[..., :C].float().cpu().permute(0, 3, 1, 2) - base_q
+    tol = 1e-4 if dtype == torch.float32 else 1e-2      # relative to max |expect| (bf16 storage)
+    assert (got - expect).abs().max() <= tol * (expect.abs().max() + base)
+    assert bool((buf[..., C:].float().cpu() == base_q).all())
+
+
+def test_engine_step_with_ssim_fp32(golden):
+    """FENEngine(ssim_weight=0.2) fp32: generator grads of L1 + 0.2 (1 - SSIM) vs oracle autograd."""
+    from src.hip.engine import FENEngine
+    from src.models import FaceEnhanceNet
+    g1 = golden("g1_config1.npz")
+    sd = {k[2:]: torch.from_numpy(v) for k, v in g1.items() if k.startswith("p/")}
+    m = FaceEnhanceNet(num_channels=64, num_groups=1, blocks_per_group=2, reduction_ratio=4, scale_factor=4,
+                       res_scale=0.2, precision="fp32")
+    m.load_state_dict(sd)
+    hr = torch.from_numpy(g1["hr"])
+    eng = FENEngine(m, batch=2, lr_hw=(32, 32), dtype=torch.float32, train=True, ssim_weight=0.2)
+    eng.hr.copy_(hr.to(DEV))
+    eng.ctx.run()
+    torch.cuda.synchronize()
+    shape = O.NetShape(64, 1, 2, 4, 4, 0.2)
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
+    out = O.forward(leaves, O.lr_from_hr(hr), shape, training=True)
+    loss = (out - hr).abs().mean() + 0.2 * (1 - O.ssim(out, hr))
+    loss.backward()
+    assert abs(float(eng.total_loss()) - float(loss.detach())) <= 1e-5 * float(loss.detach())
+    bad = {}
+    for k, gg in eng.grads.items():
+        ref = leaves[k].grad.double()
+        e = float((gg.cpu().double() - ref).norm() / max(ref.norm(), 1e-30))
+        if not e <= 1e-4:
+            bad[k] = e
+    assert not bad, bad

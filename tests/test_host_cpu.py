@@ -109,10 +109,15 @@ def test_loss_factory():
     total, parts = loss(a, b)
     assert torch.allclose(total, 2.0 * (a - b).abs().mean())
     assert set(parts) == {"l1", "total"} and loss.fused_l1_weight == 2.0 and loss.fused_perceptual is None
-    for kw in (dict(perceptual_weight=0.0, ssim_weight=0.1),
-               dict(perceptual_weight=0.0, ssim_weight=0.0, use_charbonnier=True)):
-        with pytest.raises(NotImplementedError):
-            create_loss_function(**kw)
+    with pytest.raises(NotImplementedError):
+        create_loss_function(perceptual_weight=0.0, ssim_weight=0.0, use_charbonnier=True)
+    from src.losses import CombinedLoss, LossConfig, SSIMLoss
+    with pytest.raises(NotImplementedError):
+        CombinedLoss(LossConfig(perceptual_weight=0.0, ssim_weight=0.0, ms_ssim_weight=0.1))
+    ls = create_loss_function(l1_weight=1.0, perceptual_weight=0.0, ssim_weight=0.2)
+    assert isinstance(ls.ssim, SSIMLoss) and ls.fused_ssim_weight == 0.2 and ls.ssim.window.shape == (3, 1, 11, 11)
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        ls(a, b)
     # the stage-1 recipe (stage1_psnr_config.yaml:40-50): L1 + perceptual on conv3_4
     with pytest.warns(UserWarning, match="random"):
         lp = create_loss_function(l1_weight=1.0, perceptual_weight=1.0, ssim_weight=0.0,
