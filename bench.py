@@ -118,6 +118,28 @@ def cpu_baseline(model, seconds=10.0):
             "sample": f"oracle fp32 eval forward, full 6x10 net, batch 2 of 64x64, {n} passes in {el:.1f}s"}
 
 
+def time_ssim(eng, reps=50):
+    """The stage-2 SSIM launch of a training engine (fwd map + tile sums + gradient added to
+    dL/dsr), timed with HIP events on the current stream, against the HBM roofline:
+    algorithmic bytes = pred + target (fp32 NCHW) read + dL/dsr (NHWC16 bf16) read + write."""
+    name, fn, fargs = next(op for op in eng.ctx.ops if op[0] == "ssim")
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(5):
+        fn(*fargs, s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn(*fargs, s)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    B, C, H, W = eng.B, 3, eng.H, eng.W
+    nbytes = 2 * B * C * H * W * 4 + 2 * B * H * W * 16 * 2
+    return {"kernel": "k_ssim<GRAD> (csrc/ssim.hip)", "us": round(us, 2), "bytes": nbytes,
+            "achieved_GBs": round(nbytes / us / 1e3, 1), "peak_GBs": 8000.0,
+            "frac": round(nbytes / us / 1e3 / 8000.0, 4), "bound": "hbm"}
+
+
 def load_traffic(label):
     """HBM bytes per launch of the dominant kernel from its committed PMC summary
     (profiles/pmc_*.json, tools/prof_summary.py pmc), or None when none matches it."""
@@ -231,6 +253,27 @@ def main():
                 "ms_per_step": round(1000.0 * tp / args.train_steps, 3), "steps": args.train_steps,
                 "loss": float(peng.total_loss()), "vgg": "random-init VGG19 (no ImageNet weights offline)"}
             del peng
+            torch.cuda.empty_cache()
+            # stage 2 (stage2_ssim_config.yaml:40-50): L1 x 1 + perceptual x 0.5 + (1 - SSIM) x 0.2
+            spec2 = dict(spec, weight=0.5)
+            sm = build_model("bf16")
+            seng = FENEngine(sm, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=True, device="cuda",
+                             perceptual=spec2, ssim_weight=0.2)
+            seng.hr.copy_(hr)
+            if world == 1:
+                seng.capture()
+                fn = seng.replay
+            else:
+                fn = seng.step
+            ts = timed(fn, args.train_steps, 3, world)
+            out["train_stage2"] = {
+                "metric": "training images/sec (stage-2 step: L1 + 0.5 perceptual + 0.2 (1 - SSIM)) at batch 32/GPU",
+                "value": round(B * world * args.train_steps / ts, 2),
+                "ms_per_step": round(1000.0 * ts / args.train_steps, 3), "steps": args.train_steps,
+                "loss": float(seng.total_loss())}
+            if world == 1:
+                out["aux"] = {"ssim_loss_grad": time_ssim(seng)}
+            del seng
     if cpu_model_sd is not None:
         out["cpu_baseline"] = cpu_baseline(cpu_model_sd, args.cpu_seconds)
     if rank == 0:

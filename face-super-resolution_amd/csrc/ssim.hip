@@ -21,6 +21,25 @@ struct SsimWin {
 
 inline int nblk(size_t n, int t = 256) { return (int)((n + t - 1) / t); }
 
+// Horizontal pass over NCH column chunks of CW outputs: thread keeps the CW + 10 inputs of
+// its chunk in registers and reads each LDS element once.
+template <int CW>
+__device__ __forceinline__ void hrow(const SsimWin& win, const float* p, const float* t, float (&o)[5][CW]) {
+    float pv[CW + 2 * SR], tv[CW + 2 * SR];
+#pragma unroll
+    for (int i = 0; i < CW + 2 * SR; ++i) { pv[i] = p[i]; tv[i] = t[i]; }
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2 * SR + 1; ++j) {
+            const float pp = pv[c + j], tt = tv[c + j], g = win.g[j];
+            s0 += g * pp; s1 += g * tt; s2 += g * pp * pp; s3 += g * tt * tt; s4 += g * pp * tt;
+        }
+        o[0][c] = s0; o[1][c] = s1; o[2][c] = s2; o[3][c] = s3; o[4][c] = s4;
+    }
+}
+
 template <bool GRAD, typename T>
 __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const float* __restrict__ pred,
                                               const float* __restrict__ target, const SsimWin win, float C1,
@@ -29,10 +48,18 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     constexpr int E1 = GRAD ? ST + 2 * SR : ST;   // where the map (and a, b, c) is needed
     constexpr int E2 = E1 + 2 * SR;               // where the inputs are needed
     constexpr int O1 = GRAD ? SR : 0;             // tile offset inside E1
-    __shared__ float sp[E2][E2 + 1], st[E2][E2 + 1];
-    __shared__ float hp[5][E2][E1 + 1];           // horizontal pass (reused for a, b, c)
-    __shared__ float abc[3][E1][E1 + 1];
+    constexpr int CW = GRAD ? 7 : 8;              // register block of the map passes (E1 = 6 or 4 of them)
+    constexpr int NCH = E1 / CW;
+    constexpr int CW2 = 8, NCH2 = ST / CW2;       // register block of the gradient passes
+    constexpr int PS = E2 + 1;
+    // sb: p, t on E2 x E2; after the first pass, a / b / c on E1 x E1 (3 E1 (E1+1) <= 2 E2 PS)
+    __shared__ float sb[2 * E2 * PS];
+    __shared__ float hp[5][E2][E1 + 1];           // horizontal sums (reused for a, b, c)
     __shared__ float red[256];
+    static_assert(3 * E1 * (E1 + 1) <= 2 * E2 * PS, "a/b/c alias");
+    float* sp = sb;
+    float* st = sb + E2 * PS;
+    float (*abc)[E1][E1 + 1] = (float (*)[E1][E1 + 1])sb;
     const int tid = threadIdx.x;
     const int plane = blockIdx.z, b = plane / C, ch = plane % C;
     const int h0 = blockIdx.y * ST, w0 = blockIdx.x * ST;
@@ -42,76 +69,117 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     for (int i = tid; i < E2 * E2; i += 256) {
         const int r = i / E2, c = i % E2, gy = gy0 + r, gx = gx0 + c;
         const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-        sp[r][c] = in ? pp[(size_t)gy * W + gx] : 0.f;
-        st[r][c] = in ? tp[(size_t)gy * W + gx] : 0.f;
+        sp[r * PS + c] = in ? pp[(size_t)gy * W + gx] : 0.f;
+        st[r * PS + c] = in ? tp[(size_t)gy * W + gx] : 0.f;
     }
     __syncthreads();
-    for (int i = tid; i < E2 * E1; i += 256) {
-        const int r = i / E1, c = i % E1;
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+    for (int i = tid; i < E2 * NCH; i += 256) {
+        const int r = i / NCH, c0 = (i % NCH) * CW;
+        float o[5][CW];
+        hrow<CW>(win, sp + r * PS + c0, st + r * PS + c0, o);
 #pragma unroll
-        for (int j = 0; j < 2 * SR + 1; ++j) {
-            const float p = sp[r][c + j], t = st[r][c + j], g = win.g[j];
-            s0 += g * p; s1 += g * t; s2 += g * p * p; s3 += g * t * t; s4 += g * p * t;
-        }
-        hp[0][r][c] = s0; hp[1][r][c] = s1; hp[2][r][c] = s2; hp[3][r][c] = s3; hp[4][r][c] = s4;
+        for (int k = 0; k < 5; ++k)
+#pragma unroll
+            for (int c = 0; c < CW; ++c) hp[k][r][c0 + c] = o[k][c];
     }
     __syncthreads();
+    // vertical pass: thread = (column, CW-row chunk), the chunk's CW + 10 rows read once
     float acc = 0.f;
-    for (int i = tid; i < E1 * E1; i += 256) {
-        const int r = i / E1, c = i % E1;
-        float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = tid; i < E1 * NCH; i += 256) {
+        const int c = i % E1, r0 = (i / E1) * CW;
+        float m[5][CW];
 #pragma unroll
-        for (int j = 0; j < 2 * SR + 1; ++j) {
-            const float g = win.g[j];
+        for (int k = 0; k < 5; ++k)
 #pragma unroll
-            for (int k = 0; k < 5; ++k) m[k] += g * hp[k][r + j][c];
+            for (int o = 0; o < CW; ++o) m[k][o] = 0.f;
+#pragma unroll
+        for (int rr = 0; rr < CW + 2 * SR; ++rr) {
+            float v[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) v[k] = hp[k][r0 + rr][c];
+#pragma unroll
+            for (int o = 0; o < CW; ++o) {
+                const int j = rr - o;
+                if (j >= 0 && j <= 2 * SR) {
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) m[k][o] += win.g[j] * v[k];
+                }
+            }
         }
-        const float mp = m[0], mt = m[1];
-        const float spp = m[2] - mp * mp, stt = m[3] - mt * mt, spt = m[4] - mp * mt;
-        const float A1 = 2.f * mp * mt + C1, A2 = 2.f * spt + C2;
-        const float B1 = mp * mp + mt * mt + C1, B2 = spp + stt + C2;
-        const float S = (A1 * A2) / (B1 * B2);
-        const int gy = h0 - O1 + r, gx = w0 - O1 + c;
-        const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-        const bool own = r >= O1 && r < O1 + ST && c >= O1 && c < O1 + ST;
-        if (in && own) acc += S;
-        if constexpr (GRAD) {
-            const float iB = 1.f / (B1 * B2);
-            abc[0][r][c] = in ? 2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (1.f / B1 - 1.f / B2) : 0.f;
-            abc[1][r][c] = in ? -S / B2 : 0.f;
-            abc[2][r][c] = in ? 2.f * A1 * iB : 0.f;
+#pragma unroll
+        for (int o = 0; o < CW; ++o) {
+            const int r = r0 + o;
+            const float mp = m[0][o], mt = m[1][o];
+            const float spp = m[2][o] - mp * mp, stt = m[3][o] - mt * mt, spt = m[4][o] - mp * mt;
+            const float A1 = 2.f * mp * mt + C1, A2 = 2.f * spt + C2;
+            const float B1 = mp * mp + mt * mt + C1, B2 = spp + stt + C2;
+            const float S = (A1 * A2) / (B1 * B2);
+            const int gy = h0 - O1 + r, gx = w0 - O1 + c;
+            const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+            const bool own = r >= O1 && r < O1 + ST && c >= O1 && c < O1 + ST;
+            if (in && own) acc += S;
+            if constexpr (GRAD) {
+                const float iB = 1.f / (B1 * B2);
+                abc[0][r][c] = in ? 2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (1.f / B1 - 1.f / B2) : 0.f;
+                abc[1][r][c] = in ? -S / B2 : 0.f;
+                abc[2][r][c] = in ? 2.f * A1 * iB : 0.f;
+            }
         }
     }
     if constexpr (GRAD) {
         __syncthreads();
-        for (int i = tid; i < E1 * ST; i += 256) {           // horizontal pass of a, b, c
-            const int r = i / ST, c = i % ST;
-            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        for (int i = tid; i < E1 * NCH2; i += 256) {          // horizontal pass of a, b, c
+            const int r = i / NCH2, c0 = (i % NCH2) * CW2;
 #pragma unroll
-            for (int j = 0; j < 2 * SR + 1; ++j) {
-                const float g = win.g[j];
-                s0 += g * abc[0][r][c + j]; s1 += g * abc[1][r][c + j]; s2 += g * abc[2][r][c + j];
+            for (int k = 0; k < 3; ++k) {
+                float v[CW2 + 2 * SR];
+#pragma unroll
+                for (int q = 0; q < CW2 + 2 * SR; ++q) v[q] = abc[k][r][c0 + q];
+#pragma unroll
+                for (int c = 0; c < CW2; ++c) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 2 * SR + 1; ++j) s += win.g[j] * v[c + j];
+                    hp[k][r][c0 + c] = s;
+                }
             }
-            hp[0][r][c] = s0; hp[1][r][c] = s1; hp[2][r][c] = s2;
         }
         __syncthreads();
-        for (int i = tid; i < ST * ST; i += 256) {
-            const int r = i / ST, c = i % ST, gy = h0 + r, gx = w0 + c;
-            if (gy >= H || gx >= W) continue;
-            float ga = 0.f, gb = 0.f, gc = 0.f;
+        for (int i = tid; i < ST * NCH2; i += 256) {          // vertical pass + the gradient
+            const int c = i % ST, r0 = (i / ST) * CW2, gx = w0 + c;
+            float m[3][CW2];
 #pragma unroll
-            for (int j = 0; j < 2 * SR + 1; ++j) {
-                const float g = win.g[j];
-                ga += g * hp[0][r + j][c]; gb += g * hp[1][r + j][c]; gc += g * hp[2][r + j][c];
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int o = 0; o < CW2; ++o) m[k][o] = 0.f;
+#pragma unroll
+            for (int rr = 0; rr < CW2 + 2 * SR; ++rr) {
+                float v[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) v[k] = hp[k][r0 + rr][c];
+#pragma unroll
+                for (int o = 0; o < CW2; ++o) {
+                    const int j = rr - o;
+                    if (j >= 0 && j <= 2 * SR) {
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) m[k][o] += win.g[j] * v[k];
+                    }
+                }
             }
-            const float p = sp[r + 2 * SR][c + 2 * SR], t = st[r + 2 * SR][c + 2 * SR];
-            const float d = grad_scale * (ga + 2.f * p * gb + t * gc);
-            if (grad_mode == 1) {
-                ((float*)grad)[(size_t)plane * H * W + (size_t)gy * W + gx] = d;
-            } else {
-                T* o = (T*)grad + (((size_t)b * H + gy) * W + gx) * 16 + ch;
-                *o = fromf<T>(tof<T>(*o) + d);
+            if (gx >= W) continue;
+#pragma unroll
+            for (int o = 0; o < CW2; ++o) {
+                const int gy = h0 + r0 + o;
+                if (gy >= H) break;
+                const size_t e = (size_t)gy * W + gx;
+                const float p = pp[e], t = tp[e];                // L2-hot: this block staged them
+                const float d = grad_scale * (m[0][o] + 2.f * p * m[1][o] + t * m[2][o]);
+                if (grad_mode == 1) {
+                    ((float*)grad)[(size_t)plane * H * W + e] = d;
+                } else {
+                    T* q = (T*)grad + (((size_t)b * H + gy) * W + gx) * 16 + ch;
+                    *q = fromf<T>(tof<T>(*q) + d);
+                }
             }
         }
     }
