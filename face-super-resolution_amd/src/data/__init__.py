@@ -1,7 +1,11 @@
-"""Minimal HR-image sources for the trainer (the reference's FFHQ/HDF5 loader, src/data, is
-outside this build's scope).  Each item is {'hr': [3,H,W] fp32 in
-[0,1]}; LR is synthesised on the GPU by the trainer, as the reference does (trainer.py:416).
+"""HR-image sources for the trainer.  Each batch is {'hr': [B,3,H,W] fp32 in [0,1]}; LR is
+synthesised on the GPU by the trainer, as the reference does (trainer.py:416).
 
+* DeviceHRLoader (device_loader.py): uint8 HWC images -> pinned
+  staging -> async copy -> the reference's train-mode transform (crop, flip, rot90, colour
+  jitter, /255) on the GPU (csrc/augment.hip).  get_device_loader() builds one over a
+  directory of HxWx3 uint8 .npy files with the reference's augmentation defaults
+  (scripts/train.py:174-198).
 * SyntheticHRDataset: seeded U[0,1) images (benchmarks, smoke runs).
 * NpyHRDataset: a directory of .npy files holding HxWx3 uint8 or [0,1] float arrays.
 get_dataloader() keeps the reference's signature (dataset.py:321-352) and, under
@@ -66,4 +70,40 @@ def get_dataloader(data_root: Optional[str], mode: str = "train", batch_size: in
                       num_workers=num_workers, pin_memory=True, drop_last=(mode == "train"))
 
 
-__all__ = ["SyntheticHRDataset", "NpyHRDataset", "get_dataloader"]
+class _NpyImages:
+    """Lazy uint8 HxWx3 images from .npy files (np.load, allow_pickle=False)."""
+
+    def __init__(self, files):
+        self.files = files
+
+    def __len__(self):
+        return len(self.files)
+
+    def __getitem__(self, i):
+        a = np.load(self.files[i], allow_pickle=False)
+        if a.dtype != np.uint8:
+            raise ValueError(f"{self.files[i]}: the device pipeline takes uint8 images")
+        return a
+
+
+def get_device_loader(data_root: str, mode: str = "train", batch_size: int = 16, hr_patch_size: int = 128,
+                      horizontal_flip: float = 0.5, random_rotate90: float = 0.0, color_jitter_prob: float = 0.3,
+                      brightness: float = 0.1, contrast: float = 0.1, saturation: float = 0.0, seed: int = 0,
+                      device="cuda", **unused):
+    """The GPU data path over a directory of uint8 .npy images (train: the reference's
+    transform; other modes: centre-free top-left crop, no augmentation, in order)."""
+    from .device_loader import DeviceHRLoader
+    root = os.path.join(data_root, mode) if os.path.isdir(os.path.join(data_root, mode)) else data_root
+    files = sorted(os.path.join(root, f) for f in os.listdir(root) if f.endswith(".npy"))
+    if not files:
+        raise FileNotFoundError(f"no .npy images under {root}")
+    train = mode == "train"
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        r, w = torch.distributed.get_rank(), torch.distributed.get_world_size()
+        files = files[r::w]
+    return DeviceHRLoader(_NpyImages(files), batch_size, hr_patch_size, horizontal_flip, random_rotate90,
+                          color_jitter_prob, brightness, contrast, saturation, seed=seed, shuffle=train,
+                          drop_last=train, device=device, train=train)
+
+
+__all__ = ["SyntheticHRDataset", "NpyHRDataset", "get_dataloader", "get_device_loader"]

@@ -107,6 +107,7 @@ _SIGS = {
     "fen_ssim_parts": (c_size_t, [c_int] * 4),
     "fen_ssim": (c_int, [c_int] * 5 + [c_void_p] * 3 + [c_int, c_float, c_float, c_void_p, c_void_p, c_float, c_int,
                                                         c_void_p]),
+    "fen_augment_u8": (c_int, [c_int, c_int] + [c_void_p] * 5),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
     "fen_build_info": (ctypes.c_char_p, []),
 }

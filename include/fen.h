@@ -273,6 +273,14 @@ int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred, const flo
              int window_size, float C1, float C2, float* part, void* grad, float grad_scale, int grad_mode,
              void* stream);
 
+/* ---- HR batch preparation (src/data/transforms.py:173-279 + to_tensor 260-279) ----
+ * src_u8: B uint8 HWC crops [B,P,P,3] (RGB, P even); params: B records {int flip, int
+ * jitter, float brightness, contrast, saturation, int rot90_k} drawn by the host; sums: int64
+ * [B] scratch; out: NCHW fp32 [B,3,P,P] = flip -> rot90 -> jitter (brightness, contrast about
+ * the image mean, uint8 quantisation, 8-bit HSV saturation round trip) -> / 255.          */
+int fen_augment_u8(int B, int P, const void* src_u8, const void* params, long long* sums, float* out,
+                   void* stream);
+
 const char* fen_status_string(int code);
 const char* fen_build_info(void);
 

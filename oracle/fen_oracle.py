@@ -16,6 +16,8 @@ Parameters are passed as a flat dict keyed exactly like the reference state_dict
 from __future__ import annotations
 
 import math
+
+import numpy as np
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
@@ -332,3 +334,62 @@ def ms_ssim(pred, target, window_size=11, sigma=1.5, data_range=1.0, weights=Non
     for i, m in enumerate(mcs):
         val = val * (m ** weights[i])
     return val
+
+
+# ---------------------------------------------------------------------------------------
+# train-mode HR transform (reference src/data/transforms.py:173-279, to_tensor 260-279), one
+# sample with given parameters.  Flip / rot90 / brightness / contrast / uint8 quantisation
+# follow the reference's numpy code; the HSV saturation round trip restates OpenCV's 8-bit
+# RGB2HSV_b / HSV2RGB_b (cv2 is absent offline: that step is PARITY UNPINNED).
+def _rgb2hsv8(img):
+    r, g, b = (img[..., k].astype(np.int64) for k in range(3))
+    v = np.maximum(np.maximum(b, g), r)
+    vmin = np.minimum(np.minimum(b, g), r)
+    diff = v - vmin
+    vr = np.where(v == r, -1, 0)
+    vg = np.where(v == g, -1, 0)
+    sdiv = np.where(v > 0, np.rint((255 << 12) / np.maximum(v, 1)), 0).astype(np.int64)
+    hdiv = np.where(diff > 0, np.rint((180 << 12) / (6.0 * np.maximum(diff, 1))), 0).astype(np.int64)
+    s = (diff * sdiv + (1 << 11)) >> 12
+    h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + (~vg & (r - g + 4 * diff))))
+    h = (h * hdiv + (1 << 11)) >> 12
+    h = h + np.where(h < 0, 180, 0)
+    return np.stack([h, s, v], -1)
+
+
+def _hsv2rgb8(hsv):
+    h = hsv[..., 0].astype(np.float32)
+    s = hsv[..., 1].astype(np.float32) * np.float32(1 / 255)
+    v = hsv[..., 2].astype(np.float32) * np.float32(1 / 255)
+    hh = h * np.float32(6 / 180)
+    hh = np.where(hh >= 6, hh - 6, hh)
+    sector = np.floor(hh).astype(np.int64)
+    f = (hh - sector).astype(np.float32)
+    bad = (sector < 0) | (sector >= 6)
+    sector = np.where(bad, 0, sector)
+    f = np.where(bad, np.float32(0), f)
+    tab = np.stack([v, v * (1 - s), v * (1 - s * f), v * (1 - s * (1 - f))], -1).astype(np.float32)
+    sd = np.array([[1, 3, 0], [1, 0, 2], [3, 0, 1], [0, 2, 1], [0, 1, 3], [2, 1, 0]])
+    bgr = np.take_along_axis(tab, sd[sector], -1)
+    bgr = np.where((s == 0)[..., None], v[..., None], bgr)
+    out = np.clip(np.rint(bgr * np.float32(255)), 0, 255).astype(np.uint8)
+    return out[..., ::-1]                       # b, g, r -> r, g, b
+
+
+def transform_hr(img: np.ndarray, flip: int, rot: int, jitter: int, brightness: float, contrast: float,
+                 saturation: float) -> np.ndarray:
+    """uint8 HxWx3 crop -> float32 [3,H,W] in [0,1] (transforms.py:210-257 + to_tensor)."""
+    if flip:
+        img = np.fliplr(img).copy()
+    if rot:
+        img = np.rot90(img, rot).copy()
+    if jitter:
+        f = img.astype(np.float32) / np.float32(255.0)
+        f = f * np.float32(brightness)
+        mean = f.mean()
+        f = (f - mean) * np.float32(contrast) + mean
+        img = np.clip(f * np.float32(255), 0, 255).astype(np.uint8)
+        hsv = _rgb2hsv8(img).astype(np.float32)
+        hsv[..., 1] = hsv[..., 1] * np.float32(saturation)
+        img = _hsv2rgb8(np.clip(hsv, 0, 255).astype(np.uint8))
+    return img.transpose(2, 0, 1).astype(np.float32) / np.float32(255.0)
