@@ -12,11 +12,12 @@ inline int nblk(size_t n, int t = 256) { return (int)((n + t - 1) / t); }
 // ------------------------------ conv_first (3 -> C) ------------------------------
 // reference custom.py:91-94,164; thread per (pixel, 8 output channels)
 // (also the VGG19 input conv, perceptual.py:67-72,84-95: in-bounds samples normalised by
-// (v - mean[ci]) * istd[ci] before the zero padding applies, output optionally ReLU'd)
+// (v - mean[ci]) * istd[ci] before the zero padding applies; and the discriminator's first
+// block, discriminator.py:47-55: act >= 0 applies a leaky ReLU of slope act, ReLU = 0)
 template <typename T>
 __global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
                              const float* __restrict__ w, const float* __restrict__ bias, T* __restrict__ y,
-                             const float* __restrict__ in_mean, const float* __restrict__ in_istd, int relu) {
+                             const float* __restrict__ in_mean, const float* __restrict__ in_istd, float act) {
     extern __shared__ __attribute__((aligned(16))) float sw[];  // [Ci*9][C]
     const int K = Ci * 9;
     for (int i = threadIdx.x; i < K * C; i += blockDim.x) {
@@ -47,9 +48,9 @@ __global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __
             acc[4] += v * w1.x; acc[5] += v * w1.y; acc[6] += v * w1.z; acc[7] += v * w1.w;
         }
     }
-    if (relu) {
+    if (act >= 0.f) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
+        for (int j = 0; j < 8; ++j) acc[j] = acc[j] > 0.f ? acc[j] : act * acc[j];
     }
     char* o = (char*)y + (px * C + g * 8) * sizeof(T);
     if constexpr (sizeof(T) == 2) {
@@ -821,17 +822,17 @@ __global__ void k_scale(size_t n, float* y, float s) {
 #define STREAM ((hipStream_t)stream)
 
 extern "C" int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int C, const float* x, const float* w,
-                                     const float* bias, const float* in_mean, const float* in_istd, int relu, void* y,
+                                     const float* bias, const float* in_mean, const float* in_istd, float act, void* y,
                                      void* stream) {
     if (!x || !w || !bias || !y || B <= 0 || Ci <= 0 || Ci > 3 || C % 8 || C > 128) return FEN_EINVAL;
     const size_t n = (size_t)B * H * W * (C / 8);
     const size_t lds = (size_t)Ci * 9 * C * sizeof(float);
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_conv_first<bf16>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
-                           (bf16*)y, in_mean, in_istd, relu);
+                           (bf16*)y, in_mean, in_istd, act);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_conv_first<float>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
-                           (float*)y, in_mean, in_istd, relu);
+                           (float*)y, in_mean, in_istd, act);
     else
         return FEN_EINVAL;
     FEN_CHECK_LAUNCH();
@@ -840,7 +841,7 @@ extern "C" int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int
 
 extern "C" int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x, const float* w,
                                   const float* bias, void* y, void* stream) {
-    return fen_conv_first_fwd_ex(dtype, B, Ci, H, W, C, x, w, bias, nullptr, nullptr, 0, y, stream);
+    return fen_conv_first_fwd_ex(dtype, B, Ci, H, W, C, x, w, bias, nullptr, nullptr, -1.f, y, stream);
 }
 
 extern "C" size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C) {

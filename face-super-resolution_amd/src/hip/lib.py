@@ -72,7 +72,7 @@ _SIGS = {
     "fen_rcab_workspace_status": (c_int, [c_void_p, c_int, c_int, c_int]),
     "fen_rcab_fused": (c_int, [POINTER(RcabDesc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
-    "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_int, c_void_p, c_void_p]),
+    "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),
     "fen_conv_first_wgrad": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_int, c_void_p, c_void_p]),
     "fen_conv_last_dgrad_part_rows": (c_size_t, [c_int] * 3),
@@ -108,6 +108,13 @@ _SIGS = {
     "fen_ssim": (c_int, [c_int] * 5 + [c_void_p] * 3 + [c_int, c_float, c_float, c_void_p, c_void_p, c_float, c_int,
                                                         c_void_p]),
     "fen_augment_u8": (c_int, [c_int, c_int] + [c_void_p] * 5),
+    "fen_bn_work_floats": (c_size_t, [c_int]),
+    "fen_bn_stats": (c_int, [c_int, c_size_t, c_int, c_void_p, c_float, c_float] + [c_void_p] * 5),
+    "fen_bn_apply": (c_int, [c_int, c_size_t, c_int] + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
+    "fen_bn_bwd": (c_int, [c_int, c_size_t, c_int] + [c_void_p] * 5 + [c_float] + [c_void_p] * 3 +
+                   [c_int, c_void_p, c_void_p]),
+    "fen_subsample2": (c_int, [c_int] * 5 + [c_void_p] * 3),
+    "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
     "fen_build_info": (ctypes.c_char_p, []),
 }

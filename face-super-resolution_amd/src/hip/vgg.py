@@ -146,7 +146,7 @@ class VGGPerceptual:
                 a = ctx.alloc((N, hh, ww, cout))
                 ctx.emit("vgg_conv1_1", ctx.lib.fen_conv_first_fwd_ex, ctx.code, N, 3, hh, ww, cout, ptr(x),
                          ptr(self.p["features.0.weight"]), ptr(self.p["features.0.bias"]), ptr(self.mean),
-                         ptr(self.istd), 1, ptr(a))
+                         ptr(self.istd), 0.0, ptr(a))
                 z = None
             elif is_last:
                 z = ctx.alloc((N, hh, ww, cout))

@@ -1,0 +1,291 @@
+"""VGG-style discriminator and GAN loss (reference src/models/discriminator.py:12-219) on the
+HIP path -- SURVEY.md §8f row 2 (stage-3 GAN step, trainer.py:424-455,468-475).
+
+Same classes, constructor arguments, module tree, state_dict keys and initialisation calls
+as the reference, so its checkpoints and trainer code work unchanged.  The feature stack
+(10 conv blocks) runs as one autograd Function over C-ABI launches, NHWC in the compute
+dtype:
+  block 1    conv 3->64 + bias + LeakyReLU(0.2): the K=27 input kernel (fen_conv_first_fwd_ex)
+  blocks 2-10 conv (stride 1, or stride 2 = the full-resolution conv + fen_subsample2),
+             train-mode BatchNorm statistics (+ running-stat update) and BN + LeakyReLU
+             (fen_bn_stats / fen_bn_apply; eval mode uses the running statistics)
+  backward   fen_bn_bwd (BN + LeakyReLU), fen_zero_insert2 for stride-2 layers, weight
+             gradients on fen_wgrad3x3 / fen_conv_first_wgrad, data gradients on mode-2 convs
+             (block 2's epilogue applies block 1's LeakyReLU mask), and d(input) -- needed by
+             the generator's adversarial step -- through a 64->16 conv (3 valid channels).
+The classifier head (Flatten -> Linear(32768,1024) -> LeakyReLU -> Linear(1024,1)) is two
+plain GEMMs on hipBLASLt through torch.nn.functional.linear.  use_bn=False is not wired on
+the HIP path (the reference's factory always builds use_bn=True).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
+_SLOPE = 0.2
+
+
+class _DFeatures(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, x, mod, *params):
+        from ..hip import lib as L
+        from ..hip.net import conv, wgrad  # noqa: F401
+        from ..hip.program import Ctx, ptr
+        dt = mod.compute_dtype
+        ctx = Ctx(dt, x.device)
+        lib = ctx.lib
+        B, _, H, W = x.shape
+        xin = x.detach().float().contiguous()
+        blocks = mod._hip_blocks()
+        saved = []
+        # block 1: conv 3->64 + bias + LeakyReLU
+        c0 = blocks[0]
+        a = ctx.alloc((B, H, W, c0["cout"]))
+        ctx.emit("d_conv1", lib.fen_conv_first_fwd_ex, ctx.code, B, 3, H, W, c0["cout"], ptr(xin),
+                 ptr(c0["conv"].weight.detach().float().contiguous()), ptr(c0["conv"].bias.detach().float()), 0, 0,
+                 _SLOPE, ptr(a))
+        hh, ww = H, W
+        for blk in blocks[1:]:
+            cin, cout, st = blk["cin"], blk["cout"], blk["stride"]
+            wpk = mod._packed(ctx, blk, 0)
+            z = ctx.alloc((B, hh, ww, cout))
+            conv(ctx, a, wpk, B, hh, ww, cin, cout, y=z)
+            ho, wo = (hh // 2, ww // 2) if st == 2 else (hh, ww)
+            if st == 2:
+                zs = ctx.alloc((B, ho, wo, cout))
+                ctx.emit("d_sub", lib.fen_subsample2, ctx.code, B, hh, ww, cout, ptr(z), ptr(zs))
+                z = zs
+            bn = blk["bn"]
+            npx = B * ho * wo
+            stat = ctx.alloc((2 * cout,), torch.float32)
+            if mod.training:
+                work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
+                ctx.emit("d_bn_stats", lib.fen_bn_stats, ctx.code, npx, cout, ptr(z), float(bn.eps),
+                         float(bn.momentum), ptr(stat), ptr(bn.running_mean), ptr(bn.running_var), ptr(work))
+                with torch.no_grad():
+                    bn.num_batches_tracked += 1
+            else:
+                with torch.no_grad():
+                    stat[:cout] = bn.running_mean
+                    stat[cout:] = (bn.running_var + bn.eps).rsqrt()
+            out = ctx.alloc((B, ho, wo, cout))
+            ctx.emit("d_bn_apply", lib.fen_bn_apply, ctx.code, npx, cout, ptr(z), ptr(stat), ptr(stat[cout:]),
+                     ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(out))
+            saved.append(dict(blk=blk, a_in=a, z=z, stat=stat, H=hh, W=ww, Ho=ho, Wo=wo))
+            a, hh, ww = out, ho, wo
+        fctx.saved_blocks, fctx.a1, fctx.xin, fctx.mod = saved, saved[0]["a_in"], xin, mod
+        fctx.shape = (B, H, W)
+        fctx.x_needs_grad = x.requires_grad
+        return a.float().permute(0, 3, 1, 2).contiguous()        # NCHW for the Flatten
+
+    @staticmethod
+    def backward(fctx, g):
+        from ..hip import lib as L
+        from ..hip.net import conv, wgrad
+        from ..hip.program import Ctx, ptr
+        mod = fctx.mod
+        dt = mod.compute_dtype
+        ctx = Ctx(dt, g.device)
+        lib = ctx.lib
+        B, H, W = fctx.shape
+        d = g.permute(0, 2, 3, 1).contiguous().to(dt)            # NHWC
+        blocks = mod._hip_blocks()
+        grads = {}
+        for k in range(len(fctx.saved_blocks) - 1, -1, -1):
+            sv = fctx.saved_blocks[k]
+            blk, bn = sv["blk"], sv["blk"]["bn"]
+            cin, cout = blk["cin"], blk["cout"]
+            npx = B * sv["Ho"] * sv["Wo"]
+            dz = ctx.alloc((B, sv["Ho"], sv["Wo"], cout))
+            dgam = torch.zeros(cout, device=g.device)
+            dbet = torch.zeros(cout, device=g.device)
+            work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
+            ctx.emit("d_bn_bwd", lib.fen_bn_bwd, ctx.code, npx, cout, ptr(d), ptr(sv["z"]), ptr(sv["stat"]),
+                     ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(dz), ptr(dgam), ptr(dbet), 0,
+                     ptr(work))
+            grads[bn.weight] = dgam
+            grads[bn.bias] = dbet
+            if blk["stride"] == 2:
+                dzf = ctx.alloc((B, sv["H"], sv["W"], cout))
+                ctx.emit("d_zins", lib.fen_zero_insert2, ctx.code, B, sv["Ho"], sv["Wo"], cout, ptr(dz), ptr(dzf))
+                dz = dzf
+            dw = torch.zeros_like(blk["conv"].weight)
+            wgrad(ctx, sv["a_in"], dz, B, sv["H"], sv["W"], cin, cout, dw, None)
+            grads[blk["conv"].weight] = dw
+            da = ctx.alloc((B, sv["H"], sv["W"], cin))
+            if k == 0:
+                # block 1's LeakyReLU mask on the way down: a1 > 0 <=> its pre-activation > 0
+                part = ctx.alloc((B * ((sv["H"] + 15) // 16) * ((sv["W"] + 15) // 16), cin), torch.float32)
+                conv(ctx, dz, mod._packed(ctx, blk, 2), B, sv["H"], sv["W"], cout, cin, epi=L.EPI_PRELU_BWD,
+                     alpha=mod._slopes(cin, g.device), pre_in=fctx.a1, y=da, part=part)
+            else:
+                conv(ctx, dz, mod._packed(ctx, blk, 2), B, sv["H"], sv["W"], cout, cin, y=da)
+            d = da
+        # block 1: conv 3->64 weight / bias gradient, and d(input) when asked for
+        c0 = blocks[0]
+        dw0 = torch.zeros_like(c0["conv"].weight)
+        db0 = torch.zeros_like(c0["conv"].bias)
+        work = ctx.alloc((lib.fen_conv_first_work_floats(B, 3, H, W, c0["cout"]),), torch.float32)
+        ctx.emit("d_conv1_wgrad", lib.fen_conv_first_wgrad, ctx.code, B, 3, H, W, c0["cout"], ptr(fctx.xin), ptr(d),
+                 ptr(dw0), ptr(db0), 0, ptr(work))
+        grads[c0["conv"].weight] = dw0
+        grads[c0["conv"].bias] = db0
+        dx = None
+        if fctx.x_needs_grad:
+            d16 = ctx.alloc((B, H, W, 16))
+            conv(ctx, d, mod._packed(ctx, c0, 2), B, H, W, c0["cout"], 16, y=d16)
+            dx = d16[..., :3].float().permute(0, 3, 1, 2).contiguous()
+        out = [grads.get(p) for p in mod._feature_params()]
+        return (dx, None, *out)
+
+
+class VGGStyleDiscriminator(nn.Module):
+    """VGG-style discriminator for 256x256 images (discriminator.py:12-151)."""
+
+    def __init__(self, in_channels: int = 3, base_channels: int = 64, input_size: int = 256, use_bn: bool = True,
+                 use_sigmoid: bool = False, precision: str = "bf16"):
+        super().__init__()
+        self.use_sigmoid = use_sigmoid
+        self.use_bn = use_bn
+
+        def conv_block(in_ch, out_ch, kernel_size=3, stride=1, use_bn=True):
+            layers = [nn.Conv2d(in_ch, out_ch, kernel_size, stride, padding=kernel_size // 2, bias=not use_bn)]
+            if use_bn:
+                layers.append(nn.BatchNorm2d(out_ch))
+            layers.append(nn.LeakyReLU(0.2, inplace=True))
+            return nn.Sequential(*layers)
+
+        bc = base_channels
+        self.features = nn.Sequential(
+            conv_block(in_channels, bc, use_bn=False),
+            conv_block(bc, bc, stride=2, use_bn=use_bn),
+            conv_block(bc, bc * 2, use_bn=use_bn),
+            conv_block(bc * 2, bc * 2, stride=2, use_bn=use_bn),
+            conv_block(bc * 2, bc * 4, use_bn=use_bn),
+            conv_block(bc * 4, bc * 4, stride=2, use_bn=use_bn),
+            conv_block(bc * 4, bc * 8, use_bn=use_bn),
+            conv_block(bc * 8, bc * 8, stride=2, use_bn=use_bn),
+            conv_block(bc * 8, bc * 8, use_bn=use_bn),
+            conv_block(bc * 8, bc * 8, stride=2, use_bn=use_bn),
+        )
+        feature_size = input_size // 32
+        self.classifier = nn.Sequential(
+            nn.Flatten(),
+            nn.Linear(bc * 8 * feature_size * feature_size, 1024),
+            nn.LeakyReLU(0.2, inplace=True),
+            nn.Linear(1024, 1),
+        )
+        self._initialize_weights()
+        self.compute_dtype = _DTYPES[precision]
+        self._packs = {}
+
+    def _initialize_weights(self):
+        """discriminator.py:104-116."""
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, a=0.2, mode='fan_in', nonlinearity='leaky_relu')
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.Linear):
+                nn.init.kaiming_normal_(m.weight, a=0.2, mode='fan_in', nonlinearity='leaky_relu')
+                nn.init.zeros_(m.bias)
+
+    # ---- HIP plumbing ----
+    def _hip_blocks(self) -> List[dict]:
+        out = []
+        for i, seq in enumerate(self.features):
+            cv = seq[0]
+            bn = seq[1] if isinstance(seq[1], nn.BatchNorm2d) else None
+            out.append(dict(i=i, conv=cv, bn=bn, cin=cv.in_channels, cout=cv.out_channels, stride=cv.stride[0]))
+        return out
+
+    def _feature_params(self):
+        return [p for p in self.features.parameters()]
+
+    def _packed(self, ctx, blk, mode):
+        from ..hip.program import ptr
+        w = blk["conv"].weight
+        key = (blk["i"], mode, ctx.code)
+        ent = self._packs.get(key)
+        if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+            cout, cin = w.shape[0], w.shape[1]
+            n = ctx.lib.fen_packed_elems(mode, cout, cin)
+            buf = torch.empty(n, dtype=ctx.tdtype, device=w.device)
+            src = w.detach().float().contiguous()
+            ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, cout, cin, ptr(src), ptr(buf))
+            ctx.keep(src)
+            ent = (w._version, w.data_ptr(), buf)
+            self._packs[key] = ent
+        return ent[2]
+
+    def _slopes(self, n, dev):
+        key = ("slopes", n, dev)
+        if key not in self._packs:
+            self._packs[key] = torch.full((n,), _SLOPE, device=dev)
+        return self._packs[key]
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """(B, 3, H, W) -> (B, 1) score (discriminator.py:118-136)."""
+        if not x.is_cuda:
+            raise RuntimeError("the HIP discriminator runs on a ROCm GPU tensor (got CPU); there is no CPU path")
+        if not self.use_bn:
+            raise NotImplementedError("use_bn=False is not wired on the HIP path")
+        if x.shape[1] != 3 or x.shape[2] % 32 or x.shape[3] % 32:
+            raise ValueError("input must be (B, 3, H, W) with H, W multiples of 32")
+        feats = _DFeatures.apply(x, self, *self._feature_params())
+        h = feats.flatten(1)
+        lin1, lin2 = self.classifier[1], self.classifier[3]
+        h = F.leaky_relu(F.linear(h, lin1.weight, lin1.bias), 0.2)
+        out = F.linear(h, lin2.weight, lin2.bias)
+        if self.use_sigmoid:
+            out = torch.sigmoid(out)
+        return out
+
+    def get_model_info(self) -> dict:
+        total_params = sum(p.numel() for p in self.parameters())
+        trainable_params = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        return {'name': 'VGGStyleDiscriminator', 'total_params': total_params, 'trainable_params': trainable_params,
+                'size_mb': total_params * 4 / (1024 ** 2)}
+
+
+class GANLoss(nn.Module):
+    """'vanilla' (BCE with logits), 'lsgan' (MSE), 'wgan' (raw scores) -- discriminator.py:154-206."""
+
+    def __init__(self, gan_type: str = 'vanilla', real_label: float = 1.0, fake_label: float = 0.0):
+        super().__init__()
+        self.gan_type = gan_type
+        self.real_label = real_label
+        self.fake_label = fake_label
+        if gan_type == 'vanilla':
+            self.loss = nn.BCEWithLogitsLoss()
+        elif gan_type == 'lsgan':
+            self.loss = nn.MSELoss()
+        elif gan_type == 'wgan':
+            self.loss = None
+        else:
+            raise ValueError(f"Unknown GAN type: {gan_type}")
+
+    def get_target_tensor(self, prediction: torch.Tensor, is_real: bool) -> torch.Tensor:
+        return torch.full_like(prediction, self.real_label if is_real else self.fake_label)
+
+    def forward(self, prediction: torch.Tensor, is_real: bool) -> torch.Tensor:
+        if self.gan_type == 'wgan':
+            return -prediction.mean() if is_real else prediction.mean()
+        return self.loss(prediction, self.get_target_tensor(prediction, is_real))
+
+
+def create_discriminator(input_size: int = 256, base_channels: int = 64, use_bn: bool = True,
+                         **kwargs) -> VGGStyleDiscriminator:
+    """discriminator.py:209-219."""
+    return VGGStyleDiscriminator(in_channels=3, base_channels=base_channels, input_size=input_size, use_bn=use_bn,
+                                 use_sigmoid=False, **{k: v for k, v in kwargs.items() if k == "precision"})
+
+
+__all__ = ["VGGStyleDiscriminator", "GANLoss", "create_discriminator"]

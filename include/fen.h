@@ -99,11 +99,12 @@ int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream);
 int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x,
                        const float* w, const float* bias, void* y, void* stream);
 /* ... with the VGG19 input stage (perceptual.py:67-72,84-95): in-bounds samples become
- * (x - in_mean[ci]) * in_istd[ci] before the zero padding, relu != 0 applies ReLU to y;
- * in_mean / in_istd may be NULL (identity).                                               */
+ * (x - in_mean[ci]) * in_istd[ci] before the zero padding (in_mean / in_istd may be NULL:
+ * identity); act >= 0 applies a leaky ReLU of slope act to y (0: ReLU; 0.2: the
+ * discriminator's first block, discriminator.py:47-55), act < 0 none.                     */
 int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int C, const float* x,
                           const float* w, const float* bias, const float* in_mean, const float* in_istd,
-                          int relu, void* y, void* stream);
+                          float act, void* y, void* stream);
 /* conv_first weight gradient (no data gradient: x needs none) -> dw OIHW, db              */
 size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C);
 int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const float* x,
@@ -280,6 +281,25 @@ int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred, const flo
  * the image mean, uint8 quantisation, 8-bit HSV saturation round trip) -> / 255.          */
 int fen_augment_u8(int B, int P, const void* src_u8, const void* params, long long* sums, float* out,
                    void* stream);
+
+/* ---- VGG-style discriminator (src/models/discriminator.py:12-219) ----
+ * train-mode BatchNorm2d + LeakyReLU over NHWC [npx][C] (C % 8 == 0):
+ * fen_bn_stats: stat[2C] = (mean, rstd) of y, running stats (momentum, unbiased var) updated
+ * when rmean/rvar != NULL; work = fen_bn_work_floats(C) floats.
+ * fen_bn_apply: out = lrelu((y - mean) * rstd * gamma + beta, slope) (eval: running stats).
+ * fen_bn_bwd: dy from da for out = lrelu(BN_train(y)); dgamma / dbeta set or accumulated.
+ * A stride-2 conv = fen_conv3x3 at full resolution + fen_subsample2; its gradients = the
+ * stride-1 ones of fen_zero_insert2(dy).                                                  */
+size_t fen_bn_work_floats(int C);
+int fen_bn_stats(int dtype, size_t npx, int C, const void* y, float eps, float momentum, float* stat, float* rmean,
+                 float* rvar, float* work, void* stream);
+int fen_bn_apply(int dtype, size_t npx, int C, const void* y, const float* mean, const float* rstd,
+                 const float* gamma, const float* beta, float slope, void* out, void* stream);
+int fen_bn_bwd(int dtype, size_t npx, int C, const void* da, const void* y, const float* stat, const float* gamma,
+               const float* beta, float slope, void* dy, float* dgamma, float* dbeta, int accumulate, float* work,
+               void* stream);
+int fen_subsample2(int dtype, int B, int H, int W, int C, const void* x, void* y, void* stream);
+int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const void* dy, void* out, void* stream);
 
 const char* fen_status_string(int code);
 const char* fen_build_info(void);
