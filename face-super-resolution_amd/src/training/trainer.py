@@ -114,8 +114,6 @@ class Trainer:
                  config: Optional[TrainerConfig] = None, discriminator: Optional[nn.Module] = None,
                  gan_loss: Optional[nn.Module] = None):
         self.config = config or TrainerConfig()
-        if discriminator is not None and self.config.gan_weight > 0:
-            raise NotImplementedError("GAN (stage 3) training is SURVEY.md §8f 'next' #2; not built yet")
         self.rank, self.world = dist_info()
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if not torch.cuda.is_available():
@@ -142,6 +140,15 @@ class Trainer:
         self.scheduler = self._create_scheduler()
         self._engines: Dict[tuple, FENEngine] = {}
         self._generic_opt: Optional[FusedAdamW] = None
+        # stage-3 GAN (trainer.py:230-250): the reference's discriminator optimizer object
+        self.use_gan = self.config.gan_weight > 0 and discriminator is not None
+        self.discriminator = self.optimizer_d = self.gan_loss = None
+        if self.use_gan:
+            from ..models.discriminator import GANLoss
+            self.discriminator = discriminator.to(self.device)
+            self.gan_loss = gan_loss.to(self.device) if gan_loss is not None else GANLoss(self.config.gan_type)
+            self.optimizer_d = torch.optim.AdamW(self.discriminator.parameters(), lr=self.config.d_learning_rate,
+                                                 weight_decay=self.config.d_weight_decay)
         self.early_stopping = EarlyStopping(self.config.early_stopping_patience, self.config.early_stopping_mode)
         self.checkpoint_dir = Path(self.config.checkpoint_dir)
         if self.rank == 0:
@@ -197,10 +204,49 @@ class Trainer:
         """Any other content loss: module autograd path + RCCL grad all-reduce + fused AdamW."""
         lr = bicubic_down4(hr)
         sr = self.model(lr)
-        loss, _ = self.loss_fn(sr, hr)
+        loss = self._content(sr, hr)
         for p in self.model.parameters():
             p.grad = None
         (loss / self.world).backward()
+        self._apply_generic_update()
+        return loss.detach()
+
+    def _content(self, sr: torch.Tensor, hr: torch.Tensor) -> torch.Tensor:
+        """The content loss: CombinedLoss returns (loss, components) (combined.py:158-203), a
+        plain criterion a tensor; L1 without a loss function."""
+        if self.loss_fn is None:
+            return F.l1_loss(sr, hr)
+        out = self.loss_fn(sr, hr)
+        return out[0] if isinstance(out, tuple) else out
+
+    def _gan_step(self, hr: torch.Tensor) -> torch.Tensor:
+        """One stage-3 iteration (trainer.py:424-485): d_updates_per_g discriminator updates on
+        real vs detached fake, then the generator on content + gan_weight x adversarial loss.
+        Both networks run on the HIP path through their module autograd."""
+        D, gl = self.discriminator, self.gan_loss
+        lr = bicubic_down4(hr)
+        D.train()
+        for _ in range(self.config.d_updates_per_g):
+            self.optimizer_d.zero_grad()
+            with torch.no_grad():
+                sr_d = self.model(lr)
+            d_loss = (gl(D(hr), True) + gl(D(sr_d.detach()), False)) / 2
+            (d_loss / self.world).backward()
+            if self.world > 1:
+                for p in D.parameters():
+                    if p.grad is not None:
+                        dist.all_reduce(p.grad)
+            self.optimizer_d.step()
+        sr = self.model(lr)
+        content = self._content(sr, hr)
+        loss = content + self.config.gan_weight * gl(D(sr), True)
+        for p in self.model.parameters():
+            p.grad = None
+        (loss / self.world).backward()
+        self._apply_generic_update()
+        return loss.detach()
+
+    def _apply_generic_update(self):
         if self._generic_opt is None:
             flat = self.model._fen_flat
             self._flat_g = torch.zeros_like(flat)
@@ -215,7 +261,6 @@ class Trainer:
             dist.all_reduce(self._flat_g)
         self._generic_opt.set_lr(self.lr)
         self._generic_opt.step()
-        return loss.detach()
 
     # ------------------------------------------------------------------ loops
     def _train_epoch(self) -> Dict[str, float]:
@@ -223,7 +268,9 @@ class Trainer:
         total, n = 0.0, 0
         for batch in self.train_loader:
             hr = self._shard(batch["hr"]).to(self.device, non_blocking=True)
-            if self.fused_l1 is not None:
+            if self.use_gan and self.current_epoch >= self.config.gan_start_epoch:
+                loss = self._gan_step(hr)
+            elif self.fused_l1 is not None:
                 B, _, H, W = hr.shape
                 eng = self.engine(B, H, W)
                 eng.set_lr(self.lr)
@@ -246,7 +293,7 @@ class Trainer:
         for batch in self.val_loader:
             hr = batch["hr"].to(self.device)
             sr = self.model(bicubic_down4(hr))
-            loss = F.l1_loss(sr, hr) if self.loss_fn is None else self.loss_fn(sr, hr)[0]
+            loss = self._content(sr, hr)
             tl += float(loss)
             tp += self._compute_psnr(sr, hr)
             ts += self._compute_ssim(sr, hr)
