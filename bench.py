@@ -118,6 +118,41 @@ def cpu_baseline(model, seconds=10.0):
             "sample": f"oracle fp32 eval forward, full 6x10 net, batch 2 of 64x64, {n} passes in {el:.1f}s"}
 
 
+def time_gan_step(steps, B=16):
+    """Stage 3 (stage3_gan_config.yaml:40-60, BASELINE C4, B=16/GPU): one Trainer iteration =
+    discriminator update (G forward, D on real + fake, D backward, AdamW) + generator update
+    (G forward, content L1 x 0.01 + perceptual x 1 + adversarial x 0.005 through D, backward,
+    clip, AdamW) on the module autograd path (not graph-captured)."""
+    import warnings
+    from src.losses import create_loss_function
+    from src.models import GANLoss, VGGStyleDiscriminator
+    from src.training import Trainer, TrainerConfig
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        loss_fn = create_loss_function(l1_weight=0.01, perceptual_weight=1.0, ssim_weight=0.0,
+                                       perceptual_layers=["conv3_4"])
+    torch.manual_seed(7)
+    D = VGGStyleDiscriminator(input_size=256, precision="bf16")
+    cfg = TrainerConfig(learning_rate=1e-4, weight_decay=0.0, gradient_clip=0.5, gan_weight=0.005,
+                        d_learning_rate=1e-4, use_wandb=False, scheduler_type="none",
+                        checkpoint_dir="/tmp/fen_bench_ckpt")
+    tr = Trainer(build_model("bf16"), [], None, loss_fn=loss_fn, config=cfg, discriminator=D,
+                 gan_loss=GANLoss("vanilla"))
+    hr = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(99)).cuda()
+    for _ in range(2):
+        tr._gan_step(hr)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = tr._gan_step(hr)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"metric": "training images/sec (stage-3 GAN iteration: D update + G update, L1 0.01 + perceptual 1 + "
+                      "adversarial 0.005) at batch 16/GPU", "value": round(B * steps / el, 2),
+            "ms_per_step": round(1000.0 * el / steps, 3), "steps": steps, "loss": float(loss),
+            "path": "module autograd (eager launches), VGG19 and D random-init"}
+
+
 def time_ssim(eng, reps=50):
     """The stage-2 SSIM launch of a training engine (fwd map + tile sums + gradient added to
     dL/dsr), timed with HIP events on the current stream, against the HBM roofline:
@@ -274,6 +309,9 @@ def main():
             if world == 1:
                 out["aux"] = {"ssim_loss_grad": time_ssim(seng)}
             del seng
+            torch.cuda.empty_cache()
+            if world == 1:
+                out["train_gan"] = time_gan_step(args.train_steps)
     if cpu_model_sd is not None:
         out["cpu_baseline"] = cpu_baseline(cpu_model_sd, args.cpu_seconds)
     if rank == 0:
