@@ -90,11 +90,11 @@ __device__ __forceinline__ void st_flag(int* p, int v) {
 // to 6 pixel fragments.  Slots 0..3 are output rows row0..row0+3 (columns 0..15); slot 4 is
 // row row0+4 (groups 0, 1) or an edge fragment (groups 2, 3: wave-uniform branch); slot 5
 // is a second edge fragment (group 3 only).  Fragments double-buffered one step ahead.
-//   main B: xh + mb[kw][kk] + (f + kh) * XW*128        (mb includes row0)
+//   main B: xh + hcol(c16 + kw, chunk) + (row0 + f + kh) * XW*128
 //   edge B: eh + eb[kh][kk] + kw * 128
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void conv1_phase(f32x4 (&acc)[2][6], const char* xh, const char* eh,
-                                            const char* const (&tapp)[3], int kh, const int (&mb)[3][2],
+                                            const char* const (&tapp)[3], int kh, int c16, int rowoff,
                                             const int (&e4)[2], const int (&e5)[2], bool main4, bool has5,
                                             int arow, int q) {
     // phase = kernel row kh: taps (kh, kw = 0..2); xh_k / e*_k fold the row offset in once
@@ -103,11 +103,12 @@ __device__ __forceinline__ void conv1_phase(f32x4 (&acc)[2][6], const char* xh, 
     auto load = [&](int st, uint4 (&A)[2], uint4 (&Bf)[6]) {
         const int kw = st >> 1, kk = st & 1;
         const char* wt = tapp[kw];
+        const int mb = hcol(c16 + kw, kk * 4 + q) + rowoff;   // recomputed: keeps 6 VGPRs free
 #pragma unroll
         for (int m = 0; m < 2; ++m) A[m] = *(const uint4*)(wt + swz(arow + m * 16, kk * 4 + q));
 #pragma unroll
-        for (int f = 0; f < 4; ++f) Bf[f] = *(const uint4*)(xk + mb[kw][kk] + f * (XW * 128));
-        if (main4) Bf[4] = *(const uint4*)(xk + mb[kw][kk] + 4 * (XW * 128));
+        for (int f = 0; f < 4; ++f) Bf[f] = *(const uint4*)(xk + mb + f * (XW * 128));
+        if (main4) Bf[4] = *(const uint4*)(xk + mb + 4 * (XW * 128));
         else Bf[4] = *(const uint4*)(eh + e4[kk] + kw * 128);
         if (has5) Bf[5] = *(const uint4*)(eh + e5[kk] + kw * 128);
     };
@@ -170,6 +171,14 @@ __device__ __forceinline__ void conv2_phase(f32x4 (&acc)[2][4], const char* a1, 
 // ------------------------------------------------------------------------------------
 // edge fragment eidx: rows 8*eidx + lane/2 (clamped to 17 for the pad lanes of eidx 2),
 // column 16 + lane%2; base per (kh, k-half)
+// the same for one kernel row kh (computed at each phase start instead of kept live)
+__device__ __forceinline__ void edge_base_row(int eidx, int c16, int q, int kh, int (&eb)[2]) {
+    int r = 8 * eidx + (c16 >> 1);
+    if (r > 17) r = 17;
+    const int b = c16 & 1;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) eb[kk] = ((r + kh) * 4 + b) * 128 + ekey(r + kh, kk * 4 + q);
+}
 __device__ __forceinline__ void edge_bases(int eidx, int c16, int q, int (&eb)[3][2]) {
     int r = 8 * eidx + (c16 >> 1);
     if (r > 17) r = 17;
@@ -294,13 +303,8 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     // conv1 per-lane addressing (group g: rows row0.., slot 4 main for g < 2, edges for g >= 2)
     const int row0 = g == 0 ? 0 : g == 1 ? 5 : g == 2 ? 10 : 14;
     const bool main4 = g < 2, has5 = g == 3;
-    int mbase[3][2], eb4[3][2], eb5[3][2];
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) mbase[kw][kk] = hcol(c16 + kw, kk * 4 + q) + row0 * (XW * 128);
-    edge_bases(g == 2 ? 2 : 0, c16, q, eb4);
-    edge_bases(1, c16, q, eb5);
+    const int rowoff = row0 * (XW * 128);
+    const int eidx4 = g == 2 ? 2 : 0;
     const int arow1 = ch * 32 + c16;                  // A row (co) of conv1's wave
     const int arow2 = wc * 32 + c16;
     // conv1 epilogue addressing, fixed per lane: a1-image byte offsets of slot 0 (main rows:
@@ -499,12 +503,11 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             issue_taps(P + 1);
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
                                    ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
-            const int e4[2] = {p == 0 ? eb4[0][0] : p == 1 ? eb4[1][0] : eb4[2][0],
-                               p == 0 ? eb4[0][1] : p == 1 ? eb4[1][1] : eb4[2][1]};
-            const int e5[2] = {p == 0 ? eb5[0][0] : p == 1 ? eb5[1][0] : eb5[2][0],
-                               p == 0 ? eb5[0][1] : p == 1 ? eb5[1][1] : eb5[2][1]};
+            int e4[2], e5[2];
+            edge_base_row(eidx4, c16, q, p, e4);
+            edge_base_row(1, c16, q, p, e5);
             if (k == 1 && p == 1) RSTAMP(45);
-            conv1_phase(acc1, xh, eh, tapp, p, mbase, e4, e5, main4, has5, arow1, q);
+            conv1_phase(acc1, xh, eh, tapp, p, c16, rowoff, e4, e5, main4, has5, arow1, q);
             if (k == 1 && p == 1) RSTAMP(46);
         }
         if (k == 0) RSTAMP(15);
