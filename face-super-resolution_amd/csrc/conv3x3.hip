@@ -1066,6 +1066,7 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     if (epi & FEN_EPI_LAST) {
         if (d->Cout > 4 || !d->lr || d->scale <= 0 || d->H % d->scale || d->W % d->scale) return FEN_EINVAL;
         if (epi & ~(FEN_EPI_LAST | FEN_EPI_BIAS)) return FEN_EUNSUPPORTED;
+        if (fen_detail::conv_last_fast_ok(d) && conv_variant() != 1) return fen_detail::launch_conv_last(d, s);
         return d->dtype == FEN_BF16 ? launch_s<bf16, 16>(d, s) : launch_s<float, 16>(d, s);
     }
     if (!d->y) return FEN_EINVAL;

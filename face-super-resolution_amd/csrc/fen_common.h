@@ -218,6 +218,20 @@ __device__ __forceinline__ void dma16(const i32x4& rsrc, unsigned lds_base, int 
         : "s"(lds_base), "v"(voff), "s"(rsrc)
         : "memory");
 }
+// 4 B per lane (buffer_load_dword ... lds) written to lds_base + lane*4: gathers with
+// per-element addresses (border-clamped patches)
+__device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned lds_base, int voff) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dword %2, %3, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(lds_base), "v"(voff), "s"(rsrc)
+        : "memory");
+}
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
     return (unsigned)(size_t)(const lds_void*)p;
 }
@@ -226,3 +240,9 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
     do {                                                      \
         if (hipGetLastError() != hipSuccess) return FEN_EHIP; \
     } while (0)
+
+// conv_last fast path (conv_last.hip): bf16, Cin 64, Cout <= 4, x4 skip, H and W multiples of 16
+namespace fen_detail {
+bool conv_last_fast_ok(const fen_conv_desc* d);
+int launch_conv_last(const fen_conv_desc* d, hipStream_t s);
+}  // namespace fen_detail

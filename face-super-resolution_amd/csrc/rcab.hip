@@ -494,8 +494,14 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             const int P = k * 6 + p;
             if (p > 0 || k > 0) {
                 if (k < 2) RSTAMP(2 + k * 14 + p * 2);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this phase's taps (+ halo) landed
-                arrive();                                          // ... and the last tile's partial
+                if (p == 0 && wave == 0) {
+                    // the last tile's partial store (this wave's newest op) keeps draining to
+                    // memory through phase 0; its arrival is raised at the next boundary
+                    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this phase's taps (+ halo) landed
+                    arrive();                                          // ... and the last tile's partial
+                }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 if (k < 2) RSTAMP(3 + k * 14 + p * 2);
@@ -588,6 +594,19 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         __builtin_amdgcn_sched_barrier(0);
         if (k == 1) RSTAMP(38);
         issue_taps(k * 6 + 4);
+#elif defined(RCAB_APPLY_FIRST)
+        if (k == 1) RSTAMP(38);
+        if (pend_t >= 0) {                          // residual loads not queued behind the taps
+            if constexpr (PARK) {
+                load_x(pend_t);
+                apply(pend_t);
+            } else {
+                load_x_frag(pend_t);
+                apply_frag(pend_t);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        issue_taps(k * 6 + 4);
 #else
         issue_taps(k * 6 + 4);
         if (k == 1) RSTAMP(38);
@@ -669,8 +688,8 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         __builtin_amdgcn_s_barrier();
         if (k < 2) RSTAMP(13 + k * 14);
         if (wave == 0) {
-            // tile partial -> uncached workspace; the arrival is counted after the next
-            // phase boundary's vmcnt(0) has drained this store (no stall here)
+            // tile partial -> uncached workspace; the arrival is raised at the next tile's
+            // phase-1 boundary, once a vmcnt(0) has drained this store (no stall here)
             __hip_atomic_store(part + ((size_t)tile * B + b) * 64 + lane,
                                (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);

@@ -224,6 +224,44 @@ def test_conv_last_bicubic_l1(dtype, clamp):
     assert torch.allclose(g[..., :3], sgn.to(g.dtype).float(), rtol=1e-2, atol=0)
 
 
+def test_conv_last_persistent_ring():
+    """The persistent conv_last kernel (csrc/conv_last.hip) over many tiles per CU, with an
+    uneven tile count per block (816 tiles): halo ring, deferred loss writes, border tiles.
+    Reference on the same bf16-rounded feature map and weights, fp32 on the CPU."""
+    from src.hip import lib as L, net
+    torch.manual_seed(41)
+    B, C, H, W = 3, 64, 256, 272
+    feat = torch.randn(B, C, H, W).bfloat16().float()
+    lr = torch.rand(B, 3, H // 4, W // 4)
+    hr = torch.rand(B, 3, H, W)
+    wl = (torch.randn(3, C, 3, 3) * 0.02).bfloat16().float()
+    bl = torch.randn(3) * 0.01
+    out_ref = (F.conv2d(feat.double(), wl.double(), bl.double(), padding=1) + O.bicubic(lr.double(), 4)).float()
+    n = out_ref.numel()
+    ctx = _ctx(torch.bfloat16)
+    wp = _pack(ctx, wl, 0)
+    out = ctx.alloc((B, 3, H, W), torch.float32)
+    dout = ctx.alloc((B, H, W, 16))
+    lp = ctx.alloc((B * net.tiles(H, W), 1), torch.float32)
+    lp.fill_(float("nan"))
+    net.conv(ctx, nhwc(feat, torch.bfloat16), wp, B, H, W, C, 3, bias=bl.to(DEV), epi=L.EPI_LAST, y=out,
+             lr=lr.to(DEV), scale=4, clamp=0, hr=hr.to(DEV), dout=dout, l1_scale=1.0 / n, loss_part=lp)
+    torch.cuda.synchronize()
+    o = out.cpu()
+    assert (o - out_ref).abs().max() <= 1e-4
+    # every tile's partial written, each equal to its tile's |sr - hr| sum
+    d = (o - hr).abs().double()
+    tile_ref = d.view(B, 3, H // 16, 16, W // 16, 16).sum(dim=(1, 3, 5)).reshape(-1)
+    got = lp.cpu().double().view(-1)
+    assert torch.isfinite(got).all()
+    assert torch.allclose(got, tile_ref, rtol=1e-5, atol=1e-4)
+    g = dout.float().cpu()
+    assert torch.all(g[..., 3:] == 0)
+    diff = (o - hr).permute(0, 2, 3, 1)
+    far = diff.abs() > 1e-5
+    assert torch.equal(torch.sign(g[..., :3])[far], torch.sign(diff)[far])
+
+
 def test_bicubic_down4_and_layouts():
     torch.manual_seed(5)
     from src.hip.program import ptr

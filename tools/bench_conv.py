@@ -59,6 +59,11 @@ wl = torch.randn(3, 64, 3, 3, device='cuda') * 0.01; bl = torch.zeros(3, device=
 wpl = pack(wl, 0); out = torch.empty(B, 3, 256, 256, device='cuda'); lr = torch.rand(B, 3, 64, 64, device='cuda')
 us = timeit(lambda: net.conv(ctx, y1, wpl, B, 256, 256, 64, 3, bias=bl, epi=L.EPI_LAST, y=out, lr=lr, scale=4), 10)
 res["last_us"] = round(us, 2); res["last_GBs"] = round(y1.numel() * 2 / us / 1e3, 1)
+hrt = torch.rand(B, 3, 256, 256, device='cuda'); dol = torch.empty(B, 256, 256, 16, device='cuda', dtype=dt)
+lpl = torch.empty(B * 256, 1, device='cuda')
+us = timeit(lambda: net.conv(ctx, y1, wpl, B, 256, 256, 64, 3, bias=bl, epi=L.EPI_LAST, y=out, lr=lr, scale=4,
+                             hr=hrt, dout=dol, l1_scale=1e-6, loss_part=lpl), 10)
+res["last_train_us"] = round(us, 2)
 # dgrad rcab with prelu_bwd
 wd = pack(w, 2); dz = torch.empty_like(x)
 us = timeit(lambda: net.conv(ctx, x, wd, B, 64, 64, 64, 64, epi=L.EPI_PRELU_BWD, alpha=al, pre_in=x, y=dz, part=part))

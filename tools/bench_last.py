@@ -1,0 +1,34 @@
+"""conv_last (csrc/conv_last.hip) timing at B=32 256x256, inference and training epilogues."""
+import json, os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'face-super-resolution_amd'))
+import torch
+from src.hip import lib as L, net
+from src.hip.program import Ctx, ptr
+
+B = 32
+ctx = Ctx(torch.bfloat16, 'cuda')
+x = torch.randn(B, 256, 256, 64, device='cuda', dtype=torch.bfloat16)
+wl = torch.randn(3, 64, 3, 3, device='cuda') * 0.01; bl = torch.zeros(3, device='cuda')
+wp = torch.empty(ctx.lib.fen_packed_elems(0, 3, 64), device='cuda', dtype=torch.bfloat16)
+ctx.emit('p', ctx.lib.fen_pack_conv_w, ctx.code, 0, 3, 64, ptr(wl), ptr(wp))
+out = torch.empty(B, 3, 256, 256, device='cuda'); lr = torch.rand(B, 3, 64, 64, device='cuda')
+hr = torch.rand(B, 3, 256, 256, device='cuda'); do = torch.empty(B, 256, 256, 16, device='cuda', dtype=torch.bfloat16)
+lp = torch.empty(B * 256, 1, device='cuda')
+
+
+def timeit(f, n=20):
+    for _ in range(3): f()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(); e0.record()
+    for _ in range(n): f()
+    e1.record(); torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000 / n
+
+
+res = {"lib": os.path.basename(os.environ.get("FEN_HIP_LIB", "default"))}
+us = timeit(lambda: net.conv(ctx, x, wp, B, 256, 256, 64, 3, bias=bl, epi=L.EPI_LAST, y=out, lr=lr, scale=4, clamp=1))
+res["last_us"] = round(us, 2); res["GBs"] = round(x.numel() * 2 / us / 1e3, 1)
+us = timeit(lambda: net.conv(ctx, x, wp, B, 256, 256, 64, 3, bias=bl, epi=L.EPI_LAST, y=out, lr=lr, scale=4,
+                             hr=hr, dout=do, l1_scale=1e-6, loss_part=lp))
+res["last_train_us"] = round(us, 2)
+print(json.dumps(res))
