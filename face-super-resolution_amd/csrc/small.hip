@@ -61,6 +61,87 @@ __global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __
     }
 }
 
+// The same conv, W % 4 == 0: a block computes a 2-row x 64-column output tile.  Its input
+// halo (Ci x 4 x 66, zero-padded, normalised as above) is staged once in LDS with coalesced
+// loads, and the filter with coalesced loads transposed into [k][co]; thread = (8 output
+// channels, 4 consecutive pixels of a row) reads its 3 x 6 window per channel from LDS.  The
+// one-pixel form above issued 27 global loads per thread, 8 lanes per pixel loading the same
+// addresses: address-unit bound (~25 us at B = 32, 64x64).  Same per-output operation order
+// (bias, then ci, then tap): bit-identical results.
+constexpr int CF4_TW = 64;                      // tile width (output pixels)
+template <typename T>
+__global__ __launch_bounds__(256) void k_conv_first4(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     T* __restrict__ y, const float* __restrict__ in_mean,
+                                                     const float* __restrict__ in_istd, float act) {
+    extern __shared__ __attribute__((aligned(16))) float sw[];  // [Ci*9][C], then xs [Ci][4][CF4_TW + 2]
+    constexpr int XR = CF4_TW + 2;
+    const int K = Ci * 9;
+    float* xs = sw + K * C;
+    const int twn = (W + CF4_TW - 1) / CF4_TW, thn = (H + 1) >> 1;
+    const int tile = blockIdx.x, b = tile / (thn * twn), r0 = ((tile / twn) % thn) * 2, c0 = (tile % twn) * CF4_TW;
+    for (int i = threadIdx.x; i < K * C; i += blockDim.x) {     // w [co][k] read in order
+        const int co = i / K, k = i - co * K;
+        sw[k * C + co] = w[i];
+    }
+    for (int i = threadIdx.x; i < Ci * 4 * XR; i += blockDim.x) {
+        const int ci = i / (4 * XR), rr = (i / XR) & 3, cc = i % XR;
+        const int hh = r0 - 1 + rr, ww = c0 - 1 + cc;
+        const float mu = in_mean ? in_mean[ci] : 0.f, is = in_istd ? in_istd[ci] : 1.f;
+        xs[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                    ? (x[(((size_t)b * Ci + ci) * H + hh) * W + ww] - mu) * is
+                    : 0.f;
+    }
+    __syncthreads();
+    const int G = C / 8;                          // channel groups; 256 / G threads cover the runs
+    for (int tsk = threadIdx.x; tsk < G * 2 * (CF4_TW / 4); tsk += blockDim.x) {
+        const int g = tsk % G, run = tsk / G;
+        const int row = run / (CF4_TW / 4), cr = (run % (CF4_TW / 4)) * 4;
+        const int hq = r0 + row, w0 = c0 + cr;
+        if (hq >= H || w0 >= W) continue;
+        float acc[4][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float bj = bias[g * 8 + j];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[p][j] = bj;
+        }
+        for (int ci = 0; ci < Ci; ++ci) {
+            float v[3][6];
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) v[r][c] = xs[(ci * 4 + row + r) * XR + cr + c];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float4* wp = (const float4*)(sw + (ci * 9 + t) * C + g * 8);
+                const float4 wa = wp[0], wb = wp[1];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const float vv = v[t / 3][p + t % 3];
+                    acc[p][0] += vv * wa.x; acc[p][1] += vv * wa.y; acc[p][2] += vv * wa.z; acc[p][3] += vv * wa.w;
+                    acc[p][4] += vv * wb.x; acc[p][5] += vv * wb.y; acc[p][6] += vv * wb.z; acc[p][7] += vv * wb.w;
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            if (act >= 0.f) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[p][j] = acc[p][j] > 0.f ? acc[p][j] : act * acc[p][j];
+            }
+            const size_t px = ((size_t)b * H + hq) * W + w0 + p;
+            char* o = (char*)y + (px * C + g * 8) * sizeof(T);
+            if constexpr (sizeof(T) == 2) {
+                *(uint4*)o = pack16<bf16>(acc[p]);
+            } else {
+                *(uint4*)o = pack16<float>(acc[p]);
+                *(uint4*)(o + 16) = pack16<float>(acc[p] + 4);
+            }
+        }
+    }
+}
+
 // conv_first weight gradient dw[co][ci][kh][kw] = sum_px dy[px][co] * x[ci][px + (kh-1, kw-1)]
 // (+ db = sum_px dy).  Persistent blocks walk 16x16-pixel tiles in a fixed order (deterministic
 // per-block partials): the tile's zero-padded 3 x 18 x 18 input halo is staged in LDS; wave w
@@ -827,6 +908,20 @@ extern "C" int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int
     if (!x || !w || !bias || !y || B <= 0 || Ci <= 0 || Ci > 3 || C % 8 || C > 128) return FEN_EINVAL;
     const size_t n = (size_t)B * H * W * (C / 8);
     const size_t lds = (size_t)Ci * 9 * C * sizeof(float);
+    if (W % 4 == 0) {
+        const unsigned nb = (unsigned)((size_t)B * ((H + 1) / 2) * ((W + CF4_TW - 1) / CF4_TW));
+        const size_t lds4 = lds + (size_t)Ci * 4 * (CF4_TW + 2) * sizeof(float);
+        if (dtype == FEN_BF16)
+            hipLaunchKernelGGL(k_conv_first4<bf16>, dim3(nb), dim3(256), lds4, STREAM, B, Ci, H, W, C, x, w, bias,
+                               (bf16*)y, in_mean, in_istd, act);
+        else if (dtype == FEN_F32)
+            hipLaunchKernelGGL(k_conv_first4<float>, dim3(nb), dim3(256), lds4, STREAM, B, Ci, H, W, C, x, w, bias,
+                               (float*)y, in_mean, in_istd, act);
+        else
+            return FEN_EINVAL;
+        FEN_CHECK_LAUNCH();
+        return FEN_OK;
+    }
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_conv_first<bf16>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
                            (bf16*)y, in_mean, in_istd, act);

@@ -148,9 +148,11 @@ def test_upsample_conv_shuffle_prelu(dtype):
 
 
 @pytest.mark.parametrize("dtype", DT)
-def test_conv_first(dtype):
+@pytest.mark.parametrize("B,H,W", [(2, 20, 24), (3, 17, 19), (40, 64, 64)])
+def test_conv_first(dtype, B, H, W):
+    """4-pixel runs (W % 4 == 0, grid-stride over several runs at B = 40) and the one-pixel form."""
     torch.manual_seed(3)
-    B, H, W, C = 2, 20, 24, 64
+    C = 64
     x = torch.rand(B, 3, H, W)
     w = torch.randn(C, 3, 3, 3) * 0.2
     b = torch.randn(C) * 0.1

@@ -17,11 +17,15 @@ lp = torch.empty(B * 256, 1, device='cuda')
 
 
 def timeit(f, n=20):
-    for _ in range(3): f()
+    """Device time per launch: n launches captured in one hipGraph, replayed (no host gaps)."""
+    for _ in range(2): f()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n): f()
+    g.replay(); torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(); e0.record()
-    for _ in range(n): f()
-    e1.record(); torch.cuda.synchronize()
+    e0.record(); g.replay(); e1.record(); torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1000 / n
 
 
@@ -32,3 +36,8 @@ us = timeit(lambda: net.conv(ctx, x, wp, B, 256, 256, 64, 3, bias=bl, epi=L.EPI_
                              hr=hr, dout=do, l1_scale=1e-6, loss_part=lp))
 res["last_train_us"] = round(us, 2)
 print(json.dumps(res))
+# conv_first 3 -> 64 at 64x64 (the LR input, fp32 NCHW -> bf16 NHWC)
+xl = torch.rand(B, 3, 64, 64, device='cuda'); wf = torch.randn(64, 3, 3, 3, device='cuda') * 0.2
+bf = torch.zeros(64, device='cuda'); yf = torch.empty(B, 64, 64, 64, device='cuda', dtype=torch.bfloat16)
+us = timeit(lambda: ctx.emit('cf', ctx.lib.fen_conv_first_fwd, ctx.code, B, 3, 64, 64, 64, ptr(xl), ptr(wf), ptr(bf), ptr(yf)))
+print(json.dumps({"conv_first_us": round(us, 2), "GBs": round((xl.numel() * 4 + yf.numel() * 2) / us / 1e3, 1)}))
