@@ -229,8 +229,14 @@ constexpr int WG_SLOT = HALO_SLOT + WG_TILE;   // 74752 B per slot, 2 slots
 
 __device__ __forceinline__ int wkey(int col) { return (((col >> 1) & 1) << 1) | (((col >> 3) & 1) << 2); }
 
+// NKH = 3: the block computes one kernel row kh (3 taps) and walks 3x the tiles -- 3x fewer
+// fp32 slabs to write and re-read (at 2 tiles per block the 147-KB slabs were ~half the
+// wgrad's time); the three kh blocks of a chunk fill disjoint taps of the chunk's slab and
+// sit on one XCD (block ids 8 apart), so their halo / dy reads share its L2.
+template <int NKH>
 __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int tpc, float* part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int NT = 9 / NKH;                      // taps per block
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ch = wave & 1, cq = wave >> 1;
     const int q = lane >> 4, c16 = lane & 15, qq = c16 >> 2, pp = c16 & 3;
@@ -238,7 +244,20 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
     const int ntiles = d.B * tpi;
     const int co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64;
-    const int t_begin = blockIdx.x * tpc, t_end = min(t_begin + tpc, ntiles);
+    // NKH = 3: block x -> (chunk, kh) with the kh blocks of a chunk 8 ids apart (same XCD)
+    // (NKH = 3: tpc carries the chunk count; tiles split evenly over the chunks)
+    int chunk = blockIdx.x, kh0 = 0, t_begin, t_end;
+    if (NKH == 3) {
+        const int x = blockIdx.x, grp = x / 24, r = x % 24;
+        chunk = grp * 8 + (r & 7);
+        kh0 = r >> 3;
+        if (chunk >= tpc) return;                    // padding block of the last group
+        t_begin = (int)((long long)chunk * ntiles / tpc);
+        t_end = (int)((long long)(chunk + 1) * ntiles / tpc);
+    } else {
+        t_begin = chunk * tpc;
+        t_end = min(t_begin + tpc, ntiles);
+    }
     const i32x4 xr = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * Cin * 2));
     const i32x4 yr = make_rsrc(d.dy, (unsigned)((size_t)d.B * H * W * Cout * 2));
 
@@ -287,13 +306,14 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
         }
     }
 
-    f32x4 acc[2][9], accb[2];
+    f32x4 acc[2][NT], accb[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         accb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < 9; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < NT; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    const bool do_bias = kh0 == 0;
     const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
 
     if (t_begin < t_end) issue(t_begin, smem);
@@ -304,8 +324,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
         if (t + 1 < t_end) issue(t + 1, smem + ((k + 1) & 1) * WG_SLOT);
         const char* hx = cur;
         const char* ty = cur + HALO_SLOT;
-        uint4 A0[2], B0[9], A1[2], B1[9];
-        auto load = [&](int s, uint4 (&A)[2], uint4 (&Bf)[9]) {
+        uint4 A0[2], B0[NT], A1[2], B1[NT];
+        auto load = [&](int s, uint4 (&A)[2], uint4 (&Bf)[NT]) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -316,8 +336,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
                     if (h == 0) { A[m].x = u.x; A[m].y = u.y; } else { A[m].z = u.x; A[m].w = u.y; }
                 }
 #pragma unroll
-                for (int tap = 0; tap < 9; ++tap) {
-                    const int kh = tap / 3, kw = tap % 3;
+                for (int tap = 0; tap < NT; ++tap) {
+                    const int kh = kh0 + tap / 3, kw = tap % 3;
                     const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (lds_s16x4*)(hx + offB[h][kw] + (2 * s + kh) * (HALO * 128)));
                     const uint2 u = __builtin_bit_cast(uint2, v);
@@ -325,12 +345,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
                 }
             }
         };
-        auto mma = [&](int s, const uint4 (&A)[2], const uint4 (&Bf)[9]) {
+        auto mma = [&](int s, const uint4 (&A)[2], const uint4 (&Bf)[NT]) {
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap)
+            for (int tap = 0; tap < NT; ++tap)
 #pragma unroll
                 for (int m = 0; m < 2; ++m) mma16<bf16>(acc[m][tap], A[m], Bf[tap]);
-            if ((s & 3) == cq) {
+            if ((s & 3) == cq && do_bias) {
 #pragma unroll
                 for (int m = 0; m < 2; ++m) mma16<bf16>(accb[m], A[m], ones);
             }
@@ -353,17 +373,19 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
     }
 
     // slab: OIHW [Cout][Cin][9] then [Cout] bias partials (ci0 == 0 blocks only)
-    float* slab = part + (size_t)blockIdx.x * ((size_t)Cout * Cin * 9 + Cout);
+    // slab layout [tap][Cout][Cin] (+ [Cout] bias): 16 lanes store 64 contiguous bytes; the
+    // OIHW order [Cout][Cin][9] put lanes 36 B apart (scattered partial-line writes of all
+    // blocks at once at the end of the launch).  k_wgrad_fin transposes on its one write.
+    float* slab = part + (size_t)chunk * ((size_t)Cout * Cin * 9 + Cout);
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int co = co0 + ch * 32 + m * 16 + 4 * q + r, ci = ci0 + cq * 16 + c16;
-            float* o = slab + ((size_t)co * Cin + ci) * 9;
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) o[tap] = acc[m][tap][r];
+            for (int tap = 0; tap < NT; ++tap) slab[((size_t)(kh0 * 3 + tap) * Cout + co) * Cin + ci] = acc[m][tap][r];
         }
-    if (ci0 == 0) {
+    if (ci0 == 0 && do_bias) {
         float* red = (float*)smem;   // [4 cq][64 co]; no DMA in flight, last barrier passed
         if (c16 == 0) {
 #pragma unroll
@@ -377,10 +399,11 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
     }
 }
 
-// dw (+)= sum_chunk slab[chunk][0 .. cout_valid*Cin*9), db (+)= sum_chunk slab[chunk][Cout*Cin*9 + co]:
-// column j (float4) per lane, the 8 waves split the chunks, fixed-order combine in LDS.
-__global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int nw4, int nb, int boff4,
-                                                   const float4* __restrict__ part, float* dw, float* db,
+// dw (+)= sum_chunk slab[chunk][tap][co][ci] (co < cout_valid, written OIHW), db (+)= sum_chunk
+// slab[chunk][Cout*Cin*9 + co]: column j (float4 = 4 ci of one (tap, co)) per lane, the 8 waves
+// split the chunks, fixed-order combine in LDS.
+__global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int nw4, int nb, int boff4, int Cout,
+                                                   int Cin, const float4* __restrict__ part, float* dw, float* db,
                                                    int accumulate) {
     __shared__ float4 red[8][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -418,9 +441,13 @@ __global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int 
         }
         const float v[4] = {t.x, t.y, t.z, t.w};
         if (isw) {
-            float* o = dw + (size_t)j * 4;   // scalar stores: dw views need not be 16-B aligned
+            const int e0 = j * 4, tap = e0 / (Cout * Cin), rem = e0 - tap * (Cout * Cin);
+            const int co = rem / Cin, ci = rem - co * Cin;
+            if (co < nb) {
+                float* o = dw + ((size_t)co * Cin + ci) * 9 + tap;   // scalar stores (OIHW, stride 9)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = accumulate ? o[e] + v[e] : v[e];
+                for (int e = 0; e < 4; ++e) o[e * 9] = accumulate ? o[e * 9] + v[e] : v[e];
+            }
         } else if (db) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -431,23 +458,52 @@ __global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int 
     }
 }
 
+// the persistent kernel: bf16, 64-multiple channel counts, 32-bit buffer offsets
+bool wgrad_use_p(const fen_wgrad_desc* d) {
+    const size_t xb = (size_t)d->B * d->H * d->W * d->Cin * 2, yb = (size_t)d->B * d->H * d->W * d->Cout * 2;
+    return d->dtype == FEN_BF16 && d->Cout % 64 == 0 && d->Cin % 64 == 0 && xb < 0x7fff0000u &&
+           yb < 0x7fff0000u && getenv("FEN_WGRAD_OLD") == nullptr;
+}
+
+int wgrad_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    return cus;
+}
+
+// persistent kernel with one kernel row per block (k_wgrad_p<3>), opt-in (FEN_WGRAD_KH3=1):
+// 3x fewer slabs, but every block then streams its tiles' full halo + dy for a third of the
+// MFMAs and the per-CU LDS-DMA rate (~17 GB/s) binds -- measured 31.8 us against 28.2 us for
+// the 9-tap form at B=32 64x64 (tools/gpu_t6.sh)
+bool wgrad_kh_split(const fen_wgrad_desc* d, int ntiles) {
+    return wgrad_use_p(d) && d->Cout == 64 && d->Cin == 64 && ntiles >= 16 && getenv("FEN_WGRAD_KH3") != nullptr;
+}
+
 int wgrad_geom(const fen_wgrad_desc* d, int* nchunk, int* tpc, int* cot) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int ntiles = d->B * tpi;
     *cot = d->Cout % 64 == 0 ? 64 : 16;
+    if (wgrad_kh_split(d, ntiles)) {
+        // 3 blocks per chunk, chunks in groups of 8 (one XCD each): <= 1 block per CU
+        int n = 8 * (wgrad_cus() / 24);
+        if (n < 8) n = 8;
+        if (n > ntiles) n = ntiles;
+        *nchunk = n;
+        *tpc = n;   // k_wgrad_p<3> reads the chunk count here
+        return FEN_OK;
+    }
     const int yz = (d->Cout / *cot) * (d->Cin / 64);
     int t = (ntiles * yz + 255) / 256;  // target ~256 blocks
     if (t < 1) t = 1;
     *tpc = t;
     *nchunk = (ntiles + t - 1) / t;
     return FEN_OK;
-}
-
-// the persistent kernel: bf16, 64-multiple channel counts, 32-bit buffer offsets
-bool wgrad_use_p(const fen_wgrad_desc* d) {
-    const size_t xb = (size_t)d->B * d->H * d->W * d->Cin * 2, yb = (size_t)d->B * d->H * d->W * d->Cout * 2;
-    return d->dtype == FEN_BF16 && d->Cout % 64 == 0 && d->Cin % 64 == 0 && xb < 0x7fff0000u &&
-           yb < 0x7fff0000u && getenv("FEN_WGRAD_OLD") == nullptr;
 }
 
 }  // namespace
@@ -473,17 +529,23 @@ extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
         static bool attr = false;
         const size_t lds = 2 * WG_SLOT;
         if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_wgrad_p, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            (void)hipFuncSetAttribute((const void*)k_wgrad_p<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            (void)hipFuncSetAttribute((const void*)k_wgrad_p<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             attr = true;
         }
-        hipLaunchKernelGGL(k_wgrad_p, dim3(nchunk, d->Cout / 64, d->Cin / 64), dim3(512), lds, s, *d, tpc, d->work);
+        const int ntiles = d->B * ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
+        if (wgrad_kh_split(d, ntiles))
+            hipLaunchKernelGGL(k_wgrad_p<3>, dim3((nchunk + 7) / 8 * 24), dim3(512), lds, s, *d, tpc, d->work);
+        else
+            hipLaunchKernelGGL(k_wgrad_p<1>, dim3(nchunk, d->Cout / 64, d->Cin / 64), dim3(512), lds, s, *d, tpc,
+                               d->work);
         FEN_CHECK_LAUNCH();
         const int stride4 = (d->Cout * d->Cin * 9 + d->Cout) / 4;
-        const int nw4 = d->cout_valid * d->Cin * 9 / 4;
+        const int nw4 = d->Cout * d->Cin * 9 / 4;   // tap-major: rows co >= cout_valid skipped
         const int boff4 = d->Cout * d->Cin * 9 / 4;
         const int ncol = nw4 + (d->cout_valid + 3) / 4;
         hipLaunchKernelGGL(k_wgrad_fin, dim3((ncol + 63) / 64), dim3(512), 0, s, nchunk, stride4, nw4, d->cout_valid,
-                           boff4, (const float4*)d->work, d->dw, d->db, d->accumulate);
+                           boff4, d->Cout, d->Cin, (const float4*)d->work, d->dw, d->db, d->accumulate);
         FEN_CHECK_LAUNCH();
         return FEN_OK;
     }

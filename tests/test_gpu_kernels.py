@@ -345,12 +345,13 @@ def test_se_fused(dtype, B, C, Cr, H, W):
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 24, 40, 64, 64), (1, 16, 16, 64, 256),
                                              (1, 32, 32, 64, 16), (17, 64, 64, 64, 64), (2, 20, 36, 128, 64),
-                                             (3, 32, 48, 64, 256)])
+                                             (3, 32, 48, 64, 256), (2, 64, 64, 64, 64), (3, 40, 56, 64, 64)])
 def test_wgrad(dtype, B, H, W, Cin, Cout):
     """fen_wgrad3x3 vs autograd of conv2d.  The reference runs in float64 on the operands
     rounded to the compute dtype, so bf16 is held to fp32-accumulation accuracy (rel 1e-5):
     a wrong fragment mapping or a dropped tile shows as O(1).  (17, 64, 64) puts 2 tiles per
-    block; Cout 256 / Cin 128 exercise the co-group / ci-group grid."""
+    block; Cout 256 / Cin 128 exercise the co-group / ci-group grid.  The opt-in
+    one-kernel-row-per-block form (FEN_WGRAD_KH3) is covered by test_wgrad_kh_split."""
     from src.hip import net
     torch.manual_seed(7)
     x = torch.randn(B, Cin, H, W).to(dtype).float()
@@ -368,6 +369,18 @@ def test_wgrad(dtype, B, H, W, Cin, Cout):
     rel = float((dw.cpu().double() - gw).norm() / gw.norm())
     relb = float((db.cpu().double() - gb).norm() / gb.norm())
     assert rel <= 1e-5 and relb <= 1e-5, (rel, relb)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (3, 40, 56), (17, 64, 64)])
+def test_wgrad_kh_split(B, H, W):
+    """k_wgrad_p<3> (one kernel row per block, FEN_WGRAD_KH3=1; read at launch) vs float64
+    autograd: 32 tiles (32 chunks), ragged 40 x 56, 272 tiles (80 chunks of 3-4)."""
+    import os
+    os.environ["FEN_WGRAD_KH3"] = "1"
+    try:
+        test_wgrad(torch.bfloat16, B, H, W, 64, 64)
+    finally:
+        del os.environ["FEN_WGRAD_KH3"]
 
 
 @pytest.mark.parametrize("dtype", DT)
