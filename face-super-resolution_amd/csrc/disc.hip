@@ -52,16 +52,33 @@ __global__ __launch_bounds__(256) void k_bn_stats(size_t npx, int C, const T* __
 
 // per channel: mean, rstd (biased var, eps) -> stat[0..C) mean, stat[C..2C) rstd; running
 // stats (momentum m, unbiased var) updated when running_mean != NULL
+// 64 channels per block, 16 waves each summing every 16th partial (loads in flight across the
+// waves; one thread walking all BN_BLOCKS partials took ~130 us), fixed-order combine in LDS
+constexpr int FIN_WAVES = 16;
 template <typename T>
-__global__ void k_bn_finalize(int nblocks, size_t npx, int C, const T* __restrict__ y, const float* __restrict__ part,
-                              float eps, float momentum, float* __restrict__ stat, float* __restrict__ rmean,
-                              float* __restrict__ rvar) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+__global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_finalize(int nblocks, size_t npx, int C, const T* __restrict__ y,
+                                                              const float* __restrict__ part, float eps, float momentum,
+                                                              float* __restrict__ stat, float* __restrict__ rmean,
+                                                              float* __restrict__ rvar) {
+    __shared__ double red[2][FIN_WAVES][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
     double s = 0.0, q = 0.0;
-    for (int b = 0; b < nblocks; ++b) {
-        s += part[(size_t)b * 2 * C + c];
-        q += part[(size_t)b * 2 * C + C + c];
+    if (c < C) {
+        for (int b = w; b < nblocks; b += FIN_WAVES) {
+            s += part[(size_t)b * 2 * C + c];
+            q += part[(size_t)b * 2 * C + C + c];
+        }
+    }
+    red[0][w][lane] = s;
+    red[1][w][lane] = q;
+    __syncthreads();
+    if (w != 0 || c >= C) return;
+    s = 0.0;
+    q = 0.0;
+    for (int k = 0; k < FIN_WAVES; ++k) {
+        s += red[0][k][lane];
+        q += red[1][k][lane];
     }
     const double n = (double)npx;
     const double md = s / n;                                  // mean of (y - shift)
@@ -142,14 +159,28 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(size_t npx, int C, const 
 
 // dbeta = sum dz, dgamma = sum dz xh (fixed-order over the block partials); red2 = the same
 // for the data-gradient pass
-__global__ void k_bn_bwd_finalize(int nblocks, int C, const float* __restrict__ part, float* __restrict__ dgamma,
-                                  float* __restrict__ dbeta, float* __restrict__ red2, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+__global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_bwd_finalize(int nblocks, int C, const float* __restrict__ part,
+                                                                  float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                  float* __restrict__ red2, int accumulate) {
+    __shared__ float red[2][FIN_WAVES][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
     float s = 0.f, q = 0.f;
-    for (int b = 0; b < nblocks; ++b) {
-        s += part[(size_t)b * 2 * C + c];
-        q += part[(size_t)b * 2 * C + C + c];
+    if (c < C) {
+        for (int b = w; b < nblocks; b += FIN_WAVES) {
+            s += part[(size_t)b * 2 * C + c];
+            q += part[(size_t)b * 2 * C + C + c];
+        }
+    }
+    red[0][w][lane] = s;
+    red[1][w][lane] = q;
+    __syncthreads();
+    if (w != 0 || c >= C) return;
+    s = 0.f;
+    q = 0.f;
+    for (int k = 0; k < FIN_WAVES; ++k) {
+        s += red[0][k][lane];
+        q += red[1][k][lane];
     }
     red2[c] = s;
     red2[C + c] = q;
@@ -230,12 +261,12 @@ extern "C" int fen_bn_stats(int dtype, size_t npx, int C, const void* y, float e
     if (dtype == FEN_BF16) {
         hipLaunchKernelGGL(k_bn_stats<bf16>, dim3(BN_BLOCKS), dim3(256), 0, STREAM, npx, C, (const bf16*)y, work);
         FEN_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_bn_finalize<bf16>, dim3(nblk(C)), dim3(256), 0, STREAM, BN_BLOCKS, npx, C, (const bf16*)y,
+        hipLaunchKernelGGL(k_bn_finalize<bf16>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C, (const bf16*)y,
                            work, eps, momentum, stat, rmean, rvar);
     } else if (dtype == FEN_F32) {
         hipLaunchKernelGGL(k_bn_stats<float>, dim3(BN_BLOCKS), dim3(256), 0, STREAM, npx, C, (const float*)y, work);
         FEN_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_bn_finalize<float>, dim3(nblk(C)), dim3(256), 0, STREAM, BN_BLOCKS, npx, C,
+        hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C,
                            (const float*)y, work, eps, momentum, stat, rmean, rvar);
     } else {
         return FEN_EINVAL;
@@ -280,7 +311,7 @@ extern "C" int fen_bn_bwd(int dtype, size_t npx, int C, const void* da, const vo
         return FEN_EINVAL;
     }
     FEN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(nblk(C)), dim3(256), 0, STREAM, BN_BLOCKS, C, work, dgamma, dbeta, red2,
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, C, work, dgamma, dbeta, red2,
                        accumulate);
     FEN_CHECK_LAUNCH();
     if (dtype == FEN_BF16) {
