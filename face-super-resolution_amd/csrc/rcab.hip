@@ -47,18 +47,25 @@ constexpr int O_RED = O_RING + 6 * TAP_BYTES;   // [4][64] f32 pool partials of 
 constexpr int O_CST = O_RED + 4 * 64 * 4;       // b1[64] alpha[64] b2[64]
 constexpr int O_FC = O_CST + 3 * 64 * 4;        // fc1 [16][64], fc2 [64][16] f32
 constexpr int O_FLAG = O_FC + 2 * 1024 * 4;     // block-wide scalars
+#ifdef FEN_STAMPS
+constexpr int O_STAMP = O_FLAG + 64;            // diagnostic build: [8 waves][48] u32 stamps
+constexpr int RCAB_LDS = O_STAMP + 8 * 48 * 4;
+#else
 constexpr int RCAB_LDS = O_FLAG + 64;
+#endif
 static_assert(RCAB_LDS <= 163840, "LDS budget");
 static_assert(O_RING % 16 == 0 && O_RED % 16 == 0 && O_FC % 16 == 0, "alignment");
 
 // diagnostic build (-DFEN_STAMPS): s_memrealtime per wave at phase points into d.stamps,
 // [block][wave][48]; the product build executes none of it
+// The stamps land in LDS (low 32 bits; copied out once at the end of the kernel): a global
+// store per stamp would sit in vmcnt and stretch every boundary's vmcnt(0) wait.
 #ifdef FEN_STAMPS
 #define RSTAMP(i)                                                                            \
     do {                                                                                     \
         unsigned long long _rt;                                                              \
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt)::"memory");      \
-        if (d.stamps && lane == 0 && (i) < 48) d.stamps[((size_t)blockIdx.x * 8 + wave) * 48 + (i)] = _rt; \
+        if (lane == 0 && (i) < 48) stamp_lds[wave * 48 + (i)] = (unsigned)_rt;                 \
     } while (0)
 #else
 #define RSTAMP(i) \
@@ -76,6 +83,29 @@ constexpr unsigned POLL_MAX = 1u << 20;      // ~0.5 s of s_sleep: a gate that n
 __device__ __forceinline__ int ekey(int row, int chunk) { return (chunk ^ (row & 7)) << 4; }
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// Output stores nobody in this launch reads again (y; training copies of z1 / a1).  Plain
+// stores: the non-temporal form (RCAB_NT, meant to keep x in L2 for the apply one tile
+// later) measured neutral for inference (42.3 us both) and 1.45x SLOWER for training
+// (74.7 vs 51.2 us: the 8-B fragment-layout pieces then reach HBM as partial-line writes
+// instead of merging in L2) -- tools/gpu_ab_rcab.sh
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_out16(void* p, uint4 v) {
+#ifndef RCAB_NT
+    *(uint4*)p = v;
+#else
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)p);
+#endif
+}
+__device__ __forceinline__ void st_out4(void* p, const float v[4]) {
+    const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+#ifndef RCAB_NT
+    *(uint2*)p = make_uint2(lo, hi);
+#else
+    __builtin_nontemporal_store((unsigned long long)lo | ((unsigned long long)hi << 32), (unsigned long long*)p);
+#endif
+}
 
 // sync-word access (uncached workspace: every load / store goes to memory)
 __device__ __forceinline__ int ld_poll(const int* p) {
@@ -203,8 +233,24 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     float* cst = (float*)(smem + O_CST);
     float* fcs = (float*)(smem + O_FC);
     int* lflag = (int*)(smem + O_FLAG);
+#ifdef FEN_STAMPS
+    unsigned* stamp_lds = (unsigned*)(smem + O_STAMP);
+    for (int i = threadIdx.x; i < 8 * 48; i += blockDim.x) stamp_lds[i] = 0u;
+    __syncthreads();
+#endif
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    // the wave id through readfirstlane: provably wave-uniform to the compiler, so the
+    // per-wave roles (conv1 fragment group: slot-4 main/edge, slot 5; wave 0's gate; the
+    // opt-in s_setprio of waves 4-7) compile to scalar branches.  tid >> 6 alone is divergent to
+    // hipcc: the slot-5 MFMAs and reads were exec-masked (issued by every wave) and
+    // s_setprio 1 ran unconditionally in all waves (cdna_hip_programming.md, s_setprio
+    // recipe / descriptor recipe).  RCAB_DIV_WAVE: the old form, for A/B.
+#ifdef RCAB_DIV_WAVE
+    const int wave = tid >> 6;
+#else
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#endif
     const int q = lane >> 4, c16 = lane & 15;
     const int ch = wave & 1, g = wave >> 1;          // conv1: channel half, fragment group
     const int wr = wave >> 1, wc = wave & 1;         // conv2: row group, channel half
@@ -286,8 +332,11 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         const int c = i >> 4, j = i & 15;
         fcs[1024 + i] = j < Cr ? d.fc2[c * Cr + j] : 0.f;   // [64][16]
     }
-#ifndef RCAB_NO_PRIO
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);   // second-dispatched half: MI355X_MICROARCH.md 'Two waves per SIMD' 4
+#ifdef RCAB_PRIO
+    // waves 4-7 at priority 1 (MI355X_MICROARCH.md 'Two waves per SIMD'): measured ~1 us
+    // SLOWER per launch once the wave id is uniform (before that, s_setprio ran in every
+    // wave, a no-op) -- opt-in for A/B only
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
     // this launch's epoch; announce that this block has read it
     const int ep1 = __builtin_amdgcn_readfirstlane(ld_poll(epoch)) + 1;
@@ -438,7 +487,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                 const float hi = __uint_as_float(tw[e] & 0xffff0000u) * sv[2 * e + 1] + __uint_as_float(xw[e] & 0xffff0000u);
                 ow[e] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
             }
-            *(uint4*)((char*)d.y + o) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+            st_out16((char*)d.y + o, make_uint4(ow[0], ow[1], ow[2], ow[3]));
         }
     };
     // (!PARK) y = t * s * rs + x in the MFMA fragment layout (t in tcar)
@@ -473,7 +522,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                 o[1] = __uint_as_float(tcar[m][n].x & 0xffff0000u) * sv[m][1] + __uint_as_float(xf[m][n].x & 0xffff0000u);
                 o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xf[m][n].y << 16);
                 o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xf[m][n].y & 0xffff0000u);
-                st4<bf16>((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
+                st_out4((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
             }
         }
     };
@@ -561,8 +610,8 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                         float a[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) a[r] = prelu_f(zs[m][f][r], alp[r]);
-                        st4<bf16>((char*)d.z1 + o * 2, zs[m][f]);
-                        st4<bf16>((char*)d.a1 + o * 2, a);
+                        st_out4((char*)d.z1 + o * 2, zs[m][f]);
+                        st_out4((char*)d.a1 + o * 2, a);
                     }
                 }
             }
@@ -736,6 +785,11 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             st_flag(epoch, ep1);
         }
     }
+#ifdef FEN_STAMPS
+    __syncthreads();
+    if (d.stamps && lane < 48 && stamp_lds[wave * 48 + lane] != 0u)
+        d.stamps[((size_t)blockIdx.x * 8 + wave) * 48 + lane] = stamp_lds[wave * 48 + lane];
+#endif
     (void)lflag;
 }
 

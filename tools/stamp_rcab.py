@@ -49,3 +49,11 @@ for i in range(48):
     v = np.where(v > 0, (v - t0) / 100.0, np.nan)[ok]
     out[str(i)] = [round(float(np.median(np.nanmin(v, 1))), 2), round(float(np.median(np.nanmax(v, 1))), 2)]
 print(json.dumps(out))
+# per-wave medians (over blocks) of chosen intervals: slot pairs (start, end)
+per = {}
+for nm, (s0, s1) in {"apply": (38, 39), "conv2_p3": (40, 42), "conv1_p1": (45, 46), "epi1+gate": (15, 8)}.items():
+    v0, v1 = a[:, :, s0].astype(np.float64), a[:, :, s1].astype(np.float64)
+    ok = (v0 > 0) & (v1 > 0)
+    d = np.where(ok, (v1 - v0) / 100.0, np.nan)
+    per[nm] = [round(float(np.nanmedian(d[:, w])), 2) if ok[:, w].any() else None for w in range(8)]
+print(json.dumps({"per_wave_us": per}))
