@@ -51,6 +51,11 @@ namespace {
     } while (0)
 #endif
 
+// The conv kernels keep the wave id as tid >> 6 (divergent to hipcc, so their per-wave roles
+// compile to exec-masked code): the readfirstlane form (wave_id(), fen_common.h) measured
+// slower here -- upsampler 188.9 -> 195.7 us, dgrads +0.8 / +1.2 us (tools/gpu_t10.sh) --
+// while it sped up k_rcab and k_conv_last.
+
 // s_waitcnt vmcnt(n) for a runtime n (the immediate must be a literal): waits until at
 // most n of this wave's vector-memory ops are outstanding.  Ops retire in issue order, so
 // with n = number of stores issued after the halo prefetch, the prefetch has landed while

@@ -45,7 +45,7 @@ static_assert(2 * PIECES0 <= 63 && 2 * (PIECES1 + 4) <= 63, "vmcnt field");
 template <bool TRAIN>
 __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, B = d.B, Cout = d.Cout;
     const int Hs = H >> 2, Ws = W >> 2;

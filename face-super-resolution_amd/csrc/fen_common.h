@@ -114,6 +114,10 @@ __device__ __forceinline__ float prelu_bwd_f(float dy, float pre, float a) {
 // contribution to dL/da: dy * pre where pre <= 0
 __device__ __forceinline__ float prelu_dalpha_f(float dy, float pre) { return dy * pre * (1.f - pos_step(pre)); }
 
+// The wave index, provably wave-uniform to the compiler (threadIdx.x >> 6 alone is divergent
+// to hipcc: every per-wave role built on it compiles to exec-masked code that all waves issue)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(int B, int Ci, int H, 
                                    const T* __restrict__ dy, float* __restrict__ part) {
     __shared__ float xs[3][18][19];
     __shared__ float red[4][28 * 2][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = wave_id();
     const int nc = (C + 63) / 64;
     float acc[2][28];
 #pragma unroll

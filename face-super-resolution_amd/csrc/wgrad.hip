@@ -237,7 +237,7 @@ template <int NKH>
 __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int tpc, float* part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int NT = 9 / NKH;                      // taps per block
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int ch = wave & 1, cq = wave >> 1;
     const int q = lane >> 4, c16 = lane & 15, qq = c16 >> 2, pp = c16 & 3;
     const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int 
                                                    int Cin, const float4* __restrict__ part, float* dw, float* db,
                                                    int accumulate) {
     __shared__ float4 red[8][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = wave_id();
     const int j = blockIdx.x * 64 + lane;
     const int nb4 = (nb + 3) / 4;
     const bool isw = j < nw4, isb = !isw && j < nw4 + nb4;
