@@ -132,9 +132,9 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
     // CL_DIAG_NOLOAD the compute waves alone (on the first two tiles' bytes)
 
     // ---- compute-wave constants
-    float bias[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bias[r] = ((d.epi & FEN_EPI_BIAS) && r < Cout) ? d.bias[r] : 0.f;
+    // epilogue lane (q, c16) owns output channel q of pixel c16 (q < Cout valid)
+    const bool chq = (lane >> 4) < Cout;
+    const float bias_q = ((d.epi & FEN_EPI_BIAS) && chq) ? d.bias[lane >> 4] : 0.f;
     const float inv = 0.25f;
     // this lane's column taps (fixed per lane: w0 % 4 == 0); patch column of tap 0
     const float sx = ((float)c16 + 0.5f) * inv - 0.5f;   // relative to w0 / 4
@@ -226,27 +226,31 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
             float bic = 0.f;
 #pragma unroll
             for (int k = 0; k < 4; ++k) bic += hrow[k] * cy[k];
-            float bq[4];
+            // conv value of channel q: lane (0, c16) holds co 0..3 of pixel c16 (acc[n][r], co =
+            // 4q + r); every lane takes its channel's from there -- one 48-lane store per row
+            // instead of exec-masked 16-lane stores per channel
+            float cq = 0.f;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) bq[r] = __shfl(bic, r * 16 + c16, 64);
-            float g4[4] = {0.f, 0.f, 0.f, 0.f};
-            if (q == 0) {
+            for (int r = 0; r < 4; ++r) {
+                const float t = __shfl(acc[n][r], c16, 64);
+                cq = q == r ? t : cq;
+            }
+            float v = cq + bias_q + bic;
+            if (d.clamp) v = fminf(fmaxf(v, 0.f), 1.f);
+            if (d.y && chq) ((float*)d.y)[(((size_t)b * Cout + q) * H + h) * W + w0 + c16] = v;
+            if (train) {
+                const float diff = chq ? v - hrp[q * 256 + n * 16] : 0.f;
+                lsum += fabsf(diff);
+                const float sg = diff > 0.f ? d.l1_scale : (diff < 0.f ? -d.l1_scale : 0.f);
+                // dL/dsr, NHWC16: lane (q, c16) writes channels 4q..4q+3 (only q = 0 nonzero)
+                float g4[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    if (r < Cout) {
-                        float v = acc[n][r] + bias[r] + bq[r];
-                        if (d.clamp) v = fminf(fmaxf(v, 0.f), 1.f);
-                        if (d.y) ((float*)d.y)[(((size_t)b * Cout + r) * H + h) * W + w0 + c16] = v;
-                        if (train) {
-                            const float diff = v - hrp[r * 256 + n * 16];
-                            lsum += fabsf(diff);
-                            g4[r] = diff > 0.f ? d.l1_scale : (diff < 0.f ? -d.l1_scale : 0.f);
-                        }
-                    }
+                    const float t = __shfl(sg, r * 16 + c16, 64);
+                    g4[r] = q == 0 ? t : 0.f;
                 }
+                if (d.dout) st4<bf16>((char*)d.dout + (((size_t)(b * H + h) * W + w0 + c16) * 16 + q * 4) * 2, g4);
             }
-            if (train && d.dout)
-                st4<bf16>((char*)d.dout + (((size_t)(b * H + h) * W + w0 + c16) * 16 + q * 4) * 2, g4);
         }
         if (train && d.loss_part) {
             lsum = wave_sum(lsum);
