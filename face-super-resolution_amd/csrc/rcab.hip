@@ -78,9 +78,11 @@ constexpr int CP_SC = 17;                     // buffer cache policy sc0|sc1: st
 constexpr unsigned POLL_MAX = 1u << 20;      // ~0.5 s of s_sleep: a gate that never comes
                                              // sets sync[3*B] and the kernel exits anyway
 
-// 16-B chunk position in the edge image: pixel e = row*4 + col', key = row & 7 (an edge
-// fragment's 16 lanes cover 8 rows x 2 columns: 16 distinct bank slots)
-__device__ __forceinline__ int ekey(int row, int chunk) { return (chunk ^ (row & 7)) << 4; }
+// 16-B chunk position in the edge image: pixel e = row*4 + col', key = (2 row) & 7.  Checked
+// against ds_read_b128's lane groups for every (edge fragment, kh, kw, k-half): conflict-free;
+// the key row & 7 left 2-way conflicts in a third of them (tools note in DESIGN.md)
+__device__ __forceinline__ int ekey_of(int row) { return (2 * row) & 7; }
+__device__ __forceinline__ int ekey(int row, int chunk) { return (chunk ^ ekey_of(row)) << 4; }
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
@@ -115,55 +117,6 @@ __device__ __forceinline__ void st_flag(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ------------------------------------------------------------------------------------
-// conv1 MFMAs for one phase (3 taps, tap order), one wave, 32 output channels (MT = 2) x up
-// to 6 pixel fragments.  Slots 0..3 are output rows row0..row0+3 (columns 0..15); slot 4 is
-// row row0+4 (groups 0, 1) or an edge fragment (groups 2, 3: wave-uniform branch); slot 5
-// is a second edge fragment (group 3 only).  Fragments double-buffered one step ahead.
-//   main B: xh + hcol(c16 + kw, chunk) + (row0 + f + kh) * XW*128
-//   edge B: eh + eb[kh][kk] + kw * 128
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ void conv1_phase(f32x4 (&acc)[2][6], const char* xh, const char* eh,
-                                            const char* const (&tapp)[3], int kh, int c16, int rowoff,
-                                            const int (&e4)[2], const int (&e5)[2], bool main4, bool has5,
-                                            int arow, int q) {
-    // phase = kernel row kh: taps (kh, kw = 0..2); xh_k / e*_k fold the row offset in once
-    const char* xk = xh + kh * (XW * 128);
-    uint4 A0[2], B0[6], A1[2], B1[6];
-    auto load = [&](int st, uint4 (&A)[2], uint4 (&Bf)[6]) {
-        const int kw = st >> 1, kk = st & 1;
-        const char* wt = tapp[kw];
-        const int mb = hcol(c16 + kw, kk * 4 + q) + rowoff;   // recomputed: keeps 6 VGPRs free
-#pragma unroll
-        for (int m = 0; m < 2; ++m) A[m] = *(const uint4*)(wt + swz(arow + m * 16, kk * 4 + q));
-#pragma unroll
-        for (int f = 0; f < 4; ++f) Bf[f] = *(const uint4*)(xk + mb + f * (XW * 128));
-        if (main4) Bf[4] = *(const uint4*)(xk + mb + 4 * (XW * 128));
-        else Bf[4] = *(const uint4*)(eh + e4[kk] + kw * 128);
-        if (has5) Bf[5] = *(const uint4*)(eh + e5[kk] + kw * 128);
-    };
-    auto mma = [&](const uint4 (&A)[2], const uint4 (&Bf)[6]) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-#pragma unroll
-            for (int f = 0; f < 5; ++f) mma16<bf16>(acc[m][f], A[m], Bf[f]);
-            if (has5) mma16<bf16>(acc[m][5], A[m], Bf[5]);
-        }
-    };
-    load(0, A0, B0);
-#pragma unroll
-    for (int st = 0; st < 6; st += 2) {
-        load(st + 1, A1, B1);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(A0, B0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (st + 2 < 6) load(st + 2, A0, B0);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(A1, B1);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
 // conv2 MFMAs for one phase (kernel column kw: taps (0,kw),(1,kw),(2,kw) in ring slots),
 // halo-row-reuse order on the a1 image; wave = 4 output rows x 32 channels.
 __device__ __forceinline__ void conv2_phase(f32x4 (&acc)[2][4], const char* a1, const char* const (&tapp)[3], int kw,
@@ -196,29 +149,64 @@ __device__ __forceinline__ void conv2_phase(f32x4 (&acc)[2][4], const char* a1, 
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// conv1 for one phase = kernel column kw (taps (0,kw),(1,kw),(2,kw) in ring slots 0..2), the
+// halo-row-reuse order conv2 uses: per k-half the wave loads its NR + 2 input rows once and
+// reuses them across the 3 kernel rows (13-18 fragment reads for 30-36 MFMAs; the by-row
+// order read 0.67-0.7 fragments per MFMA in 6 interleaved steps).  Slots 0..NR-1 are main
+// rows row0.. (16 columns); without MAIN4 slot 4 is edge fragment eidx4, with HAS5 slot 5 is
+// edge fragment 1 (edge reads do not reuse across kh: their lanes map to (row, column)).
+__device__ __forceinline__ int edge_base(int eidx, int c16, int kh, int chunk) {
+    int r = 8 * eidx + (c16 >> 1);
+    if (r > 17) r = 17;
+    return ((r + kh) * 4 + (c16 & 1)) * 128 + ekey(r + kh, chunk);
+}
+template <bool MAIN4, bool HAS5>
+__device__ __forceinline__ void conv1_kw(f32x4 (&acc)[2][6], const char* xh, const char* eh,
+                                         const char* const (&tapp)[3], int kw, int c16, int row0, int eidx4,
+                                         int arow, int q) {
+    constexpr int NR = MAIN4 ? 5 : 4;
+    constexpr int NB = NR + 2;
+    // opaque lane coordinates: every address below is recomputed per phase instead of being
+    // hoisted out of the tile loop (12 loop-invariant edge / A offsets live through conv2,
+    // the kernel's register peak, spilled)
+    asm volatile("" : "+v"(c16), "+v"(arow), "+v"(q));
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + q;
+        const char* xb = xh + hcol(c16 + kw, chunk) + row0 * (XW * 128);
+        uint4 Bm[NB], A[3][2], E4[3], E5[3];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) Bm[j] = *(const uint4*)(xb + j * (XW * 128));
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) A[kh][m] = *(const uint4*)(tapp[kh] + swz(arow + m * 16, chunk));
+        if constexpr (!MAIN4) {
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) E4[kh] = *(const uint4*)(eh + edge_base(eidx4, c16, kh, chunk) + kw * 128);
+        }
+        if constexpr (HAS5) {
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) E5[kh] = *(const uint4*)(eh + edge_base(1, c16, kh, chunk) + kw * 128);
+        }
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+#pragma unroll
+                for (int f = 0; f < NR; ++f) mma16<bf16>(acc[m][f], A[kh][m], Bm[f + kh]);
+                if constexpr (!MAIN4) mma16<bf16>(acc[m][4], A[kh][m], E4[kh]);
+                if constexpr (HAS5) mma16<bf16>(acc[m][5], A[kh][m], E5[kh]);
+            }
+#ifdef RCAB_C1_FENCE
+        __builtin_amdgcn_sched_barrier(0);   // A/B only: one k-half's fragments live at a time
+#endif
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // the kernel
 // ------------------------------------------------------------------------------------
-// edge fragment eidx: rows 8*eidx + lane/2 (clamped to 17 for the pad lanes of eidx 2),
-// column 16 + lane%2; base per (kh, k-half)
-// the same for one kernel row kh (computed at each phase start instead of kept live)
-__device__ __forceinline__ void edge_base_row(int eidx, int c16, int q, int kh, int (&eb)[2]) {
-    int r = 8 * eidx + (c16 >> 1);
-    if (r > 17) r = 17;
-    const int b = c16 & 1;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) eb[kk] = ((r + kh) * 4 + b) * 128 + ekey(r + kh, kk * 4 + q);
-}
-__device__ __forceinline__ void edge_bases(int eidx, int c16, int q, int (&eb)[3][2]) {
-    int r = 8 * eidx + (c16 >> 1);
-    if (r > 17) r = 17;
-    const int b = c16 & 1;
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) eb[kh][kk] = ((r + kh) * 4 + b) * 128 + ekey(r + kh, kk * 4 + q);
-}
-
 // PARK (training, d.t given): t is parked in d.t (stored for the backward anyway) and the
 // apply re-reads it with coalesced 16-B loads; else t stays in 16 VGPRs (packed bf16) and the
 // apply uses the MFMA fragment layout (fewer HBM bytes, more registers).
@@ -289,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         const int c = pc ^ ((r >> 1) & 7);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const int tap = p < 3 ? 3 * p + i : i * 3 + (p - 3);
+            const int tap = i * 3 + (p < 3 ? p : p - 3);   // slot i = tap (kh = i, kw = phase)
             const int voff = ((tap * 64 + r) * 64 + c * 8) * 2;
             dma16(p < 3 ? w1r : w2r, __builtin_amdgcn_readfirstlane(lds_addr(base + i * TAP_BYTES + wave * 1024)),
                   voff);
@@ -312,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             } else {
                 const int s = (i - XH_DMA) * 64 + lane, e = s >> 3, pc = s & 7;
                 const int hr = e >> 2, hc = 16 + (e & 3);
-                const int c = pc ^ (hr & 7);
+                const int c = pc ^ ekey_of(hr);
                 const int gh = h0 - 2 + hr, gw = w0 - 2 + hc;
                 if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) voff = (((b * H + gh) * W + gw) * 64 + c * 8) * 2;
                 base = lds_addr(eh + (i - XH_DMA) * 1024);
@@ -352,7 +340,6 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     // conv1 per-lane addressing (group g: rows row0.., slot 4 main for g < 2, edges for g >= 2)
     const int row0 = g == 0 ? 0 : g == 1 ? 5 : g == 2 ? 10 : 14;
     const bool main4 = g < 2, has5 = g == 3;
-    const int rowoff = row0 * (XW * 128);
     const int eidx4 = g == 2 ? 2 : 0;
     const int arow1 = ch * 32 + c16;                  // A row (co) of conv1's wave
     const int arow2 = wc * 32 + c16;
@@ -558,11 +545,10 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             issue_taps(P + 1);
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
                                    ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
-            int e4[2], e5[2];
-            edge_base_row(eidx4, c16, q, p, e4);
-            edge_base_row(1, c16, q, p, e5);
             if (k == 1 && p == 1) RSTAMP(45);
-            conv1_phase(acc1, xh, eh, tapp, p, c16, rowoff, e4, e5, main4, has5, arow1, q);
+            if (g < 2) conv1_kw<true, false>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
+            else if (g == 2) conv1_kw<false, false>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
+            else conv1_kw<false, true>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
             if (k == 1 && p == 1) RSTAMP(46);
         }
         if (k == 0) RSTAMP(15);
