@@ -41,3 +41,8 @@ xl = torch.rand(B, 3, 64, 64, device='cuda'); wf = torch.randn(64, 3, 3, 3, devi
 bf = torch.zeros(64, device='cuda'); yf = torch.empty(B, 64, 64, 64, device='cuda', dtype=torch.bfloat16)
 us = timeit(lambda: ctx.emit('cf', ctx.lib.fen_conv_first_fwd, ctx.code, B, 3, 64, 64, 64, ptr(xl), ptr(wf), ptr(bf), ptr(yf)))
 print(json.dumps({"conv_first_us": round(us, 2), "GBs": round((xl.numel() * 4 + yf.numel() * 2) / us / 1e3, 1)}))
+# SE backward pool: part = per-chunk sums of dy * t (B=32, 64x64x64)
+ta = torch.randn(B, 64, 64, 64, device='cuda', dtype=torch.bfloat16); tb = torch.randn_like(ta)
+pp = torch.empty(B * ctx.lib.fen_pool_parts(4096), 64, device='cuda')
+us = timeit(lambda: ctx.emit('pd', ctx.lib.fen_pool_dot, ctx.code, B, 4096, 64, ptr(ta), ptr(tb), ptr(pp)))
+print(json.dumps({"pool_dot_us": round(us, 2), "GBs": round(2 * ta.numel() * 2 / us / 1e3, 1)}))
