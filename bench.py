@@ -12,9 +12,13 @@ Also reported (field "train"): the stage-1 generator training step (bicubic /4 L
 synthesis, forward, L1, backward, RCCL gradient all-reduce over xGMI for N>1, clip,
 AdamW) at batch 32 per GPU -- the DP path of the north star.
 
-roofline: the dominant kernel is the RCAB 3x3 conv (64->64 ch, 64x64, B=32):
-  algorithmic FLOPs per launch = 2 * 32*64*64 px * 64 co * 576 (= 9 taps * 64 ci) = 9.664 GFLOP,
-  timed live here with HIP events on the launch stream; peak = 2500 TFLOP/s bf16 dense.
+roofline: the dominant kernel is the fused RCAB k_rcab (conv1 -> PReLU -> conv2 -> SE gate ->
+  residual, 64 ch, 64x64, B=32): algorithmic FLOPs per launch = 2 convs x 2 * 32*64*64 px * 64 co
+  * 576 (= 9 taps * 64 ci) = 19.33 GFLOP, timed live here with HIP events on the launch stream;
+  peak = 2500 TFLOP/s bf16 dense.
+pcie_inclusive: the same forward with the batch handed over as NCHW fp32 pinned host buffers
+(H2D of the LR batch, graph replay, D2H of the SR batch, serial on one stream) -- reported
+beside `value`, never as it.
 cpu_baseline: the CPU oracle (oracle/fen_oracle.py, fp32 PyTorch-CPU restatement of the
 reference forward) on this node's host cores, rank 0, N=1 only, bounded sample.
 """
@@ -97,6 +101,24 @@ def time_dominant_kernel(engine, reps=50):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps, label, flop  # ms
+
+
+def time_pcie_inclusive(eng, x, steps, warmup, world):
+    """images/s when the boundary hands over host buffers: NCHW fp32 LR batch in pinned host
+    memory -> H2D into the engine's input, the captured forward, SR batch D2H into pinned
+    host memory; serial on torch's current stream (no overlap of copies with compute)."""
+    hx = x.cpu().pin_memory()
+    hout = torch.empty(eng.out.shape, dtype=eng.out.dtype).pin_memory()
+
+    def step():
+        eng.x.copy_(hx, non_blocking=True)
+        eng.replay()
+        hout.copy_(eng.out, non_blocking=True)
+    t = timed(step, steps, warmup, world)
+    B = x.shape[0]
+    return {"value": round(B * world * steps / t, 2), "unit": "images/sec", "ms_per_step": round(1000.0 * t / steps, 4),
+            "bytes_h2d": hx.numel() * 4, "bytes_d2h": hout.numel() * 4,
+            "note": "NCHW fp32 pinned host in/out, copies serial with the graph replay"}
 
 
 def cpu_baseline(model, seconds=10.0):
@@ -204,9 +226,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FEN_BENCH_BACKEND=gloo + ranks sharing one device: a rehearsal of the N>1 path on a
+    # one-GPU box (the driver's multi-GPU runs use the default, RCCL, one GPU per rank)
+    backend = os.environ.get("FEN_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from src.hip.engine import FENEngine
 
     B = args.batch
@@ -244,6 +273,7 @@ def main():
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "kernel_ms": round(kern_ms, 5),
                      "flop_per_launch": kern_flop, "traffic": load_traffic(kern_label)},
     }
+    out["pcie_inclusive"] = time_pcie_inclusive(eng, x, args.steps, args.warmup, world)
     del eng
     torch.cuda.empty_cache()
     if not args.no_train:
@@ -260,8 +290,8 @@ def main():
         out["train"] = {"metric": "training images/sec (stage-1 L1 generator step) at batch 32/GPU",
                         "value": round(B * world * args.train_steps / tt, 2),
                         "ms_per_step": round(1000.0 * tt / args.train_steps, 3), "steps": args.train_steps,
-                        "loss": float(teng.loss), "allreduce": "RCCL (torch.distributed nccl backend), 8 buckets, "
-                                                               "overlapped with backward" if world > 1 else "none"}
+                        "loss": float(teng.loss), "allreduce": (("RCCL (torch.distributed nccl backend)" if backend == "nccl" else backend)
+                                      + ", 8 buckets, overlapped with backward") if world > 1 else "none"}
         del teng
         torch.cuda.empty_cache()
         if not args.no_perceptual:
