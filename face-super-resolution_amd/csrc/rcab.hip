@@ -246,7 +246,17 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     const int twn = W >> 4, tpi = twn * (H >> 4);
     const int ntiles = B * tpi;
     const int nslot = gridDim.x;
-    const int nmine = (ntiles - (int)blockIdx.x + nslot - 1) / nslot;
+    // XCD-aware slot: blocks b and b + 8 share an XCD (round-robin dispatch, observed), so
+    // slot = (b % 8) * (nslot / 8) + b / 8 puts an image's tiles -- consecutive slots -- on
+    // one XCD: neighbouring tiles' halo rows and the apply's re-read of x come from that
+    // XCD's L2 instead of another die's copy.  Any permutation is correct (all blocks are
+    // co-resident); the mapping only moves traffic.
+#ifndef RCAB_NO_XCD
+    const int slot = (nslot & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nslot >> 3) + ((int)blockIdx.x >> 3);
+#else
+    const int slot = (int)blockIdx.x;
+#endif
+    const int nmine = (ntiles - slot + nslot - 1) / nslot;
     // workspace (fen_rcab_workspace_alloc: uncached, so every access of the cross-block
     // hand-off goes to memory -- the per-XCD L2s are not coherent):
     //   part  [tpi][B][64]  tile partial sums, image-interleaved so that one image's rows
@@ -331,7 +341,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     if (tid == 0) st_flag(sflag + blockIdx.x, ep1);
     RSTAMP(0);
     issue_taps(0);
-    issue_halo(blockIdx.x);
+    issue_halo(slot);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -516,7 +526,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 
 #pragma unroll 1
     for (int k = 0; k < nmine; ++k) {
-        const int t = (int)blockIdx.x + k * nslot;
+        const int t = slot + k * nslot;
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         f32x4 acc1[2][6];
