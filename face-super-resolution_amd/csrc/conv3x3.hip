@@ -551,8 +551,13 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
     const int H = d.H, W = d.W, Cout = d.Cout;
     const int coutp = (Cout + 15) & ~15;
     const int ncot = coutp / COT;
-    const int cot = blockIdx.x % ncot, co0 = cot * COT;
-    const int nslot = gridDim.x / ncot, slot = blockIdx.x / ncot;
+#ifndef CONV_NO_XCD
+    const int bid = xcd_block();                             // a tile's co blocks + neighbours: one XCD
+#else
+    const int bid = (int)blockIdx.x;
+#endif
+    const int cot = bid % ncot, co0 = cot * COT;
+    const int nslot = gridDim.x / ncot, slot = bid / ncot;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
     const int ntiles = d.B * tpi;
 
@@ -670,8 +675,13 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, Cout = d.Cout;
     const int ncot = Cout >> 6;
-    const int cot = blockIdx.x % ncot, co0 = cot * 64;
-    const int nslot = gridDim.x / ncot, slot = blockIdx.x / ncot;
+#ifndef CONV_NO_XCD
+    const int bid = xcd_block();                             // a tile's co blocks + neighbours: one XCD
+#else
+    const int bid = (int)blockIdx.x;
+#endif
+    const int cot = bid % ncot, co0 = cot * 64;
+    const int nslot = gridDim.x / ncot, slot = bid / ncot;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
     const int ntiles = d.B * tpi;
     const int nmine = (ntiles - slot + nslot - 1) / nslot;    // tiles of this block (>= 1)

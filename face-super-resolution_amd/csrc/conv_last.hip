@@ -51,7 +51,12 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
     const int Hs = H >> 2, Ws = W >> 2;
     const int twn = W >> 4, tpi = twn * (H >> 4), ntiles = B * tpi;
     const int G = gridDim.x;
-    const int nmine = (ntiles - (int)blockIdx.x + G - 1) / G;
+#ifndef CONV_NO_XCD
+    const int slot = xcd_block();                     // neighbouring tiles on one XCD (shared halo rows)
+#else
+    const int slot = (int)blockIdx.x;
+#endif
+    const int nmine = (ntiles - slot + G - 1) / G;
     constexpr bool train = TRAIN;
     float* red = (float*)(smem + O_RED);
 
@@ -79,7 +84,7 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
         }
     }
     auto issue = [&](int i) {                     // everything my i-th tile reads -> slot i % NS
-        const int t = (int)blockIdx.x + i * G;
+        const int t = slot + i * G;
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const int sl = i % NS;
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
 #ifdef CL_DIAG_NOCOMPUTE
         continue;
 #endif
-        const int t = (int)blockIdx.x + i * G;
+        const int t = slot + i * G;
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const int sl = i % NS;
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
         float s = 0.f;
 #pragma unroll
         for (int w = 0; w < NCW; ++w) s += rp[w];
-        d.loss_part[(int)blockIdx.x + (nmine - 1) * G] = s;
+        d.loss_part[slot + (nmine - 1) * G] = s;
     }
 }
 

@@ -19,6 +19,15 @@ template <> struct Tr<bf16>  { static constexpr int CK = 64; static constexpr in
 // Byte offset of 16-B chunk `chunk` (0..7) of row `p` in a 128-B-row LDS image.  The XOR
 // key (p>>1)&7 puts 16 consecutive rows read at the same chunk on 16 distinct 16-B slots
 // of the 256-B bank row, so ds_read_b128 fragment reads are conflict-free.
+// XCD-aware block index of a 1-D grid: blocks b and b + 8 share an XCD (round-robin dispatch,
+// observed -- MI355X_MICROARCH.md, workgroup dispatch), so b -> (b % 8) * (n / 8) + b / 8 gives
+// consecutive logical indices -- neighbouring tiles, or the output-channel blocks of one tile --
+// one XCD and its L2.  Identity when n is not a multiple of 8.  A permutation: it moves
+// traffic, never results.
+__device__ __forceinline__ int xcd_block() {
+    const int b = (int)blockIdx.x, n = (int)gridDim.x;
+    return (n & 7) ? b : (b & 7) * (n >> 3) + (b >> 3);
+}
 __device__ __forceinline__ int swz(int p, int chunk) {
     return (p << 7) + ((chunk ^ ((p >> 1) & 7)) << 4);
 }

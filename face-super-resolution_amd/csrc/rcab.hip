@@ -252,7 +252,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     // XCD's L2 instead of another die's copy.  Any permutation is correct (all blocks are
     // co-resident); the mapping only moves traffic.
 #ifndef RCAB_NO_XCD
-    const int slot = (nslot & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nslot >> 3) + ((int)blockIdx.x >> 3);
+    const int slot = xcd_block();
 #else
     const int slot = (int)blockIdx.x;
 #endif
