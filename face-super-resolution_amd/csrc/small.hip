@@ -1031,8 +1031,14 @@ extern "C" int fen_se_fused(int dtype, int B, int HW, int C, int Cr, int nparts,
     return FEN_OK;
 }
 
+// pixels per pool_dot block: 64 (HW = 4096 -> 64 chunks x B images = 2048 blocks, ~32 waves
+// per CU in flight; 256 px per block left 8 waves per CU and measured 11.7 us per SE backward
+// pool inside the training step)
+#ifndef POOL_PIX
+#define POOL_PIX 64
+#endif
 extern "C" size_t fen_pool_parts(int HW) {
-    int n = HW / 256;
+    int n = HW / POOL_PIX;
     if (n < 1) n = 1;
     if (n > 64) n = 64;
     return (size_t)n;

@@ -30,7 +30,7 @@ def test_status_strings_and_pure_queries():
     assert b"gfx950" in lib.fen_build_info()
     assert lib.fen_packed_elems(0, 3, 64) == 9 * 16 * 64
     assert lib.fen_packed_elems(2, 256, 64) == 9 * 64 * 256
-    assert lib.fen_pool_parts(4096) == 16
+    assert lib.fen_pool_parts(4096) == 64
     assert lib.fen_sumsq_parts(5115651) == 1024
 
 
