@@ -602,13 +602,31 @@ __global__ __launch_bounds__(256) void k_pool_dot(int HW, int C, int nchunk, con
     }
 }
 
-// SE backward for one image (block per b)
+constexpr int SE_STAGE_MAX = 4096;   // FC weights staged in LDS up to C * Cr floats each
+
+// SE backward for one image (block per b).  Every operand the chain needs (s, hid, mean and,
+// when they fit, both FC weights) is requested up front beside the pool partials and staged in
+// LDS, so the dependent steps (sigmoid', FC2^T + ReLU', the weight-gradient rows, FC1^T) run
+// on LDS instead of paying one global round trip each.
+template <bool STAGE>
 __global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, const float* __restrict__ part,
                          const float* __restrict__ mean, const float* __restrict__ hid, const float* __restrict__ s,
                          const float* __restrict__ w1, const float* __restrict__ w2, float* g, float* dw1p,
                          float* dw2p) {
-    __shared__ float dz[512], dh[128], pr[4][256];
+    __shared__ float dz[512], dh[128], pr[4][256], ssv[512], smean[512], shid[128];
+    __shared__ float sw1[STAGE ? SE_STAGE_MAX : 1], sw2[STAGE ? SE_STAGE_MAX : 1];
     const int b = blockIdx.x, t = threadIdx.x;
+    for (int c = t; c < C; c += blockDim.x) {
+        ssv[c] = s[(size_t)b * C + c];
+        smean[c] = mean[(size_t)b * C + c];
+    }
+    for (int j = t; j < Cr; j += blockDim.x) shid[j] = hid[(size_t)b * Cr + j];
+    if constexpr (STAGE) {
+        for (int i = t; i < C * Cr; i += blockDim.x) {
+            sw1[i] = w1[i];
+            sw2[i] = w2[i];
+        }
+    }
     // pool partials: thread (c, quarter) sums every 4th part (independent loads in flight),
     // fixed-order combine of the quarters (deterministic)
     for (int c0 = 0; c0 < C; c0 += 64) {
@@ -623,7 +641,7 @@ __global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, cons
     __syncthreads();
     for (int c = t; c < C; c += blockDim.x) {
         const float a = (pr[0][c] + pr[1][c]) + (pr[2][c] + pr[3][c]);
-        const float sv = s[(size_t)b * C + c];
+        const float sv = ssv[c];
         dz[c] = a * rs * sv * (1.f - sv);                 // through sigmoid
     }
     __syncthreads();
@@ -631,21 +649,21 @@ __global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, cons
         const int lane = t & 63, nw = blockDim.x >> 6;
         for (int j = t >> 6; j < Cr; j += nw) {
             float a = 0.f;
-            for (int c = lane; c < C; c += 64) a += w2[(size_t)c * Cr + j] * dz[c];
+            for (int c = lane; c < C; c += 64) a += (STAGE ? sw2[c * Cr + j] : w2[(size_t)c * Cr + j]) * dz[c];
             a = wave_sum(a);
-            if (lane == 0) dh[j] = hid[(size_t)b * Cr + j] > 0.f ? a : 0.f;   // through ReLU
+            if (lane == 0) dh[j] = shid[j] > 0.f ? a : 0.f;   // through ReLU
         }
     }
     __syncthreads();
     for (int i = t; i < C * Cr; i += blockDim.x) {
         const int c = i / Cr, j = i % Cr;
-        dw2p[(size_t)b * C * Cr + i] = dz[c] * hid[(size_t)b * Cr + j];          // [C][Cr]
+        dw2p[(size_t)b * C * Cr + i] = dz[c] * shid[j];                        // [C][Cr]
         const int jj = i / C, cc = i % C;
-        dw1p[(size_t)b * C * Cr + i] = dh[jj] * mean[(size_t)b * C + cc];        // [Cr][C]
+        dw1p[(size_t)b * C * Cr + i] = dh[jj] * smean[cc];                      // [Cr][C]
     }
     for (int c = t; c < C; c += blockDim.x) {
         float a = 0.f;
-        for (int j = 0; j < Cr; ++j) a += w1[(size_t)j * C + c] * dh[j];
+        for (int j = 0; j < Cr; ++j) a += (STAGE ? sw1[j * C + c] : w1[(size_t)j * C + c]) * dh[j];
         g[(size_t)b * C + c] = a * inv_hw;
     }
 }
@@ -1063,8 +1081,12 @@ extern "C" int fen_se_bwd(int B, int C, int Cr, int nparts, float inv_hw, float 
                           const float* mean, const float* hid, const float* s, const float* w1, const float* w2,
                           float* g, float* dw1p, float* dw2p, void* stream) {
     if (!part || !mean || !hid || !s || !w1 || !w2 || !g || !dw1p || !dw2p || C > 512 || Cr > 128) return FEN_EINVAL;
-    hipLaunchKernelGGL(k_se_bwd, dim3(B), dim3(256), 0, STREAM, C, Cr, nparts, inv_hw, res_scale, part, mean, hid, s,
-                       w1, w2, g, dw1p, dw2p);
+    if (C * Cr <= SE_STAGE_MAX)
+        hipLaunchKernelGGL(k_se_bwd<true>, dim3(B), dim3(256), 0, STREAM, C, Cr, nparts, inv_hw, res_scale, part, mean,
+                           hid, s, w1, w2, g, dw1p, dw2p);
+    else
+        hipLaunchKernelGGL(k_se_bwd<false>, dim3(B), dim3(256), 0, STREAM, C, Cr, nparts, inv_hw, res_scale, part, mean,
+                           hid, s, w1, w2, g, dw1p, dw2p);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
