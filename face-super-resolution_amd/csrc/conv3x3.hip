@@ -909,7 +909,12 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
-    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
+#ifndef CONV_NO_XCD
+    const int tb = xcd_block();                // neighbouring tiles on one XCD (halo rows in its L2)
+#else
+    const int tb = (int)blockIdx.x;
+#endif
+    const int b = tb / tpi, tile = tb - b * tpi;
     const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
     const int co0 = blockIdx.y * COT;
     const int coutp = (Cout + 15) & ~15;
@@ -976,7 +981,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     }
     float* red = (float*)wbuf;     // LDS is free after the loop
     char* stage = (sizeof(T) == 2 && COT == 64) ? halo : nullptr;
-    conv_epilogue<T, COT, 4, 1>(d, acc, b, blockIdx.x, h0, w0, co0, stage, red, ec);
+    conv_epilogue<T, COT, 4, 1>(d, acc, b, tb, h0, w0, co0, stage, red, ec);
 }
 
 int g_num_cus = 0;
