@@ -33,6 +33,12 @@ if world == 1:
     eng.capture()
     print("graph replay ms", round(t(eng.replay), 3), flush=True)
 else:
+    from src.training import dp as DP
+    orig = DP.BucketExchange.launch
+    DP.BucketExchange.launch = lambda self, tag: None
+    print("eager step, exchange off, ms", round(t(eng.step), 3), flush=True)
+    DP.BucketExchange.launch = orig
+    import torch.distributed as dist_
     flat = eng.flat_g
     print("bare all_reduce of arena ms", round(t(lambda: dist.all_reduce(flat)), 3), flat.numel(), flush=True)
     dist.destroy_process_group()
