@@ -319,7 +319,12 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         }
     };
 
-    // ---- start-up: constants, SE weights, first taps, first halo
+    // ---- start-up: first taps + first halo (LDS-DMA) go out before anything waits on memory;
+    //      then constants, SE weights and the epoch read, whose round trips overlap the DMA
+#ifndef RCAB_OLD_PROLOGUE
+    issue_taps(0);
+    issue_halo(slot);
+#endif
     if (tid < 64) {
         cst[tid] = d.b1[tid];
         cst[64 + tid] = d.alpha[tid];
@@ -340,8 +345,10 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     const int ep1 = __builtin_amdgcn_readfirstlane(ld_poll(epoch)) + 1;
     if (tid == 0) st_flag(sflag + blockIdx.x, ep1);
     RSTAMP(0);
+#ifdef RCAB_OLD_PROLOGUE
     issue_taps(0);
     issue_halo(slot);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
