@@ -721,13 +721,20 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wts + i * 1024), 16,
                                                      ((tap * Cout + co0 + col) * 64 + c * 8) * 2, 0, 0, 0);
         }
+#ifndef CONV_OLD_PROLOGUE
+        // the halo DMA goes out before the constant loads: their LDS writes wait for vmcnt,
+        // which counts in issue order -- placed first, wave 0's halo share waited for the slab
+        if (grp == 0) issue_halo(tile_of(0, 0));
+#endif
         if (tid < 64) {
             const int cp = co0 + tid, Cq = Cout >> 2;
             const int co = SHUF ? 4 * (cp % Cq) + cp / Cq : cp;
             cst[tid] = (EPI & FEN_EPI_BIAS) ? d.bias[co] : 0.f;
             cst[64 + tid] = (PRELU || PBWD) ? d.alpha[SHUF ? cp % Cq : cp] : 0.f;
         }
+#ifdef CONV_OLD_PROLOGUE
         if (grp == 0) issue_halo(tile_of(0, 0));
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
