@@ -614,7 +614,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) a[r] = prelu_f(zs[m][f][r], alp[r]);
                         st_out4((char*)d.z1 + o * 2, zs[m][f]);
+#ifdef RCAB_A1_MASKED
                         st_out4((char*)d.a1 + o * 2, a);
+#endif
                     }
                 }
             }
@@ -674,6 +676,22 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         __builtin_amdgcn_sched_barrier(0);
 #endif
         if (k == 1) RSTAMP(39);
+#ifndef RCAB_A1_MASKED
+        if (d.a1) {
+            // training copy of a1: the tile's 16x16 interior straight from the a1 image in LDS
+            // (complete since the phase-3 barrier), 16-B lanes over whole 2-KB pixel rows, instead
+            // of exec-masked 8-B fragment stores from the conv1 epilogue.  Issued before the
+            // halo DMA so phase 4's vmcnt(#halo pieces) still leaves only the halo in flight.
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int idx = j * 512 + tid, px = idx >> 3, c = idx & 7;
+                const int ar = 1 + (px >> 4), ac = 1 + (px & 15);
+                const uint4 v = *(const uint4*)(a1s + (ar * A1W + ac) * 128 + ((c ^ (ac & 7)) << 4));
+                const size_t o = ((size_t)(b * H + h0 + (px >> 4)) * W + w0 + (px & 15)) * 128 + c * 16;
+                *(uint4*)((char*)d.a1 + o) = v;
+            }
+        }
+#endif
         const bool halo_next = k + 1 < nmine;
         if (halo_next) issue_halo(t + nslot);       // conv1 is done with xh / eh
         if (k == 1) RSTAMP(40);
