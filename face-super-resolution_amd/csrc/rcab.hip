@@ -613,12 +613,34 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                         float a[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) a[r] = prelu_f(zs[m][f][r], alp[r]);
+#ifndef RCAB_Z1_LDS
                         st_out4((char*)d.z1 + o * 2, zs[m][f]);
+#else
+                        (void)o;
+#endif
 #ifdef RCAB_A1_MASKED
                         st_out4((char*)d.a1 + o * 2, a);
 #endif
                     }
                 }
+#ifdef RCAB_Z1_LDS
+                // (opt-in, RCAB_Z1_LDS: measured neutral -- the extra barrier costs what the
+                // coalesced copy saves) z1 interior -> the x-halo buffer (free once every wave is
+                // past conv1: one extra barrier), [16x16 px][8 chunks] with the column-keyed chunk
+                // swizzle; copied out as whole pixel rows after the phase-3 barrier
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int f = 0; f < 6; ++f) {
+                        const int ar = f < 4 ? row0 + f : f == 4 ? ar4 : ar5;
+                        const int ac = f < 4 ? c16 : f == 4 ? ac4 : ac5;
+                        if (!(f < 5 || has5) || ar < 1 || ar > 16 || ac < 1 || ac > 16) continue;
+                        const int zc = ac - 1, chunk = ch * 4 + 2 * m + (q >> 1);
+                        st4<bf16>(xh + ((ar - 1) * 16 + zc) * 128 + ((chunk ^ (zc & 7)) << 4) + (q & 1) * 8, zs[m][f]);
+                    }
+#endif
             }
         }
         // the pending tile's gate (its round ended a conv1 ago): wave 0 -> LDS (RCAB_XPRE:
@@ -676,6 +698,20 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
         __builtin_amdgcn_sched_barrier(0);
 #endif
         if (k == 1) RSTAMP(39);
+#ifdef RCAB_Z1_LDS
+        if (d.z1) {
+            // z1 out of the x-halo buffer: wave w copies exactly the 1-KB pieces it refills by
+            // DMA below (i = w, w + 8, ..), so no other wave's halo DMA can overwrite a piece
+            // before its copy has read it; 64 lanes = 8 whole pixels (1 KB contiguous)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int px = (wave + 8 * j) * 8 + (lane >> 3), c = lane & 7, zc = px & 15;
+                const uint4 v = *(const uint4*)(xh + px * 128 + ((c ^ (zc & 7)) << 4));
+                const size_t o = ((size_t)(b * H + h0 + (px >> 4)) * W + w0 + zc) * 128 + c * 16;
+                *(uint4*)((char*)d.z1 + o) = v;
+            }
+        }
+#endif
 #ifndef RCAB_A1_MASKED
         if (d.a1) {
             // training copy of a1: the tile's 16x16 interior straight from the a1 image in LDS
