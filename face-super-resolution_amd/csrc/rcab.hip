@@ -519,6 +519,29 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
             const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
+#ifndef RCAB_APPLY_NOSHFL
+            // lanes q and q ^ 1 (16 lanes apart) trade one 4-channel half: the even lane stores
+            // m = 0 channels 4q..4q+7, the odd lane m = 1 channels 4(q-1)..4q+3, as 16-B stores
+            // (64 contiguous bytes per pixel per instruction instead of 32)
+            uint2 pk[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                float o[4];
+                o[0] = __uint_as_float(tcar[m][n].x << 16) * sv[m][0] + __uint_as_float(xf[m][n].x << 16);
+                o[1] = __uint_as_float(tcar[m][n].x & 0xffff0000u) * sv[m][1] + __uint_as_float(xf[m][n].x & 0xffff0000u);
+                o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xf[m][n].y << 16);
+                o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xf[m][n].y & 0xffff0000u);
+                pk[m].x = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+                pk[m].y = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+            }
+            const bool odd = q & 1;
+            const uint2 snd = odd ? pk[0] : pk[1];
+            uint2 rcv;
+            rcv.x = (unsigned)__shfl_xor((int)snd.x, 16, 64);
+            rcv.y = (unsigned)__shfl_xor((int)snd.y, 16, 64);
+            const uint4 v = odd ? make_uint4(rcv.x, rcv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, rcv.x, rcv.y);
+            st_out16((char*)d.y + (px * 64 + wc * 32 + (odd ? 16 + 4 * (q - 1) : 4 * q)) * 2, v);
+#else
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 float o[4];
@@ -528,6 +551,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                 o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xf[m][n].y & 0xffff0000u);
                 st_out4((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
             }
+#endif
         }
     };
 
