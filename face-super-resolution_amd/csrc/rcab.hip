@@ -496,6 +496,33 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     };
     // (!PARK) y = t * s * rs + x in the MFMA fragment layout (t in tcar)
     uint2 xf[2][4];
+#ifndef RCAB_XLOAD_NOSHFL
+    // x as 16-B loads in the paired-lane layout of the y stores (even lane q: m = 0 channels
+    // 4q..4q+7, odd: m = 1 channels 4(q-1)..4q+3); apply_frag trades the halves back
+    uint4 xr[4];
+    auto load_x_frag = [&](int pt) {
+        const int b = pt / tpi, tile = pt - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
+            xr[n] = *(const uint4*)((const char*)d.x + (px * 64 + wc * 32 + ((q & 1) ? 16 + 4 * (q - 1) : 4 * q)) * 2);
+        }
+    };
+    auto unpair_x = [&]() {
+        const bool odd = q & 1;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint2 lo = make_uint2(xr[n].x, xr[n].y), hi = make_uint2(xr[n].z, xr[n].w);
+            const uint2 snd = odd ? lo : hi;
+            uint2 rcv;
+            rcv.x = (unsigned)__shfl_xor((int)snd.x, 16, 64);
+            rcv.y = (unsigned)__shfl_xor((int)snd.y, 16, 64);
+            xf[0][n] = odd ? rcv : lo;
+            xf[1][n] = odd ? hi : rcv;
+        }
+    };
+#else
     auto load_x_frag = [&](int pt) {
         const int b = pt / tpi, tile = pt - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
@@ -506,10 +533,13 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             for (int m = 0; m < 2; ++m) xf[m][n] = *(const uint2*)((const char*)d.x + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2);
         }
     };
+    auto unpair_x = [&]() {};
+#endif
     auto apply_frag = [&](int pt) {
         const int b = pt / tpi, tile = pt - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const float rs = d.res_scale;
+        unpair_x();
         float sv[2][4];
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
@@ -799,13 +829,36 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                     acc2[m][n][r] += bia[r];
                     ps[m][r] += acc2[m][n][r];
                 }
+#ifdef RCAB_PARK_NOSHFL
                 if constexpr (PARK) {
                     const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
                     float v[4] = {acc2[m][n][0], acc2[m][n][1], acc2[m][n][2], acc2[m][n][3]};
                     st4<bf16>((char*)tpark + o * 2, v);
                 }
+#endif
             }
         }
+#ifndef RCAB_PARK_NOSHFL
+        if constexpr (PARK) {                         // t parked with the paired-lane 16-B stores
+            const bool odd = q & 1;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                uint2 pk[2];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    pk[m].x = (unsigned)f2bf(acc2[m][n][0]) | ((unsigned)f2bf(acc2[m][n][1]) << 16);
+                    pk[m].y = (unsigned)f2bf(acc2[m][n][2]) | ((unsigned)f2bf(acc2[m][n][3]) << 16);
+                }
+                const uint2 snd = odd ? pk[0] : pk[1];
+                uint2 rcv;
+                rcv.x = (unsigned)__shfl_xor((int)snd.x, 16, 64);
+                rcv.y = (unsigned)__shfl_xor((int)snd.y, 16, 64);
+                const uint4 v = odd ? make_uint4(rcv.x, rcv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, rcv.x, rcv.y);
+                const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
+                *(uint4*)((char*)tpark + (px * 64 + wc * 32 + (odd ? 16 + 4 * (q - 1) : 4 * q)) * 2) = v;
+            }
+        }
+#endif
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
