@@ -652,6 +652,32 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                     if (f < 5 || has5) st4<bf16>(a1s + off, a);
                 }
             }
+#if !defined(RCAB_Z1_LDS) && !defined(RCAB_A1_MASKED) && !defined(RCAB_Z1_NOSHFL)
+            if (d.z1) {
+                // interior pixels only (a1 rows / cols 1..16), training only: lanes q and q^1
+                // (same pixel) trade one 4-channel half so each store is 16 B (see apply_frag)
+                const bool odd = q & 1;
+#pragma unroll
+                for (int f = 0; f < 6; ++f) {
+                    uint2 pk[2];
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {
+                        pk[m].x = (unsigned)f2bf(zs[m][f][0]) | ((unsigned)f2bf(zs[m][f][1]) << 16);
+                        pk[m].y = (unsigned)f2bf(zs[m][f][2]) | ((unsigned)f2bf(zs[m][f][3]) << 16);
+                    }
+                    const uint2 snd = odd ? pk[0] : pk[1];
+                    uint2 rcv;
+                    rcv.x = (unsigned)__shfl_xor((int)snd.x, 16, 64);
+                    rcv.y = (unsigned)__shfl_xor((int)snd.y, 16, 64);
+                    const int ar = f < 4 ? row0 + f : f == 4 ? ar4 : ar5;
+                    const int ac = f < 4 ? c16 : f == 4 ? ac4 : ac5;
+                    if (!(f < 5 || has5) || ar < 1 || ar > 16 || ac < 1 || ac > 16) continue;
+                    const uint4 v = odd ? make_uint4(rcv.x, rcv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, rcv.x, rcv.y);
+                    const size_t o = ((size_t)(b * H + h0 - 1 + ar) * W + w0 - 1 + ac) * 64 + ch * 32 + (odd ? 16 + 4 * (q - 1) : 4 * q);
+                    *(uint4*)((char*)d.z1 + o * 2) = v;
+                }
+            }
+#else
             if (d.z1) {
                 // interior pixels only (a1 rows / cols 1..16); exec-masked stores, training only
 #pragma unroll
@@ -696,6 +722,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                     }
 #endif
             }
+#endif
         }
         // the pending tile's gate (its round ended a conv1 ago): wave 0 -> LDS (RCAB_XPRE:
         // its residual loads go out first, in flight during the gate; costs registers)
