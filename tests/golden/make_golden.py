@@ -16,8 +16,12 @@ Fixtures:
                   (fp32, and the eval output of the reference run in float64).
   g5_c128.npz     128-ch 10x20 x8 variant, B=1, 16x16 input: init statistics + output.
   g6_lite.npz     FaceEnhanceNetLite (C=32, r=2), B=1, 16x16 input: output.
+  g9_full64.npz   full 6x10 network at the north-star shape: B=2, smooth uint8 HR 256x256
+                  (tests/golden/smooth.py, seed 11) -> LR 64x64 by the reference's own
+                  bicubic /4; init statistics, eval/train outputs, the eval output of the
+                  reference run in float64, and its PSNR vs HR (trainer.py:621-628).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [g1 g2 ... g9]
 """
 import os
 import sys
@@ -166,13 +170,41 @@ def g_net(fname, ctor, x_shape, seed_x):
     np.savez_compressed(os.path.join(OUT, fname), **d)
 
 
+def g9():
+    sys.path.insert(0, OUT)
+    from smooth import smooth_images_u8
+    torch.manual_seed(0)
+    model = FaceEnhanceNet(num_channels=64, num_groups=6, blocks_per_group=10, reduction_ratio=4, scale_factor=4)
+    d = init_stats(model)
+    perturb_conv_last(model, 1)
+    hr_u8 = smooth_images_u8(2, 256, 256, 11)
+    hr = torch.from_numpy(hr_u8.astype(np.float32) / np.float32(255.0))
+    lr = F.interpolate(hr, scale_factor=0.25, mode="bicubic", align_corners=False)   # trainer.py:416-421
+    d["hr_u8"], d["lr"] = hr_u8, lr.numpy()
+    with torch.no_grad():
+        model.eval()
+        d["out_eval"] = model(lr).numpy()
+        model.train()
+        d["out_train"] = model(lr).numpy()
+        model.double().eval()
+        f64 = model(lr.double())
+        d["out_eval_f64"] = f64.float().numpy()
+        mse = torch.mean((f64 - hr.double()) ** 2)
+        d["psnr_eval_f64"] = np.array(float(10.0 * torch.log10(1.0 / mse)))
+    np.savez_compressed(os.path.join(OUT, "g9_full64.npz"), **d)
+
+
+ALL = {
+    "g1": g1, "g2": g2, "g3": g3,
+    "g4": lambda: g_net("g4_full.npz", lambda: FaceEnhanceNet(num_channels=64, num_groups=6, blocks_per_group=10,
+                                                              reduction_ratio=4, scale_factor=4), (1, 3, 32, 32), 4),
+    "g5": lambda: g_net("g5_c128.npz", lambda: FaceEnhanceNet(num_channels=128, num_groups=10, blocks_per_group=20,
+                                                              reduction_ratio=4, scale_factor=8), (1, 3, 16, 16), 6),
+    "g6": lambda: g_net("g6_lite.npz", lambda: FaceEnhanceNetLite(), (1, 3, 16, 16), 7),
+    "g9": g9,
+}
+
 if __name__ == "__main__":
-    g1()
-    g2()
-    g3()
-    g_net("g4_full.npz", lambda: FaceEnhanceNet(num_channels=64, num_groups=6, blocks_per_group=10,
-                                                reduction_ratio=4, scale_factor=4), (1, 3, 32, 32), 4)
-    g_net("g5_c128.npz", lambda: FaceEnhanceNet(num_channels=128, num_groups=10, blocks_per_group=20,
-                                                reduction_ratio=4, scale_factor=8), (1, 3, 16, 16), 6)
-    g_net("g6_lite.npz", lambda: FaceEnhanceNetLite(), (1, 3, 16, 16), 7)
+    for name in (sys.argv[1:] or list(ALL)):
+        ALL[name]()
     print("golden fixtures written to", OUT)

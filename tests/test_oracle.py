@@ -78,3 +78,21 @@ def test_config1_grads_and_step(golden):
     assert abs(loss2 - float(g["step_loss"])) < 1e-6
     for k, v in newp.items():
         np.testing.assert_allclose(v.numpy(), g["s/" + k], rtol=0, atol=2e-7, err_msg=k)
+
+
+def test_g9_north_star_shape(golden):
+    """The oracle at the north-star shape (6x10, 64x64 -> 256x256, B=2, smooth HR) vs the
+    reference's own fp32 outputs and its float64 PSNR."""
+    import math
+    from src_models_seed import seeded_full_params
+    g = golden("g9_full64.npz")
+    p = seeded_full_params(g)
+    shape = O.NetShape(64, 6, 10, 4, 4, 0.2)
+    hr = torch.from_numpy(g["hr_u8"].astype(np.float32) / np.float32(255.0))
+    lr = O.lr_from_hr(hr)
+    np.testing.assert_allclose(lr.numpy(), g["lr"], rtol=0, atol=2e-6)
+    out_e = O.forward(p, torch.from_numpy(g["lr"]), shape, training=False)
+    out_t = O.forward(p, torch.from_numpy(g["lr"]), shape, training=True)
+    np.testing.assert_allclose(out_e.numpy(), g["out_eval"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(out_t.numpy(), g["out_train"], rtol=0, atol=1e-5)
+    assert math.isclose(O.psnr(out_e, hr), float(g["psnr_eval_f64"]), abs_tol=1e-4)
