@@ -6,18 +6,18 @@
 //
 // Output tile = 16x16 pixels x COT output channels, 4 waves; each wave owns 4 output rows:
 //   D[co][px] = sum_k W[co][k] * X[k][px],  k = (tap, ci):  A = weights, B = pixels,
-//   MT*4 accumulators of v_mfma_f32_16x16x32_bf16 (or 4x v_mfma_f32_16x16x4_f32 per 16 B).
-// Every LDS image has 128-B rows (64 bf16 / 32 f32 channels = one "panel") with the
+//   MT*4 accumulators of v_mfma_f32_16x16x32_{bf16,f16} (or 4x v_mfma_f32_16x16x4_f32 per 16 B).
+// Every LDS image has 128-B rows (64 bf16/fp16 / 32 f32 channels = one "panel") with the
 // 16-B chunks XOR-swizzled by (row>>1)&7 -> conflict-free ds_read_b128 fragment reads.
 //
 // Two kernels:
-//  * k_conv3x3_p (bf16, Cin == 64 -- every 64-channel conv of the network, forward and
+//  * k_conv3x3_p (bf16 / fp16, Cin == 64 -- every 64-channel conv of the network, forward and
 //    dgrad, the x2 upsampler and conv_last): PERSISTENT, one 256-thread block per CU.
 //    The block's whole filter (9 taps x COT x 64, 72 KB) stays resident in LDS; the
 //    18x18-pixel input halo of the next tile is streamed by LDS-DMA (buffer_load ... lds,
 //    zero padding via the buffer range check) into a second buffer while the MFMAs run
 //    on the current one: one barrier per tile, none per tap.  156.7 KB LDS.
-//  * k_conv3x3_s (any Cin multiple of the panel, bf16 and f32): weights streamed per tap
+//  * k_conv3x3_s (any Cin multiple of the panel, bf16 / fp16 and f32): weights streamed per tap
 //    through a double-buffered LDS tile, halo staged through registers; 2 blocks per CU.
 //    Used for f32 (the parity path) and for Cin > 64 (upsampler dgrad, 128-ch variant).
 // The epilogue fuses bias, residual adds, PReLU (fwd) or PReLU-backward (dgrad),
@@ -107,7 +107,7 @@ __device__ __forceinline__ EpiConst<MT> epi_consts(const fen_conv_desc& d, int c
 
 // ------------------------------------------------------------------------------------
 // epilogue (shared by both kernels).  acc[m][n][r] = D[co = co0 + m*16 + 4q + r][pixel
-// (h0 + wave*4 + n, w0 + c16)].  `stage` (>= 32 KB LDS) enables the bf16 LDS-staged
+// (h0 + wave*4 + n, w0 + c16)].  `stage` (>= 32 KB LDS) enables the 16-bit LDS-staged
 // store path (COT == 64 only); `red` is >= 4*COT floats of LDS.  Contains barriers:
 // every thread of the block must call it.
 // ------------------------------------------------------------------------------------
@@ -272,7 +272,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
 
     if (stage != nullptr) {
         if constexpr (sizeof(T) == 2 && COT == 64) {
-            // ---- bf16: stage the 256 x 64 tile in LDS, leave as full 128-B rows ----
+            // ---- 16-bit: stage the 256 x 64 tile in LDS, leave as full 128-B rows ----
             int nst = 0;
             for (int k = 0; k < 2; ++k) {
                 void* dst = k == 0 ? d.y_pre : d.y;
@@ -287,7 +287,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                         float v[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) v[r] = final_v(acc[m][n][r], m, r, k);
-                        st4<bf16>(stage + swz(px, cl >> 3) + (q & 1) * 8, v);
+                        st4<T>(stage + swz(px, cl >> 3) + (q & 1) * 8, v);
                     }
                 }
                 epi_barrier<RAW>();
@@ -397,7 +397,7 @@ __device__ __forceinline__ void conv_tap(f32x4 (&acc)[MT][NT], const char* wt, c
 // All 9 taps x 2 k-halves of one tile from an LDS-resident filter, software-pipelined:
 // the fragments of step s+1 are read while the MFMAs of step s run (two register sets).
 // per_tap(tap) runs once per tap between the MFMA groups (the next tile's halo DMA).
-template <int COT, int MT, int NT, typename F>
+template <typename T, int COT, int MT, int NT, typename F>
 __device__ __forceinline__ void conv_tile_resident(f32x4 (&acc)[MT][NT], const char* wts, const char* halo, int wr,
                                                    int wc, int q, int c16, F&& per_tap) {
     uint4 A0[MT], B0[NT], A1[MT], B1[NT];
@@ -416,7 +416,7 @@ __device__ __forceinline__ void conv_tile_resident(f32x4 (&acc)[MT][NT], const c
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], A[m], Bf[n]);
+            for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A[m], Bf[n]);
     };
     // sched_barriers pin the order: each fragment set is read one MFMA group ahead of its use
     load(0, 0, A0, B0);
@@ -440,7 +440,7 @@ __device__ __forceinline__ void conv_tile_resident(f32x4 (&acc)[MT][NT], const c
 // once and applies them to all three kh taps (output row n uses halo row n + kh), so one
 // group = NT+2 pixel fragments + 3*MT filter fragments for 3*MT*NT MFMAs -- 0.5 LDS reads
 // per MFMA at MT=2, NT=4 (tap order: 0.75).  Double-buffered one group ahead.
-template <int COT, int MT, int NT>
+template <typename T, int COT, int MT, int NT>
 __device__ __forceinline__ void conv_tile_rows(f32x4 (&acc)[MT][NT], const char* wts, const char* halo, int wr,
                                                int wc, int q, int c16) {
     constexpr int NB = NT + 2;
@@ -465,7 +465,7 @@ __device__ __forceinline__ void conv_tile_rows(f32x4 (&acc)[MT][NT], const char*
 #pragma unroll
             for (int m = 0; m < MT; ++m)
 #pragma unroll
-                for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], A[kh][m], Bf[n + kh]);
+                for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A[kh][m], Bf[n + kh]);
     };
     load(0, A0, B0);
 #pragma unroll
@@ -485,7 +485,7 @@ __device__ __forceinline__ void conv_tile_rows(f32x4 (&acc)[MT][NT], const char*
 // fragments of step s+1 and the halo rows of the next (kw, k-half) group are read while
 // step s's MFMAs run -- 2*MT + 2*(NT+2) fragment registers (64 at MT=NT=4) instead of
 // 6*MT + 2*(NT+2).
-template <int COT, int MT, int NT>
+template <typename T, int COT, int MT, int NT>
 __device__ __forceinline__ void conv_tile_rows2(f32x4 (&acc)[MT][NT], const char* wts, const char* halo, int wr,
                                                 int wc, int q, int c16) {
     constexpr int NB = NT + 2;
@@ -507,7 +507,7 @@ __device__ __forceinline__ void conv_tile_rows2(f32x4 (&acc)[MT][NT], const char
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int n = 0; n < NT; ++n) mma16<bf16>(acc[m][n], A[m], Bf[n + kh]);
+            for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A[m], Bf[n + kh]);
     };
     loadB(0, B0);
     loadA(0, A0);
@@ -534,9 +534,9 @@ __device__ __forceinline__ void conv_tile_rows2(f32x4 (&acc)[MT][NT], const char
 }
 
 // ------------------------------------------------------------------------------------
-// k_conv3x3_p: persistent, resident weights, LDS-DMA double-buffered halo (bf16, Cin=64)
+// k_conv3x3_p: persistent, resident weights, LDS-DMA double-buffered halo (16-bit, Cin=64)
 // ------------------------------------------------------------------------------------
-template <int COT, int WR, int WC, int EPIC>
+template <typename T, int COT, int WR, int WC, int EPIC>
 __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MT = COT / 16 / WC, NT = 16 / WR, NW = WR * WC;
@@ -616,8 +616,8 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (!(d.debug & 2)) {
-            if (d.debug & 32) conv_tile_resident<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16, next_halo);
-            else conv_tile_rows<COT, MT, NT>(acc, wts, cur, wr, wc, q, c16);
+            if (d.debug & 32) conv_tile_resident<T, COT, MT, NT>(acc, wts, cur, wr, wc, q, c16, next_halo);
+            else conv_tile_rows<T, COT, MT, NT>(acc, wts, cur, wr, wc, q, c16);
         } else {
             for (int tap = 0; tap < 9; ++tap) next_halo(tap);
         }
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
 #pragma unroll
                 for (int n = 0; n < NT; ++n) asm volatile("" ::"v"(acc[m][n]));
         } else {
-            nst = conv_epilogue<bf16, COT, WR, WC, EPIC, true>(d, acc, b, t, h0, w0, co0,
+            nst = conv_epilogue<T, COT, WR, WC, EPIC, true>(d, acc, b, t, h0, w0, co0,
                                                                (d.debug & 64) ? nullptr : cur, red, ec);
         }
         FEN_STAMP(3 + 3 * k);
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
 }
 
 // ------------------------------------------------------------------------------------
-// k_conv3x3_g: persistent, two wave-groups in ping-pong (bf16, Cin == 64, Cout % 64 == 0).
+// k_conv3x3_g: persistent, two wave-groups in ping-pong (16-bit, Cin == 64, Cout % 64 == 0).
 // 512 threads = group A (waves 0-3) + group B (waves 4-7); each wave owns 4 output rows x
 // 16 columns x all 64 output channels of a tile (16 accumulators, halo-row-reuse MFMA
 // order).  The block's tiles alternate between the groups, and the groups alternate
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
 constexpr int G_WBYTES = 9 * 64 * 128;
 constexpr int G_LDS = G_WBYTES + 2 * HALO_SLOT + 2 * 4 * 64 * 4 + 2 * 64 * 4;
 
-template <int EPIC>
+template <typename T, int EPIC>
 __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
     constexpr int MT = 4, NT = 4;
     constexpr int NRES = EPIC >> 8;
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                 for (int m = 0; m < MT; ++m)
 #pragma unroll
                     for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-                conv_tile_rows2<64, MT, NT>(acc, wts, hslot, wr, 0, q, c16);
+                conv_tile_rows2<T, 64, MT, NT>(acc, wts, hslot, wr, 0, q, c16);
             }
         } else {
             // ---------------- service phase: retire tile jp, stream tile jp + 1 ----------------
@@ -816,16 +816,16 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                         float rf[NRES > 0 ? NRES : 1][4], pf[4];
 #pragma unroll
                         for (int k = 0; k < NRES; ++k) {
-                            rf[k][0] = __uint_as_float(rv[k][m][n].x << 16);
-                            rf[k][1] = __uint_as_float(rv[k][m][n].x & 0xffff0000u);
-                            rf[k][2] = __uint_as_float(rv[k][m][n].y << 16);
-                            rf[k][3] = __uint_as_float(rv[k][m][n].y & 0xffff0000u);
+                            rf[k][0] = lo16<T>(rv[k][m][n].x);
+                            rf[k][1] = hi16<T>(rv[k][m][n].x);
+                            rf[k][2] = lo16<T>(rv[k][m][n].y);
+                            rf[k][3] = hi16<T>(rv[k][m][n].y);
                         }
                         if constexpr (PBWD) {
-                            pf[0] = __uint_as_float(pv[m][n].x << 16);
-                            pf[1] = __uint_as_float(pv[m][n].x & 0xffff0000u);
-                            pf[2] = __uint_as_float(pv[m][n].y << 16);
-                            pf[3] = __uint_as_float(pv[m][n].y & 0xffff0000u);
+                            pf[0] = lo16<T>(pv[m][n].x);
+                            pf[1] = hi16<T>(pv[m][n].x);
+                            pf[2] = lo16<T>(pv[m][n].y);
+                            pf[3] = hi16<T>(pv[m][n].y);
                         }
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -866,10 +866,10 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                             off = ((size_t)(b * H + h) * W + w) * Cout + cob;
                         }
                         if (PRELU && d.y_pre) {
-                            st4<bf16>((char*)d.y_pre + off * 2, v);
+                            st4<T>((char*)d.y_pre + off * 2, v);
                             ++nst;
                         }
-                        st4<bf16>((char*)d.y + off * 2, o);
+                        st4<T>((char*)d.y + off * 2, o);
                         ++nst;
                     }
                 }
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
 }
 
 // ------------------------------------------------------------------------------------
-// k_conv3x3_s: streamed per-tap weights, register-staged halo (f32 / bf16, any Cin panel)
+// k_conv3x3_s: streamed per-tap weights, register-staged halo (f32 / bf16 / fp16, any Cin panel)
 // ------------------------------------------------------------------------------------
 template <typename T, int COT>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
@@ -1006,7 +1006,7 @@ int conv_variant() {
     return v;
 }
 
-template <int COT, int WR, int WC, int EPIC>
+template <typename T, int COT, int WR, int WC, int EPIC>
 int launch_p(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int ntiles = d->B * tpi;
@@ -1024,16 +1024,16 @@ int launch_p(const fen_conv_desc* d, hipStream_t s) {
     const size_t lds = 9 * COT * 128 + 2 * HALO_SLOT + WR * COT * 4 + 64;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_conv3x3_p<COT, WR, WC, EPIC>,
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_p<T, COT, WR, WC, EPIC>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_conv3x3_p<COT, WR, WC, EPIC>), dim3(grid), dim3(64 * WR * WC), lds, s, *d);
+    hipLaunchKernelGGL((k_conv3x3_p<T, COT, WR, WC, EPIC>), dim3(grid), dim3(64 * WR * WC), lds, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
 
-template <int EPIC>
+template <typename T, int EPIC>
 int launch_g(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int ntiles = d->B * tpi;
@@ -1050,10 +1050,10 @@ int launch_g(const fen_conv_desc* d, hipStream_t s) {
     if (grid > maxg) grid = maxg;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_conv3x3_g<EPIC>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_g<T, EPIC>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_conv3x3_g<EPIC>), dim3(grid), dim3(512), G_LDS, s, *d);
+    hipLaunchKernelGGL((k_conv3x3_g<T, EPIC>), dim3(grid), dim3(512), G_LDS, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
@@ -1069,32 +1069,19 @@ int launch_s(const fen_conv_desc* d, hipStream_t s) {
     return FEN_OK;
 }
 
-}  // namespace
-
-extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
-    if (!d || !d->x || !d->w || d->B <= 0 || d->H <= 0 || d->W <= 0 || d->Cin <= 0 || d->Cout <= 0)
-        return FEN_EINVAL;
-    const int CK = d->dtype == FEN_BF16 ? 64 : 32;
-    if (d->dtype != FEN_F32 && d->dtype != FEN_BF16) return FEN_EINVAL;
-    if (d->Cin % CK) return FEN_EUNSUPPORTED;
+// Kernel selection for one compute dtype T (float, bf16 or f16)
+template <typename T>
+int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
     const int epi = d->epi;
-    if ((epi & FEN_EPI_BIAS) && !d->bias) return FEN_EINVAL;
-    if ((epi & (FEN_EPI_PRELU | FEN_EPI_PRELU_BWD)) && !d->alpha) return FEN_EINVAL;
-    if ((epi & FEN_EPI_PRELU_BWD) && !d->pre_in) return FEN_EINVAL;
-    if ((epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD)) && !d->part) return FEN_EINVAL;
-    if ((epi & FEN_EPI_POOL) && (epi & FEN_EPI_PRELU_BWD)) return FEN_EUNSUPPORTED;
-    if ((epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE)) == (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE))
-        return FEN_EUNSUPPORTED;
-    // the persistent kernel addresses the input with 32-bit buffer offsets
+    constexpr bool H16 = sizeof(T) == 2;
+    // the persistent kernels address the input with 32-bit buffer offsets
     const bool small = (size_t)d->B * d->H * d->W * 128 < (size_t)0x7fff0000;
-    const bool persist = d->dtype == FEN_BF16 && d->Cin == 64 && small && !(epi & FEN_EPI_UNSHUFFLE) &&
-                         conv_variant() != 1;
-    hipStream_t s = (hipStream_t)stream;
+    const bool persist = H16 && d->Cin == 64 && small && !(epi & FEN_EPI_UNSHUFFLE) && conv_variant() != 1;
     if (epi & FEN_EPI_LAST) {
         if (d->Cout > 4 || !d->lr || d->scale <= 0 || d->H % d->scale || d->W % d->scale) return FEN_EINVAL;
         if (epi & ~(FEN_EPI_LAST | FEN_EPI_BIAS)) return FEN_EUNSUPPORTED;
         if (fen_detail::conv_last_fast_ok(d) && conv_variant() != 1) return fen_detail::launch_conv_last(d, s);
-        return d->dtype == FEN_BF16 ? launch_s<bf16, 16>(d, s) : launch_s<float, 16>(d, s);
+        return launch_s<T, 16>(d, s);
     }
     if (!d->y) return FEN_EINVAL;
     if (epi & FEN_EPI_SHUFFLE) {
@@ -1104,50 +1091,74 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     }
     if ((epi & FEN_EPI_UNSHUFFLE) && ((d->H | d->W) & 1)) return FEN_EINVAL;
     if (d->Cout % 64 == 0) {
-        if (persist) {
-            // the network's epilogue modes get their own instantiation (mode | #residuals << 8)
-            const int nres = d->res[0] ? (d->res[1] ? (d->res[2] ? 3 : 2) : 1) : 0;
-            bool dense = true;   // residual pointers packed at the front
-            for (int k = nres; k < 3; ++k) dense = dense && !d->res[k];
-            const int key = dense && conv_variant() != 2 ? (epi | (nres << 8)) : -1;
-            constexpr int B_ = FEN_EPI_BIAS;
-            if (conv_variant() == 3 && key == (B_ | FEN_EPI_PRELU)) return launch_p<64, 4, 1, B_ | FEN_EPI_PRELU>(d, s);
-            if (conv_variant() != 5 && conv_variant() != 3) {
-                // default: the ping-pong kernel, except where the one-group persistent kernel
-                // measures faster (pool epilogue 19.2 vs 20.4 us, PReLU-backward 21.8 vs
-                // 36.3 us at B=32 64x64: the latter's register-heavy epilogue does not fit
-                // the ping-pong kernel's half-size register budget)
+        if constexpr (H16) {
+            if (persist) {
+                // the network's epilogue modes get their own instantiation (mode | #residuals << 8)
+                const int nres = d->res[0] ? (d->res[1] ? (d->res[2] ? 3 : 2) : 1) : 0;
+                bool dense = true;   // residual pointers packed at the front
+                for (int k = nres; k < 3; ++k) dense = dense && !d->res[k];
+                const int key = dense && conv_variant() != 2 ? (epi | (nres << 8)) : -1;
+                constexpr int B_ = FEN_EPI_BIAS;
+                if (conv_variant() == 3 && key == (B_ | FEN_EPI_PRELU)) return launch_p<T, 64, 4, 1, B_ | FEN_EPI_PRELU>(d, s);
+                if (conv_variant() != 5 && conv_variant() != 3) {
+                    // default: the ping-pong kernel, except where the one-group persistent kernel
+                    // measures faster (pool epilogue 19.2 vs 20.4 us, PReLU-backward 21.8 vs
+                    // 36.3 us at B=32 64x64: the latter's register-heavy epilogue does not fit
+                    // the ping-pong kernel's half-size register budget)
+                    switch (key) {
+                        case B_ | FEN_EPI_PRELU: return launch_g<T, B_ | FEN_EPI_PRELU>(d, s);
+                        case B_ | FEN_EPI_POOL: return launch_p<T, 64, 4, 2, B_ | FEN_EPI_POOL>(d, s);
+                        case B_ | (1 << 8): return launch_g<T, B_ | (1 << 8)>(d, s);
+                        case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE: return launch_g<T, B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
+                        case FEN_EPI_PRELU_BWD: return launch_p<T, 64, 4, 2, FEN_EPI_PRELU_BWD>(d, s);
+                        case 0: return launch_g<T, 0>(d, s);
+                        case 1 << 8: return launch_g<T, 1 << 8>(d, s);
+                        case 2 << 8: return launch_g<T, 2 << 8>(d, s);
+                        case 3 << 8: return launch_g<T, 3 << 8>(d, s);
+                        default: break;
+                    }
+                }
                 switch (key) {
-                    case B_ | FEN_EPI_PRELU: return launch_g<B_ | FEN_EPI_PRELU>(d, s);
-                    case B_ | FEN_EPI_POOL: return launch_p<64, 4, 2, B_ | FEN_EPI_POOL>(d, s);
-                    case B_ | (1 << 8): return launch_g<B_ | (1 << 8)>(d, s);
-                    case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE: return launch_g<B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
-                    case FEN_EPI_PRELU_BWD: return launch_p<64, 4, 2, FEN_EPI_PRELU_BWD>(d, s);
-                    case 0: return launch_g<0>(d, s);
-                    case 1 << 8: return launch_g<1 << 8>(d, s);
-                    case 2 << 8: return launch_g<2 << 8>(d, s);
-                    case 3 << 8: return launch_g<3 << 8>(d, s);
-                    default: break;
+                    case B_ | FEN_EPI_PRELU: return launch_p<T, 64, 4, 2, B_ | FEN_EPI_PRELU>(d, s);
+                    case B_ | FEN_EPI_POOL: return launch_p<T, 64, 4, 2, B_ | FEN_EPI_POOL>(d, s);
+                    case B_ | (1 << 8): return launch_p<T, 64, 4, 2, B_ | (1 << 8)>(d, s);
+                    case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE:
+                        return launch_p<T, 64, 4, 2, B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
+                    case FEN_EPI_PRELU_BWD: return launch_p<T, 64, 4, 2, FEN_EPI_PRELU_BWD>(d, s);
+                    case 0: return launch_p<T, 64, 4, 2, 0>(d, s);
+                    case 1 << 8: return launch_p<T, 64, 4, 2, 1 << 8>(d, s);
+                    case 2 << 8: return launch_p<T, 64, 4, 2, 2 << 8>(d, s);
+                    case 3 << 8: return launch_p<T, 64, 4, 2, 3 << 8>(d, s);
+                    default: return launch_p<T, 64, 4, 2, -1>(d, s);
                 }
             }
-            switch (key) {
-                case B_ | FEN_EPI_PRELU: return launch_p<64, 4, 2, B_ | FEN_EPI_PRELU>(d, s);
-                case B_ | FEN_EPI_POOL: return launch_p<64, 4, 2, B_ | FEN_EPI_POOL>(d, s);
-                case B_ | (1 << 8): return launch_p<64, 4, 2, B_ | (1 << 8)>(d, s);
-                case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE:
-                    return launch_p<64, 4, 2, B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
-                case FEN_EPI_PRELU_BWD: return launch_p<64, 4, 2, FEN_EPI_PRELU_BWD>(d, s);
-                case 0: return launch_p<64, 4, 2, 0>(d, s);
-                case 1 << 8: return launch_p<64, 4, 2, 1 << 8>(d, s);
-                case 2 << 8: return launch_p<64, 4, 2, 2 << 8>(d, s);
-                case 3 << 8: return launch_p<64, 4, 2, 3 << 8>(d, s);
-                default: return launch_p<64, 4, 2, -1>(d, s);
-            }
         }
-        return d->dtype == FEN_BF16 ? launch_s<bf16, 64>(d, s) : launch_s<float, 64>(d, s);
+        return launch_s<T, 64>(d, s);
     }
-    if (d->Cout % 16 == 0) {
-        return d->dtype == FEN_BF16 ? launch_s<bf16, 16>(d, s) : launch_s<float, 16>(d, s);
-    }
+    if (d->Cout % 16 == 0) return launch_s<T, 16>(d, s);
     return FEN_EUNSUPPORTED;
+}
+
+}  // namespace
+
+extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
+    if (!d || !d->x || !d->w || d->B <= 0 || d->H <= 0 || d->W <= 0 || d->Cin <= 0 || d->Cout <= 0)
+        return FEN_EINVAL;
+    if (d->dtype != FEN_F32 && d->dtype != FEN_BF16 && d->dtype != FEN_F16) return FEN_EINVAL;
+    const int CK = d->dtype == FEN_F32 ? 32 : 64;
+    if (d->Cin % CK) return FEN_EUNSUPPORTED;
+    const int epi = d->epi;
+    if ((epi & FEN_EPI_BIAS) && !d->bias) return FEN_EINVAL;
+    if ((epi & (FEN_EPI_PRELU | FEN_EPI_PRELU_BWD)) && !d->alpha) return FEN_EINVAL;
+    if ((epi & FEN_EPI_PRELU_BWD) && !d->pre_in) return FEN_EINVAL;
+    if ((epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD)) && !d->part) return FEN_EINVAL;
+    if ((epi & FEN_EPI_POOL) && (epi & FEN_EPI_PRELU_BWD)) return FEN_EUNSUPPORTED;
+    if ((epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE)) == (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE))
+        return FEN_EUNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    switch (d->dtype) {
+        case FEN_BF16: return conv_dispatch<bf16>(d, s);
+        case FEN_F16: return conv_dispatch<f16>(d, s);
+        default: return conv_dispatch<float>(d, s);
+    }
 }

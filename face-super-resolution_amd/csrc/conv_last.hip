@@ -1,4 +1,4 @@
-// conv_last as a persistent HBM-streaming kernel (bf16, Cin = 64, Cout <= 4, x4 skip):
+// conv_last as a persistent HBM-streaming kernel (bf16 / fp16, Cin = 64, Cout <= 4, x4 skip):
 //   sr = conv3x3(a, w_last) + b_last + bicubic_x4(lr)          (custom.py:121-124, 158-161)
 //   eval: clamp to [0, 1] (custom.py:181-188); training: |sr - hr| tile sums and the L1
 //   gradient sign(sr - hr) * l1_scale in the NHWC16 layout the dgrad consumes.
@@ -42,7 +42,7 @@ constexpr int PIECES1 = HALO_DMA / 2;           // loader 1: odd halo pieces (+ 
 static_assert(CL_LDS <= 163840, "LDS budget");
 static_assert(2 * PIECES0 <= 63 && 2 * (PIECES1 + 4) <= 63, "vmcnt field");
 
-template <bool TRAIN>
+template <typename T, bool TRAIN>
 __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
 #pragma unroll
                 for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-                    for (int n = 0; n < RPW; ++n) mma16<bf16>(acc[n], A[kh], Bf[n + kh]);
+                    for (int n = 0; n < RPW; ++n) mma16<T>(acc[n], A[kh], Bf[n + kh]);
             }
         // ---- bicubic skip, lane (q, c16) evaluates channel q.  Output row h0 + m (m = RPW wave
         //      + n) = 4a + m%4 with a = h0/4 + m/4: taps at LR rows a-2..a+1 (m%4 < 2) or
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
                     const float t = __shfl(sg, r * 16 + c16, 64);
                     g4[r] = q == 0 ? t : 0.f;
                 }
-                if (d.dout) st4<bf16>((char*)d.dout + (((size_t)(b * H + h) * W + w0 + c16) * 16 + q * 4) * 2, g4);
+                if (d.dout) st4<T>((char*)d.dout + (((size_t)(b * H + h) * W + w0 + c16) * 16 + q * 4) * 2, g4);
             }
         }
         if (train && d.loss_part) {
@@ -281,7 +281,7 @@ int g_cus = 0;
 namespace fen_detail {
 
 bool conv_last_fast_ok(const fen_conv_desc* d) {
-    return d->dtype == FEN_BF16 && d->Cin == 64 && d->Cout <= 4 && d->scale == 4 && d->H % 16 == 0 &&
+    return (d->dtype == FEN_BF16 || d->dtype == FEN_F16) && d->Cin == 64 && d->Cout <= 4 && d->scale == 4 && d->H % 16 == 0 &&
            d->W % 16 == 0 && d->H <= 8192 && d->W <= 8192 && d->debug == 0 &&
            (size_t)d->B * d->H * d->W * 128 < (size_t)0x7fff0000;
 }
@@ -297,12 +297,19 @@ int launch_conv_last(const fen_conv_desc* d, hipStream_t s) {
     const int grid = ntiles < g_cus ? ntiles : g_cus;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_conv_last<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CL_LDS);
-        (void)hipFuncSetAttribute((const void*)k_conv_last<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CL_LDS);
+        (void)hipFuncSetAttribute((const void*)k_conv_last<bf16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, CL_LDS);
+        (void)hipFuncSetAttribute((const void*)k_conv_last<bf16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, CL_LDS);
+        (void)hipFuncSetAttribute((const void*)k_conv_last<f16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, CL_LDS);
+        (void)hipFuncSetAttribute((const void*)k_conv_last<f16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, CL_LDS);
         attr_set = true;
     }
-    if (d->hr) hipLaunchKernelGGL(k_conv_last<true>, dim3(grid), dim3(CL_THREADS), CL_LDS, s, *d);
-    else hipLaunchKernelGGL(k_conv_last<false>, dim3(grid), dim3(CL_THREADS), CL_LDS, s, *d);
+    if (d->dtype == FEN_F16) {
+        if (d->hr) hipLaunchKernelGGL((k_conv_last<f16, true>), dim3(grid), dim3(CL_THREADS), CL_LDS, s, *d);
+        else hipLaunchKernelGGL((k_conv_last<f16, false>), dim3(grid), dim3(CL_THREADS), CL_LDS, s, *d);
+    } else {
+        if (d->hr) hipLaunchKernelGGL((k_conv_last<bf16, true>), dim3(grid), dim3(CL_THREADS), CL_LDS, s, *d);
+        else hipLaunchKernelGGL((k_conv_last<bf16, false>), dim3(grid), dim3(CL_THREADS), CL_LDS, s, *d);
+    }
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -8,6 +8,11 @@
 
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// fp16: the reference's own mixed-precision dtype (torch.cuda.amp.autocast, trainer.py:18,227,460);
+// same MFMA rate as bf16 on gfx950 with 3 more mantissa bits (11 vs 8)
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -15,6 +20,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 template <typename T> struct Tr;
 template <> struct Tr<float> { static constexpr int CK = 32; static constexpr int EPC = 4; };
 template <> struct Tr<bf16>  { static constexpr int CK = 64; static constexpr int EPC = 8; };
+template <> struct Tr<f16>   { static constexpr int CK = 64; static constexpr int EPC = 8; };
 
 // Byte offset of 16-B chunk `chunk` (0..7) of row `p` in a 128-B-row LDS image.  The XOR
 // key (p>>1)&7 puts 16 consecutive rows read at the same chunk on 16 distinct 16-B slots
@@ -38,12 +44,33 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
     return __builtin_bit_cast(unsigned short, h);
 }
 
+// 16-bit pairs in one 32-bit word (element 0 in the low half): the bf16 forms are shifts,
+// the fp16 forms hardware conversions (v_cvt_f32_f16 / v_cvt_pk_f16_f32-style RNE)
+template <typename T> __device__ __forceinline__ float lo16(unsigned w);
+template <typename T> __device__ __forceinline__ float hi16(unsigned w);
+template <> __device__ __forceinline__ float lo16<bf16>(unsigned w) { return __uint_as_float(w << 16); }
+template <> __device__ __forceinline__ float hi16<bf16>(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+template <> __device__ __forceinline__ float lo16<f16>(unsigned w) {
+    return (float)__builtin_bit_cast(f16, (unsigned short)(w & 0xffffu));
+}
+template <> __device__ __forceinline__ float hi16<f16>(unsigned w) {
+    return (float)__builtin_bit_cast(f16, (unsigned short)(w >> 16));
+}
+template <typename T> __device__ __forceinline__ unsigned short to16(float f);
+template <> __device__ __forceinline__ unsigned short to16<bf16>(float f) { return f2bf(f); }
+template <> __device__ __forceinline__ unsigned short to16<f16>(float f) { return __builtin_bit_cast(unsigned short, (f16)f); }
+template <typename T> __device__ __forceinline__ unsigned pack2(float lo, float hi) {
+    return (unsigned)to16<T>(lo) | ((unsigned)to16<T>(hi) << 16);
+}
+
 template <typename T> __device__ __forceinline__ float tof(T v);
 template <> __device__ __forceinline__ float tof<float>(float v) { return v; }
 template <> __device__ __forceinline__ float tof<bf16>(bf16 v) { return (float)v; }
+template <> __device__ __forceinline__ float tof<f16>(f16 v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T fromf(float v);
 template <> __device__ __forceinline__ float fromf<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16 fromf<bf16>(float v) { return (bf16)v; }
+template <> __device__ __forceinline__ f16 fromf<f16>(float v) { return (f16)v; }
 
 // 4 consecutive elements <-> float[4]
 template <typename T> __device__ __forceinline__ void ld4(const void* p, float v[4]);
@@ -56,6 +83,11 @@ template <> __device__ __forceinline__ void ld4<bf16>(const void* p, float v[4])
     v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
     v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
 }
+template <> __device__ __forceinline__ void ld4<f16>(const void* p, float v[4]) {
+    uint2 x = *(const uint2*)p;
+    v[0] = lo16<f16>(x.x); v[1] = hi16<f16>(x.x);
+    v[2] = lo16<f16>(x.y); v[3] = hi16<f16>(x.y);
+}
 template <typename T> __device__ __forceinline__ void st4(void* p, const float v[4]);
 template <> __device__ __forceinline__ void st4<float>(void* p, const float v[4]) {
     *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
@@ -65,6 +97,10 @@ template <> __device__ __forceinline__ void st4<bf16>(void* p, const float v[4])
     x.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
     x.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
     *(uint2*)p = x;
+}
+
+template <> __device__ __forceinline__ void st4<f16>(void* p, const float v[4]) {
+    *(uint2*)p = make_uint2(pack2<f16>(v[0], v[1]), pack2<f16>(v[2], v[3]));
 }
 
 // 16-B vector of EPC elements <-> float[EPC]
@@ -81,6 +117,14 @@ template <> __device__ __forceinline__ void unpack16<bf16>(const uint4& u, float
         v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
 }
+template <> __device__ __forceinline__ void unpack16<f16>(const uint4& u, float* v) {
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = lo16<f16>(w[i]);
+        v[2 * i + 1] = hi16<f16>(w[i]);
+    }
+}
 template <typename T> __device__ __forceinline__ uint4 pack16(const float* v);
 template <> __device__ __forceinline__ uint4 pack16<float>(const float* v) {
     return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
@@ -95,12 +139,19 @@ template <> __device__ __forceinline__ uint4 pack16<bf16>(const float* v) {
     return u;
 }
 
+template <> __device__ __forceinline__ uint4 pack16<f16>(const float* v) {
+    return make_uint4(pack2<f16>(v[0], v[1]), pack2<f16>(v[2], v[3]), pack2<f16>(v[4], v[5]), pack2<f16>(v[6], v[7]));
+}
+
 // acc += A * B for one 16-byte fragment pair: one 16x16x32 bf16 MFMA, or four
 // 16x16x4 f32 MFMAs (exact f32; element s of the 16 B is the k-step s).
 template <typename T> __device__ __forceinline__ void mma16(f32x4& acc, const uint4& a, const uint4& b);
 template <> __device__ __forceinline__ void mma16<bf16>(f32x4& acc, const uint4& a, const uint4& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                   __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+template <> __device__ __forceinline__ void mma16<f16>(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
 }
 template <> __device__ __forceinline__ void mma16<float>(f32x4& acc, const uint4& a, const uint4& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);

@@ -99,9 +99,10 @@ __device__ __forceinline__ void st_out16(void* p, uint4 v) {
     __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)p);
 #endif
 }
+template <typename T>
 __device__ __forceinline__ void st_out4(void* p, const float v[4]) {
-    const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-    const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    const unsigned lo = (unsigned)to16<T>(v[0]) | ((unsigned)to16<T>(v[1]) << 16);
+    const unsigned hi = (unsigned)to16<T>(v[2]) | ((unsigned)to16<T>(v[3]) << 16);
 #ifndef RCAB_NT
     *(uint2*)p = make_uint2(lo, hi);
 #else
@@ -119,6 +120,7 @@ __device__ __forceinline__ void st_flag(int* p, int v) {
 
 // conv2 MFMAs for one phase (kernel column kw: taps (0,kw),(1,kw),(2,kw) in ring slots),
 // halo-row-reuse order on the a1 image; wave = 4 output rows x 32 channels.
+template <typename T>
 __device__ __forceinline__ void conv2_phase(f32x4 (&acc)[2][4], const char* a1, const char* const (&tapp)[3], int kw,
                                             int wr, int arow, int q, int c16) {
     uint4 A0[3][2], B0[6], A1[3][2], B1[6];
@@ -138,7 +140,7 @@ __device__ __forceinline__ void conv2_phase(f32x4 (&acc)[2][4], const char* a1, 
 #pragma unroll
             for (int m = 0; m < 2; ++m)
 #pragma unroll
-                for (int n = 0; n < 4; ++n) mma16<bf16>(acc[m][n], A[kh][m], Bf[n + kh]);
+                for (int n = 0; n < 4; ++n) mma16<T>(acc[m][n], A[kh][m], Bf[n + kh]);
     };
     load(0, A0, B0);
     load(1, A1, B1);
@@ -160,7 +162,7 @@ __device__ __forceinline__ int edge_base(int eidx, int c16, int kh, int chunk) {
     if (r > 17) r = 17;
     return ((r + kh) * 4 + (c16 & 1)) * 128 + ekey(r + kh, chunk);
 }
-template <bool MAIN4, bool HAS5>
+template <typename T, bool MAIN4, bool HAS5>
 __device__ __forceinline__ void conv1_kw(f32x4 (&acc)[2][6], const char* xh, const char* eh,
                                          const char* const (&tapp)[3], int kw, int c16, int row0, int eidx4,
                                          int arow, int q) {
@@ -194,9 +196,9 @@ __device__ __forceinline__ void conv1_kw(f32x4 (&acc)[2][6], const char* xh, con
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
 #pragma unroll
-                for (int f = 0; f < NR; ++f) mma16<bf16>(acc[m][f], A[kh][m], Bm[f + kh]);
-                if constexpr (!MAIN4) mma16<bf16>(acc[m][4], A[kh][m], E4[kh]);
-                if constexpr (HAS5) mma16<bf16>(acc[m][5], A[kh][m], E5[kh]);
+                for (int f = 0; f < NR; ++f) mma16<T>(acc[m][f], A[kh][m], Bm[f + kh]);
+                if constexpr (!MAIN4) mma16<T>(acc[m][4], A[kh][m], E4[kh]);
+                if constexpr (HAS5) mma16<T>(acc[m][5], A[kh][m], E5[kh]);
             }
 #ifdef RCAB_C1_FENCE
         __builtin_amdgcn_sched_barrier(0);   // A/B only: one k-half's fragments live at a time
@@ -210,7 +212,7 @@ __device__ __forceinline__ void conv1_kw(f32x4 (&acc)[2][6], const char* xh, con
 // PARK (training, d.t given): t is parked in d.t (stored for the backward anyway) and the
 // apply re-reads it with coalesced 16-B loads; else t stays in 16 VGPRs (packed bf16) and the
 // apply uses the MFMA fragment layout (fewer HBM bytes, more registers).
-template <bool PARK>
+template <typename T, bool PARK>
 __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* xh = smem + O_XH;
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
     }
 
     // t (bf16) of the tile awaiting its gate: parked in d.t (PARK) or carried in tcar
-    bf16* const tpark = (bf16*)d.t;
+    T* const tpark = (T*)d.t;
     uint2 tcar[2][4];
     (void)tcar;
     int arrive_f = -1;                                // tile flag still to be raised
@@ -487,9 +489,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             unsigned ow[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float lo = __uint_as_float(tw[e] << 16) * sv[2 * e] + __uint_as_float(xw[e] << 16);
-                const float hi = __uint_as_float(tw[e] & 0xffff0000u) * sv[2 * e + 1] + __uint_as_float(xw[e] & 0xffff0000u);
-                ow[e] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+                const float lo = lo16<T>(tw[e]) * sv[2 * e] + lo16<T>(xw[e]);
+                const float hi = hi16<T>(tw[e]) * sv[2 * e + 1] + hi16<T>(xw[e]);
+                ow[e] = (unsigned)to16<T>(lo) | ((unsigned)to16<T>(hi) << 16);
             }
             st_out16((char*)d.y + o, make_uint4(ow[0], ow[1], ow[2], ow[3]));
         }
@@ -557,12 +559,12 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 float o[4];
-                o[0] = __uint_as_float(tcar[m][n].x << 16) * sv[m][0] + __uint_as_float(xf[m][n].x << 16);
-                o[1] = __uint_as_float(tcar[m][n].x & 0xffff0000u) * sv[m][1] + __uint_as_float(xf[m][n].x & 0xffff0000u);
-                o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xf[m][n].y << 16);
-                o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xf[m][n].y & 0xffff0000u);
-                pk[m].x = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
-                pk[m].y = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+                o[0] = lo16<T>(tcar[m][n].x) * sv[m][0] + lo16<T>(xf[m][n].x);
+                o[1] = hi16<T>(tcar[m][n].x) * sv[m][1] + hi16<T>(xf[m][n].x);
+                o[2] = lo16<T>(tcar[m][n].y) * sv[m][2] + lo16<T>(xf[m][n].y);
+                o[3] = hi16<T>(tcar[m][n].y) * sv[m][3] + hi16<T>(xf[m][n].y);
+                pk[m].x = (unsigned)to16<T>(o[0]) | ((unsigned)to16<T>(o[1]) << 16);
+                pk[m].y = (unsigned)to16<T>(o[2]) | ((unsigned)to16<T>(o[3]) << 16);
             }
             const bool odd = q & 1;
             const uint2 snd = odd ? pk[0] : pk[1];
@@ -575,11 +577,11 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 float o[4];
-                o[0] = __uint_as_float(tcar[m][n].x << 16) * sv[m][0] + __uint_as_float(xf[m][n].x << 16);
-                o[1] = __uint_as_float(tcar[m][n].x & 0xffff0000u) * sv[m][1] + __uint_as_float(xf[m][n].x & 0xffff0000u);
-                o[2] = __uint_as_float(tcar[m][n].y << 16) * sv[m][2] + __uint_as_float(xf[m][n].y << 16);
-                o[3] = __uint_as_float(tcar[m][n].y & 0xffff0000u) * sv[m][3] + __uint_as_float(xf[m][n].y & 0xffff0000u);
-                st_out4((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
+                o[0] = lo16<T>(tcar[m][n].x) * sv[m][0] + lo16<T>(xf[m][n].x);
+                o[1] = hi16<T>(tcar[m][n].x) * sv[m][1] + hi16<T>(xf[m][n].x);
+                o[2] = lo16<T>(tcar[m][n].y) * sv[m][2] + lo16<T>(xf[m][n].y);
+                o[3] = hi16<T>(tcar[m][n].y) * sv[m][3] + hi16<T>(xf[m][n].y);
+                st_out4<T>((char*)d.y + (px * 64 + wc * 32 + m * 16 + 4 * q) * 2, o);
             }
 #endif
         }
@@ -617,9 +619,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
                                    ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
             if (k == 1 && p == 1) RSTAMP(45);
-            if (g < 2) conv1_kw<true, false>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
-            else if (g == 2) conv1_kw<false, false>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
-            else conv1_kw<false, true>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
+            if (g < 2) conv1_kw<T, true, false>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
+            else if (g == 2) conv1_kw<T, false, false>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
+            else conv1_kw<T, false, true>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
             if (k == 1 && p == 1) RSTAMP(46);
         }
         if (k == 0) RSTAMP(15);
@@ -649,7 +651,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                         a[r] = okf * prelu_f(z, alp[r]);
                     }
                     const int off = f < 4 ? a1m[m] + f * (A1W * 128) : f == 4 ? a1o4[m] : a1o5[m];
-                    if (f < 5 || has5) st4<bf16>(a1s + off, a);
+                    if (f < 5 || has5) st4<T>(a1s + off, a);
                 }
             }
 #if !defined(RCAB_Z1_LDS) && !defined(RCAB_A1_MASKED) && !defined(RCAB_Z1_NOSHFL)
@@ -662,8 +664,8 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                     uint2 pk[2];
 #pragma unroll
                     for (int m = 0; m < 2; ++m) {
-                        pk[m].x = (unsigned)f2bf(zs[m][f][0]) | ((unsigned)f2bf(zs[m][f][1]) << 16);
-                        pk[m].y = (unsigned)f2bf(zs[m][f][2]) | ((unsigned)f2bf(zs[m][f][3]) << 16);
+                        pk[m].x = (unsigned)to16<T>(zs[m][f][0]) | ((unsigned)to16<T>(zs[m][f][1]) << 16);
+                        pk[m].y = (unsigned)to16<T>(zs[m][f][2]) | ((unsigned)to16<T>(zs[m][f][3]) << 16);
                     }
                     const uint2 snd = odd ? pk[0] : pk[1];
                     uint2 rcv;
@@ -694,12 +696,12 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) a[r] = prelu_f(zs[m][f][r], alp[r]);
 #ifndef RCAB_Z1_LDS
-                        st_out4((char*)d.z1 + o * 2, zs[m][f]);
+                        st_out4<T>((char*)d.z1 + o * 2, zs[m][f]);
 #else
                         (void)o;
 #endif
 #ifdef RCAB_A1_MASKED
-                        st_out4((char*)d.a1 + o * 2, a);
+                        st_out4<T>((char*)d.a1 + o * 2, a);
 #endif
                     }
                 }
@@ -718,7 +720,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                         const int ac = f < 4 ? c16 : f == 4 ? ac4 : ac5;
                         if (!(f < 5 || has5) || ar < 1 || ar > 16 || ac < 1 || ac > 16) continue;
                         const int zc = ac - 1, chunk = ch * 4 + 2 * m + (q >> 1);
-                        st4<bf16>(xh + ((ar - 1) * 16 + zc) * 128 + ((chunk ^ (zc & 7)) << 4) + (q & 1) * 8, zs[m][f]);
+                        st4<T>(xh + ((ar - 1) * 16 + zc) * 128 + ((chunk ^ (zc & 7)) << 4) + (q & 1) * 8, zs[m][f]);
                     }
 #endif
             }
@@ -837,7 +839,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
                                    ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
             if (k == 1 && p == 4) RSTAMP(41);
-            conv2_phase(acc2, a1s, tapp, p - 3, wr, arow2, q, c16);
+            conv2_phase<T>(acc2, a1s, tapp, p - 3, wr, arow2, q, c16);
             if (k == 1) RSTAMP(42 + (p - 3));
         }
         if (k == 0) RSTAMP(29);
@@ -860,7 +862,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                 if constexpr (PARK) {
                     const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
                     float v[4] = {acc2[m][n][0], acc2[m][n][1], acc2[m][n][2], acc2[m][n][3]};
-                    st4<bf16>((char*)tpark + o * 2, v);
+                    st4<T>((char*)tpark + o * 2, v);
                 }
 #endif
             }
@@ -873,8 +875,8 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
                 uint2 pk[2];
 #pragma unroll
                 for (int m = 0; m < 2; ++m) {
-                    pk[m].x = (unsigned)f2bf(acc2[m][n][0]) | ((unsigned)f2bf(acc2[m][n][1]) << 16);
-                    pk[m].y = (unsigned)f2bf(acc2[m][n][2]) | ((unsigned)f2bf(acc2[m][n][3]) << 16);
+                    pk[m].x = (unsigned)to16<T>(acc2[m][n][0]) | ((unsigned)to16<T>(acc2[m][n][1]) << 16);
+                    pk[m].y = (unsigned)to16<T>(acc2[m][n][2]) | ((unsigned)to16<T>(acc2[m][n][3]) << 16);
                 }
                 const uint2 snd = odd ? pk[0] : pk[1];
                 uint2 rcv;
@@ -910,8 +912,8 @@ __global__ __launch_bounds__(512, 1) void k_rcab(const fen_rcab_desc d) {
             for (int m = 0; m < 2; ++m)
 #pragma unroll
                 for (int n = 0; n < 4; ++n) {
-                    tcar[m][n].x = (unsigned)f2bf(acc2[m][n][0]) | ((unsigned)f2bf(acc2[m][n][1]) << 16);
-                    tcar[m][n].y = (unsigned)f2bf(acc2[m][n][2]) | ((unsigned)f2bf(acc2[m][n][3]) << 16);
+                    tcar[m][n].x = (unsigned)to16<T>(acc2[m][n][0]) | ((unsigned)to16<T>(acc2[m][n][1]) << 16);
+                    tcar[m][n].y = (unsigned)to16<T>(acc2[m][n][2]) | ((unsigned)to16<T>(acc2[m][n][3]) << 16);
                 }
         }
         pend_t = t;
@@ -1016,7 +1018,7 @@ static int rcab_num_cus() {
 }
 
 extern "C" int fen_rcab_supported(int dtype, int B, int H, int W, int C, int Cr) {
-    if (dtype != FEN_BF16 || C != 64 || Cr <= 0 || Cr > 16 || B <= 0 || H <= 0 || W <= 0 || H % 16 || W % 16)
+    if ((dtype != FEN_BF16 && dtype != FEN_F16) || C != 64 || Cr <= 0 || Cr > 16 || B <= 0 || H <= 0 || W <= 0 || H % 16 || W % 16)
         return 0;
     if ((size_t)B * H * W * 128 >= (size_t)0x7fff0000) return 0;
     return (H / 16) * (W / 16) <= rcab_num_cus() ? 1 : 0;
@@ -1036,12 +1038,20 @@ extern "C" int fen_rcab_fused(const fen_rcab_desc* d, void* stream) {
     if (grid > MAX_GRID) grid = (MAX_GRID / tpi) * tpi;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_rcab<true>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
-        (void)hipFuncSetAttribute((const void*)k_rcab<false>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
+        (void)hipFuncSetAttribute((const void*)k_rcab<bf16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
+        (void)hipFuncSetAttribute((const void*)k_rcab<bf16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
+        (void)hipFuncSetAttribute((const void*)k_rcab<f16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
+        (void)hipFuncSetAttribute((const void*)k_rcab<f16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, RCAB_LDS);
         attr = true;
     }
-    if (d->t) hipLaunchKernelGGL(k_rcab<true>, dim3(grid), dim3(512), RCAB_LDS, (hipStream_t)stream, *d);
-    else hipLaunchKernelGGL(k_rcab<false>, dim3(grid), dim3(512), RCAB_LDS, (hipStream_t)stream, *d);
+    hipStream_t st = (hipStream_t)stream;
+    if (d->dtype == FEN_F16) {
+        if (d->t) hipLaunchKernelGGL((k_rcab<f16, true>), dim3(grid), dim3(512), RCAB_LDS, st, *d);
+        else hipLaunchKernelGGL((k_rcab<f16, false>), dim3(grid), dim3(512), RCAB_LDS, st, *d);
+    } else {
+        if (d->t) hipLaunchKernelGGL((k_rcab<bf16, true>), dim3(grid), dim3(512), RCAB_LDS, st, *d);
+        else hipLaunchKernelGGL((k_rcab<bf16, false>), dim3(grid), dim3(512), RCAB_LDS, st, *d);
+    }
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -54,7 +54,7 @@ __global__ void k_conv_first(int B, int Ci, int H, int W, int C, const float* __
     }
     char* o = (char*)y + (px * C + g * 8) * sizeof(T);
     if constexpr (sizeof(T) == 2) {
-        *(uint4*)o = pack16<bf16>(acc);
+        *(uint4*)o = pack16<T>(acc);
     } else {
         *(uint4*)o = pack16<float>(acc);
         *(uint4*)(o + 16) = pack16<float>(acc + 4);
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void k_conv_first4(int B, int Ci, int H, int W
             const size_t px = ((size_t)b * H + hq) * W + w0 + p;
             char* o = (char*)y + (px * C + g * 8) * sizeof(T);
             if constexpr (sizeof(T) == 2) {
-                *(uint4*)o = pack16<bf16>(acc[p]);
+                *(uint4*)o = pack16<T>(acc[p]);
             } else {
                 *(uint4*)o = pack16<float>(acc[p]);
                 *(uint4*)(o + 16) = pack16<float>(acc[p] + 4);
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
         }
         char* o = (char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 8 * k) * sizeof(T);
         if constexpr (sizeof(T) == 2) {
-            *(uint4*)o = pack16<bf16>(out);
+            *(uint4*)o = pack16<T>(out);
         } else {
             *(uint4*)o = pack16<float>(out);
             *(uint4*)(o + 16) = pack16<float>(out + 4);
@@ -719,7 +719,7 @@ __global__ __launch_bounds__(256) void k_prelu_bwd_unshuffle(int B, int H, int W
         }
         char* o = (char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 8 * k) * sizeof(T);
         if constexpr (sizeof(T) == 2) {
-            *(uint4*)o = pack16<bf16>(out);
+            *(uint4*)o = pack16<T>(out);
         } else {
             *(uint4*)o = pack16<float>(out);
             *(uint4*)(o + 16) = pack16<float>(out + 4);
@@ -948,6 +948,9 @@ extern "C" int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int
         if (dtype == FEN_BF16)
             hipLaunchKernelGGL(k_conv_first4<bf16>, dim3(nb), dim3(256), lds4, STREAM, B, Ci, H, W, C, x, w, bias,
                                (bf16*)y, in_mean, in_istd, act);
+        else if (dtype == FEN_F16)
+            hipLaunchKernelGGL(k_conv_first4<f16>, dim3(nb), dim3(256), lds4, STREAM, B, Ci, H, W, C, x, w, bias,
+                               (f16*)y, in_mean, in_istd, act);
         else if (dtype == FEN_F32)
             hipLaunchKernelGGL(k_conv_first4<float>, dim3(nb), dim3(256), lds4, STREAM, B, Ci, H, W, C, x, w, bias,
                                (float*)y, in_mean, in_istd, act);
@@ -959,6 +962,9 @@ extern "C" int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_conv_first<bf16>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
                            (bf16*)y, in_mean, in_istd, act);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_conv_first<f16>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
+                           (f16*)y, in_mean, in_istd, act);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_conv_first<float>, dim3(nblk(n)), dim3(256), lds, STREAM, B, Ci, H, W, C, x, w, bias,
                            (float*)y, in_mean, in_istd, act);
@@ -983,6 +989,9 @@ extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int 
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_conv_first_wgrad<bf16>, dim3(CF_BLOCKS), dim3(256), 0, STREAM, B, Ci, H, W, C, x,
                            (const bf16*)dy, work);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_conv_first_wgrad<f16>, dim3(CF_BLOCKS), dim3(256), 0, STREAM, B, Ci, H, W, C, x,
+                           (const f16*)dy, work);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_conv_first_wgrad<float>, dim3(CF_BLOCKS), dim3(256), 0, STREAM, B, Ci, H, W, C, x,
                            (const float*)dy, work);
@@ -1007,6 +1016,9 @@ extern "C" int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_conv_last_dgrad<bf16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co, (const bf16*)dout,
                            w, (const bf16*)pre, alpha, (bf16*)du, part);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_conv_last_dgrad<f16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co, (const f16*)dout,
+                           w, (const f16*)pre, alpha, (f16*)du, part);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_conv_last_dgrad<float>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co,
                            (const float*)dout, w, (const float*)pre, alpha, (float*)du, part);
@@ -1030,12 +1042,15 @@ extern "C" int fen_se_fwd(int B, int C, int Cr, int nparts, float inv_hw, const 
 extern "C" int fen_se_apply(int dtype, int B, int HW, int C, const void* t, const float* s, float res_scale,
                             const void* x, void* y, void* stream) {
     if (!t || !s || !x || !y) return FEN_EINVAL;
-    const int V = dtype == FEN_BF16 ? 8 : 4;
+    const int V = dtype == FEN_F32 ? 4 : 8;
     if (C % V) return FEN_EUNSUPPORTED;
     const size_t nvec = (size_t)B * HW * C / V;
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL((k_se_apply<bf16, false>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
                            (const bf16*)t, s, res_scale, x, (bf16*)y);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL((k_se_apply<f16, false>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
+                           (const f16*)t, s, res_scale, x, (f16*)y);
     else
         hipLaunchKernelGGL((k_se_apply<float, false>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
                            (const float*)t, s, res_scale, x, (float*)y);
@@ -1048,7 +1063,7 @@ extern "C" int fen_se_fused(int dtype, int B, int HW, int C, int Cr, int nparts,
                             float res_scale, const void* x, void* y, void* stream) {
     if (!part || !w1 || !w2 || !t || !x || !y || B <= 0 || HW <= 0 || nparts <= 0) return FEN_EINVAL;
     if (!se_shape_ok(C, Cr) || C * Cr > 4096) return FEN_EUNSUPPORTED;
-    const int V = dtype == FEN_BF16 ? 8 : 4;
+    const int V = dtype == FEN_F32 ? 4 : 8;
     const size_t nv = (size_t)HW * C / V;
     // 8 vectors per thread: 16 blocks per 64x64x64 bf16 image -> 512 blocks at B = 32
     constexpr int NPT = 8;
@@ -1056,6 +1071,9 @@ extern "C" int fen_se_fused(int dtype, int B, int HW, int C, int Cr, int nparts,
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL((k_se_fused<bf16, NPT>), dim3(splits, B), dim3(256), 0, STREAM, HW, C, Cr, nparts, inv_hw,
                            part, w1, w2, mean, hid, s, (const bf16*)t, res_scale, (const bf16*)x, (bf16*)y);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL((k_se_fused<f16, NPT>), dim3(splits, B), dim3(256), 0, STREAM, HW, C, Cr, nparts, inv_hw,
+                           part, w1, w2, mean, hid, s, (const f16*)t, res_scale, (const f16*)x, (f16*)y);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL((k_se_fused<float, NPT>), dim3(splits, B), dim3(256), 0, STREAM, HW, C, Cr, nparts, inv_hw,
                            part, w1, w2, mean, hid, s, (const float*)t, res_scale, (const float*)x, (float*)y);
@@ -1080,12 +1098,15 @@ extern "C" size_t fen_pool_parts(int HW) {
 
 extern "C" int fen_pool_dot(int dtype, int B, int HW, int C, const void* a, const void* b_, float* part,
                             void* stream) {
-    const int V = dtype == FEN_BF16 ? 8 : 4;
+    const int V = dtype == FEN_F32 ? 4 : 8;
     if (!a || !part || C % V || C / V > 256) return FEN_EINVAL;
     const int nchunk = (int)fen_pool_parts(HW);
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_pool_dot<bf16>, dim3(nchunk, B), dim3(256), 0, STREAM, HW, C, nchunk, (const bf16*)a,
                            (const bf16*)b_, part);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_pool_dot<f16>, dim3(nchunk, B), dim3(256), 0, STREAM, HW, C, nchunk, (const f16*)a,
+                           (const f16*)b_, part);
     else
         hipLaunchKernelGGL(k_pool_dot<float>, dim3(nchunk, B), dim3(256), 0, STREAM, HW, C, nchunk, (const float*)a,
                            (const float*)b_, part);
@@ -1110,12 +1131,15 @@ extern "C" int fen_se_bwd(int B, int C, int Cr, int nparts, float inv_hw, float 
 extern "C" int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy, const float* s, float res_scale,
                                 const float* g, void* dt, void* stream) {
     if (!dy || !s || !g || !dt) return FEN_EINVAL;
-    const int V = dtype == FEN_BF16 ? 8 : 4;
+    const int V = dtype == FEN_F32 ? 4 : 8;
     if (C % V) return FEN_EUNSUPPORTED;
     const size_t nvec = (size_t)B * HW * C / V;
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL((k_se_apply<bf16, true>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
                            (const bf16*)dy, s, res_scale, (const void*)g, (bf16*)dt);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL((k_se_apply<f16, true>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
+                           (const f16*)dy, s, res_scale, (const void*)g, (f16*)dt);
     else
         hipLaunchKernelGGL((k_se_apply<float, true>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
                            (const float*)dy, s, res_scale, (const void*)g, (float*)dt);
@@ -1163,6 +1187,8 @@ extern "C" int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const flo
     const size_t n = fen_packed_elems(mode, Cout, Cin);
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_pack<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, mode, Cout, Cin, w, (bf16*)out, n);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_pack<f16>, dim3(nblk(n)), dim3(256), 0, STREAM, mode, Cout, Cin, w, (f16*)out, n);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_pack<float>, dim3(nblk(n)), dim3(256), 0, STREAM, mode, Cout, Cin, w, (float*)out, n);
     else
@@ -1176,7 +1202,7 @@ extern "C" size_t fen_pack_table_bytes(int njobs) {
 }
 
 extern "C" int fen_pack_table(int dtype, int njobs, const fen_pack_job* jobs, void* table_host, size_t* total) {
-    if (njobs <= 0 || !jobs || !table_host || !total || (dtype != FEN_BF16 && dtype != FEN_F32)) return FEN_EINVAL;
+    if (njobs <= 0 || !jobs || !table_host || !total || (dtype != FEN_BF16 && dtype != FEN_F16 && dtype != FEN_F32)) return FEN_EINVAL;
     PackJobK* pj = (PackJobK*)table_host;
     unsigned long long* e0 = (unsigned long long*)(pj + njobs);
     unsigned long long acc = 0;
@@ -1199,6 +1225,8 @@ extern "C" int fen_pack_multi(int dtype, int njobs, const void* table_dev, size_
     const unsigned nb = (unsigned)((total + 255) / 256);
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_pack_multi<bf16>, dim3(nb), dim3(256), 0, STREAM, njobs, pj, e0, (unsigned long long)total);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_pack_multi<f16>, dim3(nb), dim3(256), 0, STREAM, njobs, pj, e0, (unsigned long long)total);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_pack_multi<float>, dim3(nb), dim3(256), 0, STREAM, njobs, pj, e0, (unsigned long long)total);
     else
@@ -1213,6 +1241,8 @@ extern "C" int fen_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cpad,
     const size_t n = (size_t)B * Cpad * H * W;
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_nchw_to_nhwc<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, Cpad, x, (bf16*)y);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_nchw_to_nhwc<f16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, Cpad, x, (f16*)y);
     else
         hipLaunchKernelGGL(k_nchw_to_nhwc<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, Cpad, x, (float*)y);
     FEN_CHECK_LAUNCH();
@@ -1227,6 +1257,9 @@ extern "C" int fen_prelu_bwd_unshuffle(int dtype, int B, int H, int W, int C, co
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_prelu_bwd_unshuffle<bf16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, (const bf16*)dy,
                            (const bf16*)pre, alpha, (bf16*)du, part);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_prelu_bwd_unshuffle<f16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, (const f16*)dy,
+                           (const f16*)pre, alpha, (f16*)du, part);
     else
         hipLaunchKernelGGL(k_prelu_bwd_unshuffle<float>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C,
                            (const float*)dy, (const float*)pre, alpha, (float*)du, part);
@@ -1239,6 +1272,8 @@ extern "C" int fen_nhwc_to_nchw(int dtype, int B, int C, int H, int W, const voi
     const size_t n = (size_t)B * C * H * W;
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_nhwc_to_nchw<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, (const bf16*)x, y);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_nhwc_to_nchw<f16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, (const f16*)x, y);
     else
         hipLaunchKernelGGL(k_nhwc_to_nchw<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, C, H, W, (const float*)x, y);
     FEN_CHECK_LAUNCH();

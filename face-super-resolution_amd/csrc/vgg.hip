@@ -124,10 +124,13 @@ __global__ __launch_bounds__(256) void k_feat_loss(size_t n, const T* __restrict
 
 extern "C" int fen_maxpool2(int dtype, int B, int H, int W, int C, const void* x, void* y, void* stream) {
     if (!x || !y || B <= 0 || (H | W) & 1 || H <= 0 || W <= 0 || C % 8) return FEN_EINVAL;
-    const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / (dtype == FEN_BF16 ? 8 : 4));
+    const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / (dtype == FEN_F32 ? 4 : 8));
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_maxpool2<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, H / 2, W / 2, C, (const bf16*)x,
                            (bf16*)y);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_maxpool2<f16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, H / 2, W / 2, C, (const f16*)x,
+                           (f16*)y);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_maxpool2<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, H / 2, W / 2, C, (const float*)x,
                            (float*)y);
@@ -140,10 +143,13 @@ extern "C" int fen_maxpool2(int dtype, int B, int H, int W, int C, const void* x
 extern "C" int fen_maxpool2_bwd_relu(int dtype, int B, int H, int W, int C, const void* dy, const void* a, void* dx,
                                      void* stream) {
     if (!dy || !a || !dx || B <= 0 || (H | W) & 1 || H <= 0 || W <= 0 || C % 8) return FEN_EINVAL;
-    const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / (dtype == FEN_BF16 ? 8 : 4));
+    const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / (dtype == FEN_F32 ? 4 : 8));
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_maxpool2_bwd_relu<bf16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, H / 2, W / 2, C,
                            (const bf16*)dy, (const bf16*)a, (bf16*)dx);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_maxpool2_bwd_relu<f16>, dim3(nblk(n)), dim3(256), 0, STREAM, B, H / 2, W / 2, C,
+                           (const f16*)dy, (const f16*)a, (f16*)dx);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_maxpool2_bwd_relu<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, H / 2, W / 2, C,
                            (const float*)dy, (const float*)a, (float*)dx);
@@ -161,6 +167,9 @@ extern "C" int fen_feat_loss(int dtype, size_t n, const void* f, int l2, float s
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_feat_loss<bf16>, dim3(FL_BLOCKS), dim3(256), 0, STREAM, n, (const bf16*)f, l2, scale,
                            (bf16*)g, accumulate, part);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL(k_feat_loss<f16>, dim3(FL_BLOCKS), dim3(256), 0, STREAM, n, (const f16*)f, l2, scale,
+                           (f16*)g, accumulate, part);
     else if (dtype == FEN_F32)
         hipLaunchKernelGGL(k_feat_loss<float>, dim3(FL_BLOCKS), dim3(256), 0, STREAM, n, (const float*)f, l2, scale,
                            (float*)g, accumulate, part);

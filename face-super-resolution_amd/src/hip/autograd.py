@@ -61,6 +61,9 @@ class Runtime:
         self.module = module
         self.weights = None
         self.shared: dict = {}            # eager contexts' long-lived state (fused-RCAB workspace)
+        # the caller's grad mode (set by the module's forward: inside Function.forward grad mode
+        # is always off, and ctx.needs_input_grad stays True for parameters under no_grad)
+        self.grad_mode = True
 
     def wt(self, device) -> LiveWeights:
         if self.weights is None or self.weights.device != device:
@@ -75,6 +78,14 @@ class Runtime:
 def _check_input(x: torch.Tensor):
     if not x.is_cuda:
         raise RuntimeError("the HIP backend runs on a ROCm GPU tensor (got a CPU tensor); there is no CPU path")
+
+
+def _check_grad(rt: "Runtime"):
+    """fp16 is an inference precision here: the reference trains fp16 only under a GradScaler
+    (trainer.py:227,482-503), and unscaled fp16 activation gradients underflow (the L1
+    gradient of a B=32 256x256 batch is 1.6e-7, a subnormal)."""
+    if rt.dtype == torch.float16:
+        raise NotImplementedError("precision='fp16' is inference-only on the HIP backend; train in 'bf16' or 'fp32'")
 
 
 # ---------------------------------------------------------------- FaceEnhanceNet pieces
@@ -96,6 +107,7 @@ class HeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, d):
+        _check_grad(ctx.rt)
         (x,) = ctx.saved_tensors
         rt = ctx.rt
         c = rt.ctx(x.device)
@@ -114,13 +126,14 @@ class GroupFn(torch.autograd.Function):
         xh = to_nhwc(x, rt.dtype)
         W = rt.wt(x.device)
         c = rt.ctx(x.device)
-        fw = Forward(rt.spec, c, W, save=any(ctx.needs_input_grad), attn=attn)
+        fw = Forward(rt.spec, c, W, save=rt.grad_mode and any(ctx.needs_input_grad), attn=attn)
         y, sv = fw.group(xh, 0, pre="")
         ctx.rt, ctx.sv = rt, sv
         return as_nchw(y)
 
     @staticmethod
     def backward(ctx, dy):
+        _check_grad(ctx.rt)
         rt, sv = ctx.rt, ctx.sv
         dyh = to_nhwc(dy, rt.dtype)
         c = rt.ctx(dy.device)
@@ -141,12 +154,13 @@ class TailFn(torch.autograd.Function):
         f0 = to_nhwc(feat0, rt.dtype)
         W = rt.wt(feat.device)
         c = rt.ctx(feat.device)
-        out, sv = Forward(rt.spec, c, W, save=True).tail(fh, f0, x, training=not clamp)
+        out, sv = Forward(rt.spec, c, W, save=rt.grad_mode).tail(fh, f0, x, training=not clamp)
         ctx.rt, ctx.sv = rt, sv
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        _check_grad(ctx.rt)
         rt, sv = ctx.rt, ctx.sv
         s = rt.spec
         B, Co, Ho, Wo = dout.shape
@@ -174,12 +188,13 @@ class RCABFn(torch.autograd.Function):
         _check_input(x)
         xh = to_nhwc(x, rt.dtype)
         c = rt.ctx(x.device)
-        y, sv = Forward(rt.spec, c, rt.wt(x.device), save=True).rcab(xh, "")
+        y, sv = Forward(rt.spec, c, rt.wt(x.device), save=rt.grad_mode).rcab(xh, "")
         ctx.rt, ctx.sv = rt, sv
         return as_nchw(y)
 
     @staticmethod
     def backward(ctx, dy):
+        _check_grad(ctx.rt)
         rt, sv = ctx.rt, ctx.sv
         c = rt.ctx(dy.device)
         named = list(rt.module.named_parameters())
@@ -218,6 +233,7 @@ class ChannelAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _check_grad(ctx.rt)
         th, mean, hid, s, w1, w2 = ctx.saved_tensors
         rt = ctx.rt
         B, H, W, C = th.shape
@@ -267,6 +283,7 @@ class UpsampleFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _check_grad(ctx.rt)
         from .net import conv
         rt, stages = ctx.rt, ctx.stages
         c = rt.ctx(dy.device)

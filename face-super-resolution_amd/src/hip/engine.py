@@ -50,6 +50,8 @@ class FENEngine:
         dict(weight=, layers=, criterion=, normalize=, params={'features.i.weight': ...},
         layer_weights=None); its gradient joins the fused L1 gradient in dL/dsr.  ssim_weight
         (training only): the stage-2 term weight * (1 - SSIM) (ssim_loss.py:174-226), likewise."""
+        if train and dtype == torch.float16:
+            raise NotImplementedError("fp16 is an inference precision on the HIP backend (train in bf16 or fp32)")
         self.spec = NetSpec.from_config(model.config)
         self.dtype, self.device, self.train = dtype, torch.device(device), train
         self.B, (self.h, self.w) = batch, lr_hw

@@ -13,7 +13,7 @@ from ctypes import POINTER, Structure, c_float, c_int, c_size_t, c_void_p
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEN_HIP_LIB", os.path.join(_HERE, "libfen_hip.so"))
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 
 EPI_BIAS = 1
 EPI_PRELU = 2
@@ -158,6 +158,8 @@ def dtype_code(torch_dtype) -> int:
         return F32
     if torch_dtype == torch.bfloat16:
         return BF16
+    if torch_dtype == torch.float16:
+        return F16
     raise FenError(f"unsupported compute dtype {torch_dtype}")
 
 

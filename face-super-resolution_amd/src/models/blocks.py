@@ -14,7 +14,8 @@ import torch.nn as nn
 from ..hip.autograd import ChannelAttentionFn, GroupFn, RCABFn, Runtime, UpsampleFn
 from ..hip.net import NetSpec
 
-_DTYPES = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+_DTYPES = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
+           "fp16": torch.float16, "float16": torch.float16}
 
 
 def compute_dtype(precision: str) -> torch.dtype:
@@ -81,6 +82,7 @@ class RCAB(nn.Module):
         self._rt = Runtime(self, spec, compute_dtype(precision))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        self._rt.grad_mode = torch.is_grad_enabled()
         return RCABFn.apply(x, self._rt, *[p for _, p in self.named_parameters()])
 
 
@@ -102,6 +104,7 @@ class ResidualGroup(nn.Module):
         self._attn = None  # set by FaceEnhanceNet.get_attention_maps
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        self._rt.grad_mode = torch.is_grad_enabled()
         return GroupFn.apply(x, self._rt, self._attn, *[p for _, p in self.named_parameters()])
 
 

@@ -6,7 +6,7 @@
  * types.  Every entry point is asynchronous on `stream`, allocates nothing, never syncs,
  * and returns 0 (FEN_OK) or a negative fen_status.  fen_status_string() names the code.
  *
- * Activations are NHWC (channels-last) in the compute dtype (FEN_F32 or FEN_BF16).
+ * Activations are NHWC (channels-last) in the compute dtype (FEN_F32, FEN_BF16 or FEN_F16).
  * Weights are the reference's OIHW fp32 tensors; fen_pack_conv_w() repacks them into the
  * kernel layout [9 taps][Cout_pad][Cin] of the compute dtype.
  *
@@ -30,7 +30,7 @@ typedef enum {
     FEN_EHIP = -3           /* a HIP launch error                               */
 } fen_status;
 
-typedef enum { FEN_F32 = 0, FEN_BF16 = 1 } fen_dtype;
+typedef enum { FEN_F32 = 0, FEN_BF16 = 1, FEN_F16 = 2 } fen_dtype;
 
 /* conv3x3 epilogue flags (fen_conv_desc.epi) */
 enum {

@@ -95,10 +95,10 @@ def _seeded(ctor, golden_npz):
         num_channels=128, num_groups=10, blocks_per_group=20, reduction_ratio=4, scale_factor=8, precision=p)),
     ("g6_lite.npz", lambda p: __import__("src.models", fromlist=["x"]).FaceEnhanceNetLite(precision=p)),
 ])
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 def test_full_networks_vs_reference(golden, name, ctor, precision):
     g = golden(name)
-    if precision == "bf16" and name == "g6_lite.npz":
+    if precision != "fp32" and name == "g6_lite.npz":
         pytest.skip("bf16 kernels need channel counts that are multiples of 64 (Lite is 32)")
     m = _seeded(lambda: ctor(precision), g).to(DEV)
     x = torch.from_numpy(g["x"]).to(DEV)
@@ -120,16 +120,19 @@ def test_full_networks_vs_reference(golden, name, ctor, precision):
         else:
             assert float((out_e.double() - f64).abs().max()) <= 2 * ref_err, ref_err
     else:
-        # PSNR parity against a fixed target (the bicubic upsample of the input, in fp64)
+        # PSNR parity against a fixed target (the bicubic upsample of the input, in fp64; these
+        # goldens have noise inputs and no HR -- g9, tests/test_gpu_northstar.py, is the HR case)
         tgt = O.bicubic(x.cpu().double(), m.scale_factor).clamp(0, 1)
-        # Tolerance 0.015 dB for the 64-channel nets: two valid bf16 implementations of the
-        # same net differ by fp32 summation order alone -- measured on g4: fused RCAB 0.0109 dB,
-        # per-op RCAB 0.0093 dB (tools/dbg_psnr.py) -- plus a per-pixel bound, 6e-3 on [0,1]
-        # outputs (measured 3.8e-3 / 4.1e-3).  The 128-channel x8 net (config 5, which the
-        # reference itself runs in fp16) carries body activations of O(1e3), so bf16's 8-bit
-        # mantissa costs more there: 0.05 dB.
-        tol = 0.05 if name == "g5_c128.npz" else 0.015
+        # 0.01 dB (north_star) for the 64-channel nets in both 16-bit formats (measured: bf16
+        # 0.0084, fp16 0.0014 dB on g4), plus a per-pixel bound, 6e-3 on [0,1] outputs.  The
+        # 128-channel x8 net (config 5, which the reference runs in fp16) carries body
+        # activations of O(1e3): fp16 0.0051 dB (gate 0.01), bf16 0.0105 dB (gate 0.02, bf16's
+        # weight rounding alone: tools/numerics_bf16.py).
+        tol = 0.01
+        if name == "g5_c128.npz" and precision == "bf16":
+            tol = 0.02
         d = abs(O.psnr(out_e, tgt) - O.psnr(ref_e, tgt))
+        print(f"{name} {precision}: dPSNR {d:.5f} dB, max|d| {float((out_e - ref_e).abs().max()):.2e}")
         assert d <= tol, d
         if name != "g5_c128.npz":
             assert float((out_e - ref_e).abs().max()) <= 6e-3
