@@ -108,13 +108,16 @@ def timed(fn, steps, warmup, world):
 
 
 def dominant_op(engine):
-    """The launch the roofline is quoted on: the fused RCAB block (fen_rcab_fused) when the
-    engine uses it, else the RCAB conv1 (64->64, 64x64, B=32) of the per-op path."""
+    """The launch the roofline is quoted on: an RCAB of the chain (fen_rcab_deferred: gate of
+    the previous RCAB applied to its input, conv1 + PReLU + conv2 + tile sums; one with a
+    deferred input, i.e. not a group's first), else the RCAB conv1 (64->64, 64x64, B=32) of
+    the per-op path."""
     for op in engine.ctx.ops:
-        if op[0] == "rcab_fused":
+        if op[0] == "rcab_deferred":
             d = op[2][0]._obj
-            return op, "k_rcab (fused RCAB: conv1+PReLU+conv2+SE gate+residual, 64ch 64x64, B=%d)" % d.B, \
-                2 * 2.0 * d.B * d.H * d.W * 64 * 576
+            if d.tp:
+                return op, "k_rcab_d (RCAB: prev. SE gate + residual applied to the input halo, conv1+PReLU+conv2+" \
+                           "tile sums, 64ch 64x64, B=%d)" % d.B, 2 * 2.0 * d.B * d.H * d.W * 64 * 576
     for op in engine.ctx.ops:
         if op[0] == "conv3x3" and op[1] is not None:
             d = op[2][0]._obj

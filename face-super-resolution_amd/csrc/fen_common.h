@@ -50,17 +50,19 @@ template <typename T> __device__ __forceinline__ float lo16(unsigned w);
 template <typename T> __device__ __forceinline__ float hi16(unsigned w);
 template <> __device__ __forceinline__ float lo16<bf16>(unsigned w) { return __uint_as_float(w << 16); }
 template <> __device__ __forceinline__ float hi16<bf16>(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
-template <> __device__ __forceinline__ float lo16<f16>(unsigned w) {
-    return (float)__builtin_bit_cast(f16, (unsigned short)(w & 0xffffu));
-}
-template <> __device__ __forceinline__ float hi16<f16>(unsigned w) {
-    return (float)__builtin_bit_cast(f16, (unsigned short)(w >> 16));
-}
+// fp16 halves through a 2-vector: v_cvt_f32_f16 (the high half via SDWA word select, one
+// instruction) and v_cvt_pk_f16_f32 (two floats, one instruction, round-to-nearest-even)
+template <> __device__ __forceinline__ float lo16<f16>(unsigned w) { return (float)__builtin_bit_cast(f16x2, w).x; }
+template <> __device__ __forceinline__ float hi16<f16>(unsigned w) { return (float)__builtin_bit_cast(f16x2, w).y; }
 template <typename T> __device__ __forceinline__ unsigned short to16(float f);
 template <> __device__ __forceinline__ unsigned short to16<bf16>(float f) { return f2bf(f); }
 template <> __device__ __forceinline__ unsigned short to16<f16>(float f) { return __builtin_bit_cast(unsigned short, (f16)f); }
 template <typename T> __device__ __forceinline__ unsigned pack2(float lo, float hi) {
     return (unsigned)to16<T>(lo) | ((unsigned)to16<T>(hi) << 16);
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <> __device__ __forceinline__ unsigned pack2<f16>(float lo, float hi) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){lo, hi}, f16x2));
 }
 
 template <typename T> __device__ __forceinline__ float tof(T v);

@@ -43,13 +43,14 @@ class PackJob(Structure):
     _fields_ = [("w", c_void_p), ("out", c_void_p), ("mode", c_int), ("Cout", c_int), ("Cin", c_int)]
 
 
-class RcabDesc(Structure):
+class RcabDeferredDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("Cr", c_int),
-        ("x", c_void_p), ("w1", c_void_p), ("b1", c_void_p), ("alpha", c_void_p), ("w2", c_void_p),
-        ("b2", c_void_p), ("fc1", c_void_p), ("fc2", c_void_p), ("res_scale", c_float), ("inv_hw", c_float),
-        ("y", c_void_p), ("z1", c_void_p), ("a1", c_void_p), ("t", c_void_p), ("s", c_void_p), ("mean", c_void_p),
-        ("hid", c_void_p), ("ws", c_void_p), ("stamps", c_void_p),
+        ("x", c_void_p), ("tp", c_void_p), ("pp", c_void_p), ("pfc1", c_void_p), ("pfc2", c_void_p),
+        ("res_scale", c_float), ("inv_hw", c_float), ("ps", c_void_p), ("pmean", c_void_p), ("phid", c_void_p),
+        ("xo", c_void_p), ("w1", c_void_p), ("b1", c_void_p), ("alpha", c_void_p), ("w2", c_void_p),
+        ("b2", c_void_p), ("t", c_void_p), ("part", c_void_p), ("z1", c_void_p), ("a1", c_void_p),
+        ("stamps", c_void_p),
     ]
 
 
@@ -65,12 +66,8 @@ _SIGS = {
     "fen_conv3x3": (c_int, [POINTER(ConvDesc), c_void_p]),
     "fen_wgrad_work_floats": (c_size_t, [POINTER(WgradDesc)]),
     "fen_wgrad3x3": (c_int, [POINTER(WgradDesc), c_void_p]),
-    "fen_rcab_supported": (c_int, [c_int] * 6),
-    "fen_rcab_workspace_bytes": (c_size_t, [c_int] * 3),
-    "fen_rcab_workspace_alloc": (c_int, [c_int] * 3 + [POINTER(c_void_p)]),
-    "fen_rcab_workspace_free": (c_int, [c_void_p]),
-    "fen_rcab_workspace_status": (c_int, [c_void_p, c_int, c_int, c_int]),
-    "fen_rcab_fused": (c_int, [POINTER(RcabDesc), c_void_p]),
+    "fen_rcab_deferred_supported": (c_int, [c_int] * 6),
+    "fen_rcab_deferred": (c_int, [POINTER(RcabDeferredDesc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
     "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),
@@ -161,20 +158,3 @@ def dtype_code(torch_dtype) -> int:
     if torch_dtype == torch.float16:
         return F16
     raise FenError(f"unsupported compute dtype {torch_dtype}")
-
-
-class RcabWorkspace:
-    """Owner of one fen_rcab_workspace_alloc buffer (uncached device memory, zeroed)."""
-
-    def __init__(self, B: int, H: int, W: int):
-        lib = load()
-        self.nbytes = lib.fen_rcab_workspace_bytes(B, H, W)
-        p = c_void_p()
-        check(lib.fen_rcab_workspace_alloc(B, H, W, ctypes.byref(p)), "rcab_workspace_alloc")
-        self.ptr = p.value
-        self._lib = lib
-
-    def __del__(self):
-        if getattr(self, "ptr", None):
-            self._lib.fen_rcab_workspace_free(self.ptr)
-            self.ptr = None

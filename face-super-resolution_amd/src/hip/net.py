@@ -50,9 +50,11 @@ class NetSpec:
                        res_scale=float(cfg.res_scale), in_ch=cfg.in_channels, out_ch=cfg.out_channels)
 
 
-# fused RCAB forward (fen_rcab_fused, one launch per RCAB) where supported; FEN_RCAB_FUSED=0
-# selects the per-op launches (B=32 64x64: 46.7 vs 52.0 us per RCAB, tools/bench_rcab.py)
-FUSED_RCAB = os.environ.get("FEN_RCAB_FUSED", "1") != "0"
+# RCAB chain implementation (FEN_RCAB): 'deferred' (default) -- fen_rcab_deferred, one launch
+# per RCAB whose SE gate is applied by the next launch (the chain end by fen_se_fused), no
+# in-launch synchronisation between blocks; 'perop' -- conv1(+PReLU) / conv2(+pool) / SE
+# launches (shapes outside the deferred kernel's envelope always take this path).
+RCAB_MODE = os.environ.get("FEN_RCAB", "deferred")
 
 
 def tiles(H: int, W: int) -> int:
@@ -198,12 +200,14 @@ class Forward:
         return feat
 
     def rcab(self, x: torch.Tensor, pre: str, out: Optional[torch.Tensor] = None, name: Optional[str] = None):
-        """RCAB (blocks.py:135-153) -> (y, saved).  One fused launch (fen_rcab_fused) where the
-        shape allows it, else conv1(+PReLU) / conv2(+pool) / SE gate+apply launches."""
+        """RCAB (blocks.py:135-153) -> (y, saved).  A one-RCAB chain on fen_rcab_deferred + the
+        fen_se_fused gate/residual where the shape allows it, else conv1(+PReLU) / conv2(+pool) /
+        SE gate+apply launches."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
-        if FUSED_RCAB and ctx.lib.fen_rcab_supported(ctx.code, B, H, W, C, s.Cr):
-            return self._rcab_fused(x, pre, out, name)
+        if self._deferred_ok(x):
+            y, saved = self._chain(x, [pre], [name], out)
+            return y, saved[0]
         a1 = ctx.alloc(x.shape) if self.save else ctx.scratch("rcab_a1", x.shape)
         z1 = ctx.alloc(x.shape) if self.save else None
         conv(ctx, x, Wt.packed(pre + "conv1", 0), B, H, W, C, C, bias=p[pre + "conv1.bias"],
@@ -230,35 +234,62 @@ class Forward:
         saved = dict(x=x, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg) if self.save else dict(s=sg)
         return y, saved
 
-    def _rcab_fused(self, x, pre, out, name):
+    def _deferred_ok(self, x) -> bool:
+        B, H, W, C = x.shape
+        return RCAB_MODE == "deferred" and bool(self.ctx.lib.fen_rcab_deferred_supported(self.ctx.code, B, H, W, C,
+                                                                                           self.s.Cr))
+
+    def _chain(self, x: torch.Tensor, pres: Sequence[str], names: Sequence[Optional[str]],
+               out: Optional[torch.Tensor] = None):
+        """A chain of RCABs (blocks.py:135-153; a ResidualGroup's blocks, blocks.py:185-188) on
+        fen_rcab_deferred: launch j computes t_j and its tile sums and applies RCAB j-1's gate to
+        build x_j; the chain end's gate and residual are fen_se_fused.  -> (y, [saved per RCAB])."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
-        d = L.RcabDesc()
-        d.dtype, d.B, d.H, d.W, d.C, d.Cr = ctx.code, B, H, W, C, s.Cr
-        ca = pre + "channel_attention.fc."
-        d.x, d.w1, d.b1 = ptr(x), ptr(Wt.packed(pre + "conv1", 0)), ptr(p[pre + "conv1.bias"])
-        d.alpha, d.w2, d.b2 = ptr(p[pre + "prelu.weight"]), ptr(Wt.packed(pre + "conv2", 0)), ptr(p[pre + "conv2.bias"])
-        d.fc1, d.fc2 = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
-        d.res_scale, d.inv_hw = float(s.res_scale), 1.0 / (H * W)
+        T = tiles(H, W)
+        n = len(pres)
+        want_s = self.save or self.attn is not None
+        saved: List[dict] = []
+        prev = None
+        for j, (pre, name) in enumerate(zip(pres, names)):
+            d = L.RcabDeferredDesc()
+            d.dtype, d.B, d.H, d.W, d.C, d.Cr = ctx.code, B, H, W, C, s.Cr
+            d.res_scale, d.inv_hw = float(s.res_scale), 1.0 / (H * W)
+            d.w1, d.b1 = ptr(Wt.packed(pre + "conv1", 0)), ptr(p[pre + "conv1.bias"])
+            d.alpha = ptr(p[pre + "prelu.weight"])
+            d.w2, d.b2 = ptr(Wt.packed(pre + "conv2", 0)), ptr(p[pre + "conv2.bias"])
+            if prev is None:
+                xin = x
+                d.x = ptr(x)
+            else:
+                xin = ctx.alloc(x.shape) if self.save else ctx.scratch(f"rd_x{j & 1}", x.shape)
+                ca = prev["pre"] + "channel_attention.fc."
+                d.x, d.tp, d.pp = ptr(prev["x"]), ptr(prev["t"]), ptr(prev["part"])
+                d.pfc1, d.pfc2 = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
+                d.ps, d.pmean, d.phid = ptr(prev["s"]), ptr(prev["mean"]), ptr(prev["hid"])
+                d.xo = ptr(xin)
+            t = ctx.alloc(x.shape) if self.save else ctx.scratch(f"rd_t{j & 1}", x.shape)
+            part = (ctx.alloc((B * T, C), torch.float32) if self.save
+                    else ctx.scratch(f"rd_p{j & 1}", (B * T, C), torch.float32))
+            d.t, d.part = ptr(t), ptr(part)
+            z1 = a1 = None
+            if self.save:
+                z1, a1 = ctx.alloc(x.shape), ctx.alloc(x.shape)
+                d.z1, d.a1 = ptr(z1), ptr(a1)
+            sg = ctx.alloc((B, C), torch.float32) if want_s else None
+            mean = ctx.alloc((B, C), torch.float32) if self.save else None
+            hid = ctx.alloc((B, s.Cr), torch.float32) if self.save else None
+            ctx.emit("rcab_deferred", ctx.lib.fen_rcab_deferred, byref(d))
+            if self.attn is not None and name is not None:
+                self.attn[name] = sg
+            prev = dict(pre=pre, x=xin, t=t, part=part, s=sg, mean=mean, hid=hid)
+            saved.append(dict(x=xin, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg) if self.save else dict(s=sg))
+        # chain end: the last RCAB's gate + residual
         y = out if out is not None else ctx.alloc(x.shape)
-        d.y = ptr(y)
-        if self.save:
-            z1, a1, t = ctx.alloc(x.shape), ctx.alloc(x.shape), ctx.alloc(x.shape)
-            mean = ctx.alloc((B, C), torch.float32)
-            hid = ctx.alloc((B, s.Cr), torch.float32)
-            sg = ctx.alloc((B, C), torch.float32)
-            d.z1, d.a1, d.t, d.mean, d.hid = ptr(z1), ptr(a1), ptr(t), ptr(mean), ptr(hid)
-        else:
-            sg = ctx.scratch("se_s", (B, C), torch.float32)
-        d.s = ptr(sg)
-        d.ws = ctx.rcab_workspace(B, H, W).ptr
-        ctx.emit("rcab_fused", ctx.lib.fen_rcab_fused, byref(d))
-        if self.attn is not None and name is not None:
-            self.attn[name] = sg
-        if self.save:
-            saved = dict(x=x, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg)
-        else:
-            saved = dict(s=sg)
+        ca = prev["pre"] + "channel_attention.fc."
+        ctx.emit("se_fused", ctx.lib.fen_se_fused, ctx.code, B, H * W, C, s.Cr, T, 1.0 / (H * W), ptr(prev["part"]),
+                 ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]), ptr(prev["mean"]), ptr(prev["hid"]),
+                 ptr(prev["s"]), ptr(prev["t"]), s.res_scale, ptr(prev["x"]), ptr(y))
         return y, saved
 
     def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None, pre: Optional[str] = None):
@@ -266,6 +297,13 @@ class Forward:
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
         pre = f"residual_groups.{g}." if pre is None else pre
+        if self._deferred_ok(x) and s.NB > 0:
+            y_last = ctx.alloc(x.shape) if self.save else ctx.scratch("rd_y", x.shape)
+            h, blocks = self._chain(x, [f"{pre}blocks.{b}." for b in range(s.NB)],
+                                    [f"group{g}_rcab{b}" for b in range(s.NB)], out=y_last)
+            y = out if out is not None else ctx.alloc(x.shape)
+            conv(ctx, h, Wt.packed(pre + "conv", 0), B, H, W, C, C, bias=p[pre + "conv.bias"], y=y, res=(x,))
+            return y, dict(blocks=blocks, x=x, x_last=h)
         blocks = []
         h = x
         for b in range(s.NB):

@@ -30,7 +30,7 @@ class Ctx:
         self._scratch: Dict[str, torch.Tensor] = {}
         self._hold: List[torch.Tensor] = []   # replaced scratch buffers still referenced by ops
         self.lib = L.load()
-        # long-lived state shared by short-lived eager contexts (the fused-RCAB workspace)
+        # long-lived state shared by short-lived eager contexts
         self._shared = {} if shared is None else shared
 
     # ---- memory ----
@@ -74,19 +74,6 @@ class Ctx:
             buf = torch.zeros(n, dtype=dtype, device=self.device)
             self._scratch[key] = buf
         return buf[:n].view(tuple(shape))
-
-    def rcab_workspace(self, B: int, H: int, W: int):
-        """The fused-RCAB hand-off workspace (grown on demand).  One per program -- or per
-        owner of `shared` for eager contexts: launches that share one must run one at a time
-        (one stream), which a program's replay and a module's forward both do."""
-        ws = self._shared.get("rcab_ws")
-        need = self.lib.fen_rcab_workspace_bytes(B, H, W)
-        if ws is None or ws.nbytes < need:
-            if ws is not None:
-                self._hold.append(ws)
-            ws = L.RcabWorkspace(B, H, W)
-            self._shared["rcab_ws"] = ws
-        return ws
 
     def keep(self, obj) -> None:
         """Keep a host object (e.g. a ctypes job table) alive as long as the program."""

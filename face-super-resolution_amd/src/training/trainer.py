@@ -97,6 +97,23 @@ def dist_info():
     return 0, 1
 
 
+def reduce_val_metrics(tl: float, tp: float, ts: float, n: int, world: int, device=None):
+    """Per-rank validation sums -> the global batch means (trainer.py:552-619 computes the mean
+    over all validation batches).  Under DP every rank validates its own shard, so the sums and
+    batch counts are all-reduced first: every rank then sees the same metrics, so plateau
+    scheduling, best-model selection and early stopping decide identically on every rank (a
+    rank-local decision would let one rank leave train() while the others block in the next
+    all-reduce)."""
+    if world > 1:
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([tl, tp, ts, float(n)], dtype=torch.float64, device=device)
+        dist.all_reduce(t)
+        tl, tp, ts, n = t.tolist()
+    n = max(n, 1)
+    return {"loss": tl / n, "psnr": tp / n, "ssim": ts / n}
+
+
 def bicubic_down4(hr: torch.Tensor) -> torch.Tensor:
     """trainer.py:416-421 LR synthesis on the GPU (fen_bicubic_down4)."""
     B, C, H, W = hr.shape
@@ -287,7 +304,9 @@ class Trainer:
         return {"loss": total / max(n, 1), "l1": total / max(n, 1)}
 
     @torch.no_grad()
+    @torch.no_grad()
     def _validate_epoch(self) -> Dict[str, float]:
+        """trainer.py:552-619 (sample grids / W&B images out of scope); DP: global means."""
         self.model.eval()
         tl, tp, ts, n = 0.0, 0.0, 0.0, 0
         for batch in self.val_loader:
@@ -298,8 +317,7 @@ class Trainer:
             tp += self._compute_psnr(sr, hr)
             ts += self._compute_ssim(sr, hr)
             n += 1
-        n = max(n, 1)
-        return {"loss": tl / n, "psnr": tp / n, "ssim": ts / n}
+        return reduce_val_metrics(tl, tp, ts, n, self.world)
 
     def _compute_ssim(self, pred: torch.Tensor, target: torch.Tensor) -> float:
         """ssim(pred, target) with the reference defaults (trainer.py:630-634), on the HIP kernel."""

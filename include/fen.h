@@ -145,45 +145,44 @@ int fen_se_bwd(int B, int C, int Cr, int nparts, float inv_hw, float res_scale,
 int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy, const float* s,
                      float res_scale, const float* g, void* dt, void* stream);
 
-/* Fused RCAB forward (blocks.py:135-153, ChannelAttention blocks.py:83-92) in ONE launch:
- *   z1 = conv1(x)+b1, a1 = PReLU(z1), t = conv2(a1)+b2, s = sigmoid(fc2 relu(fc1 mean_hw t)),
- *   y = t*s*res_scale + x.
- * bf16 NHWC, C = 64, Cr <= 16, H and W multiples of 16, (H/16)*(W/16) <= #CUs.  conv1 is
- * recomputed on each tile's 18x18 halo; the per-image SE gate is published in-kernel by the
- * last tile of the image to finish conv2.  Returns FEN_EUNSUPPORTED outside that envelope
- * (callers then use the per-op kernels; fen_rcab_supported() asks in advance).
- * ws: the hand-off workspace from fen_rcab_workspace_alloc (uncached device memory, zeroed,
- * left zeroed by every launch, so a hipGraph replays it; reusable by any launch whose B,H,W
- * fit its size, one launch at a time).                                                      */
+
+/* RCAB with the SE gate deferred to the consumer (blocks.py:135-153 + ChannelAttention
+ * blocks.py:83-92, one launch per RCAB of a ResidualGroup's chain, blocks.py:185-188).
+ * The gate of RCAB j needs the global mean of its t_j, i.e. every tile of the image; instead
+ * of a grid-wide hand-off inside the launch, launch j+1 applies it while it builds its input:
+ *     x_j = x_{j-1} + res_scale * s_{j-1} * t_{j-1}      (s_{j-1} from part_{j-1}, fc*_{j-1})
+ *     z1 = conv1(x_j)+b1, a1 = PReLU(z1), t_j = conv2(a1)+b2, part_j = per-tile sums of t_j.
+ * Chain start (tp == NULL): x_j = x (no gate).  Chain end: fen_se_fused(part, t, x) gives
+ * the group's last RCAB output.  Every block is independent (no in-launch synchronisation, any
+ * grid, graph-replayable, no workspace).  16-bit (bf16 / fp16) NHWC, C = 64, Cr <= 16, H and
+ * W multiples of 16.  part layout [B][H*W/256][64] (fen_se_fused's nparts = H*W/256).        */
 typedef struct {
-    int dtype;                 /* FEN_BF16                                                     */
+    int dtype;                 /* FEN_BF16 or FEN_F16                                          */
     int B, H, W, C, Cr;
-    const void* x;             /* NHWC [B,H,W,64]                                              */
+    const void* x;             /* x_{j-1} (deferred) or x_j (chain start), NHWC [B,H,W,64]     */
+    const void* tp;            /* t_{j-1} NHWC, or NULL at the chain start                     */
+    const float* pp;           /* part_{j-1} [B][tiles][64]                                    */
+    const float* pfc1;         /* RCAB j-1 channel_attention.fc.0.weight [Cr][64]              */
+    const float* pfc2;         /* RCAB j-1 channel_attention.fc.2.weight [64][Cr]              */
+    float res_scale;           /* 0.2                                                          */
+    float inv_hw;              /* 1/(H*W)                                                      */
+    float* ps;                 /* s_{j-1} [B][64] user copy (or NULL; written by tile 0 of b)  */
+    float* pmean;              /* mean_{j-1} [B][64] (or NULL)                                 */
+    float* phid;               /* hid_{j-1} [B][Cr] (or NULL)                                  */
+    void* xo;                  /* x_j out NHWC (deferred mode; NULL allowed only at the start) */
     const void* w1;            /* conv1 packed mode 0 [9][64][64]                              */
-    const float* b1;           /* [64]                                                         */
+    const float* b1;
     const float* alpha;        /* PReLU [64]                                                   */
     const void* w2;            /* conv2 packed mode 0                                          */
     const float* b2;
-    const float* fc1;          /* channel_attention.fc.0.weight [Cr][64]                       */
-    const float* fc2;          /* channel_attention.fc.2.weight [64][Cr]                       */
-    float res_scale;           /* 0.2                                                          */
-    float inv_hw;              /* 1/(H*W)                                                      */
-    void* y;                   /* out NHWC                                                     */
-    void* z1;                  /* training copies (or NULL): conv1 pre-activation,            */
-    void* a1;                  /*   its PReLU, conv2 output t (all NHWC)                      */
-    void* t;
-    float* s;                  /* [B][64] gate (always written)                                */
-    float* mean;               /* [B][64] or NULL                                              */
-    float* hid;                /* [B][Cr] or NULL                                              */
-    void* ws;                  /* fen_rcab_workspace_alloc()                                   */
+    void* t;                   /* t_j out NHWC                                                 */
+    float* part;               /* part_j out [B][tiles][64]                                    */
+    void* z1;                  /* training copies (or NULL): conv1 pre-activation and PReLU    */
+    void* a1;
     unsigned long long* stamps;/* NULL; diagnostic build only (-DFEN_STAMPS): phase timestamps */
-} fen_rcab_desc;
-int fen_rcab_supported(int dtype, int B, int H, int W, int C, int Cr);  /* 1 if fen_rcab_fused runs this shape */
-size_t fen_rcab_workspace_bytes(int B, int H, int W);
-int fen_rcab_workspace_alloc(int B, int H, int W, void** ws);   /* the library's only allocation */
-int fen_rcab_workspace_free(void* ws);
-int fen_rcab_workspace_status(const void* ws, int B, int H, int W);  /* test aid: nonzero sync words, syncs */
-int fen_rcab_fused(const fen_rcab_desc* d, void* stream);
+} fen_rcab_deferred_desc;
+int fen_rcab_deferred_supported(int dtype, int B, int H, int W, int C, int Cr);
+int fen_rcab_deferred(const fen_rcab_deferred_desc* d, void* stream);
 
 /* trainer.py:416-421 LR synthesis: bicubic x0.25, align_corners=False, NCHW fp32          */
 int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, float* lr, void* stream);

@@ -45,3 +45,21 @@ def test_bad_args_rejected_without_gpu():
     assert lib.fen_conv3x3(d, None) == -2
     with pytest.raises(L.FenError):
         L.check(-2, "conv")
+
+
+def test_rcab_deferred_validation_without_gpu():
+    from src.hip import lib as L
+    lib = L.load()
+    assert lib.fen_rcab_deferred(None, None) == -1
+    assert lib.fen_rcab_deferred_supported(L.BF16, 32, 64, 64, 64, 16) == 1
+    assert lib.fen_rcab_deferred_supported(L.F16, 32, 64, 64, 64, 16) == 1
+    assert lib.fen_rcab_deferred_supported(L.F32, 32, 64, 64, 64, 16) == 0      # 16-bit only
+    assert lib.fen_rcab_deferred_supported(L.BF16, 32, 64, 60, 64, 16) == 0     # W % 16
+    assert lib.fen_rcab_deferred_supported(L.BF16, 32, 64, 64, 128, 32) == 0    # C = 64 only
+    d = L.RcabDeferredDesc()
+    d.dtype, d.B, d.H, d.W, d.C, d.Cr = L.BF16, 2, 32, 32, 64, 16
+    d.x = d.w1 = d.w2 = d.b1 = d.b2 = d.alpha = d.t = d.part = 16
+    d.tp = 16                       # deferred input without part_{j-1} / fc weights / x_j out
+    assert lib.fen_rcab_deferred(d, None) == -1
+    d.tp, d.z1 = 0, 16              # z1 without a1
+    assert lib.fen_rcab_deferred(d, None) == -1

@@ -135,3 +135,34 @@ def test_dp_step_world2_matches_reference_global_step(golden, tmp_path):
     # and the step lands on the reference Trainer's post-step parameters
     ref_s = np.concatenate([g["s/" + n].reshape(-1) for n in p])
     np.testing.assert_allclose(r0["newp"], ref_s, rtol=0, atol=2e-7)
+
+
+# ------------------------------------------------------------------ validation metrics under DP
+def _val_worker(rank, world, port, out_dir):
+    """Two ranks validate different shards (different batch counts and values); after the
+    reduce both hold the global batch means, so EarlyStopping / plateau decide alike."""
+    from src.training.trainer import EarlyStopping, reduce_val_metrics
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # per-epoch shard sums: rank 0 sees 3 batches, rank 1 sees 2; rank 1's PSNR improves, rank 0's does not
+        shards = {0: [(3.0, 90.0, 2.4, 3), (3.0, 89.0, 2.4, 3), (3.0, 88.0, 2.4, 3), (3.0, 87.0, 2.4, 3)],
+                  1: [(2.0, 50.0, 1.6, 2), (2.0, 56.0, 1.6, 2), (2.0, 62.0, 1.6, 2), (2.0, 68.0, 1.6, 2)]}
+        es = EarlyStopping(patience=2, mode="max")
+        stops, metrics = [], []
+        for tl, tp, ts, n in shards[rank]:
+            m = reduce_val_metrics(tl, tp, ts, n, world)
+            metrics.append(m["psnr"])
+            stops.append(bool(es(m["psnr"])))
+        np.savez(os.path.join(out_dir, f"val{rank}.npz"), psnr=np.array(metrics), stops=np.array(stops))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_val_metrics_reduced_across_ranks(tmp_path):
+    mp.spawn(_val_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (np.load(tmp_path / f"val{r}.npz") for r in (0, 1))
+    np.testing.assert_array_equal(r0["psnr"], r1["psnr"])
+    np.testing.assert_array_equal(r0["stops"], r1["stops"])
+    # global mean over all 5 batches of each epoch: (90 + 50) / 5, ...
+    np.testing.assert_allclose(r0["psnr"], [28.0, 29.0, 30.0, 31.0])

@@ -1,6 +1,7 @@
 """Launch the bench's dominant kernel REPS times, plainly (no graph), for rocprofv3 --pmc
-passes: the fused RCAB block (fen_rcab_fused, inference form: conv1 + PReLU + conv2 + SE
-gate + residual, bf16, B=32, 64x64x64).  Prints the algorithmic bytes per launch.
+passes: one RCAB of the chain on fen_rcab_deferred (deferred input: the previous RCAB's gate
+and residual applied to the input halo, conv1 + PReLU + conv2 + tile sums), inference form,
+B=32, 64x64x64, fp16 (PREC=bf16 for bf16).  Prints the algorithmic bytes per launch.
 Usage: rocprofv3 --pmc FETCH_SIZE -d DIR -o run --output-format csv -- python tools/pmc_rcab.py"""
 import ctypes
 import os
@@ -15,29 +16,33 @@ from src.hip.net import Weights  # noqa: E402
 from src.hip.program import ptr  # noqa: E402
 
 REPS = int(os.environ.get("REPS", "20"))
-B, H, W, C, CR = 32, 64, 64, 64, 4
+dt = torch.bfloat16 if os.environ.get("PREC", "fp16") == "bf16" else torch.float16
+B, H, W, C, CR = 32, 64, 64, 64, 16
+T = (H // 16) * (W // 16)
 torch.manual_seed(0)
 p = {"conv1.weight": torch.randn(C, C, 3, 3) * 0.06, "conv1.bias": torch.zeros(C), "prelu.weight": torch.full((C,), .25),
      "conv2.weight": torch.randn(C, C, 3, 3) * 0.06, "conv2.bias": torch.zeros(C),
      "fc1": torch.randn(CR, C) * .3, "fc2": torch.randn(C, CR) * .3}
 pd = {k: v.cuda() for k, v in p.items()}
-Wt = Weights(pd, torch.bfloat16, "cuda")
-x = torch.randn(B, H, W, C, device="cuda", dtype=torch.bfloat16)
-y = torch.empty_like(x)
-s = torch.empty(B, C, device="cuda")
+Wt = Weights(pd, dt, "cuda")
+x = torch.randn(B, H, W, C, device="cuda").to(dt)
+tp = torch.randn(B, H, W, C, device="cuda").to(dt)
+pp = torch.randn(B * T, C, device="cuda")
+xo, t = torch.empty_like(x), torch.empty_like(x)
+part = torch.empty(B * T, C, device="cuda")
 lib = L.load()
-ws = L.RcabWorkspace(B, H, W)
-d = L.RcabDesc()
-d.dtype, d.B, d.H, d.W, d.C, d.Cr = L.BF16, B, H, W, C, CR
-d.x, d.w1, d.b1, d.alpha = ptr(x), ptr(Wt.packed("conv1", 0)), ptr(pd["conv1.bias"]), ptr(pd["prelu.weight"])
-d.w2, d.b2, d.fc1, d.fc2 = ptr(Wt.packed("conv2", 0)), ptr(pd["conv2.bias"]), ptr(pd["fc1"]), ptr(pd["fc2"])
+d = L.RcabDeferredDesc()
+d.dtype, d.B, d.H, d.W, d.C, d.Cr = L.dtype_code(dt), B, H, W, C, CR
+d.x, d.tp, d.pp, d.pfc1, d.pfc2, d.xo = ptr(x), ptr(tp), ptr(pp), ptr(pd["fc1"]), ptr(pd["fc2"]), ptr(xo)
+d.w1, d.b1, d.alpha = ptr(Wt.packed("conv1", 0)), ptr(pd["conv1.bias"]), ptr(pd["prelu.weight"])
+d.w2, d.b2 = ptr(Wt.packed("conv2", 0)), ptr(pd["conv2.bias"])
 d.res_scale, d.inv_hw = 0.2, 1.0 / (H * W)
-d.y, d.s, d.ws = ptr(y), ptr(s), ws.ptr
+d.t, d.part = ptr(t), ptr(part)
 stream = torch.cuda.current_stream().cuda_stream
 for _ in range(REPS):
-    L.check(lib.fen_rcab_fused(ctypes.byref(d), stream), "rcab")
+    L.check(lib.fen_rcab_deferred(ctypes.byref(d), stream), "rcab_deferred")
 torch.cuda.synchronize()
-assert lib.fen_rcab_workspace_status(ws.ptr, B, H, W) == 0
-# x in, y out, both packed filters (2 x 9 x 64 x 64 bf16), biases / alpha / fc weights, s out
-alg = 2 * x.numel() * 2 + 2 * 9 * C * C * 2 + 3 * C * 4 + 2 * CR * C * 4 + B * C * 4
+# x_{j-1} and t_{j-1} in, x_j and t_j out (16-bit NHWC), both packed filters, the previous
+# RCAB's tile partials + SE weights in, this RCAB's partials out, biases / alpha
+alg = 4 * x.numel() * 2 + 2 * 9 * C * C * 2 + 2 * B * T * C * 4 + 2 * CR * C * 4 + 3 * C * 4
 print("algorithmic_bytes_per_launch", alg)
