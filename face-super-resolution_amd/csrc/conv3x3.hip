@@ -551,11 +551,7 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void k_conv3x3_p(const fen_conv_de
     const int H = d.H, W = d.W, Cout = d.Cout;
     const int coutp = (Cout + 15) & ~15;
     const int ncot = coutp / COT;
-#ifndef CONV_NO_XCD
     const int bid = xcd_block();                             // a tile's co blocks + neighbours: one XCD
-#else
-    const int bid = (int)blockIdx.x;
-#endif
     const int cot = bid % ncot, co0 = cot * COT;
     const int nslot = gridDim.x / ncot, slot = bid / ncot;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
@@ -675,11 +671,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, Cout = d.Cout;
     const int ncot = Cout >> 6;
-#ifndef CONV_NO_XCD
     const int bid = xcd_block();                             // a tile's co blocks + neighbours: one XCD
-#else
-    const int bid = (int)blockIdx.x;
-#endif
     const int cot = bid % ncot, co0 = cot * 64;
     const int nslot = gridDim.x / ncot, slot = bid / ncot;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
@@ -721,20 +713,15 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wts + i * 1024), 16,
                                                      ((tap * Cout + co0 + col) * 64 + c * 8) * 2, 0, 0, 0);
         }
-#ifndef CONV_OLD_PROLOGUE
         // the halo DMA goes out before the constant loads: their LDS writes wait for vmcnt,
         // which counts in issue order -- placed first, wave 0's halo share waited for the slab
         if (grp == 0) issue_halo(tile_of(0, 0));
-#endif
         if (tid < 64) {
             const int cp = co0 + tid, Cq = Cout >> 2;
             const int co = SHUF ? 4 * (cp % Cq) + cp / Cq : cp;
             cst[tid] = (EPI & FEN_EPI_BIAS) ? d.bias[co] : 0.f;
             cst[64 + tid] = (PRELU || PBWD) ? d.alpha[SHUF ? cp % Cq : cp] : 0.f;
         }
-#ifdef CONV_OLD_PROLOGUE
-        if (grp == 0) issue_halo(tile_of(0, 0));
-#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -916,11 +903,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
-#ifndef CONV_NO_XCD
     const int tb = xcd_block();                // neighbouring tiles on one XCD (halo rows in its L2)
-#else
-    const int tb = (int)blockIdx.x;
-#endif
     const int b = tb / tpi, tile = tb - b * tpi;
     const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
     const int co0 = blockIdx.y * COT;

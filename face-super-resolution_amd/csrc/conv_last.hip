@@ -51,11 +51,7 @@ __global__ __launch_bounds__(CL_THREADS, 1) void k_conv_last(const fen_conv_desc
     const int Hs = H >> 2, Ws = W >> 2;
     const int twn = W >> 4, tpi = twn * (H >> 4), ntiles = B * tpi;
     const int G = gridDim.x;
-#ifndef CONV_NO_XCD
     const int slot = xcd_block();                     // neighbouring tiles on one XCD (shared halo rows)
-#else
-    const int slot = (int)blockIdx.x;
-#endif
     const int nmine = (ntiles - slot + G - 1) / G;
     constexpr bool train = TRAIN;
     float* red = (float*)(smem + O_RED);

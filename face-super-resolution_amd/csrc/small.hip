@@ -796,7 +796,6 @@ __global__ __launch_bounds__(1024) void k_colsum_multi(const ColJobs jobs) {
     if (c < cols) {
         const float* p = jb.part + c;
         int r = w;
-#ifndef COLSUM_UNROLL4
         // 8 rows in flight per lane: the tall jobs (conv_last's dalpha, 8192 rows x 64 at B=32)
         // are one block wide, so their time is rows / 128 dependent memory round trips
         float a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f;
@@ -811,7 +810,6 @@ __global__ __launch_bounds__(1024) void k_colsum_multi(const ColJobs jobs) {
             a7 += p[(size_t)(r + 112) * cols];
         }
         a0 += a4; a1 += a5; a2 += a6; a3 += a7;
-#endif
         for (; r + 48 < rows; r += 64) {
             a0 += p[(size_t)r * cols];
             a1 += p[(size_t)(r + 16) * cols];

@@ -255,12 +255,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
         t_begin = (int)((long long)chunk * ntiles / tpc);
         t_end = (int)((long long)(chunk + 1) * ntiles / tpc);
     } else {
-#ifndef WG_NO_XCD
         // consecutive chunks (neighbouring tiles: shared halo rows) on one XCD; with gridDim.x
         // a multiple of 8 the dispatch XCD is blockIdx.x % 8 whatever y, z are
         const int gx = (int)gridDim.x;
         if ((gx & 7) == 0) chunk = (chunk & 7) * (gx >> 3) + (chunk >> 3);
-#endif
         t_begin = chunk * tpc;
         t_end = min(t_begin + tpc, ntiles);
     }
