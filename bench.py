@@ -313,9 +313,10 @@ def time_ssim(eng, reps=50):
 
 def load_traffic(label):
     """HBM bytes per launch of the dominant kernel from its committed PMC summary
-    (profiles/pmc_*.json, tools/prof_summary.py pmc), or None when none matches it."""
+    (profiles/rNN_pmc_*.json, tools/prof_summary.py pmc; the latest round's first), or None
+    when none matches it."""
     import glob
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_*.json")), reverse=True):
         with open(p) as f:
             js = json.load(f)
         key = js.get("kernel_key")
