@@ -45,11 +45,14 @@ class FENEngine:
     def __init__(self, model, batch: int, lr_hw, dtype: torch.dtype = torch.bfloat16, train: bool = False,
                  device="cuda", loss_weight: float = 1.0, clip: float = 0.5, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, process_group=None,
-                 perceptual: Optional[dict] = None, ssim_weight: float = 0.0):
+                 perceptual: Optional[dict] = None, ssim_weight: float = 0.0, exchange=None):
         """perceptual (training only): the stage configs' VGG19 term (perceptual.py:144-169) as
         dict(weight=, layers=, criterion=, normalize=, params={'features.i.weight': ...},
         layer_weights=None); its gradient joins the fused L1 gradient in dL/dsr.  ssim_weight
-        (training only): the stage-2 term weight * (1 - SSIM) (ssim_loss.py:174-226), likewise."""
+        (training only): the stage-2 term weight * (1 - SSIM) (ssim_loss.py:174-226), likewise.
+        exchange (training only): a factory `(flat_grads, bucket_plan) -> obj` with `world`,
+        `launch(tag)` and `wait()` replacing the RCCL BucketExchange (the tests' stand-in rank
+        pair); the loss gradients are pre-scaled by its `world`."""
         if train and dtype == torch.float16:
             raise NotImplementedError("fp16 is an inference precision on the HIP backend (train in bf16 or fp32)")
         self.spec = NetSpec.from_config(model.config)
@@ -62,6 +65,12 @@ class FENEngine:
         self.world = 1
         if process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
             self.world = torch.distributed.get_world_size(process_group)
+        if train and exchange is not None:
+            from ..training.dp import model_bucket_plan
+            self._exchange_factory = lambda flat: exchange(flat, model_bucket_plan(model))
+        else:
+            from ..training.dp import BucketExchange, model_bucket_plan
+            self._exchange_factory = lambda flat: BucketExchange(flat, model_bucket_plan(model), process_group)
 
         model.to(self.device)
         if getattr(model, "_fen_flat", None) is None:
@@ -107,8 +116,8 @@ class FENEngine:
                 self.grads[name] = self.flat_g[off:off + p.numel()].view_as(p)
                 p.grad = self.grads[name]
                 off += p.numel()
-            from ..training.dp import BucketExchange, model_bucket_plan
-            self.exchange = BucketExchange(self.flat_g, model_bucket_plan(model), process_group)
+            self.exchange = self._exchange_factory(self.flat_g)
+            self.world = self.exchange.world
             self.scal = torch.zeros(8, device=self.device)
             self.scal[3] = lr
             self.loss = torch.zeros(1, device=self.device)

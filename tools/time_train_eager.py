@@ -29,6 +29,31 @@ def t(fn, n=5):
 
 
 print("eager step ms", round(t(eng.step), 3), "world", world, flush=True)
+
+
+def phases(n=5):
+    """host-side time of each phase of engine.step(): enqueueing the recorded program (marks
+    included), joining the buckets, enqueueing the update, then draining the stream."""
+    acc = [0.0] * 4
+    for _ in range(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.ctx.run()
+        t1 = time.perf_counter()
+        eng.exchange.wait()
+        t2 = time.perf_counter()
+        eng.upd.run()
+        eng.Wt.pack()
+        t3 = time.perf_counter()
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        for i, d in enumerate((t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+            acc[i] += 1000 * d / n
+    print("phases ms: enqueue %.3f  wait %.3f  update %.3f  drain %.3f  (ops %d)"
+          % (*acc, len(eng.ctx.ops)), flush=True)
+
+
+phases()
 if world == 1:
     eng.capture()
     print("graph replay ms", round(t(eng.replay), 3), flush=True)
