@@ -5,7 +5,8 @@ Single GPU:   python scripts/train.py --config configs/stages/stage1_psnr_config
 8 GPUs:       python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \\
                   scripts/train.py --config ... --perceptual-weight 0
 Every reference flag and YAML key is parsed; new flags: --precision {fp32,bf16} and
---synthetic N (N seeded random HR images instead of a data directory).
+--synthetic N (N seeded random HR images instead of a data directory; without it a missing
+--data-root is an error).  loss.gan.weight > 0 builds the discriminator and GANLoss (stage 3).
 """
 import argparse
 import os
@@ -24,6 +25,7 @@ import yaml  # noqa: E402
 from src.data import get_dataloader  # noqa: E402
 from src.losses import create_loss_function  # noqa: E402
 from src.models import create_face_enhance_net  # noqa: E402
+from src.models.discriminator import GANLoss, create_discriminator  # noqa: E402
 from src.training import Trainer, TrainerConfig, overfit_test  # noqa: E402
 
 
@@ -49,6 +51,18 @@ def create_model(model_type: str, config: dict, precision: str):
                                    reduction_ratio=mc.get("reduction_ratio", 4),
                                    scale_factor=mc.get("upscale_factor", 4), res_scale=mc.get("res_scale", 0.2),
                                    precision=precision)
+
+
+def create_gan(config: dict, precision: str):
+    """Stage 3 (reference scripts/train.py:335-351): the discriminator and GANLoss when
+    loss.gan.weight > 0, else (None, None)."""
+    gan = config.get("loss", {}).get("gan", {})
+    if not gan.get("weight", 0.0) > 0:
+        return None, None
+    d = create_discriminator(input_size=config.get("data", {}).get("hr_size", 256),
+                             base_channels=gan.get("d_channels", 64), use_bn=gan.get("d_use_bn", True),
+                             precision=precision)
+    return d, GANLoss(gan_type=gan.get("type", "vanilla"))
 
 
 def main(argv=None):
@@ -97,6 +111,8 @@ def main(argv=None):
                                 synthetic=max(args.synthetic // 8, batch_size) if args.synthetic else 0)
 
     model = create_model(model_type, config, args.precision)
+    discriminator, gan_loss = create_gan(config, args.precision)
+    gan = loss_cfg.get("gan", {})
     pw = args.perceptual_weight if args.perceptual_weight is not None else loss_cfg.get("perceptual_weight", 0.01)
     loss_fn = create_loss_function(l1_weight=loss_cfg.get("l1_weight", 1.0), perceptual_weight=pw,
                                    ssim_weight=loss_cfg.get("ssim_weight", 0.1),
@@ -110,7 +126,6 @@ def main(argv=None):
 
     sched = tr_cfg.get("scheduler", {})
     es = tr_cfg.get("early_stopping", {})
-    gan = loss_cfg.get("gan", {})
     tcfg = TrainerConfig(
         epochs=epochs, learning_rate=lr, weight_decay=tr_cfg.get("optimizer", {}).get("weight_decay", 0.0),
         gradient_clip=args.gradient_clip if args.gradient_clip is not None else tr_cfg.get("gradient_clip", 1.0),
@@ -127,7 +142,7 @@ def main(argv=None):
         d_updates_per_g=gan.get("d_updates_per_g", 1), gan_start_epoch=gan.get("start_epoch", 0))
     if tcfg.accumulation_steps != 1:
         raise NotImplementedError("accumulation_steps > 1 is not supported by the fused step (the stage configs use 1)")
-    trainer = Trainer(model, train_loader, val_loader, loss_fn, tcfg)
+    trainer = Trainer(model, train_loader, val_loader, loss_fn, tcfg, discriminator=discriminator, gan_loss=gan_loss)
     if args.resume:
         trainer.load_checkpoint(args.resume, weights_only=args.fine_tune)
     try:

@@ -58,8 +58,11 @@ class NpyHRDataset(Dataset):
 def get_dataloader(data_root: Optional[str], mode: str = "train", batch_size: int = 16, num_workers: int = 4,
                    hr_patch_size: int = 256, horizontal_flip: float = 0.5, synthetic: int = 0, seed: int = 0,
                    **unused) -> DataLoader:
-    if synthetic or not data_root or not os.path.isdir(data_root):
-        ds = SyntheticHRDataset(synthetic or 256, hr_patch_size, seed + (0 if mode == "train" else 1))
+    if not synthetic and (not data_root or not os.path.isdir(data_root)):
+        raise FileNotFoundError(f"data root {data_root!r} not found (synthetic=N, the CLI's --synthetic N, "
+                                "trains on N seeded synthetic images instead)")
+    if synthetic:
+        ds = SyntheticHRDataset(synthetic, hr_patch_size, seed + (0 if mode == "train" else 1))
     else:
         ds = NpyHRDataset(os.path.join(data_root, mode) if os.path.isdir(os.path.join(data_root, mode)) else data_root,
                           hr_patch_size, horizontal_flip if mode == "train" else 0.0, seed)

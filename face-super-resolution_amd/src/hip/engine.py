@@ -45,14 +45,18 @@ class FENEngine:
     def __init__(self, model, batch: int, lr_hw, dtype: torch.dtype = torch.bfloat16, train: bool = False,
                  device="cuda", loss_weight: float = 1.0, clip: float = 0.5, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, process_group=None,
-                 perceptual: Optional[dict] = None, ssim_weight: float = 0.0, exchange=None):
+                 perceptual: Optional[dict] = None, ssim_weight: float = 0.0, exchange=None,
+                 adam_state=None):
         """perceptual (training only): the stage configs' VGG19 term (perceptual.py:144-169) as
         dict(weight=, layers=, criterion=, normalize=, params={'features.i.weight': ...},
         layer_weights=None); its gradient joins the fused L1 gradient in dL/dsr.  ssim_weight
         (training only): the stage-2 term weight * (1 - SSIM) (ssim_loss.py:174-226), likewise.
         exchange (training only): a factory `(flat_grads, bucket_plan) -> obj` with `world`,
         `launch(tag)` and `wait()` replacing the RCCL BucketExchange (the tests' stand-in rank
-        pair); the loss gradients are pre-scaled by its `world`."""
+        pair); the loss gradients are pre-scaled by its `world`.  adam_state (training only): an
+        (exp_avg, exp_avg_sq, scal) triple over the parameter arena to update (the Trainer's one
+        generator optimizer state, shared by every engine and its module-path optimizer), else
+        a fresh one."""
         if train and dtype == torch.float16:
             raise NotImplementedError("fp16 is an inference precision on the HIP backend (train in bf16 or fp32)")
         self.spec = NetSpec.from_config(model.config)
@@ -109,8 +113,10 @@ class FENEngine:
                 self.hr = torch.zeros(B, s.out_ch, self.H, self.W, device=self.device)
             n = self.flat_p.numel()
             self.flat_g = torch.zeros(n, device=self.device)
-            self.flat_m = torch.zeros(n, device=self.device)
-            self.flat_v = torch.zeros(n, device=self.device)
+            if adam_state is None:
+                from ..training.optim import adamw_state
+                adam_state = adamw_state(self.flat_p)
+            self.flat_m, self.flat_v, self.scal = adam_state
             self.grads, off = {}, 0
             for name, p in model.named_parameters():
                 self.grads[name] = self.flat_g[off:off + p.numel()].view_as(p)
@@ -118,7 +124,6 @@ class FENEngine:
                 off += p.numel()
             self.exchange = self._exchange_factory(self.flat_g)
             self.world = self.exchange.world
-            self.scal = torch.zeros(8, device=self.device)
             self.scal[3] = lr
             self.loss = torch.zeros(1, device=self.device)
             ctx.emit("bicubic_down4", ctx.lib.fen_bicubic_down4, B, s.out_ch, self.H, self.W, ptr(self.hr),

@@ -16,15 +16,33 @@ from ..hip import lib as L
 from ..hip.program import Ctx, ptr
 
 
+def adamw_state(flat_p: torch.Tensor):
+    """(exp_avg, exp_avg_sq, scal) for a flat arena; scal = [grad norm, clip coef, step, lr,
+    bias corrections...] as fen_optim_prepare / fen_adamw read and write it."""
+    return torch.zeros_like(flat_p), torch.zeros_like(flat_p), torch.zeros(8, device=flat_p.device)
+
+
+def state_view(params, state, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0) -> "FusedAdamW":
+    """A FusedAdamW over an existing state triple without a step program: for state_dict()
+    and load_state_dict() only."""
+    opt = FusedAdamW.__new__(FusedAdamW)
+    opt.params = list(params)
+    opt.m, opt.v, opt.scal = state
+    opt.lr, opt.betas, opt.eps, opt.wd = float(lr), betas, eps, weight_decay
+    return opt
+
+
 class FusedAdamW:
     def __init__(self, params: List[torch.nn.Parameter], flat_p: torch.Tensor, flat_g: torch.Tensor, lr=1e-4,
-                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_norm=0.0):
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_norm=0.0, state=None):
+        """state: an existing (m, v, scal) triple to step on (the Trainer's one generator
+        state, shared with the fused engine's update program), else fresh zeros."""
         self.params = list(params)
         self.flat_p, self.flat_g = flat_p, flat_g
         dev = flat_p.device
-        self.m = torch.zeros_like(flat_p)
-        self.v = torch.zeros_like(flat_p)
-        self.scal = torch.zeros(8, device=dev)
+        if state is None:
+            state = adamw_state(flat_p)
+        self.m, self.v, self.scal = state
         self.betas, self.eps, self.wd, self.max_norm = betas, eps, weight_decay, max_norm
         self.set_lr(lr)
         n = flat_p.numel()

@@ -10,9 +10,13 @@ load_checkpoint, and overfit_test.  What changes (trainer row):
     batch stream (DistributedSampler or `shard=rank::world`), gradients are summed by RCCL
     all-reduce buckets issued from inside the backward and overlapped with it; clip and
     AdamW run after the reduce so every rank stays identical; rank 0 logs/checkpoints;
+  * one generator AdamW state (exp_avg / exp_avg_sq / step over the flat parameter arena)
+    shared by every fused engine and the module-path optimizer of the GAN / generic steps,
+    as the reference keeps one torch AdamW across all of them (trainer.py:217-221);
   * checkpoints keep the reference's dict layout (model/optimizer/scheduler state dicts,
-    torch.optim.AdamW-format optimizer state).
-Out of scope here: GAN discriminator steps, perceptual/SSIM losses, W&B.
+    torch.optim.AdamW-format optimizer state, the discriminator and its optimizer for
+    stage 3, trainer.py:701-760).
+Out of scope here: W&B logging and sample-image grids.
 """
 from __future__ import annotations
 
@@ -31,7 +35,7 @@ import torch.nn.functional as F
 from ..hip.engine import FENEngine, flatten_params
 from ..hip.program import Ctx, ptr
 from .dp import broadcast_arena
-from .optim import FusedAdamW
+from .optim import FusedAdamW, adamw_state, state_view
 
 
 @dataclass
@@ -155,6 +159,10 @@ class Trainer:
         self.optimizer = torch.optim.AdamW(self.model.parameters(), lr=self.config.learning_rate,
                                            weight_decay=self.config.weight_decay)
         self.scheduler = self._create_scheduler()
+        # the generator's one AdamW state: every engine's update program and the module-path
+        # FusedAdamW step on these buffers, so switching paths keeps moments and step count
+        self.adam_state = adamw_state(self.model._fen_flat)
+        self.adam_state[2][3] = self.lr
         self._engines: Dict[tuple, FENEngine] = {}
         self._generic_opt: Optional[FusedAdamW] = None
         # stage-3 GAN (trainer.py:230-250): the reference's discriminator optimizer object
@@ -201,13 +209,8 @@ class Trainer:
             eng = FENEngine(self.model, batch=B, lr_hw=(H // self.model.scale_factor, W // self.model.scale_factor),
                             dtype=dtype, train=True, device=self.device, loss_weight=self.fused_l1,
                             clip=self.config.gradient_clip, lr=self.lr, weight_decay=self.config.weight_decay,
-                            perceptual=self.fused_perceptual, ssim_weight=self.fused_ssim)
-            if self._engines:  # share optimizer moments/step between batch-size variants
-                first = next(iter(self._engines.values()))
-                eng.flat_m, eng.flat_v, eng.scal = first.flat_m, first.flat_v, first.scal
-                eng._build_update()
-            elif getattr(self, "_pending_opt_state", None):
-                self._load_opt_into(eng, self._pending_opt_state)
+                            perceptual=self.fused_perceptual, ssim_weight=self.fused_ssim,
+                            adam_state=self.adam_state)
             self._engines[key] = eng
         return self._engines[key]
 
@@ -268,7 +271,8 @@ class Trainer:
             flat = self.model._fen_flat
             self._flat_g = torch.zeros_like(flat)
             self._generic_opt = FusedAdamW(list(self.model.parameters()), flat, self._flat_g, lr=self.lr,
-                                           weight_decay=self.config.weight_decay, max_norm=self.config.gradient_clip)
+                                           weight_decay=self.config.weight_decay, max_norm=self.config.gradient_clip,
+                                           state=self.adam_state)
         off = 0
         for p in self.model.parameters():
             n = p.numel()
@@ -303,7 +307,6 @@ class Trainer:
             total, n = float(t[0]), int(t[1])
         return {"loss": total / max(n, 1), "l1": total / max(n, 1)}
 
-    @torch.no_grad()
     @torch.no_grad()
     def _validate_epoch(self) -> Dict[str, float]:
         """trainer.py:552-619 (sample grids / W&B images out of scope); DP: global means."""
@@ -376,16 +379,14 @@ class Trainer:
         return better
 
     # ------------------------------------------------------------------ checkpoints
+    def _adam_view(self) -> FusedAdamW:
+        return state_view(self.model.parameters(), self.adam_state, lr=self.lr,
+                          weight_decay=self.config.weight_decay)
+
     def _optimizer_state(self) -> Dict:
-        if self._engines:
-            eng = next(iter(self._engines.values()))
-            opt = FusedAdamW.__new__(FusedAdamW)
-            opt.params, opt.m, opt.v, opt.scal = list(self.model.parameters()), eng.flat_m, eng.flat_v, eng.scal
-            opt.lr, opt.betas, opt.eps, opt.wd = self.lr, eng.betas, eng.eps, eng.wd
-            return opt.state_dict()
-        if self._generic_opt is not None:
-            return self._generic_opt.state_dict()
-        return self.optimizer.state_dict()
+        """The generator's AdamW state in torch.optim.AdamW's format (empty before a step)."""
+        view = self._adam_view()
+        return view.state_dict() if view.steps > 0 else self.optimizer.state_dict()
 
     def _save_checkpoint(self, filename: str, is_best: bool = False) -> None:
         """Reference checkpoint layout (trainer.py:701-723); rank 0 only."""
@@ -402,6 +403,9 @@ class Trainer:
             "training_history": self.training_history,
             "config": dict(self.config.__dict__),
         }
+        if self.use_gan:
+            ckpt["discriminator_state_dict"] = {k: v.detach().cpu() for k, v in self.discriminator.state_dict().items()}
+            ckpt["optimizer_d_state_dict"] = self.optimizer_d.state_dict()
         torch.save(ckpt, self.checkpoint_dir / filename)
         if is_best:
             print(f"  New best model saved: {self.best_metric:.4f}")
@@ -416,21 +420,17 @@ class Trainer:
         osd = ckpt.get("optimizer_state_dict")
         if osd:
             self.optimizer.load_state_dict(osd)
-            self._pending_opt_state = osd
-            for eng in self._engines.values():
-                self._load_opt_into(eng, osd)
+            self._adam_view().load_state_dict(osd)   # the one state both step paths use
         if self.scheduler and ckpt.get("scheduler_state_dict"):
             self.scheduler.load_state_dict(ckpt["scheduler_state_dict"])
         self.current_epoch = ckpt["epoch"] + 1
         self.global_step = ckpt["global_step"]
         self.best_metric = ckpt["best_metric"]
         self.training_history = ckpt["training_history"]
-
-    def _load_opt_into(self, eng: FENEngine, osd: Dict):
-        opt = FusedAdamW.__new__(FusedAdamW)
-        opt.params, opt.m, opt.v, opt.scal = list(self.model.parameters()), eng.flat_m, eng.flat_v, eng.scal
-        opt.lr = self.lr
-        opt.load_state_dict(osd)
+        if self.use_gan and "discriminator_state_dict" in ckpt:
+            self.discriminator.load_state_dict(ckpt["discriminator_state_dict"])
+            if ckpt.get("optimizer_d_state_dict"):
+                self.optimizer_d.load_state_dict(ckpt["optimizer_d_state_dict"])
 
 
 def overfit_test(model: nn.Module, dataloader, loss_fn: nn.Module, num_images: int = 10,

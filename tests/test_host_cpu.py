@@ -143,6 +143,11 @@ def test_data_sources(tmp_path):
     img = (np.arange(40 * 40 * 3) % 251).astype(np.uint8).reshape(40, 40, 3)
     for i in range(3):
         np.save(tmp_path / f"im{i}.npy", img)
+    # a missing data root is an error unless synthetic data is asked for explicitly
+    with pytest.raises(FileNotFoundError, match="synthetic"):
+        get_dataloader(str(tmp_path / "missing"), "train", batch_size=2, num_workers=0, hr_patch_size=32)
+    with pytest.raises(FileNotFoundError):
+        get_dataloader(None, "val", batch_size=2, num_workers=0, hr_patch_size=32)
     nd = NpyHRDataset(str(tmp_path), hr_patch_size=32)
     t = nd[0]["hr"]
     assert t.shape == (3, 32, 32)
@@ -166,3 +171,28 @@ def test_train_cli_parses_reference_flags():
                  "--perceptual-weight", "--patience", "--resume", "--fine-tune", "--overfit-test", "--device",
                  "--no-wandb", "--precision", "--synthetic"):
         assert flag in r.stdout, flag
+
+
+def _train_script():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "fen_train_script", os.path.join(ROOT, "face-super-resolution_amd", "scripts", "train.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_train_cli_builds_gan_for_stage3():
+    """loss.gan.weight > 0 (stage3_gan_config.yaml's keys) -> the discriminator and GANLoss the
+    reference's scripts/train.py:335-351 builds; weight 0 -> none."""
+    from src.models import GANLoss, VGGStyleDiscriminator
+    ts = _train_script()
+    cfg = {"data": {"hr_size": 128}, "loss": {"gan": {"weight": 0.005, "type": "lsgan", "d_channels": 32,
+                                                       "d_use_bn": False}}}
+    d, gl = ts.create_gan(cfg, "fp32")
+    assert isinstance(d, VGGStyleDiscriminator) and isinstance(gl, GANLoss)
+    assert gl.gan_type == "lsgan"
+    assert d.features[0][0].out_channels == 32
+    assert not any(isinstance(m, torch.nn.BatchNorm2d) for m in d.modules())
+    assert ts.create_gan({"loss": {"gan": {"weight": 0.0}}}, "fp32") == (None, None)
+    assert ts.create_gan({}, "fp32") == (None, None)
