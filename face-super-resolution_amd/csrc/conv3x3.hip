@@ -17,9 +17,10 @@
 //    18x18-pixel input halo of the next tile is streamed by LDS-DMA (buffer_load ... lds,
 //    zero padding via the buffer range check) into a second buffer while the MFMAs run
 //    on the current one: one barrier per tile, none per tap.  156.7 KB LDS.
-//  * k_conv3x3_s (any Cin multiple of the panel, bf16 / fp16 and f32): weights streamed per tap
+//  * k_conv3x3_s (any Cin multiple of 16 B, bf16 / fp16 and f32): weights streamed per tap
 //    through a double-buffered LDS tile, halo staged through registers; 2 blocks per CU.
-//    Used for f32 (the parity path) and for Cin > 64 (upsampler dgrad, 128-ch variant).
+//    Used for f32 (the parity path), for Cin > 64 (upsampler dgrad, 128-ch variant) and for
+//    Cin < 64 (FaceEnhanceNetLite's 32 channels; the panel's upper half is zeros).
 // The epilogue fuses bias, residual adds, PReLU (fwd) or PReLU-backward (dgrad),
 // PixelShuffle / inverse-PixelShuffle stores, SE global-average-pool partials, and for
 // conv_last the bicubic skip + eval clamp + L1-loss gradient.
@@ -919,7 +920,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
         for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     const EpiConst<MT> ec = epi_consts<MT>(d, co0 + q * 4);   // latency hidden by the main loop
 
-    const int npan = Cin / CK;
+    // a last partial panel (Cin % CK: FaceEnhanceNetLite's 32 channels in 16-bit) reads zeros
+    // past Cin, in the halo and in the filter
+    const int npan = (Cin + CK - 1) / CK;
     for (int pn = 0; pn < npan; ++pn) {
         // ---- stage the input halo of panel pn (zero padding outside the image) ----
         constexpr int HPT = (HP * 8 + 255) / 256;   // 11 chunks per thread: loads first, then writes
@@ -932,7 +935,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
                 const int p = i >> 3, ch = i & 7;
                 const int hr = p / HALO, hc = p - hr * HALO;
                 const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-                if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
+                if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W && pn * 128 + ch * 16 < (int)xrow)
                     hv[j] = *(const uint4*)(xb + ((size_t)(b * H + gh) * W + gw) * xrow + pn * 128 + ch * 16);
             }
         }
@@ -949,7 +952,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
             for (int j = 0; j < WPT; ++j) {
                 const int i = (tid + j * 256) % WCH;
                 const int r = i >> 3, ch = i & 7;
-                wr[j] = *(const uint4*)(wb + (size_t)(tap * coutp + co0 + r) * xrow + pn * 128 + ch * 16);
+                wr[j] = pn * 128 + ch * 16 < (int)xrow
+                            ? *(const uint4*)(wb + (size_t)(tap * coutp + co0 + r) * xrow + pn * 128 + ch * 16)
+                            : make_uint4(0, 0, 0, 0);
             }
         };
         auto store_w = [&](char* dst) {
@@ -1128,8 +1133,8 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     if (!d || !d->x || !d->w || d->B <= 0 || d->H <= 0 || d->W <= 0 || d->Cin <= 0 || d->Cout <= 0)
         return FEN_EINVAL;
     if (d->dtype != FEN_F32 && d->dtype != FEN_BF16 && d->dtype != FEN_F16) return FEN_EINVAL;
-    const int CK = d->dtype == FEN_F32 ? 32 : 64;
-    if (d->Cin % CK) return FEN_EUNSUPPORTED;
+    // 16-B channel chunks: Cin % 8 (16-bit) / % 4 (f32); Cin == 64 takes the persistent kernels
+    if ((d->Cin * (d->dtype == FEN_F32 ? 4 : 2)) % 16) return FEN_EUNSUPPORTED;
     const int epi = d->epi;
     if ((epi & FEN_EPI_BIAS) && !d->bias) return FEN_EINVAL;
     if ((epi & (FEN_EPI_PRELU | FEN_EPI_PRELU_BWD)) && !d->alpha) return FEN_EINVAL;

@@ -67,7 +67,9 @@ __global__ __launch_bounds__(576, 1) void k_wgrad(const fen_wgrad_desc d, int tp
             const int hr = p / HALO, hc = p - hr * HALO;
             const int gh = h0 + hr - 1, gw = w0 + hc - 1;
             uint4 v = make_uint4(0, 0, 0, 0);
-            if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
+            // channels past Cin (a partial 64-ci group: Lite's 32 channels) stage as zeros
+            if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W &&
+                (ci0 + pn * CK) * (int)sizeof(T) + ch * 16 < Cin * (int)sizeof(T))
                 v = *(const uint4*)((const char*)d.x +
                                     (((size_t)(b * H + gh) * W + gw) * Cin + ci0 + pn * CK) * sizeof(T) + ch * 16);
             *(uint4*)(hx + pn * PANEL_HALO + swz(p, ch)) = v;
@@ -153,7 +155,7 @@ __global__ __launch_bounds__(576, 1) void k_wgrad(const fen_wgrad_desc d, int tp
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int co = co0 + m * 16 + q * 4 + r, ci = ci0 + n * 16 + c16;
-                slab[((size_t)tap * Cout + co) * Cin + ci] = acc[m][n][r];
+                if (ci < Cin) slab[((size_t)tap * Cout + co) * Cin + ci] = acc[m][n][r];
             }
     if (do_db && c16 == 0) {
 #pragma unroll
@@ -511,7 +513,7 @@ int wgrad_geom(const fen_wgrad_desc* d, int* nchunk, int* tpc, int* cot) {
         *tpc = n;   // k_wgrad_p<3> reads the chunk count here
         return FEN_OK;
     }
-    const int yz = (d->Cout / *cot) * (d->Cin / 64);
+    const int yz = (d->Cout / *cot) * ((d->Cin + 63) / 64);
     int t = (ntiles * yz + 255) / 256;  // target ~256 blocks
     if (t < 1) t = 1;
     *tpc = t;
@@ -532,7 +534,9 @@ extern "C" size_t fen_wgrad_work_floats(const fen_wgrad_desc* d) {
 extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
     if (!d || !d->x || !d->dy || !d->dw || !d->work) return FEN_EINVAL;
     if (d->dtype != FEN_F32 && d->dtype != FEN_BF16) return FEN_EINVAL;
-    if (d->B <= 0 || d->H <= 0 || d->W <= 0 || d->Cin % 64 || d->Cout % 16 || d->cout_valid <= 0 ||
+    // Cin: 16-B channel chunks (% 8 bf16, % 4 f32); a partial last 64-ci group reads zeros
+    if (d->B <= 0 || d->H <= 0 || d->W <= 0 || (d->Cin * (d->dtype == FEN_F32 ? 4 : 2)) % 16 || d->Cout % 16 ||
+        d->cout_valid <= 0 ||
         d->cout_valid > d->Cout)
         return FEN_EUNSUPPORTED;
     int nchunk, tpc, cot;
@@ -564,7 +568,7 @@ extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
     }
     float* part = d->work;
     float* dbpart = d->work + (size_t)nchunk * 9 * d->Cout * d->Cin;
-    dim3 grid(nchunk, d->Cout / cot, d->Cin / 64);
+    dim3 grid(nchunk, d->Cout / cot, (d->Cin + 63) / 64);
     const int npx = d->dtype == FEN_BF16 ? 1 : 2;
     const int npy = d->dtype == FEN_BF16 ? 1 : (cot * 4 > 128 ? 2 : 1);
     const size_t lds = (size_t)npx * PANEL_HALO + (size_t)npy * PANEL_TILE;

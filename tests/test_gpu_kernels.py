@@ -45,7 +45,8 @@ DT_FWD = DT + [torch.float16]     # the forward kernels also run fp16 (inference
 
 @pytest.mark.parametrize("dtype", DT_FWD)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 20, 36, 64, 64), (2, 32, 16, 128, 64),
-                                             (1, 16, 32, 64, 256), (1, 8, 8, 64, 16)])
+                                             (1, 16, 32, 64, 256), (1, 8, 8, 64, 16), (2, 16, 16, 32, 32),
+                                             (1, 20, 24, 32, 128), (2, 16, 16, 96, 32), (1, 16, 16, 32, 16)])
 def test_conv3x3_plain(dtype, B, H, W, Cin, Cout):
     from src.hip import net
     torch.manual_seed(0)
@@ -312,7 +313,9 @@ def test_se_fused(dtype, B, C, Cr, H, W):
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 24, 40, 64, 64), (1, 16, 16, 64, 256),
                                              (1, 32, 32, 64, 16), (17, 64, 64, 64, 64), (2, 20, 36, 128, 64),
-                                             (3, 32, 48, 64, 256), (2, 64, 64, 64, 64), (3, 40, 56, 64, 64)])
+                                             (3, 32, 48, 64, 256), (2, 64, 64, 64, 64), (3, 40, 56, 64, 64),
+                                             (2, 16, 16, 32, 32), (1, 24, 40, 32, 128), (2, 32, 32, 32, 16),
+                                             (1, 16, 16, 96, 64)])
 def test_wgrad(dtype, B, H, W, Cin, Cout):
     """fen_wgrad3x3 vs autograd of conv2d.  The reference runs in float64 on the operands
     rounded to the compute dtype, so bf16 is held to fp32-accumulation accuracy (rel 1e-5):

@@ -98,8 +98,6 @@ def _seeded(ctor, golden_npz):
 @pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 def test_full_networks_vs_reference(golden, name, ctor, precision):
     g = golden(name)
-    if precision != "fp32" and name == "g6_lite.npz":
-        pytest.skip("bf16 kernels need channel counts that are multiples of 64 (Lite is 32)")
     m = _seeded(lambda: ctor(precision), g).to(DEV)
     x = torch.from_numpy(g["x"]).to(DEV)
     with torch.no_grad():
