@@ -40,7 +40,7 @@ def test_bad_args_rejected_without_gpu():
     lib = L.load()
     d = L.ConvDesc()
     assert lib.fen_conv3x3(None, None) == L.load().fen_conv3x3(None, None) == -1
-    d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = 1, 1, 8, 8, 48, 64  # Cin not a multiple of 64 (bf16 panel)
+    d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = 1, 1, 8, 8, 36, 64  # 72-B pixel rows: not whole 16-B chunks
     d.x = d.w = d.y = 16
     assert lib.fen_conv3x3(d, None) == -2
     with pytest.raises(L.FenError):
