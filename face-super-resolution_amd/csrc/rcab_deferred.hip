@@ -222,7 +222,6 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
     const i32x4 xr4 = make_rsrc(d.x, (unsigned)act_bytes);
     const i32x4 w1r = make_rsrc(d.w1, 9u * 64u * 128u);
     const i32x4 w2r = make_rsrc(d.w2, 9u * 64u * 128u);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)act_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t trs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(DEFER ? d.tp : d.x), 0, (int)act_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ors =
@@ -609,9 +608,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
                 const float s = group16_sum(ps[m][r]);
                 if (c16 == 0) red[wr * 64 + wc * 32 + m * 16 + 4 * q + r] = s;
             }
-        // the next halo (DMA + t chunks) landed before this barrier in every wave (deferred: the
-        // combine below reads other waves' DMA bytes); the t stores above keep draining
-        if (DEFER && next) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // the next halo (DMA + t chunks) landed at the phase-5 wait (vmcnt(0)) in every wave, so
+        // the combine below may read other waves' DMA bytes after this barrier; the next tile's
+        // first taps (issued at phase 5) and the t stores above stay in flight
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (wave == 0)

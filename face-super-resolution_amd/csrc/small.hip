@@ -668,6 +668,129 @@ __global__ void k_se_bwd(int C, int Cr, int nparts, float inv_hw, float rs, cons
     }
 }
 
+// SE backward + its apply in one launch (the backward of ChannelAttention and of the RCAB's
+// scaled residual, blocks.py:88-92,150-153): grid (splits, B), every block recomputes its
+// image's SE backward from the pool_dot partials -- the same arithmetic in the same order as
+// k_se_bwd (thread (c, quarter) sums every 4th partial, fixed-order combine, one wave per
+// hidden unit) -- and applies dt = dy * rs * s[c] + g[c] to its slice; block 0 of each image
+// writes the FC weight-gradient rows (and g when asked).  The partials, both FC weights and
+// the per-image vectors are requested first, then each thread's NPT dy vectors, so the
+// streaming loads are in flight while the chain runs on LDS.  C <= 64, nparts <= 64,
+// C * Cr <= 4096.
+template <typename T, int NPT>
+__global__ __launch_bounds__(256) void k_se_bwd_fused(int HW, int C, int Cr, int nparts, float inv_hw, float rs,
+                                                      const float* __restrict__ part, const float* __restrict__ mean,
+                                                      const float* __restrict__ hid, const float* __restrict__ s,
+                                                      const float* __restrict__ w1, const float* __restrict__ w2,
+                                                      const T* __restrict__ dy, float* g_out, float* dw1p, float* dw2p,
+                                                      T* __restrict__ dt) {
+    __shared__ float dz[64], dh[64], pr[4][64], ssv[64], smean[64], shid[64], sgv[64];
+    __shared__ __attribute__((aligned(16))) float sw1[4096], sw2[4096];
+    constexpr int V = 16 / sizeof(T);
+    const int t = threadIdx.x, b = blockIdx.y;
+    const int c = t & 63, qr = t >> 6;
+    // ---- 1. the chain's operands
+    float pv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int pidx = qr + 4 * i;
+        pv[i] = (c < C && pidx < nparts) ? part[((size_t)b * nparts + pidx) * C + c] : 0.f;
+    }
+    const int nw4 = C * Cr / 4;
+    float4 w1v[4], w2v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = t + j * 256;
+        if (i < nw4) {
+            w1v[j] = ((const float4*)w1)[i];
+            w2v[j] = ((const float4*)w2)[i];
+        }
+    }
+    float sv0 = 0.f, mv0 = 0.f, hv0 = 0.f;
+    if (t < C) {
+        sv0 = s[(size_t)b * C + t];
+        mv0 = mean[(size_t)b * C + t];
+    }
+    if (t < Cr) hv0 = hid[(size_t)b * Cr + t];
+    // ---- 2. streaming operands
+    const size_t nv = (size_t)HW * C / V;
+    const size_t base = (size_t)b * nv;
+    const size_t v0 = (size_t)blockIdx.x * (256 * NPT) + t;
+    uint4 yv[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+        const size_t v = v0 + (size_t)j * 256;
+        if (v < nv) yv[j] = *(const uint4*)(dy + (base + v) * V);
+    }
+    // ---- 3. SE backward (k_se_bwd's order)
+    {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a += pv[i];
+        if (c < C) pr[qr][c] = a;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = t + j * 256;
+        if (i < nw4) {
+            ((float4*)sw1)[i] = w1v[j];
+            ((float4*)sw2)[i] = w2v[j];
+        }
+    }
+    if (t < C) {
+        ssv[t] = sv0;
+        smean[t] = mv0;
+    }
+    if (t < Cr) shid[t] = hv0;
+    __syncthreads();
+    if (t < C) {
+        const float a = (pr[0][t] + pr[1][t]) + (pr[2][t] + pr[3][t]);
+        const float sv = ssv[t];
+        dz[t] = a * rs * sv * (1.f - sv);                 // through sigmoid
+    }
+    __syncthreads();
+    {
+        const int lane = t & 63;
+        for (int j = t >> 6; j < Cr; j += 4) {
+            float a = 0.f;
+            for (int cc = lane; cc < C; cc += 64) a += sw2[cc * Cr + j] * dz[cc];
+            a = wave_sum(a);
+            if (lane == 0) dh[j] = shid[j] > 0.f ? a : 0.f;   // through ReLU
+        }
+    }
+    __syncthreads();
+    const bool first = blockIdx.x == 0;
+    if (first) {
+        for (int i = t; i < C * Cr; i += 256) {
+            const int cc = i / Cr, j = i % Cr;
+            dw2p[(size_t)b * C * Cr + i] = dz[cc] * shid[j];                       // [C][Cr]
+            const int jj = i / C, c2 = i % C;
+            dw1p[(size_t)b * C * Cr + i] = dh[jj] * smean[c2];                     // [Cr][C]
+        }
+    }
+    if (t < C) {
+        float a = 0.f;
+        for (int j = 0; j < Cr; ++j) a += sw1[j * C + t] * dh[j];
+        const float gv = a * inv_hw;
+        sgv[t] = gv;
+        if (first && g_out) g_out[(size_t)b * C + t] = gv;
+    }
+    __syncthreads();
+    // ---- 4. dt = dy * rs * s[c] + g[c]  (k_se_apply<BWD>'s expression)
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+        const size_t v = v0 + (size_t)j * 256;
+        if (v < nv) {
+            const int c0 = (int)((v * V) % C);
+            float av[V], o[V];
+            unpack16<T>(yv[j], av);
+#pragma unroll
+            for (int k = 0; k < V; ++k) o[k] = av[k] * rs * ssv[c0 + k] + sgv[c0 + k];
+            *(uint4*)(dt + (base + v) * V) = pack16<T>(o);
+        }
+    }
+}
+
 // ------------------------------ resampling / layout ------------------------------
 __global__ void k_bicubic_down4(int B, int C, int H, int W, const float* __restrict__ hr, float* __restrict__ lr) {
     const int Ho = H / 4, Wo = W / 4;
@@ -1141,6 +1264,33 @@ extern "C" int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy,
     else
         hipLaunchKernelGGL((k_se_apply<float, true>), dim3(nblk(nvec)), dim3(256), 0, STREAM, nvec, HW, C,
                            (const float*)dy, s, res_scale, (const void*)g, (float*)dt);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_se_bwd_fused(int dtype, int B, int HW, int C, int Cr, int nparts, float inv_hw, float res_scale,
+                                const float* part, const float* mean, const float* hid, const float* s,
+                                const float* w1, const float* w2, const void* dy, float* g, float* dw1p, float* dw2p,
+                                void* dt, void* stream) {
+    if (!part || !mean || !hid || !s || !w1 || !w2 || !dy || !dw1p || !dw2p || !dt || B <= 0 || HW <= 0)
+        return FEN_EINVAL;
+    const int V = dtype == FEN_F32 ? 4 : 8;
+    if (C <= 0 || C > 64 || C % V || Cr <= 0 || Cr > 64 || C * Cr > 4096 || (C * Cr) % 4 || nparts <= 0 || nparts > 64)
+        return FEN_EUNSUPPORTED;
+    const size_t nv = (size_t)HW * C / V;
+    constexpr int NPT = 8;
+    const unsigned splits = (unsigned)((nv + 256 * NPT - 1) / (256 * NPT));
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL((k_se_bwd_fused<bf16, NPT>), dim3(splits, B), dim3(256), 0, STREAM, HW, C, Cr, nparts, inv_hw,
+                           res_scale, part, mean, hid, s, w1, w2, (const bf16*)dy, g, dw1p, dw2p, (bf16*)dt);
+    else if (dtype == FEN_F16)
+        hipLaunchKernelGGL((k_se_bwd_fused<f16, NPT>), dim3(splits, B), dim3(256), 0, STREAM, HW, C, Cr, nparts, inv_hw,
+                           res_scale, part, mean, hid, s, w1, w2, (const f16*)dy, g, dw1p, dw2p, (f16*)dt);
+    else if (dtype == FEN_F32)
+        hipLaunchKernelGGL((k_se_bwd_fused<float, NPT>), dim3(splits, B), dim3(256), 0, STREAM, HW, C, Cr, nparts,
+                           inv_hw, res_scale, part, mean, hid, s, w1, w2, (const float*)dy, g, dw1p, dw2p, (float*)dt);
+    else
+        return FEN_EINVAL;
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

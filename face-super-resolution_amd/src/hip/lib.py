@@ -80,6 +80,7 @@ _SIGS = {
     "fen_pool_parts": (c_size_t, [c_int]),
     "fen_pool_dot": (c_int, [c_int] * 4 + [c_void_p] * 3 + [c_void_p]),
     "fen_se_bwd": (c_int, [c_int] * 4 + [c_float, c_float] + [c_void_p] * 9 + [c_void_p]),
+    "fen_se_bwd_fused": (c_int, [c_int] * 6 + [c_float, c_float] + [c_void_p] * 11 + [c_void_p]),
     "fen_se_bwd_apply": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
     "fen_bicubic_down4": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_void_p]),
     "fen_colsum": (c_int, [c_int, c_int, c_void_p, c_float, c_void_p, c_int, c_void_p]),

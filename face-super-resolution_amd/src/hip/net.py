@@ -55,6 +55,10 @@ class NetSpec:
 # in-launch synchronisation between blocks; 'perop' -- conv1(+PReLU) / conv2(+pool) / SE
 # launches (shapes outside the deferred kernel's envelope always take this path).
 RCAB_MODE = os.environ.get("FEN_RCAB", "deferred")
+# RCAB backward: the SE backward and its apply as one fen_se_bwd_fused launch (default) or
+# the fen_se_bwd + fen_se_bwd_apply pair (FEN_SE_BWD=pair; shapes outside the fused
+# kernel's envelope always take the pair)
+SE_BWD_FUSED = os.environ.get("FEN_SE_BWD", "fused") != "pair"
 
 
 def tiles(H: int, W: int) -> int:
@@ -371,18 +375,23 @@ class Backward:
         npart = ctx.lib.fen_pool_parts(HW)
         part = ctx.scratch("bw_pool", (B * npart, C), torch.float32)
         ctx.emit("pool_dot", ctx.lib.fen_pool_dot, ctx.code, B, HW, C, ptr(dy), ptr(sv["t"]), ptr(part))
-        g = ctx.scratch("bw_g", (B, C), torch.float32)
         dw1p = ctx.scratch("bw_dw1p" + pre, (B, s.Cr * C), torch.float32)
         dw2p = ctx.scratch("bw_dw2p" + pre, (B, s.Cr * C), torch.float32)
         ca = pre + "channel_attention.fc."
-        ctx.emit("se_bwd", ctx.lib.fen_se_bwd, B, C, s.Cr, npart, 1.0 / HW, s.res_scale, ptr(part), ptr(sv["mean"]),
-                 ptr(sv["hid"]), ptr(sv["s"]), ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]), ptr(g), ptr(dw1p),
-                 ptr(dw2p))
+        dt = ctx.scratch("bw_dt", dy.shape)
+        se_args = (npart, 1.0 / HW, s.res_scale, ptr(part), ptr(sv["mean"]), ptr(sv["hid"]), ptr(sv["s"]),
+                   ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]))
+        if SE_BWD_FUSED and C <= 64 and npart <= 64 and C * s.Cr <= 4096:
+            # SE backward + dt in one launch (same arithmetic as the pair below)
+            ctx.emit("se_bwd_fused", ctx.lib.fen_se_bwd_fused, ctx.code, B, HW, C, s.Cr, *se_args, ptr(dy), None,
+                     ptr(dw1p), ptr(dw2p), ptr(dt))
+        else:
+            g = ctx.scratch("bw_g", (B, C), torch.float32)
+            ctx.emit("se_bwd", ctx.lib.fen_se_bwd, B, C, s.Cr, *se_args, ptr(g), ptr(dw1p), ptr(dw2p))
+            ctx.emit("se_bwd_apply", ctx.lib.fen_se_bwd_apply, ctx.code, B, HW, C, ptr(dy), ptr(sv["s"]), s.res_scale,
+                     ptr(g), ptr(dt))
         self.cs.add(dw1p, B, s.Cr * C, G[ca + "0.weight"])
         self.cs.add(dw2p, B, s.Cr * C, G[ca + "2.weight"])
-        dt = ctx.scratch("bw_dt", dy.shape)
-        ctx.emit("se_bwd_apply", ctx.lib.fen_se_bwd_apply, ctx.code, B, HW, C, ptr(dy), ptr(sv["s"]), s.res_scale,
-                 ptr(g), ptr(dt))
         self._wg(pre + "conv2", sv["a1"], dt, B, H, W, C, C)
         dz1 = ctx.scratch("bw_dz1", dy.shape)
         T = tiles(H, W)

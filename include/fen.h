@@ -141,6 +141,14 @@ int fen_pool_dot(int dtype, int B, int HW, int C, const void* a, const void* b_,
 int fen_se_bwd(int B, int C, int Cr, int nparts, float inv_hw, float res_scale,
                const float* part, const float* mean, const float* hid, const float* s,
                const float* w1, const float* w2, float* g, float* dw1p, float* dw2p, void* stream);
+/* fen_se_bwd + fen_se_bwd_apply in one launch (same arithmetic, same results): every block
+ * recomputes its image's SE backward from the pool_dot partials and writes its slice of
+ * dt = dy * res_scale * s[b,c] + g[b,c]; g (may be NULL), dw1p, dw2p as fen_se_bwd.
+ * C <= 64, nparts <= 64, C * Cr <= 4096 (else FEN_EUNSUPPORTED: use the pair).             */
+int fen_se_bwd_fused(int dtype, int B, int HW, int C, int Cr, int nparts, float inv_hw, float res_scale,
+                     const float* part, const float* mean, const float* hid, const float* s,
+                     const float* w1, const float* w2, const void* dy, float* g, float* dw1p, float* dw2p,
+                     void* dt, void* stream);
 /* dt = dy * s[b,c] * res_scale + g[b,c]                                                    */
 int fen_se_bwd_apply(int dtype, int B, int HW, int C, const void* dy, const float* s,
                      float res_scale, const float* g, void* dt, void* stream);

@@ -402,3 +402,50 @@ def test_dgrad_unshuffle(dtype):
              pre_in=nhwc(v, dtype), y=du, part=part)
     torch.cuda.synchronize()
     assert (nchw(du) - ref).abs().max() <= _tol(dtype, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("B,HW,C,Cr", [(3, 4096, 64, 16), (2, 1024, 32, 8), (1, 256, 64, 16)])
+def test_se_bwd_fused_matches_pair(dtype, B, HW, C, Cr):
+    """fen_se_bwd_fused == fen_se_bwd + fen_se_bwd_apply bit for bit (the backward of
+    ChannelAttention and the RCAB's scaled residual, blocks.py:88-92,150-153), and dt agrees
+    with a float64 restatement of the chain."""
+    from src.hip import lib as L
+    from src.hip.program import ptr
+    lib = L.load()
+    code = L.dtype_code(dtype)
+    stream = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(B * 7 + C)
+    npart = int(lib.fen_pool_parts(HW))
+    part = torch.randn(B * npart, C, device=DEV)
+    mean = torch.randn(B, C, device=DEV) * 0.1
+    hid = torch.relu(torch.randn(B, Cr, device=DEV))
+    s = torch.sigmoid(torch.randn(B, C, device=DEV))
+    w1 = torch.randn(Cr, C, device=DEV) * 0.3
+    w2 = torch.randn(C, Cr, device=DEV) * 0.3
+    dy = torch.randn(B, HW, C, device=DEV).to(dtype)
+    rs = 0.2
+    g = torch.empty(B, C, device=DEV)
+    dw1p, dw2p = torch.empty(B, Cr * C, device=DEV), torch.empty(B, Cr * C, device=DEV)
+    dt = torch.empty_like(dy)
+    args = (npart, 1.0 / HW, rs, ptr(part), ptr(mean), ptr(hid), ptr(s), ptr(w1), ptr(w2))
+    L.check(lib.fen_se_bwd(B, C, Cr, *args, ptr(g), ptr(dw1p), ptr(dw2p), stream), "se_bwd")
+    L.check(lib.fen_se_bwd_apply(code, B, HW, C, ptr(dy), ptr(s), rs, ptr(g), ptr(dt), stream), "se_bwd_apply")
+    g2 = torch.full_like(g, 7.0)
+    f1, f2 = torch.full_like(dw1p, 7.0), torch.full_like(dw2p, 7.0)
+    dt2 = torch.zeros_like(dy)
+    L.check(lib.fen_se_bwd_fused(code, B, HW, C, Cr, *args, ptr(dy), ptr(g2), ptr(f1), ptr(f2), ptr(dt2), stream),
+            "se_bwd_fused")
+    torch.cuda.synchronize()
+    assert torch.equal(g2, g)
+    assert torch.equal(f1, dw1p) and torch.equal(f2, dw2p)
+    assert torch.equal(dt2, dt)
+    # float64 restatement: a = sum of partials, dz = a rs s (1-s), dh = relu'(hid) W2^T dz, g = W1^T dh / HW
+    a = part.double().view(B, npart, C).sum(1)
+    sd = s.double()
+    dz = a * rs * sd * (1 - sd)
+    dh = (dz @ w2.double()) * (hid.double() > 0)
+    gref = dh @ w1.double() / HW
+    dtref = dy.double() * rs * sd[:, None, :] + gref[:, None, :]
+    tol = {torch.float32: 1e-5, torch.bfloat16: 1e-2, torch.float16: 2e-3}[dtype]
+    assert float((dt2.double() - dtref).abs().max() / dtref.abs().max()) <= tol
