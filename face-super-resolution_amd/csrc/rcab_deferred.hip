@@ -339,6 +339,15 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
         // FC1 -> ReLU -> FC2 -> sigmoid through the wave's LDS scratch
         float* fcs = (float*)(smem + O_PFC);
         const int Cr = d.Cr;
+        // the first 16 tile partials of this wave's first tile go out before the SE weights'
+        // round trip through LDS, so the two latencies overlap (one round trip, not two)
+        float v0[16];
+        if (wave < nmine) {
+            const int b = (slot + wave * nslot) / tpi;
+            const float* pp = d.pp + (size_t)b * tpi * 64 + lane;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v0[u] = u < tpi ? pp[(size_t)u * 64] : 0.f;
+        }
         for (int i = tid; i < 1024; i += 512) {
             fcs[i] = i < Cr * 64 ? d.pfc1[i] : 0.f;          // [16][64], zero-padded hidden units
             const int c = i >> 4, j = i & 15;
@@ -349,12 +358,18 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
         for (int k = wave; k < nmine; k += 8) {
             const int t = slot + k * nslot, b = t / tpi;
             const float* pp = d.pp + (size_t)b * tpi * 64 + lane;
-            // 16 tile partials in flight per lane (a dependent chain of loads took ~4 us)
+            // 16 tile partials in flight per lane (a dependent chain of loads took ~4 us), summed
+            // in tile order
             float m = 0.f;
             for (int i0 = 0; i0 < tpi; i0 += 16) {
                 float v[16];
+                if (i0 == 0 && k == wave) {
 #pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = i0 + u < tpi ? pp[(size_t)(i0 + u) * 64] : 0.f;
+                    for (int u = 0; u < 16; ++u) v[u] = v0[u];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) v[u] = i0 + u < tpi ? pp[(size_t)(i0 + u) * 64] : 0.f;
+                }
 #pragma unroll
                 for (int u = 0; u < 16; ++u) m += v[u];
             }
