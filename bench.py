@@ -21,10 +21,11 @@ Also reported (field "train"): the stage-1 generator training step (bicubic /4 L
 synthesis, forward, L1, backward, RCCL gradient all-reduce over xGMI for N>1, clip,
 AdamW) at batch 32 per GPU -- the DP path of the north star.
 
-roofline: the dominant kernel is the fused RCAB k_rcab (conv1 -> PReLU -> conv2 -> SE gate ->
-  residual, 64 ch, 64x64, B=32): algorithmic FLOPs per launch = 2 convs x 2 * 32*64*64 px * 64 co
-  * 576 (= 9 taps * 64 ci) = 19.33 GFLOP, timed live here with HIP events on the launch stream;
-  peak = 2500 TFLOP/s bf16 dense.
+roofline: the dominant kernel is the deferred-gate RCAB k_rcab_d (the previous RCAB's SE gate
+  and scaled residual applied to the input halo, conv1 -> PReLU -> conv2 -> tile sums, 64 ch,
+  64x64, B=32): algorithmic FLOPs per launch = 2 convs x 2 * 32*64*64 px * 64 co * 576 (= 9 taps
+  * 64 ci) = 19.33 GFLOP, timed live here with HIP events on the launch stream; peak = 2500
+  TFLOP/s fp16 / bf16 dense.
 pcie_inclusive: the same forward with the batch handed over as NCHW fp32 pinned host buffers
 (H2D of the LR batch, graph replay, D2H of the SR batch, serial on one stream) -- reported
 beside `value`, never as it.
@@ -258,7 +259,8 @@ def time_gan_step(steps, B=16):
     """Stage 3 (stage3_gan_config.yaml:40-60, BASELINE C4, B=16/GPU): one Trainer iteration =
     discriminator update (G forward, D on real + fake, D backward, AdamW) + generator update
     (G forward, content L1 x 0.01 + perceptual x 1 + adversarial x 0.005 through D, backward,
-    clip, AdamW) on the module autograd path (not graph-captured)."""
+    clip, AdamW) on the module autograd path; timed as the Trainer runs it (replayed from a
+    captured hipGraph) and eagerly ("eager")."""
     import warnings
     from src.losses import create_loss_function
     from src.models import GANLoss, VGGStyleDiscriminator
@@ -275,18 +277,25 @@ def time_gan_step(steps, B=16):
     tr = Trainer(build_model("bf16"), [], None, loss_fn=loss_fn, config=cfg, discriminator=D,
                  gan_loss=GANLoss("vanilla"))
     hr = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(99)).cuda()
-    for _ in range(2):
-        tr._gan_step(hr)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        loss = tr._gan_step(hr)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+
+    def run(fn):
+        for _ in range(3):               # the captured path: 2 eager warm-ups + the capture
+            fn(hr)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = fn(hr)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, float(loss)
+
+    el_e, _ = run(tr._gan_step)
+    el, loss = run(tr._gan_iteration)
     return {"metric": "training images/sec (stage-3 GAN iteration: D update + G update, L1 0.01 + perceptual 1 + "
                       "adversarial 0.005) at batch 16/GPU", "value": round(B * steps / el, 2),
-            "ms_per_step": round(1000.0 * el / steps, 3), "steps": steps, "loss": float(loss),
-            "path": "module autograd (eager launches), VGG19 and D random-init"}
+            "ms_per_step": round(1000.0 * el / steps, 3), "steps": steps, "loss": loss,
+            "path": "Trainer iteration replayed from a captured hipGraph (capture_gan_step; module autograd "
+                    "over the HIP kernels), VGG19 and D random-init",
+            "eager": {"value": round(B * steps / el_e, 2), "ms_per_step": round(1000.0 * el_e / steps, 3)}}
 
 
 def time_ssim(eng, reps=50):

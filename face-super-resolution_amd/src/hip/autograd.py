@@ -12,6 +12,9 @@ from typing import Dict, List, Sequence
 
 import torch
 
+# diagnostic: FEN_FORCE_REPACK=1 re-packs conv weights on every use, as inside a graph capture
+_FORCE_REPACK = __import__("os").environ.get("FEN_FORCE_REPACK") == "1"
+
 from . import lib as L
 from .net import Backward, Forward, NetSpec, Weights, colsum, tiles, wgrad
 from .program import Ctx, ptr
@@ -45,6 +48,16 @@ class LiveWeights(Weights):
         w = self.params[key + ".weight"]
         stamp = (w.data_ptr(), w._version)
         k = (key, mode)
+        if k in self.packs and (torch.cuda.is_current_stream_capturing() or _FORCE_REPACK):
+            # inside a graph capture the pack is re-issued into the same buffer whatever the
+            # stamp says, so every replay packs the weights its own optimizer step left
+            buf = self.packs[k]
+            cout, cin = int(w.shape[0]), int(w.shape[1])
+            L.check(self.pack_ctx.lib.fen_pack_conv_w(L.dtype_code(self.dtype), mode, cout, cin, w.data_ptr(),
+                                                      buf.data_ptr(), torch.cuda.current_stream().cuda_stream),
+                    "pack_conv_w")
+            self._stamp[k] = stamp
+            return buf
         if k in self.packs and self._stamp.get(k) != stamp:
             del self.packs[k]   # stale copy: re-packed (and the multi-pack table rebuilt) below
         buf = super().packed(key, mode)

@@ -117,6 +117,7 @@ class FENEngine:
                 from ..training.optim import adamw_state
                 adam_state = adamw_state(self.flat_p)
             self.flat_m, self.flat_v, self.scal = adam_state
+            self._model_params = [p for _, p in model.named_parameters()]
             self.grads, off = {}, 0
             for name, p in model.named_parameters():
                 self.grads[name] = self.flat_g[off:off + p.numel()].view_as(p)
@@ -217,6 +218,8 @@ class FENEngine:
         self.exchange.wait()
         self.upd.run()
         self.Wt.pack()
+        from ..training.optim import bump_versions
+        bump_versions(self._model_params)   # the module path re-packs the updated weights
         return self.total_loss()
 
     def total_loss(self) -> torch.Tensor:
@@ -246,6 +249,9 @@ class FENEngine:
         with torch.cuda.stream(s):  # warm-up on the side stream (allocator + lazy init)
             self._replay_body()
         torch.cuda.current_stream().wait_stream(s)
+        if self.train:              # the warm-up was a training step
+            from ..training.optim import bump_versions
+            bump_versions(self._model_params)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._replay_body()
@@ -260,3 +266,6 @@ class FENEngine:
 
     def replay(self):
         self.graph.replay()
+        if self.train:
+            from ..training.optim import bump_versions
+            bump_versions(self._model_params)

@@ -22,6 +22,9 @@ from __future__ import annotations
 from typing import List
 
 import torch
+
+# diagnostic: FEN_FORCE_REPACK=1 re-packs conv weights on every use, as inside a graph capture
+_FORCE_REPACK = __import__("os").environ.get("FEN_FORCE_REPACK") == "1"
 import torch.nn as nn
 import torch.nn.functional as F
 
@@ -214,6 +217,12 @@ class VGGStyleDiscriminator(nn.Module):
         w = blk["conv"].weight
         key = (blk["i"], mode, ctx.code)
         ent = self._packs.get(key)
+        if ent is not None and (torch.cuda.is_current_stream_capturing() or _FORCE_REPACK):
+            # graph capture: re-pack into the same buffer unconditionally (each replay packs the
+            # weights its own optimizer step left)
+            cout, cin = w.shape[0], w.shape[1]
+            ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, cout, cin, ptr(w.detach()), ptr(ent[2]))
+            return ent[2]
         if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
             cout, cin = w.shape[0], w.shape[1]
             n = ctx.lib.fen_packed_elems(mode, cout, cin)

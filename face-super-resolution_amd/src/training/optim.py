@@ -22,6 +22,15 @@ def adamw_state(flat_p: torch.Tensor):
     return torch.zeros_like(flat_p), torch.zeros_like(flat_p), torch.zeros(8, device=flat_p.device)
 
 
+def bump_versions(params) -> None:
+    """The update kernels write the parameters through raw pointers, which torch's version
+    counters do not see; bump them, so everything keyed on `p._version` (the module path's
+    packed-weight caches: hip/autograd.py LiveWeights, the discriminator's packs) re-packs
+    before the next forward instead of running on the pre-update weights."""
+    for p in params:
+        torch.autograd.graph.increment_version(p)
+
+
 def state_view(params, state, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0) -> "FusedAdamW":
     """A FusedAdamW over an existing state triple without a step program: for state_dict()
     and load_state_dict() only."""
@@ -58,11 +67,15 @@ class FusedAdamW:
                       b1, b2, float(eps))
 
     def set_lr(self, lr: float):
+        # (inside a graph capture the device value is left as it is: a host write cannot be
+        # captured, and the trainer sets the rate before each replay instead)
         self.lr = float(lr)
-        self.scal[3] = self.lr
+        if not torch.cuda.is_current_stream_capturing():
+            self.scal[3] = self.lr
 
     def step(self):
         self.ctx.run()
+        bump_versions(self.params)
 
     @property
     def grad_norm(self) -> torch.Tensor:

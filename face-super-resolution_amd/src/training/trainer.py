@@ -35,7 +35,7 @@ import torch.nn.functional as F
 from ..hip.engine import FENEngine, flatten_params
 from ..hip.program import Ctx, ptr
 from .dp import broadcast_arena
-from .optim import FusedAdamW, adamw_state, state_view
+from .optim import FusedAdamW, adamw_state, bump_versions, state_view
 
 
 @dataclass
@@ -69,6 +69,10 @@ class TrainerConfig:
     d_weight_decay: float = 0.0
     d_updates_per_g: int = 1
     gan_start_epoch: int = 0
+    # (HIP extension) stage-3 iterations replay from one captured hipGraph after two eager
+    # warm-up iterations -- world size 1; re-captured when the batch shape or a learning rate
+    # changes; results identical to the eager iteration (tests/test_gpu_gan_capture.py)
+    capture_gan_step: bool = True
 
 
 class EarlyStopping:
@@ -174,6 +178,11 @@ class Trainer:
             self.gan_loss = gan_loss.to(self.device) if gan_loss is not None else GANLoss(self.config.gan_type)
             self.optimizer_d = torch.optim.AdamW(self.discriminator.parameters(), lr=self.config.d_learning_rate,
                                                  weight_decay=self.config.d_weight_decay)
+            if self._capture_gan():
+                for g in self.optimizer_d.param_groups:   # its step counts live on the device
+                    g["capturable"] = True
+        self._gan_graph: Optional[dict] = None
+        self._gan_eager_left = 2
         self.early_stopping = EarlyStopping(self.config.early_stopping_patience, self.config.early_stopping_mode)
         self.checkpoint_dir = Path(self.config.checkpoint_dir)
         if self.rank == 0:
@@ -266,6 +275,38 @@ class Trainer:
         self._apply_generic_update()
         return loss.detach()
 
+    def _capture_gan(self) -> bool:
+        return bool(self.config.capture_gan_step) and self.world == 1 and torch.cuda.is_available()
+
+    def _gan_iteration(self, hr: torch.Tensor) -> torch.Tensor:
+        """_gan_step, eagerly or (config.capture_gan_step) replayed from a hipGraph: the first
+        two iterations run eagerly (lazy initialisation, allocator warm-up), the third is
+        captured and every later one copies its batch into the captured input and replays.
+        The update kernels write the parameters behind torch's version counters, so both
+        networks' counters are bumped after a replay (the module path then re-packs)."""
+        if not self._capture_gan():
+            return self._gan_step(hr)
+        key = (tuple(hr.shape), float(self.lr), tuple(float(g["lr"]) for g in self.optimizer_d.param_groups),
+               self.config.d_updates_per_g)
+        st = self._gan_graph
+        if st is not None and st["key"] != key:
+            self._gan_graph = st = None
+        if st is None:
+            if self._gan_eager_left > 0:
+                self._gan_eager_left -= 1
+                return self._gan_step(hr)
+            static_hr = hr.detach().clone()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                loss = self._gan_step(static_hr)
+            st = self._gan_graph = {"graph": graph, "hr": static_hr, "loss": loss, "key": key}
+        st["hr"].copy_(hr)
+        if self._generic_opt is not None:
+            self._generic_opt.set_lr(self.lr)
+        st["graph"].replay()
+        bump_versions(list(self.model.parameters()) + list(self.discriminator.parameters()))
+        return st["loss"]
+
     def _apply_generic_update(self):
         if self._generic_opt is None:
             flat = self.model._fen_flat
@@ -290,7 +331,7 @@ class Trainer:
         for batch in self.train_loader:
             hr = self._shard(batch["hr"]).to(self.device, non_blocking=True)
             if self.use_gan and self.current_epoch >= self.config.gan_start_epoch:
-                loss = self._gan_step(hr)
+                loss = self._gan_iteration(hr)
             elif self.fused_l1 is not None:
                 B, _, H, W = hr.shape
                 eng = self.engine(B, H, W)
@@ -414,6 +455,7 @@ class Trainer:
         """Full resume or fine-tune (weights only) from a reference-format checkpoint
         (trainer.py:725-760).  Loaded with torch.load(weights_only=True)."""
         ckpt = torch.load(path, map_location="cpu", weights_only=True)
+        self._gan_graph = None          # a captured iteration holds the pre-load state tensors
         self.model.load_state_dict(ckpt["model_state_dict"])
         if weights_only:
             return
