@@ -12,9 +12,6 @@ from typing import Dict, List, Sequence
 
 import torch
 
-# diagnostic: FEN_FORCE_REPACK=1 re-packs conv weights on every use, as inside a graph capture
-_FORCE_REPACK = __import__("os").environ.get("FEN_FORCE_REPACK") == "1"
-
 from . import lib as L
 from .net import Backward, Forward, NetSpec, Weights, colsum, tiles, wgrad
 from .program import Ctx, ptr
@@ -48,18 +45,17 @@ class LiveWeights(Weights):
         w = self.params[key + ".weight"]
         stamp = (w.data_ptr(), w._version)
         k = (key, mode)
-        if k in self.packs and (torch.cuda.is_current_stream_capturing() or _FORCE_REPACK):
-            # inside a graph capture the pack is re-issued into the same buffer whatever the
-            # stamp says, so every replay packs the weights its own optimizer step left
-            buf = self.packs[k]
-            cout, cin = int(w.shape[0]), int(w.shape[1])
-            L.check(self.pack_ctx.lib.fen_pack_conv_w(L.dtype_code(self.dtype), mode, cout, cin, w.data_ptr(),
-                                                      buf.data_ptr(), torch.cuda.current_stream().cuda_stream),
-                    "pack_conv_w")
-            self._stamp[k] = stamp
-            return buf
-        if k in self.packs and self._stamp.get(k) != stamp:
-            del self.packs[k]   # stale copy: re-packed (and the multi-pack table rebuilt) below
+        old = self._stamp.get(k)
+        if k in self.packs and old != stamp:
+            if old[0] == stamp[0]:
+                # updated in place (an optimizer step bumps every parameter's version): re-pack
+                # every known copy in ONE fen_pack_multi launch, instead of one launch per use
+                self.pack()
+                for kk in self.packs:
+                    ww = self.params[kk[0] + ".weight"]
+                    self._stamp[kk] = (ww.data_ptr(), ww._version)
+                return self.packs[k]
+            del self.packs[k]   # re-homed: a new copy from the new storage (table rebuilt) below
         buf = super().packed(key, mode)
         self._stamp[k] = stamp
         return buf

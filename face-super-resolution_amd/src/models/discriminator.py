@@ -22,9 +22,6 @@ from __future__ import annotations
 from typing import List
 
 import torch
-
-# diagnostic: FEN_FORCE_REPACK=1 re-packs conv weights on every use, as inside a graph capture
-_FORCE_REPACK = __import__("os").environ.get("FEN_FORCE_REPACK") == "1"
 import torch.nn as nn
 import torch.nn.functional as F
 
@@ -217,16 +214,13 @@ class VGGStyleDiscriminator(nn.Module):
         w = blk["conv"].weight
         key = (blk["i"], mode, ctx.code)
         ent = self._packs.get(key)
-        if ent is not None and (torch.cuda.is_current_stream_capturing() or _FORCE_REPACK):
-            # graph capture: re-pack into the same buffer unconditionally (each replay packs the
-            # weights its own optimizer step left)
-            cout, cin = w.shape[0], w.shape[1]
-            ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, cout, cin, ptr(w.detach()), ptr(ent[2]))
-            return ent[2]
         if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+            # (a captured GAN iteration records the re-packs its Python saw: the optimizer
+            # steps bump the versions at capture time exactly as in every eager iteration)
             cout, cin = w.shape[0], w.shape[1]
             n = ctx.lib.fen_packed_elems(mode, cout, cin)
-            buf = torch.empty(n, dtype=ctx.tdtype, device=w.device)
+            buf = ent[2] if ent is not None and ent[1] == w.data_ptr() else \
+                torch.empty(n, dtype=ctx.tdtype, device=w.device)
             src = w.detach().float().contiguous()
             ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, cout, cin, ptr(src), ptr(buf))
             ctx.keep(src)

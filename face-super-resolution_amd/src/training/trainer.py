@@ -314,11 +314,13 @@ class Trainer:
             self._generic_opt = FusedAdamW(list(self.model.parameters()), flat, self._flat_g, lr=self.lr,
                                            weight_decay=self.config.weight_decay, max_norm=self.config.gradient_clip,
                                            state=self.adam_state)
-        off = 0
-        for p in self.model.parameters():
-            n = p.numel()
-            self._flat_g[off:off + n].copy_(p.grad.reshape(-1))
-            off += n
+        if getattr(self, "_flat_g_views", None) is None:
+            self._flat_g_views, off = [], 0
+            for p in self.model.parameters():
+                self._flat_g_views.append(self._flat_g[off:off + p.numel()].view_as(p))
+                off += p.numel()
+        # one multi-tensor copy (a few launches) instead of one copy per parameter (444 here)
+        torch._foreach_copy_(self._flat_g_views, [p.grad for p in self.model.parameters()])
         if self.world > 1:
             dist.all_reduce(self._flat_g)
         self._generic_opt.set_lr(self.lr)
