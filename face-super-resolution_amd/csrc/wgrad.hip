@@ -222,23 +222,29 @@ __global__ __launch_bounds__(256) void k_wgrad_finalize(int nchunk, int Cout, in
 // their 16-B chunk positions by bits 1 and 3 of the pixel column (wkey), which makes every
 // transposed fragment read bank-conflict free.  The bias gradient rides along as MFMAs
 // against a ones fragment, spread over the 4 ci-quarter waves (2 of the 8 k-steps each).
-// One fp32 slab per block in OIHW order [Cout][Cin][3][3] + [Cout] (bias); a second
-// launch sums the slabs in fixed order (bitwise reproducible).
+//
+// A launch carries up to WG_MAXJ jobs of one shape (fen_wgrad3x3_multi): the grid's x
+// blocks are (job, chunk) pairs, so n jobs share the CUs and each block reduces n x as many
+// tiles into its one fp32 slab -- the slabs (147 KB per block for a 64x64 conv, written
+// and re-read by the finalize) shrink n-fold.  A second launch sums each job's slabs in a
+// fixed order (bitwise reproducible) into its OIHW dW / db.
 // ------------------------------------------------------------------------------------
 constexpr int WG_TILE = 256 * 128;             // dy tile image, 32 KB
 constexpr int WG_TILE_DMA = WG_TILE / 1024;    // 32 pieces
 constexpr int WG_SLOT = HALO_SLOT + WG_TILE;   // 74752 B per slot, 2 slots
+constexpr int WG_MAXJ = FEN_WGRAD_MAXJOBS;
+
+// per-job operands (the shape is common to the launch: jobs.d[0])
+struct WgJobs {
+    const void* x[WG_MAXJ];
+    const void* dy[WG_MAXJ];
+    int n, nchunk, tpc;
+};
 
 __device__ __forceinline__ int wkey(int col) { return (((col >> 1) & 1) << 1) | (((col >> 3) & 1) << 2); }
 
-// NKH = 3: the block computes one kernel row kh (3 taps) and walks 3x the tiles -- 3x fewer
-// fp32 slabs to write and re-read (at 2 tiles per block the 147-KB slabs were ~half the
-// wgrad's time); the three kh blocks of a chunk fill disjoint taps of the chunk's slab and
-// sit on one XCD (block ids 8 apart), so their halo / dy reads share its L2.
-template <int NKH>
-__global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int tpc, float* part) {
+__global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, const WgJobs J, float* part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int NT = 9 / NKH;                      // taps per block
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int ch = wave & 1, cq = wave >> 1;
     const int q = lane >> 4, c16 = lane & 15, qq = c16 >> 2, pp = c16 & 3;
@@ -246,32 +252,22 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
     const int ntiles = d.B * tpi;
     const int co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64;
-    // NKH = 3: block x -> (chunk, kh) with the kh blocks of a chunk 8 ids apart (same XCD)
-    // (NKH = 3: tpc carries the chunk count; tiles split evenly over the chunks)
-    int chunk = blockIdx.x, kh0 = 0, t_begin, t_end;
-    if (NKH == 3) {
-        const int x = blockIdx.x, grp = x / 24, r = x % 24;
-        chunk = grp * 8 + (r & 7);
-        kh0 = r >> 3;
-        if (chunk >= tpc) return;                    // padding block of the last group
-        t_begin = (int)((long long)chunk * ntiles / tpc);
-        t_end = (int)((long long)(chunk + 1) * ntiles / tpc);
-    } else {
-        // consecutive chunks (neighbouring tiles: shared halo rows) on one XCD; with gridDim.x
-        // a multiple of 8 the dispatch XCD is blockIdx.x % 8 whatever y, z are
-        const int gx = (int)gridDim.x;
-        if ((gx & 7) == 0) chunk = (chunk & 7) * (gx >> 3) + (chunk >> 3);
-        t_begin = chunk * tpc;
-        t_end = min(t_begin + tpc, ntiles);
-    }
-    const i32x4 xr = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * Cin * 2));
-    const i32x4 yr = make_rsrc(d.dy, (unsigned)((size_t)d.B * H * W * Cout * 2));
+    // consecutive (job, chunk) slots -- neighbouring tiles of one job, sharing halo rows -- on
+    // one XCD; with gridDim.x a multiple of 8 the dispatch XCD is blockIdx.x % 8 whatever y, z
+    int slot = blockIdx.x;
+    const int gx = (int)gridDim.x;
+    if ((gx & 7) == 0) slot = (slot & 7) * (gx >> 3) + (slot >> 3);
+    const int job = __builtin_amdgcn_readfirstlane(slot / J.nchunk);
+    const int chunk = slot - job * J.nchunk;
+    const int t_begin = chunk * J.tpc, t_end = min(t_begin + J.tpc, ntiles);
+    const i32x4 xr = make_rsrc(J.x[job], (unsigned)((size_t)d.B * H * W * Cin * 2));
+    const i32x4 yr = make_rsrc(J.dy[job], (unsigned)((size_t)d.B * H * W * Cout * 2));
 
     // every wave issues its share of the tile's 41 halo + 32 dy pieces
-    auto issue = [&](int t, const char* slot) {
+    auto issue = [&](int t, const char* slotp) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        const unsigned hbase = lds_addr(slot), ybase = lds_addr(slot + HALO_SLOT);
+        const unsigned hbase = lds_addr(slotp), ybase = lds_addr(slotp + HALO_SLOT);
         for (int i = wave; i < HALO_DMA + WG_TILE_DMA; i += 8) {
             if (i < HALO_DMA) {
                 const int s = i * 64 + lane, p = s >> 3, pos = s & 7;
@@ -312,14 +308,13 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
         }
     }
 
-    f32x4 acc[2][NT], accb[2];
+    f32x4 acc[2][9], accb[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         accb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < 9; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const bool do_bias = kh0 == 0;
     const uint4 ones = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
 
     if (t_begin < t_end) issue(t_begin, smem);
@@ -330,8 +325,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
         if (t + 1 < t_end) issue(t + 1, smem + ((k + 1) & 1) * WG_SLOT);
         const char* hx = cur;
         const char* ty = cur + HALO_SLOT;
-        uint4 A0[2], B0[NT], A1[2], B1[NT];
-        auto load = [&](int s, uint4 (&A)[2], uint4 (&Bf)[NT]) {
+        uint4 A0[2], B0[9], A1[2], B1[9];
+        auto load = [&](int s, uint4 (&A)[2], uint4 (&Bf)[9]) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -342,8 +337,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
                     if (h == 0) { A[m].x = u.x; A[m].y = u.y; } else { A[m].z = u.x; A[m].w = u.y; }
                 }
 #pragma unroll
-                for (int tap = 0; tap < NT; ++tap) {
-                    const int kh = kh0 + tap / 3, kw = tap % 3;
+                for (int tap = 0; tap < 9; ++tap) {
+                    const int kh = tap / 3, kw = tap % 3;
                     const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (lds_s16x4*)(hx + offB[h][kw] + (2 * s + kh) * (HALO * 128)));
                     const uint2 u = __builtin_bit_cast(uint2, v);
@@ -351,12 +346,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
                 }
             }
         };
-        auto mma = [&](int s, const uint4 (&A)[2], const uint4 (&Bf)[NT]) {
+        auto mma = [&](int s, const uint4 (&A)[2], const uint4 (&Bf)[9]) {
 #pragma unroll
-            for (int tap = 0; tap < NT; ++tap)
+            for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
                 for (int m = 0; m < 2; ++m) mma16<bf16>(acc[m][tap], A[m], Bf[tap]);
-            if ((s & 3) == cq && do_bias) {
+            if ((s & 3) == cq) {
 #pragma unroll
                 for (int m = 0; m < 2; ++m) mma16<bf16>(accb[m], A[m], ones);
             }
@@ -378,20 +373,19 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
         __builtin_amdgcn_s_barrier();                         // ... for everyone; cur is free
     }
 
-    // slab: OIHW [Cout][Cin][9] then [Cout] bias partials (ci0 == 0 blocks only)
     // slab layout [tap][Cout][Cin] (+ [Cout] bias): 16 lanes store 64 contiguous bytes; the
     // OIHW order [Cout][Cin][9] put lanes 36 B apart (scattered partial-line writes of all
     // blocks at once at the end of the launch).  k_wgrad_fin transposes on its one write.
-    float* slab = part + (size_t)chunk * ((size_t)Cout * Cin * 9 + Cout);
+    float* slab = part + (size_t)slot * ((size_t)Cout * Cin * 9 + Cout);
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int co = co0 + ch * 32 + m * 16 + 4 * q + r, ci = ci0 + cq * 16 + c16;
 #pragma unroll
-            for (int tap = 0; tap < NT; ++tap) slab[((size_t)(kh0 * 3 + tap) * Cout + co) * Cin + ci] = acc[m][tap][r];
+            for (int tap = 0; tap < 9; ++tap) slab[((size_t)tap * Cout + co) * Cin + ci] = acc[m][tap][r];
         }
-    if (ci0 == 0 && do_bias) {
+    if (ci0 == 0) {
         float* red = (float*)smem;   // [4 cq][64 co]; no DMA in flight, last barrier passed
         if (c16 == 0) {
 #pragma unroll
@@ -405,21 +399,30 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, int 
     }
 }
 
+// per-job outputs of the finalize
+struct WgFinJobs {
+    float* dw[WG_MAXJ];
+    float* db[WG_MAXJ];
+    int accumulate[WG_MAXJ];
+};
+
 // dw (+)= sum_chunk slab[chunk][tap][co][ci] (co < cout_valid, written OIHW), db (+)= sum_chunk
 // slab[chunk][Cout*Cin*9 + co]: a block owns FIN_COLS float4 columns (4 ci of one (tap, co));
 // lane = (column, sub-stream), so the block's 8 waves split the chunks into 8 * 64 / FIN_COLS
 // streams, combined in a fixed order in LDS (bitwise reproducible).  64 columns per block
 // (144 blocks for a 64x64 wgrad): 16 columns (576 blocks, 4x the streams) measured 0.5%
 // slower on the training step -- the 37.7 MB slab read runs at ~5 TB/s either way.
-#ifndef WGFIN_COLS
-#define WGFIN_COLS 64
-#endif
-constexpr int FIN_COLS = WGFIN_COLS;
+// blockIdx.y = job: its slabs are chunks [job * nchunk, (job + 1) * nchunk).
+constexpr int FIN_COLS = 64;
 __global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int nw4, int nb, int boff4, int Cout,
-                                                   int Cin, const float4* __restrict__ part, float* dw, float* db,
-                                                   int accumulate) {
+                                                   int Cin, const float4* __restrict__ part_all, const WgFinJobs F) {
     constexpr int SUB = 64 / FIN_COLS, NS = 8 * SUB;
     __shared__ float4 red[NS][FIN_COLS];
+    const int job = blockIdx.y;
+    const float4* part = part_all + (size_t)job * nchunk * stride4;
+    float* dw = F.dw[job];
+    float* db = F.db[job];
+    const int accumulate = F.accumulate[job];
     const int lane = threadIdx.x & 63, w = wave_id();
     const int cl = lane % FIN_COLS, st = w * SUB + lane / FIN_COLS;
     const int j = blockIdx.x * FIN_COLS + cl;
@@ -476,8 +479,7 @@ __global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int 
 // the persistent kernel: bf16, 64-multiple channel counts, 32-bit buffer offsets
 bool wgrad_use_p(const fen_wgrad_desc* d) {
     const size_t xb = (size_t)d->B * d->H * d->W * d->Cin * 2, yb = (size_t)d->B * d->H * d->W * d->Cout * 2;
-    return d->dtype == FEN_BF16 && d->Cout % 64 == 0 && d->Cin % 64 == 0 && xb < 0x7fff0000u &&
-           yb < 0x7fff0000u && getenv("FEN_WGRAD_OLD") == nullptr;
+    return d->dtype == FEN_BF16 && d->Cout % 64 == 0 && d->Cin % 64 == 0 && xb < 0x7fff0000u && yb < 0x7fff0000u;
 }
 
 int wgrad_cus() {
@@ -492,32 +494,68 @@ int wgrad_cus() {
     return cus;
 }
 
-// persistent kernel with one kernel row per block (k_wgrad_p<3>), opt-in (FEN_WGRAD_KH3=1):
-// 3x fewer slabs, but every block then streams its tiles' full halo + dy for a third of the
-// MFMAs and the per-CU LDS-DMA rate (~17 GB/s) binds -- measured 31.8 us against 28.2 us for
-// the 9-tap form at B=32 64x64 (tools/gpu_t6.sh)
-bool wgrad_kh_split(const fen_wgrad_desc* d, int ntiles) {
-    return wgrad_use_p(d) && d->Cout == 64 && d->Cin == 64 && ntiles >= 16 && getenv("FEN_WGRAD_KH3") != nullptr;
-}
-
-int wgrad_geom(const fen_wgrad_desc* d, int* nchunk, int* tpc, int* cot) {
+// tiles per chunk / chunks per job for njobs jobs sharing ~256 blocks
+int wgrad_geom(const fen_wgrad_desc* d, int njobs, int* nchunk, int* tpc, int* cot) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int ntiles = d->B * tpi;
     *cot = d->Cout % 64 == 0 ? 64 : 16;
-    if (wgrad_kh_split(d, ntiles)) {
-        // 3 blocks per chunk, chunks in groups of 8 (one XCD each): <= 1 block per CU
-        int n = 8 * (wgrad_cus() / 24);
-        if (n < 8) n = 8;
-        if (n > ntiles) n = ntiles;
-        *nchunk = n;
-        *tpc = n;   // k_wgrad_p<3> reads the chunk count here
-        return FEN_OK;
-    }
     const int yz = (d->Cout / *cot) * ((d->Cin + 63) / 64);
-    int t = (ntiles * yz + 255) / 256;  // target ~256 blocks
+    int t = (ntiles * yz * njobs + 255) / 256;  // target ~256 blocks
     if (t < 1) t = 1;
     *tpc = t;
     *nchunk = (ntiles + t - 1) / t;
+    return FEN_OK;
+}
+
+size_t slab_floats(const fen_wgrad_desc* d) { return (size_t)d->Cout * d->Cin * 9 + d->Cout; }
+
+bool same_shape(const fen_wgrad_desc* a, const fen_wgrad_desc* b) {
+    return a->dtype == b->dtype && a->B == b->B && a->H == b->H && a->W == b->W && a->Cin == b->Cin &&
+           a->Cout == b->Cout && a->cout_valid == b->cout_valid;
+}
+
+int check_desc(const fen_wgrad_desc* d) {
+    if (!d || !d->x || !d->dy || !d->dw) return FEN_EINVAL;
+    if (d->dtype != FEN_F32 && d->dtype != FEN_BF16) return FEN_EINVAL;
+    // Cin: 16-B channel chunks (% 8 bf16, % 4 f32); a partial last 64-ci group reads zeros
+    if (d->B <= 0 || d->H <= 0 || d->W <= 0 || (d->Cin * (d->dtype == FEN_F32 ? 4 : 2)) % 16 || d->Cout % 16 ||
+        d->cout_valid <= 0 || d->cout_valid > d->Cout)
+        return FEN_EUNSUPPORTED;
+    return FEN_OK;
+}
+
+// n jobs of one persistent-kernel shape, workspace `work`
+int launch_p(int n, const fen_wgrad_desc* ds, float* work, hipStream_t s) {
+    const fen_wgrad_desc* d = &ds[0];
+    int nchunk, tpc, cot;
+    wgrad_geom(d, n, &nchunk, &tpc, &cot);
+    static bool attr = false;
+    const size_t lds = 2 * WG_SLOT;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_wgrad_p, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    WgJobs J{};
+    WgFinJobs F{};
+    for (int i = 0; i < n; ++i) {
+        J.x[i] = ds[i].x;
+        J.dy[i] = ds[i].dy;
+        F.dw[i] = ds[i].dw;
+        F.db[i] = ds[i].db;
+        F.accumulate[i] = ds[i].accumulate;
+    }
+    J.n = n;
+    J.nchunk = nchunk;
+    J.tpc = tpc;
+    hipLaunchKernelGGL(k_wgrad_p, dim3(n * nchunk, d->Cout / 64, d->Cin / 64), dim3(512), lds, s, *d, J, work);
+    FEN_CHECK_LAUNCH();
+    const int stride4 = (int)(slab_floats(d) / 4);
+    const int nw4 = d->Cout * d->Cin * 9 / 4;   // tap-major: rows co >= cout_valid skipped
+    const int boff4 = d->Cout * d->Cin * 9 / 4;
+    const int ncol = nw4 + (d->cout_valid + 3) / 4;
+    hipLaunchKernelGGL(k_wgrad_fin, dim3((ncol + FIN_COLS - 1) / FIN_COLS, n), dim3(512), 0, s, nchunk, stride4, nw4,
+                       d->cout_valid, boff4, d->Cout, d->Cin, (const float4*)work, F);
+    FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
 
@@ -526,46 +564,29 @@ int wgrad_geom(const fen_wgrad_desc* d, int* nchunk, int* tpc, int* cot) {
 extern "C" size_t fen_wgrad_work_floats(const fen_wgrad_desc* d) {
     if (!d || d->B <= 0 || d->Cin <= 0 || d->Cout <= 0) return 0;
     int nchunk, tpc, cot;
-    wgrad_geom(d, &nchunk, &tpc, &cot);
-    if (wgrad_use_p(d)) return (size_t)nchunk * ((size_t)d->Cout * d->Cin * 9 + d->Cout);
+    wgrad_geom(d, 1, &nchunk, &tpc, &cot);
+    if (wgrad_use_p(d)) return (size_t)nchunk * slab_floats(d);
     return (size_t)nchunk * 9 * d->Cout * d->Cin + (size_t)nchunk * d->Cout;
 }
 
-extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
-    if (!d || !d->x || !d->dy || !d->dw || !d->work) return FEN_EINVAL;
-    if (d->dtype != FEN_F32 && d->dtype != FEN_BF16) return FEN_EINVAL;
-    // Cin: 16-B channel chunks (% 8 bf16, % 4 f32); a partial last 64-ci group reads zeros
-    if (d->B <= 0 || d->H <= 0 || d->W <= 0 || (d->Cin * (d->dtype == FEN_F32 ? 4 : 2)) % 16 || d->Cout % 16 ||
-        d->cout_valid <= 0 ||
-        d->cout_valid > d->Cout)
-        return FEN_EUNSUPPORTED;
+extern "C" size_t fen_wgrad_multi_work_floats(int n, const fen_wgrad_desc* ds) {
+    if (!ds || n <= 0 || n > WG_MAXJ) return 0;
+    const size_t one = fen_wgrad_work_floats(&ds[0]);
+    if (!wgrad_use_p(&ds[0])) return one;   // jobs run one after another in the one workspace
     int nchunk, tpc, cot;
-    wgrad_geom(d, &nchunk, &tpc, &cot);
+    wgrad_geom(&ds[0], n, &nchunk, &tpc, &cot);
+    const size_t multi = (size_t)n * nchunk * slab_floats(&ds[0]);
+    return multi > one ? multi : one;
+}
+
+extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
+    const int st = check_desc(d);
+    if (st != FEN_OK) return st;
+    if (!d->work) return FEN_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    if (wgrad_use_p(d)) {
-        static bool attr = false;
-        const size_t lds = 2 * WG_SLOT;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_wgrad_p<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            (void)hipFuncSetAttribute((const void*)k_wgrad_p<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        const int ntiles = d->B * ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
-        if (wgrad_kh_split(d, ntiles))
-            hipLaunchKernelGGL(k_wgrad_p<3>, dim3((nchunk + 7) / 8 * 24), dim3(512), lds, s, *d, tpc, d->work);
-        else
-            hipLaunchKernelGGL(k_wgrad_p<1>, dim3(nchunk, d->Cout / 64, d->Cin / 64), dim3(512), lds, s, *d, tpc,
-                               d->work);
-        FEN_CHECK_LAUNCH();
-        const int stride4 = (d->Cout * d->Cin * 9 + d->Cout) / 4;
-        const int nw4 = d->Cout * d->Cin * 9 / 4;   // tap-major: rows co >= cout_valid skipped
-        const int boff4 = d->Cout * d->Cin * 9 / 4;
-        const int ncol = nw4 + (d->cout_valid + 3) / 4;
-        hipLaunchKernelGGL(k_wgrad_fin, dim3((ncol + FIN_COLS - 1) / FIN_COLS), dim3(512), 0, s, nchunk, stride4, nw4, d->cout_valid,
-                           boff4, d->Cout, d->Cin, (const float4*)d->work, d->dw, d->db, d->accumulate);
-        FEN_CHECK_LAUNCH();
-        return FEN_OK;
-    }
+    if (wgrad_use_p(d)) return launch_p(1, d, d->work, s);
+    int nchunk, tpc, cot;
+    wgrad_geom(d, 1, &nchunk, &tpc, &cot);
     float* part = d->work;
     float* dbpart = d->work + (size_t)nchunk * 9 * d->Cout * d->Cin;
     dim3 grid(nchunk, d->Cout / cot, (d->Cin + 63) / 64);
@@ -585,5 +606,23 @@ extern "C" int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream) {
     hipLaunchKernelGGL(k_wgrad_finalize, dim3(nb), dim3(256), 0, s, nchunk, d->Cout, d->Cin, d->cout_valid,
                        part, dbpart, d->dw, d->db, d->accumulate);
     FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_wgrad3x3_multi(int n, const fen_wgrad_desc* ds, void* stream) {
+    if (!ds || n <= 0 || n > WG_MAXJ || !ds[0].work) return FEN_EINVAL;
+    for (int i = 0; i < n; ++i) {
+        const int st = check_desc(&ds[i]);
+        if (st != FEN_OK) return st;
+        if (!same_shape(&ds[0], &ds[i])) return FEN_EINVAL;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (wgrad_use_p(&ds[0])) return launch_p(n, ds, ds[0].work, s);
+    for (int i = 0; i < n; ++i) {   // generic kernel: one job at a time in the shared workspace
+        fen_wgrad_desc d = ds[i];
+        d.work = ds[0].work;
+        const int st = fen_wgrad3x3(&d, stream);
+        if (st != FEN_OK) return st;
+    }
     return FEN_OK;
 }

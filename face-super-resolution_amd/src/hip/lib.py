@@ -66,6 +66,8 @@ _SIGS = {
     "fen_conv3x3": (c_int, [POINTER(ConvDesc), c_void_p]),
     "fen_wgrad_work_floats": (c_size_t, [POINTER(WgradDesc)]),
     "fen_wgrad3x3": (c_int, [POINTER(WgradDesc), c_void_p]),
+    "fen_wgrad_multi_work_floats": (c_size_t, [c_int, c_void_p]),
+    "fen_wgrad3x3_multi": (c_int, [c_int, c_void_p, c_void_p]),
     "fen_rcab_deferred_supported": (c_int, [c_int] * 6),
     "fen_rcab_deferred": (c_int, [POINTER(RcabDeferredDesc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),

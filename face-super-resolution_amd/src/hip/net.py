@@ -153,6 +153,48 @@ def wgrad(ctx: Ctx, x, dy, B, H, W, Cin, Cout, dw, db, cout_valid=None) -> None:
     ctx.emit("wgrad3x3", ctx.lib.fen_wgrad3x3, byref(d))
 
 
+# weight gradients of the RCAB convs issued per launch (fen_wgrad3x3_multi jobs, <= 8): the
+# jobs share the CUs, so the per-block fp32 slabs shrink by that factor (FEN_WGRAD_BATCH=1:
+# one launch per conv)
+WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
+
+
+class WgradBatch:
+    """Weight gradients of one shape queued by the backward builder and issued as ONE
+    fen_wgrad3x3_multi launch pair once `size` jobs are queued, on a shape change or at
+    flush().  The caller keeps each job's x / dy alive (unwritten) until the flush."""
+
+    def __init__(self, ctx: Ctx, size: int = WGRAD_BATCH):
+        self.ctx, self.size = ctx, size
+        self.jobs: List[L.WgradDesc] = []
+        self.hold: List[torch.Tensor] = []   # eager mode: x / dy must outlive the launch
+
+    def add(self, x, dy, B, H, W, Cin, Cout, dw, db) -> None:
+        d = L.WgradDesc()
+        d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = self.ctx.code, B, H, W, Cin, Cout
+        d.cout_valid = Cout
+        d.x, d.dy, d.dw, d.db, d.accumulate = ptr(x), ptr(dy), ptr(dw), ptr(db), 0
+        if self.jobs and (B, H, W, Cin, Cout) != (self.jobs[0].B, self.jobs[0].H, self.jobs[0].W,
+                                                   self.jobs[0].Cin, self.jobs[0].Cout):
+            self.flush()
+        self.jobs.append(d)
+        self.hold += [x, dy]
+        if len(self.jobs) >= self.size:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.jobs:
+            return
+        n = len(self.jobs)
+        arr = (L.WgradDesc * n)(*self.jobs)
+        nwork = self.ctx.lib.fen_wgrad_multi_work_floats(n, ctypes.cast(arr, ctypes.c_void_p))
+        work = self.ctx.scratch("wgrad_work", (nwork,), torch.float32)
+        arr[0].work = ptr(work)
+        self.ctx.emit("wgrad3x3_multi", self.ctx.lib.fen_wgrad3x3_multi, n, ctypes.cast(arr, ctypes.c_void_p))
+        self.ctx.keep(arr)
+        self.jobs, self.hold = [], []
+
+
 def colsum(ctx: Ctx, part, rows, cols, out, scale=1.0) -> None:
     ctx.emit("colsum", ctx.lib.fen_colsum, rows, cols, ptr(part), float(scale), ptr(out), 0)
 
@@ -361,6 +403,8 @@ class Backward:
     def __init__(self, spec: NetSpec, ctx: Ctx, Wt: Weights, G: Dict[str, torch.Tensor]):
         self.s, self.ctx, self.Wt, self.G = spec, ctx, Wt, G
         self.cs = ColsumBatch(ctx)   # flushed at the end of every group / the tail
+        self.wb = WgradBatch(ctx)    # RCAB conv weight gradients; flushed with self.cs
+        self._rc = 0                 # RCAB backward counter: rotates the dt / dz1 buffers
 
     def _wg(self, key, x, dy, B, H, W, Cin, Cout, cout_valid=None):
         wgrad(self.ctx, x, dy, B, H, W, Cin, Cout, self.G[key + ".weight"], self.G.get(key + ".bias"), cout_valid)
@@ -378,7 +422,11 @@ class Backward:
         dw1p = ctx.scratch("bw_dw1p" + pre, (B, s.Cr * C), torch.float32)
         dw2p = ctx.scratch("bw_dw2p" + pre, (B, s.Cr * C), torch.float32)
         ca = pre + "channel_attention.fc."
-        dt = ctx.scratch("bw_dt", dy.shape)
+        # dt / dz1 stay untouched until the queued weight gradients that read them are issued:
+        # a batch of n jobs spans at most n // 2 + 1 RCABs, so n rotating buffers suffice
+        rot = self._rc % self.wb.size
+        self._rc += 1
+        dt = ctx.scratch(f"bw_dt{rot}", dy.shape)
         se_args = (npart, 1.0 / HW, s.res_scale, ptr(part), ptr(sv["mean"]), ptr(sv["hid"]), ptr(sv["s"]),
                    ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]))
         if SE_BWD_FUSED and C <= 64 and npart <= 64 and C * s.Cr <= 4096:
@@ -392,19 +440,23 @@ class Backward:
                      ptr(g), ptr(dt))
         self.cs.add(dw1p, B, s.Cr * C, G[ca + "0.weight"])
         self.cs.add(dw2p, B, s.Cr * C, G[ca + "2.weight"])
-        self._wg(pre + "conv2", sv["a1"], dt, B, H, W, C, C)
-        dz1 = ctx.scratch("bw_dz1", dy.shape)
+        self.wb.add(sv["a1"], dt, B, H, W, C, C, G[pre + "conv2.weight"], G[pre + "conv2.bias"])
+        dz1 = ctx.scratch(f"bw_dz1{rot}", dy.shape)
         T = tiles(H, W)
         dal = ctx.scratch("bw_dal" + pre, (B * T, C), torch.float32)
         conv(ctx, dt, Wt.packed(pre + "conv2", 2), B, H, W, C, C, epi=L.EPI_PRELU_BWD, alpha=p[pre + "prelu.weight"],
              pre_in=sv["z1"], y=dz1, part=dal)
         self.cs.add(dal, B * T, C, G[pre + "prelu.weight"])
-        self._wg(pre + "conv1", sv["x"], dz1, B, H, W, C, C)
+        self.wb.add(sv["x"], dz1, B, H, W, C, C, G[pre + "conv1.weight"], G[pre + "conv1.bias"])
         dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
         conv(ctx, dz1, Wt.packed(pre + "conv1", 2), B, H, W, C, C, y=dx, res=(dy,) + tuple(extra_res))
         if flush:
-            self.cs.flush()
+            self.flush()
         return dx
+
+    def flush(self) -> None:
+        self.wb.flush()
+        self.cs.flush()
 
     def group(self, sv: dict, dy: torch.Tensor, g: int, extra_res: Sequence = (), dx_out=None,
               pre: Optional[str] = None) -> torch.Tensor:
@@ -421,7 +473,7 @@ class Backward:
             else:
                 d = self.rcab(sv["blocks"][b], d, f"{pre}blocks.{b}.",
                               dx_out=ctx.scratch(f"bw_rg_pp{b & 1}", dy.shape), flush=False)
-        self.cs.flush()
+        self.flush()
         return d
 
     def tail(self, sv: dict) -> torch.Tensor:

@@ -95,6 +95,17 @@ typedef struct {
 size_t fen_wgrad_work_floats(const fen_wgrad_desc* d);
 int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream);
 
+/* n (<= FEN_WGRAD_MAXJOBS) independent weight gradients of one shape (B, H, W, Cin, Cout,
+ * dtype) in one launch pair: the CUs are split between the jobs, so each block reduces n x
+ * as many pixel tiles into its fp32 slab and the slabs (written and re-read) shrink n-fold.
+ * One shared workspace: descs[0].work, fen_wgrad_multi_work_floats() floats (the other
+ * descs' work fields are ignored).  Results equal fen_wgrad3x3 per job up to fp32
+ * summation order (deterministic run to run).  The backward's conv1/conv2 weight gradients
+ * of consecutive RCABs (autograd of blocks.py:135-153's convs; trainer.py:482-485).       */
+#define FEN_WGRAD_MAXJOBS 8
+size_t fen_wgrad_multi_work_floats(int n, const fen_wgrad_desc* descs);
+int fen_wgrad3x3_multi(int n, const fen_wgrad_desc* descs, void* stream);
+
 /* conv_first forward: NCHW fp32 [B,Ci,H,W] -> NHWC [B,H,W,C] (custom.py:91-94,164)          */
 int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C, const float* x,
                        const float* w, const float* bias, void* y, void* stream);

@@ -63,3 +63,27 @@ def test_rcab_deferred_validation_without_gpu():
     assert lib.fen_rcab_deferred(d, None) == -1
     d.tp, d.z1 = 0, 16              # z1 without a1
     assert lib.fen_rcab_deferred(d, None) == -1
+
+
+def test_wgrad_multi_validation_without_gpu():
+    """fen_wgrad3x3_multi: job count bounds, one shape per launch, workspace size (n jobs of
+    the persistent kernel share the ~256 slabs of one job)."""
+    import ctypes
+    from src.hip import lib as L
+    lib = L.load()
+    arr = (L.WgradDesc * 9)()
+    for d in arr:
+        d.dtype, d.B, d.H, d.W, d.Cin, d.Cout, d.cout_valid = L.BF16, 32, 64, 64, 64, 64, 64
+        d.x = d.dy = d.dw = d.work = 16
+    p = ctypes.cast(arr, ctypes.c_void_p)
+    assert lib.fen_wgrad3x3_multi(0, p, None) == -1
+    assert lib.fen_wgrad3x3_multi(9, p, None) == -1
+    assert lib.fen_wgrad_multi_work_floats(9, p) == 0
+    one = lib.fen_wgrad_work_floats(ctypes.byref(arr[0]))
+    assert one == 256 * (64 * 64 * 9 + 64)
+    assert lib.fen_wgrad_multi_work_floats(4, p) == one          # 4 jobs x 64 chunks
+    arr[2].H = 32                                                 # shapes differ
+    assert lib.fen_wgrad3x3_multi(4, p, None) == -1
+    arr[2].H = 64
+    arr[3].x = None
+    assert lib.fen_wgrad3x3_multi(4, p, None) == -1

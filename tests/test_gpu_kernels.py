@@ -320,8 +320,8 @@ def test_wgrad(dtype, B, H, W, Cin, Cout):
     """fen_wgrad3x3 vs autograd of conv2d.  The reference runs in float64 on the operands
     rounded to the compute dtype, so bf16 is held to fp32-accumulation accuracy (rel 1e-5):
     a wrong fragment mapping or a dropped tile shows as O(1).  (17, 64, 64) puts 2 tiles per
-    block; Cout 256 / Cin 128 exercise the co-group / ci-group grid.  The opt-in
-    one-kernel-row-per-block form (FEN_WGRAD_KH3) is covered by test_wgrad_kh_split."""
+    block; Cout 256 / Cin 128 exercise the co-group / ci-group grid.  Several jobs per launch:
+    test_wgrad_multi."""
     from src.hip import net
     torch.manual_seed(7)
     x = torch.randn(B, Cin, H, W).to(dtype).float()
@@ -341,16 +341,51 @@ def test_wgrad(dtype, B, H, W, Cin, Cout):
     assert rel <= 1e-5 and relb <= 1e-5, (rel, relb)
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (3, 40, 56), (17, 64, 64)])
-def test_wgrad_kh_split(B, H, W):
-    """k_wgrad_p<3> (one kernel row per block, FEN_WGRAD_KH3=1; read at launch) vs float64
-    autograd: 32 tiles (32 chunks), ragged 40 x 56, 272 tiles (80 chunks of 3-4)."""
-    import os
-    os.environ["FEN_WGRAD_KH3"] = "1"
-    try:
-        test_wgrad(torch.bfloat16, B, H, W, 64, 64)
-    finally:
-        del os.environ["FEN_WGRAD_KH3"]
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,B,H,W,Cin,Cout", [(2, 2, 64, 64, 64, 64), (4, 32, 64, 64, 64, 64),
+                                               (3, 3, 40, 56, 64, 64), (8, 1, 16, 16, 64, 64),
+                                               (4, 17, 64, 64, 64, 64), (2, 2, 32, 32, 64, 256),
+                                               (3, 2, 16, 16, 32, 32)])
+def test_wgrad_multi(dtype, n, B, H, W, Cin, Cout):
+    """fen_wgrad3x3_multi (n jobs of one shape in one launch pair, the CUs split between them)
+    vs float64 autograd per job, rel 1e-5 as test_wgrad.  Covers the bench's B=32 64x64 batch
+    of 4, ragged tiles, a one-tile job set (8 jobs x 1 tile), the co-group grid (Cout 256), a
+    job with accumulate=1 and, for fp32 / 32 channels, the generic kernel run job by job."""
+    from src.hip import lib as L
+    from src.hip.program import ptr
+    torch.manual_seed(11)
+    ctx = _ctx(dtype)
+    arr = (L.WgradDesc * n)()
+    refs, outs, keep = [], [], []
+    for i in range(n):
+        x = torch.randn(B, Cin, H, W).to(dtype).float()
+        dy = torch.randn(B, Cout, H, W).to(dtype).float()
+        w = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
+        bb = torch.zeros(Cout, dtype=torch.float64, requires_grad=True)
+        F.conv2d(x.double(), w, bb, padding=1).mul(dy.double()).sum().backward()
+        acc = 1 if i == 1 else 0
+        dw0 = torch.randn(Cout, Cin, 3, 3) if acc else torch.zeros(Cout, Cin, 3, 3)
+        db0 = torch.randn(Cout) if acc else torch.zeros(Cout)
+        refs.append((w.grad + dw0.double() * acc, bb.grad + db0.double() * acc))
+        xd, dyd = nhwc(x, dtype), nhwc(dy, dtype)
+        dw, db = dw0.to(DEV), db0.to(DEV)
+        keep += [xd, dyd]
+        outs.append((dw, db))
+        d = arr[i]
+        d.dtype, d.B, d.H, d.W, d.Cin, d.Cout, d.cout_valid = ctx.code, B, H, W, Cin, Cout, Cout
+        d.x, d.dy, d.dw, d.db, d.accumulate = ptr(xd), ptr(dyd), ptr(dw), ptr(db), acc
+    import ctypes
+    nwork = ctx.lib.fen_wgrad_multi_work_floats(n, ctypes.cast(arr, ctypes.c_void_p))
+    assert nwork >= ctx.lib.fen_wgrad_work_floats(ctypes.byref(arr[0]))
+    work = ctx.alloc((nwork,), torch.float32)
+    arr[0].work = ptr(work)
+    L.check(ctx.lib.fen_wgrad3x3_multi(n, ctypes.cast(arr, ctypes.c_void_p), torch.cuda.current_stream().cuda_stream),
+            "wgrad_multi")
+    torch.cuda.synchronize()
+    for (gw, gb), (dw, db) in zip(refs, outs):
+        rel = float((dw.cpu().double() - gw).norm() / gw.norm())
+        relb = float((db.cpu().double() - gb).norm() / gb.norm())
+        assert rel <= 1e-5 and relb <= 1e-5, (rel, relb)
 
 
 @pytest.mark.parametrize("dtype", DT)
