@@ -236,6 +236,12 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                         v[r] = prelu_bwd_f(v[r], pv[r], al4[r]);
                     }
                 }
+                if (epi & FEN_EPI_DOT) {
+                    float pv[4];
+                    ld4<T>((const char*)d.pre_in + oi * sizeof(T), pv);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) psum[m][r] += rnd16<T>(v[r]) * pv[r];
+                }
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[m][n][r] = v[r];
@@ -247,7 +253,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
     }
 
     // per-channel partial sums (SE pool or PReLU dalpha): 16-lane butterfly, then across waves
-    if (epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD)) {
+    if (epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD | FEN_EPI_DOT)) {
         // red[] was last read before the previous tile's closing barrier: no barrier needed here
 #pragma unroll
         for (int m = 0; m < MT; ++m)
@@ -661,7 +667,9 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
     constexpr int NRES = EPIC >> 8;
     constexpr int EPI = EPIC & 0xff;
     constexpr bool PRELU = EPI & FEN_EPI_PRELU, PBWD = EPI & FEN_EPI_PRELU_BWD, POOL = EPI & FEN_EPI_POOL;
-    constexpr bool SHUF = EPI & FEN_EPI_SHUFFLE;
+    constexpr bool SHUF = EPI & FEN_EPI_SHUFFLE, DOT = EPI & FEN_EPI_DOT;
+    constexpr bool PART = POOL || PBWD || DOT;                // per-tile channel partials
+    constexpr bool PIN = PBWD || DOT;                         // reads pre_in
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* wts = smem;
     float* red = (float*)(smem + G_WBYTES + 2 * HALO_SLOT);   // [grp][wr][64]
@@ -736,7 +744,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
         int nst = 0;
         if ((ph & 1) == grp) {
             // ---------------- compute phase: tile j = (ph - grp) / 2 ----------------
-            if ((POOL || PBWD) && pending_part >= 0 && wr == 0) {
+            if (PART && pending_part >= 0 && wr == 0) {
                 const float* rg = red + grp * 256;
                 d.part[(size_t)pending_part * Cout + co0 + lane] =
                     (rg[lane] + rg[64 + lane]) + (rg[128 + lane] + rg[192 + lane]);
@@ -759,7 +767,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
             const bool ret = ph > grp && jp >= 0 && jp < myn;
             if (jp + 1 < myn) issue_halo(tile_of(grp, jp + 1));
             uint2 rv[NRES > 0 ? NRES : 1][MT][NT];
-            uint2 pv[PBWD ? MT : 1][PBWD ? NT : 1];
+            uint2 pv[PIN ? MT : 1][PIN ? NT : 1];
             int b = 0, h0 = 0, w0 = 0, t = 0;
             bool full = true;
             if (ret) {
@@ -777,7 +785,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                     for (int m = 0; m < MT; ++m) {
 #pragma unroll
                         for (int k = 0; k < NRES; ++k) rv[k][m][n] = *(const uint2*)((const char*)d.res[k] + (oi + m * 16) * 2);
-                        if constexpr (PBWD) pv[m][n] = *(const uint2*)((const char*)d.pre_in + (oi + m * 16) * 2);
+                        if constexpr (PIN) pv[m][n] = *(const uint2*)((const char*)d.pre_in + (oi + m * 16) * 2);
                     }
                 }
             }
@@ -809,7 +817,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                             rf[k][2] = lo16<T>(rv[k][m][n].y);
                             rf[k][3] = hi16<T>(rv[k][m][n].y);
                         }
-                        if constexpr (PBWD) {
+                        if constexpr (PIN) {
                             pf[0] = lo16<T>(pv[m][n].x);
                             pf[1] = hi16<T>(pv[m][n].x);
                             pf[2] = lo16<T>(pv[m][n].y);
@@ -826,6 +834,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                                 v = prelu_bwd_f(v, pr, al4[r]);
                             }
                             if constexpr (POOL) psum[m][r] += okf * v;
+                            if constexpr (DOT) psum[m][r] += okf * rnd16<T>(v) * pf[r];
                             acc[m][n][r] = v;
                         }
                     }
@@ -861,7 +870,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                         ++nst;
                     }
                 }
-                if constexpr (POOL || PBWD) {
+                if constexpr (PART) {
                     float* rg = red + grp * 256 + wr * 64;
 #pragma unroll
                     for (int m = 0; m < MT; ++m)
@@ -881,7 +890,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
         __builtin_amdgcn_s_barrier();
         FEN_STAMP(3 + 2 * ph);
     }
-    if ((POOL || PBWD) && pending_part >= 0 && wr == 0) {
+    if (PART && pending_part >= 0 && wr == 0) {
         const float* rg = red + grp * 256;
         d.part[(size_t)pending_part * Cout + co0 + lane] = (rg[lane] + rg[64 + lane]) + (rg[128 + lane] + rg[192 + lane]);
     }
@@ -1074,7 +1083,7 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
     if (!d->y) return FEN_EINVAL;
     if (epi & FEN_EPI_SHUFFLE) {
         if (d->Cout % 64) return FEN_EUNSUPPORTED;
-        if (epi & (FEN_EPI_PRELU_BWD | FEN_EPI_POOL) || d->res[0] || d->res[1] || d->res[2])
+        if (epi & (FEN_EPI_PRELU_BWD | FEN_EPI_POOL | FEN_EPI_DOT) || d->res[0] || d->res[1] || d->res[2])
             return FEN_EUNSUPPORTED;
     }
     if ((epi & FEN_EPI_UNSHUFFLE) && ((d->H | d->W) & 1)) return FEN_EINVAL;
@@ -1103,6 +1112,8 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
                         case 1 << 8: return launch_g<T, 1 << 8>(d, s);
                         case 2 << 8: return launch_g<T, 2 << 8>(d, s);
                         case 3 << 8: return launch_g<T, 3 << 8>(d, s);
+                        case FEN_EPI_DOT: return launch_g<T, FEN_EPI_DOT>(d, s);
+                        case FEN_EPI_DOT | (1 << 8): return launch_g<T, FEN_EPI_DOT | (1 << 8)>(d, s);
                         default: break;
                     }
                 }
@@ -1138,9 +1149,14 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     const int epi = d->epi;
     if ((epi & FEN_EPI_BIAS) && !d->bias) return FEN_EINVAL;
     if ((epi & (FEN_EPI_PRELU | FEN_EPI_PRELU_BWD)) && !d->alpha) return FEN_EINVAL;
-    if ((epi & FEN_EPI_PRELU_BWD) && !d->pre_in) return FEN_EINVAL;
-    if ((epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD)) && !d->part) return FEN_EINVAL;
-    if ((epi & FEN_EPI_POOL) && (epi & FEN_EPI_PRELU_BWD)) return FEN_EUNSUPPORTED;
+    if ((epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT)) && !d->pre_in) return FEN_EINVAL;
+    if ((epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD | FEN_EPI_DOT)) && !d->part) return FEN_EINVAL;
+    // one partial-sum stream per launch
+    {
+        const int np = !!(epi & FEN_EPI_POOL) + !!(epi & FEN_EPI_PRELU_BWD) + !!(epi & FEN_EPI_DOT);
+        if (np > 1) return FEN_EUNSUPPORTED;
+    }
+    if ((epi & FEN_EPI_DOT) && (epi & (FEN_EPI_UNSHUFFLE | FEN_EPI_LAST))) return FEN_EUNSUPPORTED;
     if ((epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE)) == (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE))
         return FEN_EUNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;

@@ -70,9 +70,14 @@ template <> __device__ __forceinline__ float tof<float>(float v) { return v; }
 template <> __device__ __forceinline__ float tof<bf16>(bf16 v) { return (float)v; }
 template <> __device__ __forceinline__ float tof<f16>(f16 v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T fromf(float v);
+// v as stored in T (the value a later pass would read back)
+template <typename T> __device__ __forceinline__ float rnd16(float v);
 template <> __device__ __forceinline__ float fromf<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16 fromf<bf16>(float v) { return (bf16)v; }
 template <> __device__ __forceinline__ f16 fromf<f16>(float v) { return (f16)v; }
+template <> __device__ __forceinline__ float rnd16<float>(float v) { return v; }
+template <> __device__ __forceinline__ float rnd16<bf16>(float v) { return (float)(bf16)v; }
+template <> __device__ __forceinline__ float rnd16<f16>(float v) { return (float)(f16)v; }
 
 // 4 consecutive elements <-> float[4]
 template <typename T> __device__ __forceinline__ void ld4(const void* p, float v[4]);

@@ -22,6 +22,7 @@ EPI_PRELU_BWD = 8
 EPI_UNSHUFFLE = 16
 EPI_POOL = 32
 EPI_LAST = 64
+EPI_DOT = 128
 
 
 class ConvDesc(Structure):

@@ -156,6 +156,9 @@ def wgrad(ctx: Ctx, x, dy, B, H, W, Cin, Cout, dw, db, cout_valid=None) -> None:
 # weight gradients of the RCAB convs issued per launch (fen_wgrad3x3_multi jobs, <= 8): the
 # jobs share the CUs, so the per-block fp32 slabs shrink by that factor (FEN_WGRAD_BATCH=1:
 # one launch per conv)
+# sum(dy * t) of the SE backward from the producing dgrad's epilogue (FEN_EPI_DOT) instead of
+# a fen_pool_dot pass over dy and t (FEN_SE_DOT=pass: the separate pass)
+DOT_FUSED = os.environ.get("FEN_SE_DOT", "fused") != "pass"
 WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
 
 
@@ -405,20 +408,39 @@ class Backward:
         self.cs = ColsumBatch(ctx)   # flushed at the end of every group / the tail
         self.wb = WgradBatch(ctx)    # RCAB conv weight gradients; flushed with self.cs
         self._rc = 0                 # RCAB backward counter: rotates the dt / dz1 buffers
+        # (partials, parts per image) of sum dy*t for the next rcab(), computed by the epilogue
+        # of the dgrad that produced its dy (FEN_EPI_DOT) instead of a fen_pool_dot pass
+        self._dot = None
 
     def _wg(self, key, x, dy, B, H, W, Cin, Cout, cout_valid=None):
         wgrad(self.ctx, x, dy, B, H, W, Cin, Cout, self.G[key + ".weight"], self.G.get(key + ".bias"), cout_valid)
 
+    def _dot_conv(self, t_next, B, H, W, C) -> dict:
+        """conv() kwargs that make a dgrad also emit sum(output * t_next) per tile and channel
+        (the next rcab()'s SE-backward operand); {} without t_next."""
+        if t_next is None or not DOT_FUSED:
+            return {}
+        T = tiles(H, W)
+        part = self.ctx.scratch(f"bw_dot{self._rc & 1}", (B * T, C), torch.float32)
+        self._dot = (part, T)
+        return dict(epi=L.EPI_DOT, pre_in=t_next, part=part)
+
     def rcab(self, sv: dict, dy: torch.Tensor, pre: str, extra_res: Sequence = (), dx_out=None,
-             flush: bool = True) -> torch.Tensor:
+             flush: bool = True, t_next=None) -> torch.Tensor:
         """RCAB backward; its PReLU / SE weight-gradient column sums are queued on self.cs and
-        issued at the end (flush=True) or by the caller (group() batches a whole group)."""
+        issued at the end (flush=True) or by the caller (group() batches a whole group).
+        t_next: the SE input t of the RCAB whose backward follows (its dy is this one's dx),
+        dotted with dx in the conv1 dgrad's epilogue."""
         s, ctx, Wt, p, G = self.s, self.ctx, self.Wt, self.Wt.p, self.G
         B, H, W, C = dy.shape
         HW = H * W
-        npart = ctx.lib.fen_pool_parts(HW)
-        part = ctx.scratch("bw_pool", (B * npart, C), torch.float32)
-        ctx.emit("pool_dot", ctx.lib.fen_pool_dot, ctx.code, B, HW, C, ptr(dy), ptr(sv["t"]), ptr(part))
+        if self._dot is not None:
+            part, npart = self._dot          # sum dy*t per tile, from dy's producer
+            self._dot = None
+        else:
+            npart = ctx.lib.fen_pool_parts(HW)
+            part = ctx.scratch("bw_pool", (B * npart, C), torch.float32)
+            ctx.emit("pool_dot", ctx.lib.fen_pool_dot, ctx.code, B, HW, C, ptr(dy), ptr(sv["t"]), ptr(part))
         dw1p = ctx.scratch("bw_dw1p" + pre, (B, s.Cr * C), torch.float32)
         dw2p = ctx.scratch("bw_dw2p" + pre, (B, s.Cr * C), torch.float32)
         ca = pre + "channel_attention.fc."
@@ -449,7 +471,8 @@ class Backward:
         self.cs.add(dal, B * T, C, G[pre + "prelu.weight"])
         self.wb.add(sv["x"], dz1, B, H, W, C, C, G[pre + "conv1.weight"], G[pre + "conv1.bias"])
         dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
-        conv(ctx, dz1, Wt.packed(pre + "conv1", 2), B, H, W, C, C, y=dx, res=(dy,) + tuple(extra_res))
+        conv(ctx, dz1, Wt.packed(pre + "conv1", 2), B, H, W, C, C, y=dx, res=(dy,) + tuple(extra_res),
+             **self._dot_conv(t_next, B, H, W, C))
         if flush:
             self.flush()
         return dx
@@ -465,14 +488,17 @@ class Backward:
         pre = f"residual_groups.{g}." if pre is None else pre
         self._wg(pre + "conv", sv["x_last"], dy, B, H, W, C, C)
         d = ctx.scratch("bw_rg_in", dy.shape)
-        conv(ctx, dy, Wt.packed(pre + "conv", 2), B, H, W, C, C, y=d)
+        blocks = sv["blocks"]
+        conv(ctx, dy, Wt.packed(pre + "conv", 2), B, H, W, C, C, y=d,
+             **(self._dot_conv(blocks[-1].get("t"), B, H, W, C) if s.NB > 0 else {}))
         for b in reversed(range(s.NB)):
             if b == 0:
-                d = self.rcab(sv["blocks"][b], d, f"{pre}blocks.{b}.", extra_res=(dy,) + tuple(extra_res),
+                d = self.rcab(blocks[b], d, f"{pre}blocks.{b}.", extra_res=(dy,) + tuple(extra_res),
                               dx_out=dx_out, flush=False)
             else:
-                d = self.rcab(sv["blocks"][b], d, f"{pre}blocks.{b}.",
-                              dx_out=ctx.scratch(f"bw_rg_pp{b & 1}", dy.shape), flush=False)
+                d = self.rcab(blocks[b], d, f"{pre}blocks.{b}.",
+                              dx_out=ctx.scratch(f"bw_rg_pp{b & 1}", dy.shape), flush=False,
+                              t_next=blocks[b - 1].get("t"))
         self.flush()
         return d
 

@@ -40,7 +40,8 @@ enum {
     FEN_EPI_PRELU_BWD = 8,  /* y = v*(pre>0?1:alpha[co]); part[blk][co] = sum v*pre*(pre<=0)     */
     FEN_EPI_UNSHUFFLE = 16, /* inverse PixelShuffle(2) store: y is [B,H/2,W/2,4*Cout]           */
     FEN_EPI_POOL = 32,      /* part[b][tile][co] = sum over the tile's pixels of the stored v   */
-    FEN_EPI_LAST = 64       /* conv_last: + bicubic skip, eval clamp, NCHW fp32 out, L1 grad    */
+    FEN_EPI_LAST = 64,      /* conv_last: + bicubic skip, eval clamp, NCHW fp32 out, L1 grad    */
+    FEN_EPI_DOT = 128       /* part[b][tile][co] = sum over the tile of (stored v) * pre_in      */
 };
 
 /* 3x3, stride 1, pad 1 convolution as an implicit GEMM on MFMA.
@@ -62,7 +63,9 @@ typedef struct {
                                   UNSHUFFLE [B,H/2,W/2,4*Cout] | LAST NCHW fp32 [B,Cout,H,W]     */
     void* y_pre;               /* FEN_EPI_PRELU: pre-activation copy, same layout as y (or NULL) */
     const void* res[3];        /* residual tensors NHWC [B,H,W,Cout] added to v (or NULL)       */
-    const void* pre_in;        /* FEN_EPI_PRELU_BWD: pre-activation NHWC [B,H,W,Cout]          */
+    const void* pre_in;        /* FEN_EPI_PRELU_BWD: pre-activation NHWC [B,H,W,Cout]; FEN_EPI_DOT:
+                                  the tensor dotted with the output (the next RCAB's SE input t:
+                                  the SE backward's sum dy*t, blocks.py:83-92, without a pass)   */
     float* part;               /* POOL / PRELU_BWD partial sums [B*tiles][Cout], tiles=ceil(H/16)*ceil(W/16) */
     /* FEN_EPI_LAST only */
     const float* lr;           /* LR input NCHW fp32 [B,Cout,H/scale,W/scale] for the bicubic skip */

@@ -87,3 +87,20 @@ def test_wgrad_multi_validation_without_gpu():
     arr[2].H = 64
     arr[3].x = None
     assert lib.fen_wgrad3x3_multi(4, p, None) == -1
+
+
+def test_conv_dot_epilogue_validation_without_gpu():
+    """FEN_EPI_DOT needs pre_in (the dotted tensor) and part, and is one partial-sum stream:
+    not combinable with POOL / PRELU_BWD, SHUFFLE / UNSHUFFLE or LAST."""
+    from src.hip import lib as L
+    lib = L.load()
+    d = L.ConvDesc()
+    d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = L.BF16, 1, 16, 16, 64, 64
+    d.x = d.w = d.y = 16
+    d.epi = L.EPI_DOT
+    assert lib.fen_conv3x3(d, None) == -1            # no pre_in / part
+    d.pre_in = d.part = 16
+    d.epi = L.EPI_DOT | L.EPI_POOL
+    assert lib.fen_conv3x3(d, None) == -2
+    d.epi = L.EPI_DOT | L.EPI_UNSHUFFLE
+    assert lib.fen_conv3x3(d, None) == -2

@@ -94,6 +94,44 @@ def test_conv3x3_prelu_pool_res(dtype):
 
 
 @pytest.mark.parametrize("dtype", DT_FWD)
+@pytest.mark.parametrize("B,H,W,nres", [(2, 64, 64, 0), (2, 64, 64, 1), (3, 40, 56, 1), (1, 16, 16, 2),
+                                         (32, 64, 64, 1)])
+def test_conv_dot_epilogue(dtype, B, H, W, nres):
+    """FEN_EPI_DOT: the conv's output (after residual adds) as stored, dotted with pre_in per
+    16x16 tile and channel (the SE backward's sum dy*t for the next RCAB).  The output must
+    equal the plain conv's bit for bit, and the partials the tile sums of y_stored * t
+    (rel 1e-5; a wrong tile / channel mapping is O(1)).  (2, 64, 64) with 0 / 1 residual are
+    the ping-pong kernel's DOT instantiations, 2 residuals the generic one-group kernel,
+    40x56 ragged tiles, B=32 the training batch."""
+    from src.hip import lib as L, net
+    torch.manual_seed(5)
+    C = 64
+    x = torch.randn(B, C, H, W)
+    w = torch.randn(C, C, 3, 3) * 0.05
+    t = torch.randn(B, C, H, W)
+    res = [torch.randn(B, C, H, W) for _ in range(nres)]
+    ctx = _ctx(dtype)
+    wp = _pack(ctx, w, 0)
+    xd, td = nhwc(x, dtype), nhwc(t, dtype)
+    rd = [nhwc(r, dtype) for r in res]
+    y0 = ctx.alloc((B, H, W, C))
+    net.conv(ctx, xd, wp, B, H, W, C, C, y=y0, res=rd)
+    T = net.tiles(H, W)
+    part = ctx.alloc((B * T, C), torch.float32)
+    y1 = ctx.alloc((B, H, W, C))
+    net.conv(ctx, xd, wp, B, H, W, C, C, y=y1, res=rd, epi=L.EPI_DOT, pre_in=td, part=part)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    prod = (y1.float() * td.float()).cpu()                            # [B, H, W, C]
+    th, tw = (H + 15) // 16, (W + 15) // 16
+    pad = torch.zeros(B, th * 16, tw * 16, C)
+    pad[:, :H, :W] = prod
+    ref = pad.view(B, th, 16, tw, 16, C).sum((2, 4)).reshape(B * T, C)
+    rel = float((part.cpu() - ref).norm() / ref.norm())
+    assert rel <= 1e-5, rel
+
+
+@pytest.mark.parametrize("dtype", DT_FWD)
 def test_upsample_conv_shuffle_prelu(dtype):
     from src.hip import lib as L, net
     torch.manual_seed(2)
