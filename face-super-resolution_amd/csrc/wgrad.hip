@@ -229,9 +229,6 @@ __global__ __launch_bounds__(256) void k_wgrad_finalize(int nchunk, int Cout, in
 // and re-read by the finalize) shrink n-fold.  A second launch sums each job's slabs in a
 // fixed order (bitwise reproducible) into its OIHW dW / db.
 // ------------------------------------------------------------------------------------
-constexpr int WG_TILE = 256 * 128;             // dy tile image, 32 KB
-constexpr int WG_TILE_DMA = WG_TILE / 1024;    // 32 pieces
-constexpr int WG_SLOT = HALO_SLOT + WG_TILE;   // 74752 B per slot, 2 slots
 constexpr int WG_MAXJ = FEN_WGRAD_MAXJOBS;
 
 // per-job operands (the shape is common to the launch: jobs.d[0])
@@ -242,16 +239,33 @@ struct WgJobs {
 };
 
 __device__ __forceinline__ int wkey(int col) { return (((col >> 1) & 1) << 1) | (((col >> 3) & 1) << 2); }
+// COT = 16 (conv_last's zero-padded 16-channel dL/dsr): 32-B dy pixel rows; pixels 8..15 of
+// each 16 trade places in groups of 4 so a transposed read's two 8-pixel halves fall in
+// different bank halves (an involution: the same map converts LDS <-> tile pixel index)
+__device__ __forceinline__ int pswap16(int p) { return p ^ (((p >> 3) & 1) << 2); }
 
+// COT = 64: 8 waves = 2 co halves x 4 ci quarters; COT = 16: 4 waves = 4 ci quarters
+template <int COT>
+struct WgCfg {
+    static constexpr int NW = COT == 64 ? 8 : 4;
+    static constexpr int MC = COT == 64 ? 2 : 1;            // 16-row co blocks per wave
+    static constexpr int TILE = 256 * COT * 2;              // dy tile image
+    static constexpr int TILE_DMA = TILE / 1024;            // 32 / 8 pieces
+    static constexpr int SLOT = HALO_SLOT + TILE;           // 2 slots
+};
+
+template <int COT>
 __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, const WgJobs J, float* part) {
+    using Cfg = WgCfg<COT>;
+    constexpr int NW = Cfg::NW, MC = Cfg::MC;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-    const int ch = wave & 1, cq = wave >> 1;
+    const int ch = COT == 64 ? (wave & 1) : 0, cq = COT == 64 ? (wave >> 1) : wave;
     const int q = lane >> 4, c16 = lane & 15, qq = c16 >> 2, pp = c16 & 3;
     const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
     const int ntiles = d.B * tpi;
-    const int co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64;
+    const int co0 = blockIdx.y * COT, ci0 = blockIdx.z * 64;
     // consecutive (job, chunk) slots -- neighbouring tiles of one job, sharing halo rows -- on
     // one XCD; with gridDim.x a multiple of 8 the dispatch XCD is blockIdx.x % 8 whatever y, z
     int slot = blockIdx.x;
@@ -263,12 +277,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
     const i32x4 xr = make_rsrc(J.x[job], (unsigned)((size_t)d.B * H * W * Cin * 2));
     const i32x4 yr = make_rsrc(J.dy[job], (unsigned)((size_t)d.B * H * W * Cout * 2));
 
-    // every wave issues its share of the tile's 41 halo + 32 dy pieces
+    // every wave issues its share of the tile's 41 halo + TILE_DMA dy pieces
     auto issue = [&](int t, const char* slotp) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const unsigned hbase = lds_addr(slotp), ybase = lds_addr(slotp + HALO_SLOT);
-        for (int i = wave; i < HALO_DMA + WG_TILE_DMA; i += 8) {
+        for (int i = wave; i < HALO_DMA + Cfg::TILE_DMA; i += NW) {
             if (i < HALO_DMA) {
                 const int s = i * 64 + lane, p = s >> 3, pos = s & 7;
                 const int hr = p / HALO, hc = p - hr * HALO;
@@ -279,8 +293,15 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
                 dma16(xr, __builtin_amdgcn_readfirstlane(hbase + i * 1024), voff);
             } else {
                 const int j = i - HALO_DMA;
-                const int s = j * 64 + lane, p = s >> 3, pos = s & 7;
-                const int c = pos ^ wkey(p & 15);
+                const int s = j * 64 + lane;
+                int p, c;
+                if constexpr (COT == 64) {
+                    p = s >> 3;
+                    c = (s & 7) ^ wkey(p & 15);
+                } else {
+                    p = pswap16(s >> 1);
+                    c = s & 1;
+                }
                 const int gh = h0 + (p >> 4), gw = w0 + (p & 15);
                 const bool in = gh < H && gw < W;
                 const int voff = in ? (((b * H + gh) * W + gw) * Cout + co0 + c * 8) * 2 : 0x7ffffff0;
@@ -291,15 +312,19 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
 
     // per-lane fragment offsets (see k_wgrad for the transposed-read lane mapping): lane
     // (q, qq, pp) of half h reads pixel k = 8q + 4h + qq of the 32-pixel k-step, 4 channels
-    // from 4*pp.  A (dy): + s*4096; B (halo, tap kh,kw): + (2s + kh) * 2304.
-    int offA[2][2], offB[2][3];
+    // from 4*pp.  A (dy): + s * (32 px of the dy image); B (halo, tap kh,kw): + (2s + kh) * 2304.
+    constexpr int ASTEP = 32 * COT * 2;
+    int offA[2][MC], offB[2][3];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int k = 8 * q + 4 * h + qq, r = k >> 4, pc = k & 15;
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
+        for (int m = 0; m < MC; ++m) {
             const int c = ch * 32 + m * 16 + 4 * pp;
-            offA[h][m] = (r * 16 + pc) * 128 + (((c >> 3) ^ wkey(pc)) << 4) + (c & 7) * 2;
+            if constexpr (COT == 64)
+                offA[h][m] = (r * 16 + pc) * 128 + (((c >> 3) ^ wkey(pc)) << 4) + (c & 7) * 2;
+            else
+                offA[h][m] = pswap16(r * 16 + pc) * 32 + c * 2;
         }
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
@@ -308,9 +333,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
         }
     }
 
-    f32x4 acc[2][9], accb[2];
+    f32x4 acc[MC][9], accb[MC];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
+    for (int m = 0; m < MC; ++m) {
         accb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -321,18 +346,18 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int k = 0, t = t_begin; t < t_end; ++k, ++t) {
-        const char* cur = smem + (k & 1) * WG_SLOT;
-        if (t + 1 < t_end) issue(t + 1, smem + ((k + 1) & 1) * WG_SLOT);
+        const char* cur = smem + (k & 1) * Cfg::SLOT;
+        if (t + 1 < t_end) issue(t + 1, smem + ((k + 1) & 1) * Cfg::SLOT);
         const char* hx = cur;
         const char* ty = cur + HALO_SLOT;
-        uint4 A0[2], B0[9], A1[2], B1[9];
-        auto load = [&](int s, uint4 (&A)[2], uint4 (&Bf)[9]) {
+        uint4 A0[MC], B0[9], A1[MC], B1[9];
+        auto load = [&](int s, uint4 (&A)[MC], uint4 (&Bf)[9]) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
-                for (int m = 0; m < 2; ++m) {
+                for (int m = 0; m < MC; ++m) {
                     const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(ty + offA[h][m] + s * 4096));
+                        (lds_s16x4*)(ty + offA[h][m] + s * ASTEP));
                     const uint2 u = __builtin_bit_cast(uint2, v);
                     if (h == 0) { A[m].x = u.x; A[m].y = u.y; } else { A[m].z = u.x; A[m].w = u.y; }
                 }
@@ -346,14 +371,14 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
                 }
             }
         };
-        auto mma = [&](int s, const uint4 (&A)[2], const uint4 (&Bf)[9]) {
+        auto mma = [&](int s, const uint4 (&A)[MC], const uint4 (&Bf)[9]) {
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-                for (int m = 0; m < 2; ++m) mma16<bf16>(acc[m][tap], A[m], Bf[tap]);
+                for (int m = 0; m < MC; ++m) mma16<bf16>(acc[m][tap], A[m], Bf[tap]);
             if ((s & 3) == cq) {
 #pragma unroll
-                for (int m = 0; m < 2; ++m) mma16<bf16>(accb[m], A[m], ones);
+                for (int m = 0; m < MC; ++m) mma16<bf16>(accb[m], A[m], ones);
             }
         };
         load(0, A0, B0);
@@ -378,7 +403,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
     // blocks at once at the end of the launch).  k_wgrad_fin transposes on its one write.
     float* slab = part + (size_t)slot * ((size_t)Cout * Cin * 9 + Cout);
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MC; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int co = co0 + ch * 32 + m * 16 + 4 * q + r, ci = ci0 + cq * 16 + c16;
@@ -386,16 +411,17 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
             for (int tap = 0; tap < 9; ++tap) slab[((size_t)tap * Cout + co) * Cin + ci] = acc[m][tap][r];
         }
     if (ci0 == 0) {
-        float* red = (float*)smem;   // [4 cq][64 co]; no DMA in flight, last barrier passed
+        float* red = (float*)smem;   // [4 cq][COT co]; no DMA in flight, last barrier passed
         if (c16 == 0) {
 #pragma unroll
-            for (int m = 0; m < 2; ++m)
+            for (int m = 0; m < MC; ++m)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) red[cq * 64 + ch * 32 + m * 16 + 4 * q + r] = accb[m][r];
+                for (int r = 0; r < 4; ++r) red[cq * COT + ch * 32 + m * 16 + 4 * q + r] = accb[m][r];
         }
         __syncthreads();
-        if (tid < 64)
-            slab[(size_t)Cout * Cin * 9 + co0 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+        if (tid < COT)
+            slab[(size_t)Cout * Cin * 9 + co0 + tid] =
+                (red[tid] + red[COT + tid]) + (red[2 * COT + tid] + red[3 * COT + tid]);
     }
 }
 
@@ -476,10 +502,11 @@ __global__ __launch_bounds__(512) void k_wgrad_fin(int nchunk, int stride4, int 
     }
 }
 
-// the persistent kernel: bf16, 64-multiple channel counts, 32-bit buffer offsets
+// the persistent kernel: bf16, Cin % 64 == 0, Cout % 64 == 0 or Cout == 16, 32-bit offsets
 bool wgrad_use_p(const fen_wgrad_desc* d) {
     const size_t xb = (size_t)d->B * d->H * d->W * d->Cin * 2, yb = (size_t)d->B * d->H * d->W * d->Cout * 2;
-    return d->dtype == FEN_BF16 && d->Cout % 64 == 0 && d->Cin % 64 == 0 && xb < 0x7fff0000u && yb < 0x7fff0000u;
+    return d->dtype == FEN_BF16 && (d->Cout % 64 == 0 || d->Cout == 16) && d->Cin % 64 == 0 && xb < 0x7fff0000u &&
+           yb < 0x7fff0000u;
 }
 
 int wgrad_cus() {
@@ -530,9 +557,11 @@ int launch_p(int n, const fen_wgrad_desc* ds, float* work, hipStream_t s) {
     int nchunk, tpc, cot;
     wgrad_geom(d, n, &nchunk, &tpc, &cot);
     static bool attr = false;
-    const size_t lds = 2 * WG_SLOT;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_wgrad_p, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_wgrad_p<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * WgCfg<64>::SLOT);
+        (void)hipFuncSetAttribute((const void*)k_wgrad_p<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * WgCfg<16>::SLOT);
         attr = true;
     }
     WgJobs J{};
@@ -547,7 +576,12 @@ int launch_p(int n, const fen_wgrad_desc* ds, float* work, hipStream_t s) {
     J.n = n;
     J.nchunk = nchunk;
     J.tpc = tpc;
-    hipLaunchKernelGGL(k_wgrad_p, dim3(n * nchunk, d->Cout / 64, d->Cin / 64), dim3(512), lds, s, *d, J, work);
+    if (cot == 64)
+        hipLaunchKernelGGL(k_wgrad_p<64>, dim3(n * nchunk, d->Cout / 64, d->Cin / 64), dim3(64 * WgCfg<64>::NW),
+                           2 * WgCfg<64>::SLOT, s, *d, J, work);
+    else
+        hipLaunchKernelGGL(k_wgrad_p<16>, dim3(n * nchunk, 1, d->Cin / 64), dim3(64 * WgCfg<16>::NW),
+                           2 * WgCfg<16>::SLOT, s, *d, J, work);
     FEN_CHECK_LAUNCH();
     const int stride4 = (int)(slab_floats(d) / 4);
     const int nw4 = d->Cout * d->Cin * 9 / 4;   // tap-major: rows co >= cout_valid skipped

@@ -353,13 +353,14 @@ def test_se_fused(dtype, B, C, Cr, H, W):
                                              (1, 32, 32, 64, 16), (17, 64, 64, 64, 64), (2, 20, 36, 128, 64),
                                              (3, 32, 48, 64, 256), (2, 64, 64, 64, 64), (3, 40, 56, 64, 64),
                                              (2, 16, 16, 32, 32), (1, 24, 40, 32, 128), (2, 32, 32, 32, 16),
-                                             (1, 16, 16, 96, 64)])
+                                             (1, 16, 16, 96, 64), (3, 64, 48, 64, 16)])
 def test_wgrad(dtype, B, H, W, Cin, Cout):
     """fen_wgrad3x3 vs autograd of conv2d.  The reference runs in float64 on the operands
     rounded to the compute dtype, so bf16 is held to fp32-accumulation accuracy (rel 1e-5):
     a wrong fragment mapping or a dropped tile shows as O(1).  (17, 64, 64) puts 2 tiles per
-    block; Cout 256 / Cin 128 exercise the co-group / ci-group grid.  Several jobs per launch:
-    test_wgrad_multi."""
+    block; Cout 256 / Cin 128 exercise the co-group / ci-group grid; Cout 16 (conv_last's
+    padded dL/dsr, 3 valid rows) the persistent kernel's 4-wave 16-channel form at bf16.
+    Several jobs per launch: test_wgrad_multi."""
     from src.hip import net
     torch.manual_seed(7)
     x = torch.randn(B, Cin, H, W).to(dtype).float()
@@ -383,7 +384,7 @@ def test_wgrad(dtype, B, H, W, Cin, Cout):
 @pytest.mark.parametrize("n,B,H,W,Cin,Cout", [(2, 2, 64, 64, 64, 64), (4, 32, 64, 64, 64, 64),
                                                (3, 3, 40, 56, 64, 64), (8, 1, 16, 16, 64, 64),
                                                (4, 17, 64, 64, 64, 64), (2, 2, 32, 32, 64, 256),
-                                               (3, 2, 16, 16, 32, 32)])
+                                               (3, 2, 16, 16, 32, 32), (2, 2, 48, 64, 64, 16)])
 def test_wgrad_multi(dtype, n, B, H, W, Cin, Cout):
     """fen_wgrad3x3_multi (n jobs of one shape in one launch pair, the CUs split between them)
     vs float64 autograd per job, rel 1e-5 as test_wgrad.  Covers the bench's B=32 64x64 batch

@@ -1,0 +1,80 @@
+"""The engine's bucket exchange over RCCL itself (torch.distributed backend "nccl" = RCCL on
+ROCm), on the one GPU of the test box: a one-rank process group, with every bucket's
+all_reduce issued even at world size 1 (BucketExchange skips them there), so the RCCL
+collectives run on their own stream beside the backward exactly as at N > 1, and the join
+before the update is RCCL's work.wait().  A one-rank SUM is the identity, so two fused
+steps must equal the exchange-free step bit for bit (gradients, weights, grad norm).  The
+N > 1 numerics (1/world pre-scale, mark order, join) are covered by test_gpu_dp_engine.py
+and tests/test_dp_cpu.py (gloo, world 2)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class RcclExchange:
+    """dp.BucketExchange with the all-reduces forced at world size 1."""
+    world = 1
+
+    def __init__(self, flat, plan, log):
+        self.plan = plan
+        self.views = {tag: flat[lo:hi] for tag, lo, hi in plan}
+        self.works, self.log = [], log
+
+    def launch(self, tag):
+        self.log.append(tag)
+        self.works.append(dist.all_reduce(self.views[tag], op=dist.ReduceOp.SUM, async_op=True))
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_engine_step_over_rccl(precision):
+    from src.hip.engine import FENEngine
+    from src.models import FaceEnhanceNet
+    from src.training.dp import broadcast_arena
+
+    def model():
+        torch.manual_seed(4)
+        m = FaceEnhanceNet(num_channels=64, num_groups=2, blocks_per_group=2, precision=precision)
+        with torch.no_grad():
+            m.conv_last.weight.normal_(0, 1e-3, generator=torch.Generator().manual_seed(5))
+        return m
+
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
+    hr = torch.rand(2, 3, 128, 128, generator=torch.Generator().manual_seed(7)).to(DEV)
+    e1 = FENEngine(model(), batch=2, lr_hw=(32, 32), dtype=dt, train=True, clip=0.5, lr=1e-3)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        assert dist.get_backend() == "nccl"
+        log = []
+        e2 = FENEngine(model(), batch=2, lr_hw=(32, 32), dtype=dt, train=True, clip=0.5, lr=1e-3,
+                       exchange=lambda flat, plan: RcclExchange(flat, plan, log))
+        broadcast_arena(e2.flat_p)                       # a no-op at one rank, as at N > 1 for rank 0
+        for step in range(2):
+            log.clear()
+            l1 = e1.step(hr)
+            l2 = e2.step(hr)
+            torch.cuda.synchronize()
+            assert log == [t for t, _, _ in e2.exchange.plan], log
+            assert torch.equal(l1, l2)
+            assert torch.equal(e2.flat_g, e1.flat_g), step
+            assert torch.equal(e2.flat_p, e1.flat_p), step
+    finally:
+        dist.destroy_process_group()
