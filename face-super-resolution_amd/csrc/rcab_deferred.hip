@@ -181,12 +181,32 @@ __device__ __forceinline__ void vm_wait(int n) {
     }
 }
 
+// kernel arguments: the forward descriptor, plus the backward form's operands
+struct RdArgs {
+    fen_rcab_deferred_desc d;
+    // BWD: the RCAB's data gradient through both convs (see fen_rcab_bwd): d.x = dt,
+    // d.w1 / d.w2 = conv2 / conv1 mode-2 packs, d.alpha, d.t = dx out, d.part = the DOT
+    // partials (or NULL)
+    const void* z1;            // saved conv1 pre-activation
+    void* dz1;                 // out: dz1 (conv1's weight-gradient operand)
+    float* dpart;              // out: per-tile PReLU slope-gradient partials
+    const void* dy;            // added to dx (the RCAB's output gradient)
+    const void* dot_t;         // t of the next RCAB backward (with d.part)
+};
+
 // ------------------------------------------------------------------------------------
 // the kernel.  DEFER: the input is (x_{j-1}, t_{j-1}, part_{j-1}) and the gate is applied
 // while building the halo; else x_j is read directly.  TRAIN: z1 / a1 copies for the backward.
 // ------------------------------------------------------------------------------------
-template <typename T, bool DEFER, bool TRAIN>
-__global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc d) {
+// BWD (DEFER = TRAIN = false): the RCAB backward's two data gradients in one launch, the
+// same tile pipeline on transposed filters -- dz1 = conv2^T(dt) on the 18x18 halo, times the
+// PReLU derivative at the saved z1 (its 18x18 halo DMA'd into the a1 image, then overwritten
+// in place by dz1; slope-gradient partials over the tile interior), dx = conv1^T(dz1) +
+// dy (+ the tile sums of dx * t_next for the next SE backward).
+template <typename T, bool DEFER, bool TRAIN, bool BWD = false>
+__global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
+    const fen_rcab_deferred_desc& d = A.d;
+    static_assert(!(BWD && (DEFER || TRAIN)), "the backward form is its own mode");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* xh = smem + O_XH;
     char* eh = smem + O_EH;
@@ -291,6 +311,24 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
             tv[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trs, off, 0, 0));
         }
     };
+    // BWD: the saved z1's 18x18 halo into the a1 image (its layout; zero outside the image).
+    // 41 pieces, the last one half: its upper 32 lanes are exec-masked off (no LDS write past
+    // the image, which ends where the filter ring starts)
+    const i32x4 zr4 = make_rsrc(BWD ? A.z1 : d.x, (unsigned)act_bytes);
+    auto issue_z1 = [&](int t) {
+        constexpr int ZCH = A1W * A1W * 8, ZDMA = (ZCH + 63) / 64;
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        for (int i = wave; i < ZDMA; i += 8) {
+            const int L = i * 64 + lane, P = L >> 3;
+            const int ar = P / A1W, ac = P - ar * A1W;
+            const int c = (L & 7) ^ (ac & 7);
+            const int gh = h0 - 1 + ar, gw = w0 - 1 + ac;
+            const int voff = ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
+                                 ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
+            if (L < ZCH) dma16(zr4, __builtin_amdgcn_readfirstlane(lds_addr(a1s + i * 1024)), voff);
+        }
+    };
     // x_j = x_{j-1} (DMA'd halo image) + (res_scale s) t_{j-1}, in place, + the edge copy and,
     // for the tile's own 16x16 pixels, x_j out (buffer stores: the halo ring's offsets fall out
     // of range and are dropped, so every wave issues exactly nch stores).  Each thread rewrites
@@ -327,11 +365,12 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
     uint4 tv0[HPT];
     issue_taps(0);
     issue_halo(slot);
+    if constexpr (BWD) issue_z1(slot);
     if constexpr (DEFER) load_t(slot, tv0);
     if (tid < 64) {
-        cst[tid] = d.b1[tid];
+        cst[tid] = BWD ? 0.f : d.b1[tid];
         cst[64 + tid] = d.alpha[tid];
-        cst[128 + tid] = d.b2[tid];
+        cst[128 + tid] = BWD ? 0.f : d.b2[tid];
     }
     if constexpr (DEFER) {
         // the gates of this block's tiles (<= MAXG): wave w handles tiles w, w + 8; lane c sums
@@ -437,7 +476,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
     // output stores this wave issues after the next tile's first taps (t and, for wave 0, the
     // tile's partial row; deferred: + the x_j chunks): the phase-0 wait leaves them in flight.
     // (Without DEFER the next halo's DMA is older than those taps: waited for as well.)
-    const int nst_tail = 4 + (wave == 0 ? 1 : 0) + (DEFER ? nch : 0);
+    const int nst_tail = 4 + ((wave == 0 && d.part) ? 1 : 0) + (DEFER ? nch : 0);
 
 #pragma unroll 1
     for (int k = 0; k < nmine; ++k) {
@@ -462,6 +501,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
                 if (k < 2) RSTAMP(3 + k * 14 + p * 2);
             }
             issue_taps(P + 1);
+            if constexpr (BWD) {
+                if (p == 0 && k > 0) issue_z1(t);   // the a1 image is free since the last barrier
+            }
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
                                    ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
             if (g < 2) conv1_kw<T, true, false>(acc1, xh, eh, tapp, p, c16, row0, eidx4, arow1, q);
@@ -476,6 +518,49 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
             const bool ok4 = (unsigned)(h0 - 1 + ar4) < (unsigned)H && (unsigned)(w0 - 1 + ac4) < (unsigned)W;
             const bool ok5 = (unsigned)(h0 - 1 + ar5) < (unsigned)H && (unsigned)(w0 - 1 + ac5) < (unsigned)W;
             float zs[2][6][4];
+            if constexpr (BWD) {
+                // dz1 = conv2^T(dt) * PReLU'(z1) (zero outside the image = conv1^T's padding),
+                // in place over the DMA'd z1; slope partials over the tile interior
+                float dal[2][4];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const float4 aa = *(const float4*)(cst + 64 + ch * 32 + m * 16 + 4 * q);
+                    const float alp[4] = {aa.x, aa.y, aa.z, aa.w};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dal[m][r] = 0.f;
+#pragma unroll
+                    for (int f = 0; f < 6; ++f) {
+                        if (!(f < 5 || has5)) continue;
+                        bool ok;
+                        if (f < 4) ok = colok && (unsigned)(h0 - 1 + row0 + f) < (unsigned)H;
+                        else ok = f == 4 ? ok4 : ok5;
+                        const int ar = f < 4 ? row0 + f : f == 4 ? ar4 : ar5;
+                        const int ac = f < 4 ? c16 : f == 4 ? ac4 : ac5;
+                        const bool inner = ok && (unsigned)(ar - 1) < 16u && (unsigned)(ac - 1) < 16u;
+                        const float okf = ok ? 1.f : 0.f;
+                        const int off = f < 4 ? a1m[m] + f * (A1W * 128) : f == 4 ? a1o4[m] : a1o5[m];
+                        float z[4], a[4];
+                        ld4<T>(a1s + off, z);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float v = acc1[m][f][r];
+                            a[r] = okf * prelu_bwd_f(v, z[r], alp[r]);
+                            zs[m][f][r] = a[r];
+                            if (inner) dal[m][r] += prelu_dalpha_f(v, z[r]);
+                        }
+                        st4<T>(a1s + off, a);
+                    }
+                }
+                // per-channel sums of this wave's fragment group -> its row of the (otherwise
+                // unused) gate area; combined in a fixed order after the phase-3 barrier
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float sm = group16_sum(dal[m][r]);
+                        if (c16 == 0) gate[g * 64 + ch * 32 + m * 16 + 4 * q + r] = sm;
+                    }
+            } else {
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
                 const float4 bb = *(const float4*)(cst + ch * 32 + m * 16 + 4 * q);
@@ -498,7 +583,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
                     if (f < 5 || has5) st4<T>(a1s + off, a);
                 }
             }
-            if constexpr (TRAIN) {
+            }
+            if constexpr (TRAIN || BWD) {
+                void* zout = BWD ? A.dz1 : d.z1;
                 // interior pixels only (a1 rows / cols 1..16): lanes q and q^1 (same pixel) trade
                 // one 4-channel half so each store is 16 B
                 const bool odd = q & 1;
@@ -519,7 +606,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
                     if (!(f < 5 || has5) || ar < 1 || ar > 16 || ac < 1 || ac > 16) continue;
                     const uint4 v = odd ? make_uint4(rcv.x, rcv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, rcv.x, rcv.y);
                     const size_t o = ((size_t)(b * H + h0 - 1 + ar) * W + w0 - 1 + ac) * 64 + ch * 32 + (odd ? 16 + 4 * (q - 1) : 4 * q);
-                    *(uint4*)((char*)d.z1 + o * 2) = v;
+                    *(uint4*)((char*)zout + o * 2) = v;
                 }
             }
         }
@@ -531,6 +618,12 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
         // (issuing them before the conv1 epilogue behind an extra barrier measured slower:
         // 34.0 -> 34.3 us per launch; the LDS-DMA of a phase's taps takes ~1.1-1.4 us to land,
         // so conv2's 0.64-us phases 4 and 5 wait ~0.7 us each)
+        if constexpr (BWD) {
+            // (stored before taps(4): the phase-4 wait covers it)
+            if (wave == 0)
+                A.dpart[((size_t)b * tpi + tile) * 64 + lane] =
+                    (gate[lane] + gate[64 + lane]) + (gate[128 + lane] + gate[192 + lane]);
+        }
         issue_taps(k * 6 + 4);
         if constexpr (TRAIN) {
             // a1 for the backward: the tile's 16x16 interior straight from the a1 image, 16-B
@@ -562,6 +655,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
         if (k < 2) RSTAMP(10 + k * 14);
         // ================= conv2: phases 3..5 =================
         f32x4 acc2[2][4];
+        uint2 rv[2][4], dv[2][4];
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -574,6 +668,20 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
+                if constexpr (BWD) {
+                    // the epilogue's residual / t_next operands, ahead of the next tile's taps:
+                    // the epilogue's vmcnt(3) leaves only those taps in flight
+                    if (p == 5) {
+#pragma unroll
+                        for (int m = 0; m < 2; ++m)
+#pragma unroll
+                            for (int n = 0; n < 4; ++n) {
+                                const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
+                                rv[m][n] = *(const uint2*)((const char*)A.dy + o * 2);
+                                if (A.dot_t) dv[m][n] = *(const uint2*)((const char*)A.dot_t + o * 2);
+                            }
+                    }
+                }
                 if (!(k + 1 == nmine && p == 5)) issue_taps(P + 1);
             }
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
@@ -583,6 +691,29 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
         }
         // ---- conv2 epilogue: t_j = acc + b2 (paired-lane 16-B stores), pool partial
         float ps[2][4];
+        if constexpr (BWD) {
+            // dx = conv1^T(dz1) + dy; DOT: tile sums of dx (as stored) * t_next
+            if (k + 1 < nmine) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ps[m][r] = 0.f;
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    acc2[m][n][0] += lo16<T>(rv[m][n].x);
+                    acc2[m][n][1] += hi16<T>(rv[m][n].x);
+                    acc2[m][n][2] += lo16<T>(rv[m][n].y);
+                    acc2[m][n][3] += hi16<T>(rv[m][n].y);
+                    if (A.dot_t) {
+                        const float tn[4] = {lo16<T>(dv[m][n].x), hi16<T>(dv[m][n].x), lo16<T>(dv[m][n].y),
+                                             hi16<T>(dv[m][n].y)};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) ps[m][r] += rnd16<T>(acc2[m][n][r]) * tn[r];
+                    }
+                }
+            }
+        } else {
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
             const float4 bb = *(const float4*)(cst + 128 + wc * 32 + m * 16 + 4 * q);
@@ -596,6 +727,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
                     acc2[m][n][r] += bia[r];
                     ps[m][r] += acc2[m][n][r];
                 }
+        }
         }
         {
             const bool odd = q & 1;
@@ -628,7 +760,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
         // first taps (issued at phase 5) and the t stores above stay in flight
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (wave == 0)
+        if (wave == 0 && d.part)
             d.part[((size_t)b * tpi + tile) * 64 + lane] = (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]);
         if (k < 2) RSTAMP(14 + k * 14);
         // ---- the next tile's x_j: halo image + edge copy + its interior out
@@ -648,26 +780,28 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const fen_rcab_deferred_desc 
 
 int g_cus = 0;
 
-template <typename T, bool DEFER, bool TRAIN>
-void launch_rd(const fen_rcab_deferred_desc* d, int grid, hipStream_t s) {
+template <typename T, bool DEFER, bool TRAIN, bool BWD = false>
+void launch_rd(const RdArgs& a, int grid, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_rcab_d<T, DEFER, TRAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  RD_LDS);
+        (void)hipFuncSetAttribute((const void*)k_rcab_d<T, DEFER, TRAIN, BWD>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, RD_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL((k_rcab_d<T, DEFER, TRAIN>), dim3(grid), dim3(512), RD_LDS, s, *d);
+    hipLaunchKernelGGL((k_rcab_d<T, DEFER, TRAIN, BWD>), dim3(grid), dim3(512), RD_LDS, s, a);
 }
 
 template <typename T>
 void launch_rd_t(const fen_rcab_deferred_desc* d, int grid, hipStream_t s) {
     const bool defer = d->tp != nullptr, train = d->z1 != nullptr;
+    RdArgs a{};
+    a.d = *d;
     if (defer) {
-        if (train) launch_rd<T, true, true>(d, grid, s);
-        else launch_rd<T, true, false>(d, grid, s);
+        if (train) launch_rd<T, true, true>(a, grid, s);
+        else launch_rd<T, true, false>(a, grid, s);
     } else {
-        if (train) launch_rd<T, false, true>(d, grid, s);
-        else launch_rd<T, false, false>(d, grid, s);
+        if (train) launch_rd<T, false, true>(a, grid, s);
+        else launch_rd<T, false, false>(a, grid, s);
     }
 }
 
@@ -703,6 +837,37 @@ extern "C" int fen_rcab_deferred(const fen_rcab_deferred_desc* d, void* stream) 
     hipStream_t s = (hipStream_t)stream;
     if (d->dtype == FEN_F16) launch_rd_t<f16>(d, grid, s);
     else launch_rd_t<bf16>(d, grid, s);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_rcab_bwd(const fen_rcab_bwd_desc* b, void* stream) {
+    if (!b || !b->dt || !b->w2t || !b->w1t || !b->z1 || !b->alpha || !b->dz1 || !b->dalpha_part || !b->dx ||
+        !b->dy)
+        return FEN_EINVAL;
+    if ((b->dot_t != nullptr) != (b->dot_part != nullptr)) return FEN_EINVAL;
+    if (!fen_rcab_deferred_supported(b->dtype, b->B, b->H, b->W, b->C, 16)) return FEN_EUNSUPPORTED;
+    RdArgs a{};
+    fen_rcab_deferred_desc& d = a.d;
+    d.dtype = b->dtype;
+    d.B = b->B, d.H = b->H, d.W = b->W, d.C = b->C, d.Cr = 16;
+    d.x = b->dt;
+    d.w1 = b->w2t;
+    d.w2 = b->w1t;
+    d.alpha = b->alpha;
+    d.t = b->dx;
+    d.part = b->dot_part;
+    a.z1 = b->z1;
+    a.dz1 = b->dz1;
+    a.dpart = b->dalpha_part;
+    a.dy = b->dy;
+    a.dot_t = b->dot_t;
+    const int ncu = rd_num_cus();
+    const int ntiles = b->B * (b->H / 16) * (b->W / 16);
+    const int grid = ntiles < ncu ? ntiles : ncu;
+    hipStream_t s = (hipStream_t)stream;
+    if (b->dtype == FEN_F16) launch_rd<f16, false, false, true>(a, grid, s);
+    else launch_rd<bf16, false, false, true>(a, grid, s);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -55,6 +55,15 @@ class RcabDeferredDesc(Structure):
     ]
 
 
+class RcabBwdDesc(Structure):
+    _fields_ = [
+        ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int),
+        ("dt", c_void_p), ("w2t", c_void_p), ("z1", c_void_p), ("alpha", c_void_p), ("w1t", c_void_p),
+        ("dy", c_void_p), ("dz1", c_void_p), ("dalpha_part", c_void_p), ("dx", c_void_p),
+        ("dot_t", c_void_p), ("dot_part", c_void_p),
+    ]
+
+
 class WgradDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
@@ -71,6 +80,7 @@ _SIGS = {
     "fen_wgrad3x3_multi": (c_int, [c_int, c_void_p, c_void_p]),
     "fen_rcab_deferred_supported": (c_int, [c_int] * 6),
     "fen_rcab_deferred": (c_int, [POINTER(RcabDeferredDesc), c_void_p]),
+    "fen_rcab_bwd": (c_int, [POINTER(RcabBwdDesc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
     "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),

@@ -156,6 +156,10 @@ def wgrad(ctx: Ctx, x, dy, B, H, W, Cin, Cout, dw, db, cout_valid=None) -> None:
 # weight gradients of the RCAB convs issued per launch (fen_wgrad3x3_multi jobs, <= 8): the
 # jobs share the CUs, so the per-block fp32 slabs shrink by that factor (FEN_WGRAD_BATCH=1:
 # one launch per conv)
+# RCAB backward data gradients: both convs (+ PReLU backward, + dy, + the next DOT partials) in
+# one fen_rcab_bwd launch where the deferred kernel's envelope holds ('fused', default), or the
+# conv2 dgrad (PReLU-backward epilogue) + conv1 dgrad (residual epilogue) pair (FEN_RCAB_BWD=pair)
+RCAB_BWD_FUSED = os.environ.get("FEN_RCAB_BWD", "fused") != "pair"
 # sum(dy * t) of the SE backward from the producing dgrad's epilogue (FEN_EPI_DOT) instead of
 # a fen_pool_dot pass over dy and t (FEN_SE_DOT=pass: the separate pass)
 DOT_FUSED = os.environ.get("FEN_SE_DOT", "fused") != "pass"
@@ -466,11 +470,27 @@ class Backward:
         dz1 = ctx.scratch(f"bw_dz1{rot}", dy.shape)
         T = tiles(H, W)
         dal = ctx.scratch("bw_dal" + pre, (B * T, C), torch.float32)
+        dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
+        if (RCAB_BWD_FUSED and not extra_res and ctx.code != L.F32
+                and ctx.lib.fen_rcab_deferred_supported(ctx.code, B, H, W, C, s.Cr)):
+            d = L.RcabBwdDesc()
+            d.dtype, d.B, d.H, d.W, d.C = ctx.code, B, H, W, C
+            d.dt, d.w2t, d.z1 = ptr(dt), ptr(Wt.packed(pre + "conv2", 2)), ptr(sv["z1"])
+            d.alpha, d.w1t, d.dy = ptr(p[pre + "prelu.weight"]), ptr(Wt.packed(pre + "conv1", 2)), ptr(dy)
+            d.dz1, d.dalpha_part, d.dx = ptr(dz1), ptr(dal), ptr(dx)
+            dk = self._dot_conv(t_next, B, H, W, C)
+            if dk:
+                d.dot_t, d.dot_part = ptr(dk["pre_in"]), ptr(dk["part"])
+            ctx.emit("rcab_bwd", ctx.lib.fen_rcab_bwd, byref(d))
+            self.cs.add(dal, B * T, C, G[pre + "prelu.weight"])
+            self.wb.add(sv["x"], dz1, B, H, W, C, C, G[pre + "conv1.weight"], G[pre + "conv1.bias"])
+            if flush:
+                self.flush()
+            return dx
         conv(ctx, dt, Wt.packed(pre + "conv2", 2), B, H, W, C, C, epi=L.EPI_PRELU_BWD, alpha=p[pre + "prelu.weight"],
              pre_in=sv["z1"], y=dz1, part=dal)
         self.cs.add(dal, B * T, C, G[pre + "prelu.weight"])
         self.wb.add(sv["x"], dz1, B, H, W, C, C, G[pre + "conv1.weight"], G[pre + "conv1.bias"])
-        dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
         conv(ctx, dz1, Wt.packed(pre + "conv1", 2), B, H, W, C, C, y=dx, res=(dy,) + tuple(extra_res),
              **self._dot_conv(t_next, B, H, W, C))
         if flush:

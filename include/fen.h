@@ -206,6 +206,30 @@ typedef struct {
 int fen_rcab_deferred_supported(int dtype, int B, int H, int W, int C, int Cr);
 int fen_rcab_deferred(const fen_rcab_deferred_desc* d, void* stream);
 
+/* The RCAB backward's two data gradients in one launch (autograd of blocks.py:145-147):
+ *   dz1 = conv2^T(dt) * PReLU'(z1),  dalpha_part[b][tile][c] = sum over the tile of
+ *   conv2^T(dt) * z1 * (z1 <= 0),  dx = conv1^T(dz1) + dy,
+ *   optionally dot_part[b][tile][c] = sum over the tile of dx (as stored) * dot_t.
+ * dt is the SE backward's output, w2t / w1t the conv2 / conv1 mode-2 packs (no bias), z1
+ * the saved pre-activation.  The same persistent tile pipeline as fen_rcab_deferred (dz1
+ * recomputed on each tile's 18x18 halo); the envelope of fen_rcab_deferred_supported.     */
+typedef struct {
+    int dtype;                 /* FEN_BF16 or FEN_F16                                          */
+    int B, H, W, C;            /* C = 64                                                        */
+    const void* dt;            /* NHWC [B,H,W,64]                                               */
+    const void* w2t;           /* conv2 packed mode 2                                           */
+    const void* z1;            /* conv1 pre-activation NHWC                                     */
+    const float* alpha;        /* PReLU slopes [64]                                             */
+    const void* w1t;           /* conv1 packed mode 2                                           */
+    const void* dy;            /* the RCAB's output gradient, added to dx (the residual path)   */
+    void* dz1;                 /* out NHWC (conv1's weight-gradient operand)                    */
+    float* dalpha_part;        /* out [B*tiles][64]                                             */
+    void* dx;                  /* out NHWC                                                      */
+    const void* dot_t;         /* NULL or NHWC: the next RCAB's t (with dot_part)                */
+    float* dot_part;           /* NULL or out [B*tiles][64]                                     */
+} fen_rcab_bwd_desc;
+int fen_rcab_bwd(const fen_rcab_bwd_desc* d, void* stream);
+
 /* trainer.py:416-421 LR synthesis: bicubic x0.25, align_corners=False, NCHW fp32          */
 int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, float* lr, void* stream);
 

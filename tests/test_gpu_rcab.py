@@ -137,3 +137,70 @@ def test_rcab_chain_graph_replay():
         assert torch.equal(h, ref)
     h2, _, _, _ = _run(p, n, x, False, "perop", torch.bfloat16)
     assert _rel(ref.float(), h2.float()) <= 1e-2
+
+
+def _round(x, dtype):
+    return x.to(dtype).float()
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("B,H,W,dot", [(2, 32, 32, True), (17, 64, 64, True), (1, 48, 80, False), (1, 16, 16, True),
+                                        (32, 64, 64, True)])
+def test_rcab_bwd_fused(prec, B, H, W, dot):
+    """fen_rcab_bwd (the RCAB backward's conv2^T -> PReLU' -> conv1^T + dy in one launch, + the
+    next RCAB's DOT partials) vs a torch fp32 restatement on the same rounded operands:
+    g2 = conv2^T(dt), dz1 = g2 * PReLU'(z1), dalpha per tile = sum g2 * z1 * (z1 <= 0),
+    dx = conv1^T(dz1 as stored) + dy, DOT per tile = sum dx (as stored) * t_next.
+    rel-L2 <= 3e-3 (bf16) / 1e-3 (fp16) on dz1 and dx; 5e-3 / 2e-3 on the partial sums (a
+    wrong tap, halo row, edge fragment or tile shows up as O(1))."""
+    import torch.nn.functional as F
+    from src.hip import lib as L
+    from src.hip.net import Weights, tiles
+    from src.hip.program import Ctx, ptr
+    dtype = DT[prec]
+    g = torch.Generator().manual_seed(9)
+    C = 64
+    w1 = torch.randn(C, C, 3, 3, generator=g) * 0.06
+    w2 = torch.randn(C, C, 3, 3, generator=g) * 0.06
+    alpha = torch.rand(C, generator=g) * 0.5
+    dt = _round(torch.randn(B, C, H, W, generator=g), dtype)
+    z1 = _round(torch.randn(B, C, H, W, generator=g), dtype)
+    dy = _round(torch.randn(B, C, H, W, generator=g), dtype)
+    tn = _round(torch.randn(B, C, H, W, generator=g), dtype)
+    w1r, w2r = _round(w1, dtype), _round(w2, dtype)
+    # reference
+    g2 = F.conv_transpose2d(dt, w2r, padding=1)
+    a = alpha.view(1, C, 1, 1)
+    dz1_ref = g2 * torch.where(z1 > 0, torch.ones_like(z1), a.expand_as(z1))
+    dal_ref = (g2 * z1 * (z1 <= 0)).view(B, C, H // 16, 16, W // 16, 16).sum((3, 5))
+    dal_ref = dal_ref.permute(0, 2, 3, 1).reshape(B * tiles(H, W), C)
+    dx_ref = F.conv_transpose2d(_round(dz1_ref, dtype), w1r, padding=1) + dy
+    dot_ref = (_round(dx_ref, dtype) * tn).view(B, C, H // 16, 16, W // 16, 16).sum((3, 5))
+    dot_ref = dot_ref.permute(0, 2, 3, 1).reshape(B * tiles(H, W), C)
+
+    nh = lambda t: t.permute(0, 2, 3, 1).contiguous().to(DEV, dtype)
+    ctx = Ctx(dtype, DEV)
+    Wt = Weights({"c1.weight": w1.to(DEV), "c2.weight": w2.to(DEV)}, dtype, DEV)
+    T = tiles(H, W)
+    dtd, z1d, dyd, tnd = nh(dt), nh(z1), nh(dy), nh(tn)
+    dz1 = ctx.alloc((B, H, W, C))
+    dx = ctx.alloc((B, H, W, C))
+    dal = ctx.alloc((B * T, C), torch.float32)
+    dotp = ctx.alloc((B * T, C), torch.float32)
+    ad = alpha.to(DEV)
+    d = L.RcabBwdDesc()
+    d.dtype, d.B, d.H, d.W, d.C = ctx.code, B, H, W, C
+    d.dt, d.w2t, d.z1, d.alpha = ptr(dtd), ptr(Wt.packed("c2", 2)), ptr(z1d), ptr(ad)
+    d.w1t, d.dy, d.dz1, d.dalpha_part, d.dx = ptr(Wt.packed("c1", 2)), ptr(dyd), ptr(dz1), ptr(dal), ptr(dx)
+    if dot:
+        d.dot_t, d.dot_part = ptr(tnd), ptr(dotp)
+    L.check(ctx.lib.fen_rcab_bwd(d, torch.cuda.current_stream().cuda_stream), "rcab_bwd")
+    torch.cuda.synchronize()
+    tol, tolp = (3e-3, 5e-3) if prec == "bf16" else (1e-3, 2e-3)
+    rel = lambda a_, b_: float((a_ - b_).norm() / b_.norm())
+    nc = lambda t: t.float().cpu().permute(0, 3, 1, 2)
+    assert rel(nc(dz1), dz1_ref) <= tol
+    assert rel(nc(dx), dx_ref) <= tol
+    assert rel(dal.cpu(), dal_ref) <= tolp
+    if dot:
+        assert rel(dotp.cpu(), dot_ref) <= tolp
