@@ -652,10 +652,23 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
                 nhalo += nch;
             }
         }
+        // BWD: the epilogue's dy / t_next operands, behind the next halo: the phase-4 wait leaves
+        // them in flight, phase 5's vmcnt(0) retires them (two conv2 phases of lead)
+        uint2 rv[2][4], dv[2][4];
+        if constexpr (BWD) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
+                    rv[m][n] = *(const uint2*)((const char*)A.dy + o * 2);
+                    if (A.dot_t) dv[m][n] = *(const uint2*)((const char*)A.dot_t + o * 2);
+                }
+            nhalo += A.dot_t ? 16 : 8;
+        }
         if (k < 2) RSTAMP(10 + k * 14);
         // ================= conv2: phases 3..5 =================
         f32x4 acc2[2][4];
-        uint2 rv[2][4], dv[2][4];
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -668,20 +681,6 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
-                if constexpr (BWD) {
-                    // the epilogue's residual / t_next operands, ahead of the next tile's taps:
-                    // the epilogue's vmcnt(3) leaves only those taps in flight
-                    if (p == 5) {
-#pragma unroll
-                        for (int m = 0; m < 2; ++m)
-#pragma unroll
-                            for (int n = 0; n < 4; ++n) {
-                                const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
-                                rv[m][n] = *(const uint2*)((const char*)A.dy + o * 2);
-                                if (A.dot_t) dv[m][n] = *(const uint2*)((const char*)A.dot_t + o * 2);
-                            }
-                    }
-                }
                 if (!(k + 1 == nmine && p == 5)) issue_taps(P + 1);
             }
             const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
@@ -693,8 +692,6 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
         float ps[2][4];
         if constexpr (BWD) {
             // dx = conv1^T(dz1) + dy; DOT: tile sums of dx (as stored) * t_next
-            if (k + 1 < nmine) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int m = 0; m < 2; ++m) {
 #pragma unroll
