@@ -192,6 +192,8 @@ struct RdArgs {
     float* dpart;              // out: per-tile PReLU slope-gradient partials
     const void* dy;            // added to dx (the RCAB's output gradient)
     const void* dot_t;         // t of the next RCAB backward (with d.part)
+    // GC: the group conv (d.w2 / d.b2 = its pack and bias, d.t = its output) + this residual
+    const void* gres;
 };
 
 // ------------------------------------------------------------------------------------
@@ -203,10 +205,15 @@ struct RdArgs {
 // PReLU derivative at the saved z1 (its 18x18 halo DMA'd into the a1 image, then overwritten
 // in place by dz1; slope-gradient partials over the tile interior), dx = conv1^T(dz1) +
 // dy (+ the tile sums of dx * t_next for the next SE backward).
-template <typename T, bool DEFER, bool TRAIN, bool BWD = false>
+// GC (DEFER, not TRAIN): a ResidualGroup's end -- the last RCAB's gate and scaled residual
+// applied while building the input (straight into the a1 image, 18x18), then the group conv
+// (one 3x3 conv on the conv2 path) + bias + the group's residual (blocks.py:185-189): the
+// chain end's separate gate/apply launch and its tensor round trip disappear.
+template <typename T, bool DEFER, bool TRAIN, bool BWD = false, bool GC = false>
 __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     const fen_rcab_deferred_desc& d = A.d;
     static_assert(!(BWD && (DEFER || TRAIN)), "the backward form is its own mode");
+    static_assert(!GC || (DEFER && !TRAIN && !BWD), "the group end is a deferred single conv");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* xh = smem + O_XH;
     char* eh = smem + O_EH;
@@ -250,7 +257,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     // ring: phase P of the block's sequence (6 per tile) uses slots (P & 1) * 3 + i.
     // phase p = 0..2: conv1 taps 3p..3p+2 column-wise; p = 3..5: conv2 taps (kh, kw = p - 3)
     auto issue_taps = [&](int P) {
-        const int p = P % 6;
+        const int p = GC ? P % 3 + 3 : P % 6;   // GC: three phases per tile, all on w2
         char* base = ring + (P & 1) * 3 * TAP_BYTES;
         const int s = wave * 64 + lane, r = s >> 3, pc = s & 7;
         const int c = pc ^ ((r >> 1) & 7);
@@ -353,8 +360,13 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) y[e] = tf[e] * s8[e] + xf[e];
             const uint4 v = pack16<T>(y);
-            *(uint4*)px = v;
-            if (hc >= 16) *(uint4*)(eh + (hr * 4 + (hc - 16)) * 128 + ekey(hr, c)) = v;
+            if constexpr (GC) {
+                if ((unsigned)(hr - 1) < 18u && (unsigned)(hc - 1) < 18u)
+                    *(uint4*)(a1s + (hr - 1) * (A1W * 128) + hcol(hc - 1, c)) = v;
+            } else {
+                *(uint4*)px = v;
+                if (hc >= 16) *(uint4*)(eh + (hr * 4 + (hc - 16)) * 128 + ekey(hr, c)) = v;
+            }
             const bool own = (unsigned)(hr - 2) < 16u && (unsigned)(hc - 2) < 16u;
             const int off = own ? (((b * H + h0 - 2 + hr) * W + w0 - 2 + hc) * 64 + c * 8) * 2 : 0x7ffffff0;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), ors, off, 0, 0);
@@ -369,7 +381,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     if constexpr (DEFER) load_t(slot, tv0);
     if (tid < 64) {
         cst[tid] = BWD ? 0.f : d.b1[tid];
-        cst[64 + tid] = d.alpha[tid];
+        cst[64 + tid] = GC ? 0.f : d.alpha[tid];   // (the group conv has no PReLU: d.alpha unset)
         cst[128 + tid] = BWD ? 0.f : d.b2[tid];
     }
     if constexpr (DEFER) {
@@ -452,6 +464,97 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
         __builtin_amdgcn_s_barrier();                         // a1 scratch and the halo image
     }
     RSTAMP(1);
+
+    if constexpr (GC) {
+        // ---- the group conv on the a1 image (the combine wrote y there), 3 tap phases per
+        // tile; the next tile's x / t go out at phase 1 into the free halo image / registers
+        const int arow2 = wc * 32 + c16;
+        const int nst_gc = 4 + nch;                      // out stores + the combine's y stores
+#pragma unroll 1
+        for (int k = 0; k < nmine; ++k) {
+            const int t = slot + k * nslot;
+            const int b = t / tpi, tile = t - b * tpi;
+            const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+            const bool next = k + 1 < nmine;
+            f32x4 acc2[2][4];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) acc2[m][n] = zero4();
+            uint2 rv[2][4];
+            uint4 tv[HPT];
+            int nhalo = 0;
+#pragma unroll 1
+            for (int p = 0; p < 3; ++p) {
+                const int P = k * 3 + p;
+                if (p > 0 || k > 0) {
+                    if (p == 0) vm_wait(nst_gc);         // this phase's taps; the last tile's stores drain on
+                    else if (p == 1) vm_wait(8);         // this phase's taps; the residual loads may trail
+                    else vm_wait(nhalo);                 // this phase's taps; the next halo stays in flight
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                }
+                if (p < 2 || next) issue_taps(P + 1);
+                if (p == 0) {
+#pragma unroll
+                    for (int m = 0; m < 2; ++m)
+#pragma unroll
+                        for (int n = 0; n < 4; ++n) {
+                            const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
+                            rv[m][n] = *(const uint2*)((const char*)A.gres + o * 2);
+                        }
+                }
+                if (p == 1 && next) {
+                    issue_halo(t + nslot);
+                    load_t(t + nslot, tv);
+                    nhalo = ndma + nch;
+                }
+                const char* tapp[3] = {ring + (P & 1) * 3 * TAP_BYTES, ring + (P & 1) * 3 * TAP_BYTES + TAP_BYTES,
+                                       ring + (P & 1) * 3 * TAP_BYTES + 2 * TAP_BYTES};
+                conv2_phase<T>(acc2, a1s, tapp, p, wr, arow2, q, c16);
+            }
+            // ---- out = conv + bias + the group's residual (paired-lane 16-B stores)
+            const bool odd = q & 1;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const float4 bb = *(const float4*)(cst + 128 + wc * 32 + m * 16 + 4 * q);
+                const float bia[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    acc2[m][n][0] += bia[0] + lo16<T>(rv[m][n].x);
+                    acc2[m][n][1] += bia[1] + hi16<T>(rv[m][n].x);
+                    acc2[m][n][2] += bia[2] + lo16<T>(rv[m][n].y);
+                    acc2[m][n][3] += bia[3] + hi16<T>(rv[m][n].y);
+                }
+            }
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                uint2 pk[2];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    pk[m].x = pack2<T>(acc2[m][n][0], acc2[m][n][1]);
+                    pk[m].y = pack2<T>(acc2[m][n][2], acc2[m][n][3]);
+                }
+                const uint2 snd = odd ? pk[0] : pk[1];
+                uint2 rcv;
+                rcv.x = (unsigned)__shfl_xor((int)snd.x, 16, 64);
+                rcv.y = (unsigned)__shfl_xor((int)snd.y, 16, 64);
+                const uint4 v = odd ? make_uint4(rcv.x, rcv.y, pk[1].x, pk[1].y) : make_uint4(pk[0].x, pk[0].y, rcv.x, rcv.y);
+                const size_t px = (size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16;
+                *(uint4*)((char*)d.t + (px * 64 + wc * 32 + (odd ? 16 + 4 * (q - 1) : 4 * q)) * 2) = v;
+            }
+            if (next) {
+                // the next halo (DMA + t chunks) landed in every wave; the next taps (3) and the
+                // out stores (4) stay in flight; everyone is past phase 2's reads of the a1 image
+                asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                combine_halo(t + nslot, k + 1, tv);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
 
     // conv1 per-lane addressing (group g: rows row0.., slot 4 main for g < 2, edges for g >= 2)
     const int row0 = g == 0 ? 0 : g == 1 ? 5 : g == 2 ? 10 : 14;
@@ -777,15 +880,15 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
 
 int g_cus = 0;
 
-template <typename T, bool DEFER, bool TRAIN, bool BWD = false>
+template <typename T, bool DEFER, bool TRAIN, bool BWD = false, bool GC = false>
 void launch_rd(const RdArgs& a, int grid, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_rcab_d<T, DEFER, TRAIN, BWD>,
+        (void)hipFuncSetAttribute((const void*)k_rcab_d<T, DEFER, TRAIN, BWD, GC>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, RD_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL((k_rcab_d<T, DEFER, TRAIN, BWD>), dim3(grid), dim3(512), RD_LDS, s, a);
+    hipLaunchKernelGGL((k_rcab_d<T, DEFER, TRAIN, BWD, GC>), dim3(grid), dim3(512), RD_LDS, s, a);
 }
 
 template <typename T>
@@ -865,6 +968,30 @@ extern "C" int fen_rcab_bwd(const fen_rcab_bwd_desc* b, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (b->dtype == FEN_F16) launch_rd<f16, false, false, true>(a, grid, s);
     else launch_rd<bf16, false, false, true>(a, grid, s);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_rcab_group_end(const fen_rcab_deferred_desc* d, const void* w, const float* bias, const void* res,
+                                  void* out, void* stream) {
+    if (!d || !d->x || !d->tp || !d->pp || !d->pfc1 || !d->pfc2 || !w || !bias || !res || !out) return FEN_EINVAL;
+    if (!fen_rcab_deferred_supported(d->dtype, d->B, d->H, d->W, d->C, d->Cr)) return FEN_EUNSUPPORTED;
+    RdArgs a{};
+    a.d = *d;
+    a.d.w1 = w;
+    a.d.w2 = w;
+    a.d.b1 = bias;
+    a.d.b2 = bias;
+    a.d.t = out;
+    a.d.part = nullptr;
+    a.d.z1 = a.d.a1 = nullptr;
+    a.gres = res;
+    const int ncu = rd_num_cus();
+    const int ntiles = d->B * (d->H / 16) * (d->W / 16);
+    const int grid = ntiles < ncu ? ntiles : ncu;
+    hipStream_t s = (hipStream_t)stream;
+    if (d->dtype == FEN_F16) launch_rd<f16, true, false, false, true>(a, grid, s);
+    else launch_rd<bf16, true, false, false, true>(a, grid, s);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -81,6 +81,7 @@ _SIGS = {
     "fen_rcab_deferred_supported": (c_int, [c_int] * 6),
     "fen_rcab_deferred": (c_int, [POINTER(RcabDeferredDesc), c_void_p]),
     "fen_rcab_bwd": (c_int, [POINTER(RcabBwdDesc), c_void_p]),
+    "fen_rcab_group_end": (c_int, [POINTER(RcabDeferredDesc)] + [c_void_p] * 5),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
     "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),

@@ -55,6 +55,9 @@ class NetSpec:
 # in-launch synchronisation between blocks; 'perop' -- conv1(+PReLU) / conv2(+pool) / SE
 # launches (shapes outside the deferred kernel's envelope always take this path).
 RCAB_MODE = os.environ.get("FEN_RCAB", "deferred")
+# a ResidualGroup's end on the deferred path: the last RCAB's gate + residual and the group conv
+# in one fen_rcab_group_end launch ('fused', default) or fen_se_fused + fen_conv3x3 ('split')
+GROUP_END_FUSED = os.environ.get("FEN_GROUP_END", "fused") != "split"
 # RCAB backward: the SE backward and its apply as one fen_se_bwd_fused launch (default) or
 # the fen_se_bwd + fen_se_bwd_apply pair (FEN_SE_BWD=pair; shapes outside the fused
 # kernel's envelope always take the pair)
@@ -293,10 +296,12 @@ class Forward:
                                                                                            self.s.Cr))
 
     def _chain(self, x: torch.Tensor, pres: Sequence[str], names: Sequence[Optional[str]],
-               out: Optional[torch.Tensor] = None):
+               out: Optional[torch.Tensor] = None, gconv: Optional[dict] = None):
         """A chain of RCABs (blocks.py:135-153; a ResidualGroup's blocks, blocks.py:185-188) on
         fen_rcab_deferred: launch j computes t_j and its tile sums and applies RCAB j-1's gate to
-        build x_j; the chain end's gate and residual are fen_se_fused.  -> (y, [saved per RCAB])."""
+        build x_j; the chain end's gate and residual are fen_se_fused -- or, with gconv = {w, b,
+        res, y}, fen_rcab_group_end, which also runs the group conv (y = conv(chain out) + res;
+        `out`, the chain's output, is then written only when given).  -> (y, [saved per RCAB])."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
         T = tiles(H, W)
@@ -337,9 +342,20 @@ class Forward:
                 self.attn[name] = sg
             prev = dict(pre=pre, x=xin, t=t, part=part, s=sg, mean=mean, hid=hid)
             saved.append(dict(x=xin, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg) if self.save else dict(s=sg))
+        ca = prev["pre"] + "channel_attention.fc."
+        if gconv is not None:
+            d = L.RcabDeferredDesc()
+            d.dtype, d.B, d.H, d.W, d.C, d.Cr = ctx.code, B, H, W, C, s.Cr
+            d.res_scale, d.inv_hw = float(s.res_scale), 1.0 / (H * W)
+            d.x, d.tp, d.pp = ptr(prev["x"]), ptr(prev["t"]), ptr(prev["part"])
+            d.pfc1, d.pfc2 = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
+            d.ps, d.pmean, d.phid = ptr(prev["s"]), ptr(prev["mean"]), ptr(prev["hid"])
+            d.xo = ptr(out)
+            ctx.emit("rcab_group_end", ctx.lib.fen_rcab_group_end, byref(d), ptr(gconv["w"]), ptr(gconv["b"]),
+                     ptr(gconv["res"]), ptr(gconv["y"]))
+            return gconv["y"], saved
         # chain end: the last RCAB's gate + residual
         y = out if out is not None else ctx.alloc(x.shape)
-        ca = prev["pre"] + "channel_attention.fc."
         ctx.emit("se_fused", ctx.lib.fen_se_fused, ctx.code, B, H * W, C, s.Cr, T, 1.0 / (H * W), ptr(prev["part"]),
                  ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]), ptr(prev["mean"]), ptr(prev["hid"]),
                  ptr(prev["s"]), ptr(prev["t"]), s.res_scale, ptr(prev["x"]), ptr(y))
@@ -351,10 +367,17 @@ class Forward:
         B, H, W, C = x.shape
         pre = f"residual_groups.{g}." if pre is None else pre
         if self._deferred_ok(x) and s.NB > 0:
-            y_last = ctx.alloc(x.shape) if self.save else ctx.scratch("rd_y", x.shape)
-            h, blocks = self._chain(x, [f"{pre}blocks.{b}." for b in range(s.NB)],
-                                    [f"group{g}_rcab{b}" for b in range(s.NB)], out=y_last)
+            pres = [f"{pre}blocks.{b}." for b in range(s.NB)]
+            names = [f"group{g}_rcab{b}" for b in range(s.NB)]
             y = out if out is not None else ctx.alloc(x.shape)
+            if GROUP_END_FUSED:
+                # the chain's output (the group conv's input) is materialised only for backward
+                y_last = ctx.alloc(x.shape) if self.save else None
+                _, blocks = self._chain(x, pres, names, out=y_last,
+                                        gconv=dict(w=Wt.packed(pre + "conv", 0), b=p[pre + "conv.bias"], res=x, y=y))
+                return y, dict(blocks=blocks, x=x, x_last=y_last)
+            y_last = ctx.alloc(x.shape) if self.save else ctx.scratch("rd_y", x.shape)
+            h, blocks = self._chain(x, pres, names, out=y_last)
             conv(ctx, h, Wt.packed(pre + "conv", 0), B, H, W, C, C, bias=p[pre + "conv.bias"], y=y, res=(x,))
             return y, dict(blocks=blocks, x=x, x_last=h)
         blocks = []

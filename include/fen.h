@@ -206,6 +206,15 @@ typedef struct {
 int fen_rcab_deferred_supported(int dtype, int B, int H, int W, int C, int Cr);
 int fen_rcab_deferred(const fen_rcab_deferred_desc* d, void* stream);
 
+/* A ResidualGroup's end in one launch (blocks.py:185-189): the last RCAB's gate and scaled
+ * residual, y = x + res_scale * s * t, applied while building the input (d describes that
+ * RCAB exactly as for a deferred launch: x, tp, pp, pfc1, pfc2, res_scale, inv_hw, the
+ * optional ps / pmean / phid copies, and xo = y out or NULL), then the group conv
+ * out = conv(y; w packed mode 0, bias) + res (the group's input).  d's conv fields are
+ * ignored.  Replaces fen_se_fused + fen_conv3x3 at the chain end.                          */
+int fen_rcab_group_end(const fen_rcab_deferred_desc* d, const void* w, const float* bias, const void* res,
+                       void* out, void* stream);
+
 /* The RCAB backward's two data gradients in one launch (autograd of blocks.py:145-147):
  *   dz1 = conv2^T(dt) * PReLU'(z1),  dalpha_part[b][tile][c] = sum over the tile of
  *   conv2^T(dt) * z1 * (z1 <= 0),  dx = conv1^T(dz1) + dy,

@@ -204,3 +204,50 @@ def test_rcab_bwd_fused(prec, B, H, W, dot):
     assert rel(dal.cpu(), dal_ref) <= tolp
     if dot:
         assert rel(dotp.cpu(), dot_ref) <= tolp
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("B,H,W,train", [(2, 32, 32, False), (17, 64, 64, True), (1, 48, 80, False),
+                                          (32, 64, 64, False), (3, 16, 16, True)])
+def test_group_end_fused(prec, B, H, W, train):
+    """fen_rcab_group_end (the last RCAB's gate + residual applied while building the input,
+    then the group conv + bias + the group's residual, one launch) vs the split chain end
+    (fen_se_fused, then fen_conv3x3 with the residual epilogue) in Forward.group: the group
+    output at rel-L2 <= 2e-3 (bf16) / 5e-4 (fp16) -- both round y to the 16-bit format before
+    the conv; the gate product's fp32 order and the accumulation order differ -- and, in
+    training, the saved chain output (the group conv's weight-gradient operand, same bound)
+    and the last RCAB's gate s (|d| <= 1e-5)."""
+    from src.hip import net
+    from src.hip.net import Forward, NetSpec, Weights
+    from src.hip.program import Ctx
+    dtype = DT[prec]
+    n = 3
+    p = _params(n)
+    g = torch.Generator().manual_seed(21)
+    q = {}
+    for k, v in p.items():
+        q["rg." + k.replace("b", "blocks.", 1)] = v
+    q["rg.conv.weight"] = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    q["rg.conv.bias"] = torch.randn(64, generator=g) * 0.1
+    x = torch.randn(B, H, W, 64, generator=g).to(DEV, dtype)
+    outs = {}
+    for fused in (True, False):
+        old = net.GROUP_END_FUSED
+        net.GROUP_END_FUSED = fused
+        try:
+            ctx = Ctx(dtype, DEV)
+            pd = {k: v.to(DEV) for k, v in q.items()}
+            Wt = Weights(pd, dtype, DEV)
+            fw = Forward(NetSpec(C=64, G=1, NB=n, Cr=16), ctx, Wt, save=train)
+            y, sv = fw.group(x, 0, pre="rg.")
+            torch.cuda.synchronize()
+            outs[fused] = (y.float().cpu(), sv)
+        finally:
+            net.GROUP_END_FUSED = old
+    tol = 2e-3 if prec == "bf16" else 5e-4
+    rel = lambda a_, b_: float((a_ - b_).norm() / b_.norm())
+    assert rel(outs[True][0], outs[False][0]) <= tol
+    if train:
+        a, b_ = outs[True][1], outs[False][1]
+        assert rel(a["x_last"].float().cpu(), b_["x_last"].float().cpu()) <= tol
+        assert float((a["blocks"][-1]["s"] - b_["blocks"][-1]["s"]).abs().max()) <= 1e-5
