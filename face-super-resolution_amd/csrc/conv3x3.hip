@@ -932,7 +932,21 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     // a last partial panel (Cin % CK: FaceEnhanceNetLite's 32 channels in 16-bit) reads zeros
     // past Cin, in the halo and in the filter
     const int npan = (Cin + CK - 1) / CK;
+    // space-to-depth stride-2 convs (fen_conv_desc.s2d_in / s2d_out): only the taps the
+    // scattered filter fills, (1 + a)(1 + b) of 9 for phase (a, b) -- forward taps kh', kw' in
+    // {1} u ({0} if the phase bit is set); the mode-2 (flipped) data gradient's in {1} u {2}
+    auto live_taps = [&](int ph, bool flipped) -> unsigned {
+        const unsigned r = (ph >> 1) ? (flipped ? 6u : 3u) : 2u;     // bit set of kh' (or kh'')
+        const unsigned c = (ph & 1) ? (flipped ? 6u : 3u) : 2u;
+        unsigned m = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            if ((r >> (t / 3)) & (c >> (t % 3)) & 1u) m |= 1u << t;
+        return m;
+    };
+    const unsigned mask_out = d.s2d_out > 0 ? live_taps(co0 / d.s2d_out, true) : 0x1ffu;
     for (int pn = 0; pn < npan; ++pn) {
+        const unsigned mask = d.s2d_in > 0 ? live_taps(pn * CK / d.s2d_in, false) : mask_out;
         // ---- stage the input halo of panel pn (zero padding outside the image) ----
         constexpr int HPT = (HP * 8 + 255) / 256;   // 11 chunks per thread: loads first, then writes
         uint4 hv[HPT];
@@ -973,14 +987,23 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
                 *(uint4*)(dst + swz(i >> 3, i & 7)) = wr[j];
             }
         };
-        load_w(0);
+        // live taps in order (mask is block-uniform: scalar bit walk)
+        unsigned rem = mask;
+        int tap = __builtin_ctz(rem);
+        rem &= rem - 1;
+        load_w(tap);
         store_w(wbuf);
         __syncthreads();
-        for (int tap = 0; tap < 9; ++tap) {
-            if (tap < 8) load_w(tap + 1);      // issue early, write after the MFMAs
-            conv_tap<T, MT, 4>(acc, wbuf + (tap & 1) * COT * 128, halo, tap, wave, 0, q, c16);
-            if (tap < 8) store_w(wbuf + ((tap + 1) & 1) * COT * 128);
+        for (int it = 0;; ++it) {
+            const bool more = rem != 0;
+            const int ntap = more ? __builtin_ctz(rem) : 0;
+            if (more) load_w(ntap);            // issue early, write after the MFMAs
+            conv_tap<T, MT, 4>(acc, wbuf + (it & 1) * COT * 128, halo, tap, wave, 0, q, c16);
+            if (more) store_w(wbuf + ((it + 1) & 1) * COT * 128);
             __syncthreads();
+            if (!more) break;
+            rem &= rem - 1;
+            tap = ntap;
         }
     }
     float* red = (float*)wbuf;     // LDS is free after the loop
@@ -1073,7 +1096,8 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
     constexpr bool H16 = sizeof(T) == 2;
     // the persistent kernels address the input with 32-bit buffer offsets
     const bool small = (size_t)d->B * d->H * d->W * 128 < (size_t)0x7fff0000;
-    const bool persist = H16 && d->Cin == 64 && small && !(epi & FEN_EPI_UNSHUFFLE) && conv_variant() != 1;
+    const bool s2d = d->s2d_in > 0 || d->s2d_out > 0;
+    const bool persist = H16 && d->Cin == 64 && small && !(epi & FEN_EPI_UNSHUFFLE) && conv_variant() != 1 && !s2d;
     if (epi & FEN_EPI_LAST) {
         if (d->Cout > 4 || !d->lr || d->scale <= 0 || d->H % d->scale || d->W % d->scale) return FEN_EINVAL;
         if (epi & ~(FEN_EPI_LAST | FEN_EPI_BIAS)) return FEN_EUNSUPPORTED;
@@ -1157,6 +1181,12 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
         if (np > 1) return FEN_EUNSUPPORTED;
     }
     if ((epi & FEN_EPI_DOT) && (epi & (FEN_EPI_UNSHUFFLE | FEN_EPI_LAST))) return FEN_EUNSUPPORTED;
+    // space-to-depth stride-2 form: whole 64-channel panels / output tiles per phase
+    if (d->s2d_in < 0 || d->s2d_out < 0 || (d->s2d_in && d->s2d_out)) return FEN_EINVAL;
+    if (d->s2d_in && (d->s2d_in % 64 || d->Cin != 4 * d->s2d_in)) return FEN_EINVAL;
+    if (d->s2d_out && (d->s2d_out % 64 || d->Cout != 4 * d->s2d_out)) return FEN_EINVAL;
+    if ((d->s2d_in || d->s2d_out) && (epi & (FEN_EPI_LAST | FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE)))
+        return FEN_EUNSUPPORTED;
     if ((epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE)) == (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE))
         return FEN_EUNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;

@@ -254,6 +254,25 @@ __global__ __launch_bounds__(256) void k_subsample2(int B, int Ho, int Wo, int C
     *(uint4*)(y + po * C + g * V) = *(const uint4*)(x + src);
 }
 
+// space-to-depth by 2 (the stride-2 conv's input as a stride-1 conv's, phase-major channels):
+// s[b][i][j][(2a + c2) * C + c] = x[b][2i + a][2j + c2][c]; INV: x <- s (every element written)
+template <typename T, bool INV>
+__global__ __launch_bounds__(256) void k_s2d2(int B, int Ho, int Wo, int C, const T* __restrict__ src,
+                                              T* __restrict__ dst) {
+    constexpr int V = 16 / sizeof(T);
+    const int G = C / V;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // over s2d vectors
+    if (i >= (size_t)B * Ho * Wo * 4 * G) return;
+    const int g = (int)(i % G);
+    const int ph = (int)((i / G) & 3);
+    const size_t po = i / (4 * (size_t)G);
+    const int wo = (int)(po % Wo), ho = (int)((po / Wo) % Ho), b = (int)(po / ((size_t)Wo * Ho));
+    const size_t full = (((size_t)b * 2 * Ho + 2 * ho + (ph >> 1)) * (2 * Wo) + 2 * wo + (ph & 1)) * C + g * V;
+    const size_t s2d = po * 4 * C + (size_t)ph * C + g * V;
+    if constexpr (INV) *(uint4*)(dst + full) = *(const uint4*)(src + s2d);
+    else *(uint4*)(dst + s2d) = *(const uint4*)(src + full);
+}
+
 // out[b][2h][2w] = dy[b][h][w], zero elsewhere (every element of out written)
 template <typename T>
 __global__ __launch_bounds__(256) void k_zero_insert2(int B, int Ho, int Wo, int C, const T* __restrict__ dy,
@@ -379,6 +398,32 @@ extern "C" int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const v
         const size_t n = (size_t)B * 2 * Ho * 2 * Wo * (C / 4);
         hipLaunchKernelGGL(k_zero_insert2<float>, dim3(nblk(n)), dim3(256), 0, STREAM, B, Ho, Wo, C,
                            (const float*)dy, (float*)out);
+    } else {
+        return FEN_EINVAL;
+    }
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_s2d2(int dtype, int B, int H, int W, int C, const void* x, void* y, int inverse, void* stream) {
+    if (!x || !y || B <= 0 || H <= 0 || W <= 0 || (H | W) & 1 || C % 8) return FEN_EINVAL;
+    const int V = dtype == FEN_F32 ? 4 : 8;
+    const size_t n = (size_t)B * H * W * C / V;
+    const int Ho = H / 2, Wo = W / 2;
+    if (dtype == FEN_BF16 || dtype == FEN_F16) {
+        if (inverse)
+            hipLaunchKernelGGL((k_s2d2<bf16, true>), dim3(nblk(n)), dim3(256), 0, STREAM, B, Ho, Wo, C, (const bf16*)x,
+                               (bf16*)y);
+        else
+            hipLaunchKernelGGL((k_s2d2<bf16, false>), dim3(nblk(n)), dim3(256), 0, STREAM, B, Ho, Wo, C, (const bf16*)x,
+                               (bf16*)y);
+    } else if (dtype == FEN_F32) {
+        if (inverse)
+            hipLaunchKernelGGL((k_s2d2<float, true>), dim3(nblk(n)), dim3(256), 0, STREAM, B, Ho, Wo, C, (const float*)x,
+                               (float*)y);
+        else
+            hipLaunchKernelGGL((k_s2d2<float, false>), dim3(nblk(n)), dim3(256), 0, STREAM, B, Ho, Wo, C,
+                               (const float*)x, (float*)y);
     } else {
         return FEN_EINVAL;
     }

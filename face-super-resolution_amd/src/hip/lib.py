@@ -32,6 +32,7 @@ class ConvDesc(Structure):
         ("y", c_void_p), ("y_pre", c_void_p), ("res", c_void_p * 3), ("pre_in", c_void_p),
         ("part", c_void_p), ("lr", c_void_p), ("scale", c_int), ("clamp", c_int), ("hr", c_void_p),
         ("dout", c_void_p), ("l1_scale", c_float), ("loss_part", c_void_p), ("debug", c_int),
+        ("s2d_in", c_int), ("s2d_out", c_int),
     ]
 
 
@@ -126,6 +127,7 @@ _SIGS = {
     "fen_bn_bwd": (c_int, [c_int, c_size_t, c_int] + [c_void_p] * 5 + [c_float] + [c_void_p] * 3 +
                    [c_int, c_void_p, c_void_p]),
     "fen_subsample2": (c_int, [c_int] * 5 + [c_void_p] * 3),
+    "fen_s2d2": (c_int, [c_int] * 5 + [c_void_p] * 2 + [c_int, c_void_p]),
     "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
     "fen_build_info": (ctypes.c_char_p, []),

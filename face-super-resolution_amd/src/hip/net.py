@@ -130,7 +130,7 @@ class Weights:
 # --------------------------------------------------------------------------------------
 def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, y=None, y_pre=None,
          res: Sequence = (), pre_in=None, part=None, lr=None, scale=0, clamp=0, hr=None, dout=None,
-         l1_scale=0.0, loss_part=None, debug=0) -> None:
+         l1_scale=0.0, loss_part=None, debug=0, s2d_in=0, s2d_out=0) -> None:
     d = L.ConvDesc()
     d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = ctx.code, B, H, W, Cin, Cout
     d.x, d.w, d.bias = ptr(x), ptr(wpk), ptr(bias)
@@ -142,7 +142,38 @@ def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, 
     d.lr, d.scale, d.clamp, d.hr, d.dout = ptr(lr), scale, clamp, ptr(hr), ptr(dout)
     d.l1_scale, d.loss_part = float(l1_scale), ptr(loss_part)
     d.debug = debug
+    d.s2d_in, d.s2d_out = s2d_in, s2d_out
     ctx.emit("conv3x3", ctx.lib.fen_conv3x3, byref(d))
+
+
+# stride-2 3x3 conv as a stride-1 conv over the space-to-depth input (fen_s2d2): filter tap
+# (kh, kw) -> (input phase (a, b), tap (kh', kw')) of the phase-major filter
+#   kh = 0 -> a = 1, kh' = 0;  kh = 1 -> a = 0, kh' = 1;  kh = 2 -> a = 1, kh' = 1  (kw likewise)
+_S2D_TAP = {0: (1, 0), 1: (0, 1), 2: (1, 1)}
+
+
+def s2d_filter(w: torch.Tensor) -> torch.Tensor:
+    """OIHW [Cout, C, 3, 3] -> the phase-major [Cout, 4C, 3, 3] filter (zeros elsewhere)."""
+    co, c = w.shape[0], w.shape[1]
+    out = w.new_zeros(co, 4 * c, 3, 3)
+    for kh in range(3):
+        a, kh2 = _S2D_TAP[kh]
+        for kw in range(3):
+            b, kw2 = _S2D_TAP[kw]
+            ph = 2 * a + b
+            out[:, ph * c:(ph + 1) * c, kh2, kw2] = w[:, :, kh, kw]
+    return out
+
+
+def s2d_filter_grad(g4: torch.Tensor, out: torch.Tensor) -> None:
+    """The phase-major filter's gradient [Cout, 4C, 3, 3] -> the OIHW gradient (into out)."""
+    c = out.shape[1]
+    for kh in range(3):
+        a, kh2 = _S2D_TAP[kh]
+        for kw in range(3):
+            b, kw2 = _S2D_TAP[kw]
+            ph = 2 * a + b
+            out[:, :, kh, kw] = g4[:, ph * c:(ph + 1) * c, kh2, kw2]
 
 
 def wgrad(ctx: Ctx, x, dy, B, H, W, Cin, Cout, dw, db, cout_valid=None) -> None:

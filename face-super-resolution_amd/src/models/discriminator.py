@@ -6,10 +6,16 @@ as the reference, so its checkpoints and trainer code work unchanged.  The featu
 (10 conv blocks) runs as one autograd Function over C-ABI launches, NHWC in the compute
 dtype:
   block 1    conv 3->64 + bias + LeakyReLU(0.2): the K=27 input kernel (fen_conv_first_fwd_ex)
-  blocks 2-10 conv (stride 1, or stride 2 = the full-resolution conv + fen_subsample2),
+  blocks 2-10 conv (stride 1; stride 2 = a stride-1 conv over the space-to-depth input,
+             fen_s2d2, with the phase-major filter -- only the filled taps run, a quarter of
+             the full-resolution conv's work; FEN_D_S2D=0: the full-resolution conv +
+             fen_subsample2),
              train-mode BatchNorm statistics (+ running-stat update) and BN + LeakyReLU
              (fen_bn_stats / fen_bn_apply; eval mode uses the running statistics)
-  backward   fen_bn_bwd (BN + LeakyReLU), fen_zero_insert2 for stride-2 layers, weight
+  backward   fen_bn_bwd (BN + LeakyReLU); stride-2 layers: the weight gradient of the
+             phase-major filter on the space-to-depth input (gathered back to OIHW) and the
+             data gradient through the same masked conv + the inverse fen_s2d2 (or, with
+             FEN_D_S2D=0, fen_zero_insert2 + the full-resolution gradients); weight
              gradients on fen_wgrad3x3 / fen_conv_first_wgrad, data gradients on mode-2 convs
              (block 2's epilogue applies block 1's LeakyReLU mask), and d(input) -- needed by
              the generator's adversarial step -- through a 64->16 conv (3 valid channels).
@@ -19,6 +25,7 @@ the HIP path (the reference's factory always builds use_bn=True).
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -27,6 +34,10 @@ import torch.nn.functional as F
 
 _DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
 _SLOPE = 0.2
+_S2D = os.environ.get("FEN_D_S2D", "1") != "0"
+# (the 64-channel stride-2 layer stays on the full-resolution persistent kernels)
+_S2D_MIN_CIN = int(os.environ.get("FEN_D_S2D_MIN_CIN", "128"))
+_S2D_MAX_CIN = int(os.environ.get("FEN_D_S2D_MAX_CIN", "256"))
 
 
 class _DFeatures(torch.autograd.Function):
@@ -51,14 +62,22 @@ class _DFeatures(torch.autograd.Function):
         hh, ww = H, W
         for blk in blocks[1:]:
             cin, cout, st = blk["cin"], blk["cout"], blk["stride"]
-            wpk = mod._packed(ctx, blk, 0)
-            z = ctx.alloc((B, hh, ww, cout))
-            conv(ctx, a, wpk, B, hh, ww, cin, cout, y=z)
-            ho, wo = (hh // 2, ww // 2) if st == 2 else (hh, ww)
-            if st == 2:
-                zs = ctx.alloc((B, ho, wo, cout))
-                ctx.emit("d_sub", lib.fen_subsample2, ctx.code, B, hh, ww, cout, ptr(z), ptr(zs))
-                z = zs
+            xs = None
+            if st == 2 and _S2D and _S2D_MIN_CIN <= cin <= _S2D_MAX_CIN:
+                ho, wo = hh // 2, ww // 2
+                xs = ctx.alloc((B, ho, wo, 4 * cin))
+                ctx.emit("d_s2d", lib.fen_s2d2, ctx.code, B, hh, ww, cin, ptr(a), ptr(xs), 0)
+                z = ctx.alloc((B, ho, wo, cout))
+                conv(ctx, xs, mod._packed(ctx, blk, 0, s2d=True), B, ho, wo, 4 * cin, cout, y=z, s2d_in=cin)
+            else:
+                wpk = mod._packed(ctx, blk, 0)
+                z = ctx.alloc((B, hh, ww, cout))
+                conv(ctx, a, wpk, B, hh, ww, cin, cout, y=z)
+                ho, wo = (hh // 2, ww // 2) if st == 2 else (hh, ww)
+                if st == 2:
+                    zs = ctx.alloc((B, ho, wo, cout))
+                    ctx.emit("d_sub", lib.fen_subsample2, ctx.code, B, hh, ww, cout, ptr(z), ptr(zs))
+                    z = zs
             bn = blk["bn"]
             npx = B * ho * wo
             stat = ctx.alloc((2 * cout,), torch.float32)
@@ -75,7 +94,7 @@ class _DFeatures(torch.autograd.Function):
             out = ctx.alloc((B, ho, wo, cout))
             ctx.emit("d_bn_apply", lib.fen_bn_apply, ctx.code, npx, cout, ptr(z), ptr(stat), ptr(stat[cout:]),
                      ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(out))
-            saved.append(dict(blk=blk, a_in=a, z=z, stat=stat, H=hh, W=ww, Ho=ho, Wo=wo))
+            saved.append(dict(blk=blk, a_in=a, xs=xs, z=z, stat=stat, H=hh, W=ww, Ho=ho, Wo=wo))
             a, hh, ww = out, ho, wo
         fctx.saved_blocks, fctx.a1, fctx.xin, fctx.mod = saved, saved[0]["a_in"], xin, mod
         fctx.shape = (B, H, W)
@@ -85,7 +104,7 @@ class _DFeatures(torch.autograd.Function):
     @staticmethod
     def backward(fctx, g):
         from ..hip import lib as L
-        from ..hip.net import conv, wgrad
+        from ..hip.net import conv, s2d_filter_grad, tiles, wgrad
         from ..hip.program import Ctx, ptr
         mod = fctx.mod
         dt = mod.compute_dtype
@@ -109,6 +128,25 @@ class _DFeatures(torch.autograd.Function):
                      ptr(work))
             grads[bn.weight] = dgam
             grads[bn.bias] = dbet
+            if sv["xs"] is not None:
+                # stride 2 over the space-to-depth input: the phase-major filter's gradients
+                ho, wo, c4 = sv["Ho"], sv["Wo"], 4 * cin
+                dw4 = torch.zeros(cout, c4, 3, 3, device=g.device)
+                wgrad(ctx, sv["xs"], dz, B, ho, wo, c4, cout, dw4, None)
+                dw = torch.empty_like(blk["conv"].weight)
+                s2d_filter_grad(dw4, dw)
+                grads[blk["conv"].weight] = dw
+                dxs = ctx.alloc((B, ho, wo, c4))
+                if k == 0:
+                    part = ctx.alloc((B * tiles(ho, wo), c4), torch.float32)
+                    conv(ctx, dz, mod._packed(ctx, blk, 2, s2d=True), B, ho, wo, cout, c4, epi=L.EPI_PRELU_BWD,
+                         alpha=mod._slopes(c4, g.device), pre_in=sv["xs"], y=dxs, part=part, s2d_out=cin)
+                else:
+                    conv(ctx, dz, mod._packed(ctx, blk, 2, s2d=True), B, ho, wo, cout, c4, y=dxs, s2d_out=cin)
+                da = ctx.alloc((B, sv["H"], sv["W"], cin))
+                ctx.emit("d_s2d_inv", lib.fen_s2d2, ctx.code, B, sv["H"], sv["W"], cin, ptr(dxs), ptr(da), 1)
+                d = da
+                continue
             if blk["stride"] == 2:
                 dzf = ctx.alloc((B, sv["H"], sv["W"], cout))
                 ctx.emit("d_zins", lib.fen_zero_insert2, ctx.code, B, sv["Ho"], sv["Wo"], cout, ptr(dz), ptr(dzf))
@@ -209,19 +247,20 @@ class VGGStyleDiscriminator(nn.Module):
     def _feature_params(self):
         return [p for p in self.features.parameters()]
 
-    def _packed(self, ctx, blk, mode):
+    def _packed(self, ctx, blk, mode, s2d=False):
+        from ..hip.net import s2d_filter
         from ..hip.program import ptr
         w = blk["conv"].weight
-        key = (blk["i"], mode, ctx.code)
+        key = (blk["i"], mode, ctx.code, s2d)
         ent = self._packs.get(key)
         if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
             # (a captured GAN iteration records the re-packs its Python saw: the optimizer
             # steps bump the versions at capture time exactly as in every eager iteration)
-            cout, cin = w.shape[0], w.shape[1]
+            cout, cin = w.shape[0], w.shape[1] * (4 if s2d else 1)
             n = ctx.lib.fen_packed_elems(mode, cout, cin)
             buf = ent[2] if ent is not None and ent[1] == w.data_ptr() else \
                 torch.empty(n, dtype=ctx.tdtype, device=w.device)
-            src = w.detach().float().contiguous()
+            src = s2d_filter(w.detach().float()) if s2d else w.detach().float().contiguous()
             ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, cout, cin, ptr(src), ptr(buf))
             ctx.keep(src)
             ent = (w._version, w.data_ptr(), buf)

@@ -76,6 +76,13 @@ typedef struct {
     float l1_scale;            /* dL/dsr = sign(sr-hr) * l1_scale   (weight / numel)             */
     float* loss_part;          /* [B*tiles] partial sums of |sr-hr|                              */
     int debug;                 /* 0; tuning ablations only (1: skip epilogue, 2: skip MFMA loop)  */
+    /* stride-2 convs as stride-1 convs over the space-to-depth input (fen_s2d2): a 3x3 stride-2
+     * conv of C channels = this conv with Cin = 4C and the filter scattered by fen_s2d_filter
+     * rule, of which only (1 + a)(1 + b) taps are non-zero for input phase (a, b).  s2d_in = C:
+     * skip the zero taps per input panel (forward, mode-0 pack); s2d_out = C: per output channel
+     * tile (its data gradient, mode-2 pack, Cout = 4C).  0 = off.  Streamed kernel only.       */
+    int s2d_in;
+    int s2d_out;
 } fen_conv_desc;
 
 int fen_conv3x3(const fen_conv_desc* d, void* stream);
@@ -353,6 +360,13 @@ int fen_bn_bwd(int dtype, size_t npx, int C, const void* da, const void* y, cons
                const float* beta, float slope, void* dy, float* dgamma, float* dbeta, int accumulate, float* work,
                void* stream);
 int fen_subsample2(int dtype, int B, int H, int W, int C, const void* x, void* y, void* stream);
+/* space-to-depth by 2: y[b][i][j][(2a + c2) * C + c] = x[b][2i + a][2j + c2][c] (x [B,H,W,C] ->
+ * y [B,H/2,W/2,4C]); inverse = 1 maps y back.  With the phase-major filter
+ * W'[co][(2a + c2) C + c][kh'][kw'] = W[co][c][kh][kw] (kh = 1 -> a = 0, kh' = 1; kh = 0 ->
+ * a = 1, kh' = 0; kh = 2 -> a = 1, kh' = 1; kw likewise) a stride-2 conv (discriminator.py:
+ * 47-82) is a stride-1 conv of y at a quarter of the pixels, and its data gradient comes back
+ * through the inverse.                                                                     */
+int fen_s2d2(int dtype, int B, int H, int W, int C, const void* x, void* y, int inverse, void* stream);
 int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const void* dy, void* out, void* stream);
 
 const char* fen_status_string(int code);

@@ -523,3 +523,54 @@ def test_se_bwd_fused_matches_pair(dtype, B, HW, C, Cr):
     dtref = dy.double() * rs * sd[:, None, :] + gref[:, None, :]
     tol = {torch.float32: 1e-5, torch.bfloat16: 1e-2, torch.float16: 2e-3}[dtype]
     assert float((dt2.double() - dtref).abs().max() / dtref.abs().max()) <= tol
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 32, 64, 64), (2, 16, 16, 128, 128), (1, 64, 48, 64, 128),
+                                             (2, 16, 16, 256, 256), (3, 32, 16, 128, 256)])
+def test_s2d_stride2_conv(dtype, B, H, W, Cin, Cout):
+    """The discriminator's stride-2 3x3 conv (discriminator.py:47-82) as a stride-1 conv over
+    the space-to-depth input (fen_s2d2) with the phase-major filter, only its filled taps run
+    (fen_conv_desc.s2d_in / s2d_out): forward, data gradient (mode-2 pack, inverse fen_s2d2)
+    and weight gradient (gathered back to OIHW) vs float64 autograd of F.conv2d(stride=2) on
+    the same rounded operands; fp32 rel 1e-5, bf16 rel 1e-2 (output rounding) / 1e-5 (wgrad,
+    fp32 accumulation of rounded operands)."""
+    from src.hip import lib as L, net
+    from src.hip.program import ptr
+    torch.manual_seed(17)
+    x = torch.randn(B, Cin, H, W).to(dtype).float()
+    w = (torch.randn(Cout, Cin, 3, 3) * 0.05).to(dtype).float()
+    dy = torch.randn(B, Cout, H // 2, W // 2).to(dtype).float()
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    y_ref = F.conv2d(xr, wr, padding=1, stride=2)
+    y_ref.mul(dy.double()).sum().backward()
+    ctx = _ctx(dtype)
+    s = torch.cuda.current_stream().cuda_stream
+    Ho, Wo = H // 2, W // 2
+    xd = nhwc(x, dtype)
+    xs = ctx.alloc((B, Ho, Wo, 4 * Cin))
+    L.check(ctx.lib.fen_s2d2(ctx.code, B, H, W, Cin, ptr(xd), ptr(xs), 0, s), "s2d")
+    w4 = net.s2d_filter(w.to(DEV))
+    y = ctx.alloc((B, Ho, Wo, Cout))
+    net.conv(ctx, xs, _pack(ctx, w4, 0), B, Ho, Wo, 4 * Cin, Cout, y=y, s2d_in=Cin)
+    dyd = nhwc(dy, dtype)
+    dxs = ctx.alloc((B, Ho, Wo, 4 * Cin))
+    net.conv(ctx, dyd, _pack(ctx, w4, 2), B, Ho, Wo, Cout, 4 * Cin, y=dxs, s2d_out=Cin)
+    dx = ctx.alloc((B, H, W, Cin))
+    L.check(ctx.lib.fen_s2d2(ctx.code, B, H, W, Cin, ptr(dxs), ptr(dx), 1, s), "s2d_inv")
+    dw4 = torch.zeros(Cout, 4 * Cin, 3, 3, device=DEV)
+    net.wgrad(ctx, xs, dyd, B, Ho, Wo, 4 * Cin, Cout, dw4, None)
+    dw = torch.empty(Cout, Cin, 3, 3, device=DEV)
+    net.s2d_filter_grad(dw4, dw)
+    torch.cuda.synchronize()
+    rel = lambda a, b: float((a.double() - b).norm() / b.norm())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(nchw(y), y_ref.detach()) <= tol
+    assert rel(nchw(dx), xr.grad) <= tol
+    assert rel(dw.cpu(), wr.grad) <= 1e-5
+    # the s2d round trip is exact
+    back = ctx.alloc((B, H, W, Cin))
+    L.check(ctx.lib.fen_s2d2(ctx.code, B, H, W, Cin, ptr(xs), ptr(back), 1, s), "s2d_inv")
+    torch.cuda.synchronize()
+    assert torch.equal(back, xd)

@@ -1,0 +1,14 @@
+# space-to-depth stride-2 discriminator convs: kernel test, D / GAN parity tests, GAN A/B
+set -e
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "s2d" -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_s2d.log 2>&1 || { tail -40 gpurun_out/pytest_s2d.log; exit 1; }
+tail -2 gpurun_out/pytest_s2d.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_disc.py tests/test_gpu_gan_step.py tests/test_gpu_gan_capture.py tests/test_gpu_trainer_resume.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_s2d2.log 2>&1 || { tail -40 gpurun_out/pytest_s2d2.log; exit 1; }
+tail -2 gpurun_out/pytest_s2d2.log
+for r in 1 2; do
+  for v in FEN_D_S2D=0 FEN_D_S2D=1; do
+    echo "$v | $(env $v timeout -k 10 300 python tools/gan_step.py | tail -1)"
+  done
+done
