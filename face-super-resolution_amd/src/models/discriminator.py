@@ -120,8 +120,9 @@ class _DFeatures(torch.autograd.Function):
             cin, cout = blk["cin"], blk["cout"]
             npx = B * sv["Ho"] * sv["Wo"]
             dz = ctx.alloc((B, sv["Ho"], sv["Wo"], cout))
-            dgam = torch.zeros(cout, device=g.device)
-            dbet = torch.zeros(cout, device=g.device)
+            # (every gradient buffer below is written whole by its kernel: no zero fill)
+            dgam = torch.empty(cout, device=g.device)
+            dbet = torch.empty(cout, device=g.device)
             work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
             ctx.emit("d_bn_bwd", lib.fen_bn_bwd, ctx.code, npx, cout, ptr(d), ptr(sv["z"]), ptr(sv["stat"]),
                      ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(dz), ptr(dgam), ptr(dbet), 0,
@@ -131,7 +132,7 @@ class _DFeatures(torch.autograd.Function):
             if sv["xs"] is not None:
                 # stride 2 over the space-to-depth input: the phase-major filter's gradients
                 ho, wo, c4 = sv["Ho"], sv["Wo"], 4 * cin
-                dw4 = torch.zeros(cout, c4, 3, 3, device=g.device)
+                dw4 = torch.empty(cout, c4, 3, 3, device=g.device)
                 wgrad(ctx, sv["xs"], dz, B, ho, wo, c4, cout, dw4, None)
                 dw = torch.empty_like(blk["conv"].weight)
                 s2d_filter_grad(dw4, dw)
@@ -151,7 +152,7 @@ class _DFeatures(torch.autograd.Function):
                 dzf = ctx.alloc((B, sv["H"], sv["W"], cout))
                 ctx.emit("d_zins", lib.fen_zero_insert2, ctx.code, B, sv["Ho"], sv["Wo"], cout, ptr(dz), ptr(dzf))
                 dz = dzf
-            dw = torch.zeros_like(blk["conv"].weight)
+            dw = torch.empty_like(blk["conv"].weight)
             wgrad(ctx, sv["a_in"], dz, B, sv["H"], sv["W"], cin, cout, dw, None)
             grads[blk["conv"].weight] = dw
             da = ctx.alloc((B, sv["H"], sv["W"], cin))
@@ -165,8 +166,8 @@ class _DFeatures(torch.autograd.Function):
             d = da
         # block 1: conv 3->64 weight / bias gradient, and d(input) when asked for
         c0 = blocks[0]
-        dw0 = torch.zeros_like(c0["conv"].weight)
-        db0 = torch.zeros_like(c0["conv"].bias)
+        dw0 = torch.empty_like(c0["conv"].weight)
+        db0 = torch.empty_like(c0["conv"].bias)
         work = ctx.alloc((lib.fen_conv_first_work_floats(B, 3, H, W, c0["cout"]),), torch.float32)
         ctx.emit("d_conv1_wgrad", lib.fen_conv_first_wgrad, ctx.code, B, 3, H, W, c0["cout"], ptr(fctx.xin), ptr(d),
                  ptr(dw0), ptr(db0), 0, ptr(work))
