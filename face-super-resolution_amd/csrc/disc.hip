@@ -430,3 +430,38 @@ extern "C" int fen_s2d2(int dtype, int B, int H, int W, int C, const void* x, vo
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
+
+// The phase-major filter of a space-to-depth stride-2 conv (see fen_s2d2), fp32 OIHW:
+// scatter: W' [Cout][4C][3][3] from W [Cout][C][3][3] (every element written, zeros where no
+// tap of W lands); gather: dW [Cout][C][3][3] from dW'.  Tap kh -> (phase bit, kh'):
+// 0 -> (1, 0), 1 -> (0, 1), 2 -> (1, 1); kw likewise.
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_s2d_filter(int Cout, int C, const float* __restrict__ src,
+                                                    float* __restrict__ dst) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (GATHER) {
+        if (i >= (size_t)Cout * C * 9) return;
+        const int tap = (int)(i % 9), c = (int)((i / 9) % C), co = (int)(i / (9 * (size_t)C));
+        const int kh = tap / 3, kw = tap % 3;
+        const int a = kh == 1 ? 0 : 1, kh2 = kh == 0 ? 0 : 1;
+        const int b = kw == 1 ? 0 : 1, kw2 = kw == 0 ? 0 : 1;
+        dst[i] = src[((size_t)co * 4 * C + (2 * a + b) * C + c) * 9 + kh2 * 3 + kw2];
+    } else {
+        if (i >= (size_t)Cout * 4 * C * 9) return;
+        const int tap = (int)(i % 9), cc = (int)((i / 9) % (4 * C)), co = (int)(i / (36 * (size_t)C));
+        const int ph = cc / C, c = cc % C, a = ph >> 1, b = ph & 1;
+        const int kh2 = tap / 3, kw2 = tap % 3;
+        const bool live = kh2 <= 1 && kw2 <= 1 && (a || kh2 == 1) && (b || kw2 == 1);
+        const int kh = a == 0 ? 1 : (kh2 == 0 ? 0 : 2), kw = b == 0 ? 1 : (kw2 == 0 ? 0 : 2);
+        dst[i] = live ? src[((size_t)co * C + c) * 9 + kh * 3 + kw] : 0.f;
+    }
+}
+
+extern "C" int fen_s2d_filter(int Cout, int C, const float* src, float* dst, int gather, void* stream) {
+    if (!src || !dst || Cout <= 0 || C <= 0) return FEN_EINVAL;
+    const size_t n = (size_t)Cout * C * 9 * (gather ? 1 : 4);
+    if (gather) hipLaunchKernelGGL(k_s2d_filter<true>, dim3(nblk(n)), dim3(256), 0, STREAM, Cout, C, src, dst);
+    else hipLaunchKernelGGL(k_s2d_filter<false>, dim3(nblk(n)), dim3(256), 0, STREAM, Cout, C, src, dst);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}

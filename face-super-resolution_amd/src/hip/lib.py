@@ -128,6 +128,7 @@ _SIGS = {
                    [c_int, c_void_p, c_void_p]),
     "fen_subsample2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_s2d2": (c_int, [c_int] * 5 + [c_void_p] * 2 + [c_int, c_void_p]),
+    "fen_s2d_filter": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
     "fen_build_info": (ctypes.c_char_p, []),

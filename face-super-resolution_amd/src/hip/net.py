@@ -149,31 +149,22 @@ def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, 
 # stride-2 3x3 conv as a stride-1 conv over the space-to-depth input (fen_s2d2): filter tap
 # (kh, kw) -> (input phase (a, b), tap (kh', kw')) of the phase-major filter
 #   kh = 0 -> a = 1, kh' = 0;  kh = 1 -> a = 0, kh' = 1;  kh = 2 -> a = 1, kh' = 1  (kw likewise)
-_S2D_TAP = {0: (1, 0), 1: (0, 1), 2: (1, 1)}
-
-
 def s2d_filter(w: torch.Tensor) -> torch.Tensor:
-    """OIHW [Cout, C, 3, 3] -> the phase-major [Cout, 4C, 3, 3] filter (zeros elsewhere)."""
-    co, c = w.shape[0], w.shape[1]
-    out = w.new_zeros(co, 4 * c, 3, 3)
-    for kh in range(3):
-        a, kh2 = _S2D_TAP[kh]
-        for kw in range(3):
-            b, kw2 = _S2D_TAP[kw]
-            ph = 2 * a + b
-            out[:, ph * c:(ph + 1) * c, kh2, kw2] = w[:, :, kh, kw]
+    """OIHW fp32 [Cout, C, 3, 3] (GPU) -> the phase-major [Cout, 4C, 3, 3] filter (fen_s2d_filter,
+    zeros where no tap lands), on the current stream."""
+    w = w.contiguous()
+    co, c = int(w.shape[0]), int(w.shape[1])
+    out = torch.empty(co, 4 * c, 3, 3, dtype=torch.float32, device=w.device)
+    L.check(L.load().fen_s2d_filter(co, c, w.data_ptr(), out.data_ptr(), 0, torch.cuda.current_stream().cuda_stream),
+            "s2d_filter")
     return out
 
 
 def s2d_filter_grad(g4: torch.Tensor, out: torch.Tensor) -> None:
     """The phase-major filter's gradient [Cout, 4C, 3, 3] -> the OIHW gradient (into out)."""
-    c = out.shape[1]
-    for kh in range(3):
-        a, kh2 = _S2D_TAP[kh]
-        for kw in range(3):
-            b, kw2 = _S2D_TAP[kw]
-            ph = 2 * a + b
-            out[:, :, kh, kw] = g4[:, ph * c:(ph + 1) * c, kh2, kw2]
+    co, c = int(out.shape[0]), int(out.shape[1])
+    L.check(L.load().fen_s2d_filter(co, c, g4.contiguous().data_ptr(), out.data_ptr(), 1,
+                                    torch.cuda.current_stream().cuda_stream), "s2d_filter_grad")
 
 
 def wgrad(ctx: Ctx, x, dy, B, H, W, Cin, Cout, dw, db, cout_valid=None) -> None:

@@ -367,6 +367,9 @@ int fen_subsample2(int dtype, int B, int H, int W, int C, const void* x, void* y
  * 47-82) is a stride-1 conv of y at a quarter of the pixels, and its data gradient comes back
  * through the inverse.                                                                     */
 int fen_s2d2(int dtype, int B, int H, int W, int C, const void* x, void* y, int inverse, void* stream);
+/* that phase-major filter from W (gather = 0: W [Cout][C][3][3] fp32 -> W' [Cout][4C][3][3],
+ * zeros where no tap lands) and the OIHW gradient back from the phase-major one (gather = 1)  */
+int fen_s2d_filter(int Cout, int C, const float* src, float* dst, int gather, void* stream);
 int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const void* dy, void* out, void* stream);
 
 const char* fen_status_string(int code);
