@@ -4,6 +4,7 @@
 // packing, deterministic column reductions and the fused clip_grad_norm_ + AdamW.
 // All vector accesses are 16 B per lane.
 #include "fen_common.h"
+#include <type_traits>
 
 namespace {
 
@@ -234,6 +235,102 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(int B, int Ci, int H, 
         const int j = jk / 28, k = jk % 28, co = lanei + 64 * j;
         if (co < C) part[((size_t)blockIdx.x * 28 + k) * C + co] = sum;
     }
+}
+
+// The same weight gradient on the fp32 matrix cores: dW^T[co][k] = sum_px dy[px][co] X[px][k]
+// with K = pixels, k = (ci, kh, kw) < 27 and k = 27 the bias column (X = 1), as
+// v_mfma_f32_16x16x4_f32 (fp32 operands: the input image stays fp32, as in the VALU form).
+// Persistent blocks walk 16x16-pixel tiles; per tile the 3 x 18 x 18 input halo and the
+// 256 x C dy tile sit in LDS, each wave takes 4 pixel rows (16 k-steps of 4 pixels) for all
+// C output channels (MB 16-row blocks) and both 16-column k blocks; the next tile's halo
+// and dy are loaded into registers while the current one computes.  Each wave writes its own
+// partial rows (4 per block), summed in fixed order by k_conv_first_finalize.
+constexpr int CFM_WAVES = 4;
+template <typename T, int MB>
+__global__ __launch_bounds__(256) void k_conv_first_wgrad_m(int B, int Ci, int H, int W, int C,
+                                                            const float* __restrict__ x, const T* __restrict__ dy,
+                                                            float* __restrict__ part) {
+    constexpr int CC = MB * 16;                              // channels held (C <= CC)
+    constexpr int V = 16 / (int)sizeof(T);                   // dy elements per 16-B load
+    constexpr int YV = 256 * CC / V / 256;                   // dy vectors per thread
+    __shared__ float xs[3 * 18 * 18];
+    __shared__ __attribute__((aligned(16))) T ys[256 * CC];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int q = lane >> 4, c16 = lane & 15;
+    const int th = (H + 15) >> 4, tw = (W + 15) >> 4;
+    const int ntiles = B * th * tw;
+    // this lane's B-operand column k = nb * 16 + c16: halo offset (k < 27), bias (k = 27), 0
+    int boff[2];
+    float bconst[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        const int k = nb * 16 + c16;
+        boff[nb] = k < 27 ? (k / 9) * 324 + ((k % 9) / 3) * 18 + (k % 3) : -1;
+        bconst[nb] = k == 27 ? 1.f : 0.f;
+    }
+    f32x4 acc[MB][2];
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[m][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float xv[4];
+    uint4 yv[YV];
+    auto load = [&](int t) {
+        const int b = t / (th * tw), tt = t - b * th * tw;
+        const int h0 = (tt / tw) << 4, w0 = (tt % tw) << 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = tid + u * 256;
+            const int ci = i / 324, r = (i / 18) % 18, c = i % 18;
+            const int hh = h0 - 1 + r, ww = w0 - 1 + c;
+            xv[u] = (i < 972 && ci < Ci && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                        ? x[(((size_t)b * Ci + ci) * H + hh) * W + ww] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < YV; ++u) {
+            const int i = tid + u * 256;                     // vector i: pixel i / (CC / V), chunk
+            const int px = i / (CC / V), ch = i % (CC / V);
+            const int hh = h0 + (px >> 4), ww = w0 + (px & 15);
+            yv[u] = (hh < H && ww < W && ch * V < C)
+                        ? *(const uint4*)(dy + (((size_t)b * H + hh) * W + ww) * C + ch * V) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    if ((int)blockIdx.x < ntiles) load(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        __syncthreads();                                     // the previous tile's reads are done
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (tid + u * 256 < 972) xs[tid + u * 256] = xv[u];
+#pragma unroll
+        for (int u = 0; u < YV; ++u) *(uint4*)(ys + (size_t)(tid + u * 256) * V) = yv[u];
+        __syncthreads();
+        if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);   // the next tile, in flight
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+            const int px = wave * 64 + s * 4 + q, pr = px >> 4, pc = px & 15;
+            float a[MB], bv[2];
+#pragma unroll
+            for (int m = 0; m < MB; ++m) a[m] = tof<T>(ys[px * CC + m * 16 + c16]);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) bv[nb] = boff[nb] >= 0 ? xs[boff[nb] + pr * 18 + pc] : bconst[nb];
+#pragma unroll
+            for (int m = 0; m < MB; ++m)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+                    acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], bv[nb], acc[m][nb], 0, 0, 0);
+        }
+    }
+    // lane holds D[co = m*16 + 4q + r][k = nb*16 + c16]; this wave's partial rows
+    float* pw = part + (size_t)(blockIdx.x * CFM_WAVES + wave) * 28 * C;
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = nb * 16 + c16, co = m * 16 + 4 * q + r;
+                if (k < 28 && co < C) pw[(size_t)k * C + co] = acc[m][nb][r];
+            }
 }
 
 // block = one of the 28 rows k (27 weights + bias), 256 threads: thread (co, quarter) sums every
@@ -1101,12 +1198,42 @@ extern "C" int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C,
 }
 
 extern "C" size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C) {
-    return (size_t)CF_BLOCKS * 28 * C;
+    return (size_t)CF_BLOCKS * CFM_WAVES * 28 * C;   // the MFMA form: one partial row set per wave
 }
 
 extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const float* x, const void* dy,
                                     float* dw, float* db, int accumulate, float* work, void* stream) {
     if (!x || !dy || !dw || !work || Ci > 3 || C > 128 || B <= 0) return FEN_EINVAL;
+    if (C % 16 == 0) {   // (the VALU form below: 223 vs ~70 us at 256x256, B=32; kept for odd C)
+        // matrix-core form: MB = 16-channel blocks (C = 32, 64 or 128 on the path)
+        auto go = [&](auto tag, auto mb) {
+            using TT = decltype(tag);
+            constexpr int MBv = decltype(mb)::value;
+            hipLaunchKernelGGL((k_conv_first_wgrad_m<TT, MBv>), dim3(CF_BLOCKS), dim3(256), 0, STREAM, B, Ci, H, W, C, x,
+                               (const TT*)dy, work);
+        };
+        const int mb = C <= 32 ? 2 : C <= 64 ? 4 : 8;
+        if (dtype == FEN_BF16) {
+            if (mb == 2) go(bf16{}, std::integral_constant<int, 2>{});
+            else if (mb == 4) go(bf16{}, std::integral_constant<int, 4>{});
+            else go(bf16{}, std::integral_constant<int, 8>{});
+        } else if (dtype == FEN_F16) {
+            if (mb == 2) go(f16{}, std::integral_constant<int, 2>{});
+            else if (mb == 4) go(f16{}, std::integral_constant<int, 4>{});
+            else go(f16{}, std::integral_constant<int, 8>{});
+        } else if (dtype == FEN_F32) {
+            if (mb == 2) go(float{}, std::integral_constant<int, 2>{});
+            else if (mb == 4) go(float{}, std::integral_constant<int, 4>{});
+            else go(float{}, std::integral_constant<int, 8>{});
+        } else {
+            return FEN_EINVAL;
+        }
+        FEN_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_conv_first_finalize, dim3(28), dim3(256), 0, STREAM, CF_BLOCKS * CFM_WAVES, Ci, C, work,
+                           dw, db, accumulate);
+        FEN_CHECK_LAUNCH();
+        return FEN_OK;
+    }
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_conv_first_wgrad<bf16>, dim3(CF_BLOCKS), dim3(256), 0, STREAM, B, Ci, H, W, C, x,
                            (const bf16*)dy, work);
