@@ -143,6 +143,137 @@ __global__ __launch_bounds__(256) void k_conv_first4(int B, int Ci, int H, int W
     }
 }
 
+// The same conv for 16-bit outputs on the f16 matrix cores: y^T[co][px] = W'[co][k] X[k][px]
+// with K = 27 taps + a bias column (x = 1) padded to 32, one v_mfma_f32_16x16x32_f16 per
+// (16 channels, 16 pixels).  fp32 accuracy is kept by splitting both operands into f16 hi + lo
+// parts and summing hi*hi + hi*lo + lo*hi (the dropped lo*lo term is ~2^-22 relative), three
+// MFMAs instead of 27 fp32 FMAs per output.  Blocks grid-stride over 16x16-pixel tiles: the
+// normalised, zero-padded 3 x 18 x 18 halo is staged in LDS; wave w takes tile rows 4w..4w+3,
+// lane = (pixel c16, k-slot group q).  The filter operand is built once per block in
+// registers.  Each lane's accumulator holds 4 consecutive channels of one pixel; a wave stages
+// its 16-pixel row in LDS and stores it as whole 16-byte lanes (the row is contiguous in NHWC),
+// and the next tile's halo loads are in flight during the current tile's MFMAs.  The fp32 form above issued
+// ~27 x 64 VALU FMAs per pixel (VALU bound at ~47 TFLOP/s on VGG conv1_1, 64 x 256^2).
+constexpr int CFM16_BLOCKS = 2048;
+template <typename T, int MB>
+__global__ __launch_bounds__(256) void k_conv_first_m16(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       T* __restrict__ y, const float* __restrict__ in_mean,
+                                                       const float* __restrict__ in_istd, float act) {
+    __shared__ float xs[3 * 18 * 18];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int q = lane >> 4, c16 = lane & 15;
+    const int th = (H + 15) >> 4, tw = (W + 15) >> 4;
+    const int ntiles = B * th * tw, K = Ci * 9;
+    // filter operand: lane holds W'[co = m*16 + c16][k = 8q + j], split hi / lo
+    f16x8 ahi[MB], alo[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+        const int co = m * 16 + c16;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 8 * q + j;
+            const float v = co < C ? (k < K ? w[(size_t)co * K + k] : (k == 27 ? bias[co] : 0.f)) : 0.f;
+            const f16 h = (f16)v;
+            ahi[m][j] = h;
+            alo[m][j] = (f16)(v - (float)h);
+        }
+    }
+    // activation operand: lane reads halo offset boff[j] (+ the pixel's), or the constant
+    int boff[8];
+    float bconst[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 8 * q + j;
+        boff[j] = k < K ? (k / 9) * 324 + ((k % 9) / 3) * 18 + (k % 3) : -1;
+        bconst[j] = k == 27 ? 1.f : 0.f;
+    }
+    // halo element i = tid + 256u: its channel is fixed per lane, so the normalisation is too;
+    // loads are unconditional (clamped addresses, out-of-image elements zeroed at the LDS write)
+    // so the prefetch stays in flight under the tile's MFMAs and stores
+    float xv[4], mu[4], is[4];
+    unsigned inb = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int ci = min((tid + u * 256) / 324, Ci - 1);
+        mu[u] = in_mean ? in_mean[ci] : 0.f;
+        is[u] = in_istd ? in_istd[ci] : 1.f;
+    }
+    auto load = [&](int t) {
+        const int b = t / (th * tw), tt = t - b * th * tw;
+        const int h0 = (tt / tw) << 4, w0 = (tt % tw) << 4;
+        inb = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = min(tid + u * 256, 971);
+            const int ci = i / 324, r = (i / 18) % 18, c = i % 18;
+            const int hh = h0 - 1 + r, ww = w0 - 1 + c;
+            if (ci < Ci && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) inb |= 1u << u;
+            const int hc = min(max(hh, 0), H - 1), wc = min(max(ww, 0), W - 1);
+            xv[u] = x[(((size_t)b * Ci + min(ci, Ci - 1)) * H + hc) * W + wc];
+        }
+    };
+    constexpr int CC = MB * 16, PS = CC * 2 + 16;            // output staging: pixel stride (bytes)
+    __shared__ __attribute__((aligned(16))) unsigned char ob[4][16 * PS];
+    unsigned char* obw = ob[wave];
+    if ((int)blockIdx.x < ntiles) load(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int b = t / (th * tw), tt = t - b * th * tw;
+        const int h0 = (tt / tw) << 4, w0 = (tt % tw) << 4;
+        __syncthreads();                                     // the previous tile's reads are done
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (tid + u * 256 < 972) xs[tid + u * 256] = (inb >> u) & 1 ? (xv[u] - mu[u]) * is[u] : 0.f;
+        __syncthreads();
+        if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);   // the next tile, in flight
+        // ragged edges: rows past H and columns past W recompute the last valid row / column, and
+        // their stores rewrite those bytes with the same values, so every wave issues the same
+        // unconditional stores on every tile (the next halo's wait then skips them: vmcnt(8))
+        const int nw = min(16, W - w0), rmax = H - 1 - h0;
+        const int cc = min(c16, nw - 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int r = min(wave * 4 + g, rmax), hh = h0 + r;
+            f16x8 bhi, blo;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = boff[j] >= 0 ? xs[boff[j] + r * 18 + cc] : bconst[j];
+                const f16 h = (f16)v;
+                bhi[j] = h;
+                blo[j] = (f16)(v - (float)h);
+            }
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[m], bhi, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[m], blo, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[m], bhi, acc, 0, 0, 0);
+                // lane holds D[co = m*16 + 4q + e][px = c16]: staged as the row's NHWC image
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = act >= 0.f && acc[e] < 0.f ? act * acc[e] : acc[e];
+                uint2 pk;
+                pk.x = (unsigned)__builtin_bit_cast(unsigned short, (T)v[0]) |
+                       ((unsigned)__builtin_bit_cast(unsigned short, (T)v[1]) << 16);
+                pk.y = (unsigned)__builtin_bit_cast(unsigned short, (T)v[2]) |
+                       ((unsigned)__builtin_bit_cast(unsigned short, (T)v[3]) << 16);
+                *(uint2*)(obw + c16 * PS + (m * 16 + 4 * q) * 2) = pk;
+            }
+            // the row's outputs are contiguous in y (C = CC): 16-byte lanes, whole lines
+            char* o = (char*)(y + (((size_t)b * H + hh) * W + w0) * CC);
+            constexpr int CPP = CC / 8;                      // 16-byte chunks per pixel
+#pragma unroll
+            for (int s = 0; s < (16 * CPP + 63) / 64; ++s) {
+                const int i = lane + 64 * s;
+                if (16 * CPP >= 64 * (s + 1) || i < 16 * CPP) {
+                    const int px = i / CPP, ch = i % CPP, pc = min(px, nw - 1);
+                    *(uint4*)(o + (size_t)(pc * CPP + ch) * 16) = *(const uint4*)(obw + px * PS + ch * 16);
+                }
+            }
+        }
+    }
+}
+
 // conv_first weight gradient dw[co][ci][kh][kw] = sum_px dy[px][co] * x[ci][px + (kh-1, kw-1)]
 // (+ db = sum_px dy).  Persistent blocks walk 16x16-pixel tiles in a fixed order (deterministic
 // per-block partials): the tile's zero-padded 3 x 18 x 18 input halo is staged in LDS; wave w
@@ -1160,6 +1291,34 @@ extern "C" int fen_conv_first_fwd_ex(int dtype, int B, int Ci, int H, int W, int
     if (!x || !w || !bias || !y || B <= 0 || Ci <= 0 || Ci > 3 || C % 8 || C > 128) return FEN_EINVAL;
     const size_t n = (size_t)B * H * W * (C / 8);
     const size_t lds = (size_t)Ci * 9 * C * sizeof(float);
+    static int m16 = -1;                                 // FEN_CF_M16=0: the VALU forms (A/B runs)
+    if (m16 < 0) {
+        const char* e = getenv("FEN_CF_M16");
+        m16 = e ? atoi(e) : 1;
+    }
+    if (m16 && (dtype == FEN_BF16 || dtype == FEN_F16) && (C == 16 || C == 32 || C == 64 || C == 128)) {
+        const int ntiles = B * ((H + 15) >> 4) * ((W + 15) >> 4);
+        const unsigned nb = (unsigned)std::min(ntiles, CFM16_BLOCKS);
+#define CFM16_LAUNCH(TT, MBv)                                                                                   \
+    hipLaunchKernelGGL((k_conv_first_m16<TT, MBv>), dim3(nb), dim3(256), 0, STREAM, B, Ci, H, W, C, x, w, bias, \
+                       (TT*)y, in_mean, in_istd, act)
+#define CFM16_MB(TT)                      \
+    switch (C / 16) {                     \
+        case 1: CFM16_LAUNCH(TT, 1); break; \
+        case 2: CFM16_LAUNCH(TT, 2); break; \
+        case 4: CFM16_LAUNCH(TT, 4); break; \
+        default: CFM16_LAUNCH(TT, 8); break; \
+    }
+        if (dtype == FEN_BF16) {
+            CFM16_MB(bf16);
+        } else {
+            CFM16_MB(f16);
+        }
+#undef CFM16_MB
+#undef CFM16_LAUNCH
+        FEN_CHECK_LAUNCH();
+        return FEN_OK;
+    }
     if (W % 4 == 0) {
         const unsigned nb = (unsigned)((size_t)B * ((H + 1) / 2) * ((W + CF4_TW - 1) / CF4_TW));
         const size_t lds4 = lds + (size_t)Ci * 4 * (CF4_TW + 2) * sizeof(float);

@@ -172,6 +172,29 @@ def test_conv_first(dtype, B, H, W):
     assert (nchw(y) - ref).abs().max() <= _tol(dtype, ref)
 
 
+@pytest.mark.parametrize("dtype", DT_FWD)
+@pytest.mark.parametrize("B,H,W,C", [(2, 20, 24, 16), (3, 17, 19, 48), (2, 33, 40, 64), (1, 16, 32, 128),
+                                     (70, 64, 64, 64)])
+def test_conv_first_ex(dtype, B, H, W, C):
+    """fen_conv_first_fwd_ex with the VGG input normalisation and LeakyReLU(0.2): the split-f16
+    matrix-core form for 16-bit outputs (C % 16 == 0, ragged tiles, grid-stride at B = 70)."""
+    torch.manual_seed(4)
+    x = torch.rand(B, 3, H, W)
+    w = torch.randn(C, 3, 3, 3) * 0.2
+    b = torch.randn(C) * 0.1
+    mean, std = torch.tensor([0.485, 0.456, 0.406]), torch.tensor([0.229, 0.224, 0.225])
+    ref = F.leaky_relu(F.conv2d((x - mean.view(1, 3, 1, 1)) / std.view(1, 3, 1, 1), w, b, padding=1), 0.2)
+    ctx = _ctx(dtype)
+    from src.hip.program import ptr
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    md, isd = mean.to(DEV), (1.0 / std).to(DEV)
+    y = ctx.alloc((B, H, W, C))
+    ctx.emit("cf", ctx.lib.fen_conv_first_fwd_ex, ctx.code, B, 3, H, W, C, ptr(xd), ptr(wd), ptr(bd), ptr(md),
+             ptr(isd), 0.2, ptr(y))
+    torch.cuda.synchronize()
+    assert (nchw(y) - ref).abs().max() <= _tol(dtype, ref)
+
+
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("B,H,W,C", [(2, 20, 24, 64), (1, 16, 16, 64), (3, 37, 19, 64), (4, 64, 64, 64),
                                      (1, 16, 32, 128)])
