@@ -376,7 +376,6 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(int B, int Ci, int H, 
 // C output channels (MB 16-row blocks) and both 16-column k blocks; the next tile's halo
 // and dy are loaded into registers while the current one computes.  Each wave writes its own
 // partial rows (4 per block), summed in fixed order by k_conv_first_finalize.
-constexpr int CFM_WAVES = 4;
 template <typename T, int MB>
 __global__ __launch_bounds__(256) void k_conv_first_wgrad_m(int B, int Ci, int H, int W, int C,
                                                             const float* __restrict__ x, const T* __restrict__ dy,
@@ -451,8 +450,10 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad_m(int B, int Ci, int H
                     acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], bv[nb], acc[m][nb], 0, 0, 0);
         }
     }
-    // lane holds D[co = m*16 + 4q + r][k = nb*16 + c16]; this wave's partial rows
-    float* pw = part + (size_t)(blockIdx.x * CFM_WAVES + wave) * 28 * C;
+    // lane holds D[co = m*16 + 4q + r][k = nb*16 + c16]: the 4 waves' sums meet in LDS (over
+    // ys, 448 * CC of its 512 * CC bytes) and the block writes one partial row set
+    __syncthreads();
+    float* red = (float*)ys;                                 // [wave][28][CC]
 #pragma unroll
     for (int m = 0; m < MB; ++m)
 #pragma unroll
@@ -460,15 +461,22 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad_m(int B, int Ci, int H
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int k = nb * 16 + c16, co = m * 16 + 4 * q + r;
-                if (k < 28 && co < C) pw[(size_t)k * C + co] = acc[m][nb][r];
+                if (k < 28) red[(wave * 28 + k) * CC + co] = acc[m][nb][r];
             }
+    __syncthreads();
+    float* pb = part + (size_t)blockIdx.x * 28 * C;
+    for (int i = tid; i < 28 * C; i += 256) {
+        const int k = i / C, co = i - k * C;
+        const float* rr = red + k * CC + co;
+        pb[i] = (rr[0] + rr[28 * CC]) + (rr[56 * CC] + rr[84 * CC]);
+    }
 }
 
 // block = one of the 28 rows k (27 weights + bias), 256 threads: thread (co, quarter) sums every
 // 4th partial block (coalesced over co), fixed-order LDS combine -- deterministic
-__global__ __launch_bounds__(256) void k_conv_first_finalize(int nb, int Ci, int C, const float* part, float* dw,
-                                                             float* db, int accum) {
-    __shared__ float red[4][128];
+__global__ __launch_bounds__(1024) void k_conv_first_finalize(int nb, int Ci, int C, const float* part, float* dw,
+                                                              float* db, int accum) {
+    __shared__ float red[16][64];
     const int k = blockIdx.x;
     if (k >= Ci * 9 && k != 27) return;
     for (int c0 = 0; c0 < C; c0 += 64) {
@@ -476,12 +484,14 @@ __global__ __launch_bounds__(256) void k_conv_first_finalize(int nb, int Ci, int
         float a = 0.f;
         if (co < C) {
 #pragma unroll 8
-            for (int r = qr; r < nb; r += 4) a += part[((size_t)r * 28 + k) * C + co];
+            for (int r = qr; r < nb; r += 16) a += part[((size_t)r * 28 + k) * C + co];
         }
         red[qr][threadIdx.x & 63] = a;
         __syncthreads();
         if (threadIdx.x < 64 && co < C) {
-            const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) s += red[j][threadIdx.x];
             if (k == 27) {
                 if (db) db[co] = accum ? db[co] + s : s;
             } else {
@@ -1357,7 +1367,7 @@ extern "C" int fen_conv_first_fwd(int dtype, int B, int Ci, int H, int W, int C,
 }
 
 extern "C" size_t fen_conv_first_work_floats(int B, int Ci, int H, int W, int C) {
-    return (size_t)CF_BLOCKS * CFM_WAVES * 28 * C;   // the MFMA form: one partial row set per wave
+    return (size_t)CF_BLOCKS * 28 * C;               // one partial row set per block
 }
 
 extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const float* x, const void* dy,
@@ -1388,7 +1398,7 @@ extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int 
             return FEN_EINVAL;
         }
         FEN_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_conv_first_finalize, dim3(28), dim3(256), 0, STREAM, CF_BLOCKS * CFM_WAVES, Ci, C, work,
+        hipLaunchKernelGGL(k_conv_first_finalize, dim3(28), dim3(1024), 0, STREAM, CF_BLOCKS, Ci, C, work,
                            dw, db, accumulate);
         FEN_CHECK_LAUNCH();
         return FEN_OK;
@@ -1405,7 +1415,7 @@ extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int 
     else
         return FEN_EINVAL;
     FEN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_conv_first_finalize, dim3(28), dim3(256), 0, STREAM, CF_BLOCKS, Ci, C, work, dw, db,
+    hipLaunchKernelGGL(k_conv_first_finalize, dim3(28), dim3(1024), 0, STREAM, CF_BLOCKS, Ci, C, work, dw, db,
                        accumulate);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
