@@ -194,6 +194,12 @@ struct RdArgs {
     const void* dot_t;         // t of the next RCAB backward (with d.part)
     // GC: the group conv (d.w2 / d.b2 = its pack and bias, d.t = its output) + this residual
     const void* gres;
+    // SEB: the SE backward folded in -- d.x = dy (the halo source), d.pp = the DOT partials
+    // [B][tiles][64], A.se_s / d.pmean / d.phid the saved s / mean / hid, d.pfc1 / d.pfc2 the
+    // FC weights, d.xo = dt out; FC weight-gradient rows per image
+    const float* se_s;
+    float* se_dw1p;
+    float* se_dw2p;
 };
 
 // ------------------------------------------------------------------------------------
@@ -205,15 +211,20 @@ struct RdArgs {
 // PReLU derivative at the saved z1 (its 18x18 halo DMA'd into the a1 image, then overwritten
 // in place by dz1; slope-gradient partials over the tile interior), dx = conv1^T(dz1) +
 // dy (+ the tile sums of dx * t_next for the next SE backward).
+// SEB (with BWD): the SE backward and its apply folded into the input path -- every block
+// recomputes its tiles' images' SE backward in the prologue (k_se_bwd_fused's arithmetic and
+// order) and the DMA'd dy halo becomes dt = dy * rs * s + g in place (zero outside the image),
+// the tile's own dt going out for conv2's weight gradient: no separate dt pass over HBM.
 // GC (DEFER, not TRAIN): a ResidualGroup's end -- the last RCAB's gate and scaled residual
 // applied while building the input (straight into the a1 image, 18x18), then the group conv
 // (one 3x3 conv on the conv2 path) + bias + the group's residual (blocks.py:185-189): the
 // chain end's separate gate/apply launch and its tensor round trip disappear.
-template <typename T, bool DEFER, bool TRAIN, bool BWD = false, bool GC = false>
+template <typename T, bool DEFER, bool TRAIN, bool BWD = false, bool GC = false, bool SEB = false>
 __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     const fen_rcab_deferred_desc& d = A.d;
     static_assert(!(BWD && (DEFER || TRAIN)), "the backward form is its own mode");
     static_assert(!GC || (DEFER && !TRAIN && !BWD), "the group end is a deferred single conv");
+    static_assert(!SEB || BWD, "the SE backward folds into the backward form");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* xh = smem + O_XH;
     char* eh = smem + O_EH;
@@ -271,7 +282,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     };
     // x halo (20x20, hcol key) + edge copy (halo columns 16..19, row key) by LDS-DMA; deferred
     // mode DMAs x_{j-1} without the edge copy (the combine writes both from registers)
-    constexpr int NDMA = DEFER ? XH_DMA : XH_DMA + EH_DMA;
+    constexpr int NDMA = (DEFER || SEB) ? XH_DMA : XH_DMA + EH_DMA;
     auto issue_halo = [&](int t) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
@@ -343,7 +354,10 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     auto combine_halo = [&](int t, int k, const uint4 (&tv)[HPT]) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-        const float* sv = gate + (k % MAXG) * 64;
+        // this thread's 8 channels (c = tid & 7 for every chunk): the gate in registers once
+        const float* sv = gate + (k % MAXG) * 64 + (tid & 7) * 8;
+        const float4 s0 = *(const float4*)sv, s1 = *(const float4*)(sv + 4);
+        const float s8[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
         int tq = tid;
         asm volatile("" : "+v"(tq));   // opaque: per-chunk addresses are not hoisted out of the tile loop
 #pragma unroll
@@ -352,8 +366,6 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
             const int i = tq + 512 * j, p = i >> 3, c = i & 7;
             const int hr = p / XW, hc = p - hr * XW;
             char* px = xh + hr * (XW * 128) + hcol(hc, c);
-            const float4 s0 = *(const float4*)(sv + c * 8), s1 = *(const float4*)(sv + c * 8 + 4);
-            const float s8[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
             float xf[8], tf[8], y[8];
             unpack16<T>(*(const uint4*)px, xf);
             unpack16<T>(tv[j], tf);
@@ -372,18 +384,97 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), ors, off, 0, 0);
         }
     };
+    // SEB: dt = dy * rs * s + g over the DMA'd dy halo image in place (+ the edge copy; zero
+    // outside the image), the tile's own dt out (nch buffer stores per wave, as combine_halo)
+    auto se_halo = [&](int t, int k) {
+#ifdef FEN_SEB_NOHALO
+        return;                                              // timing diagnostic only (wrong results)
+#endif
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const float rs = d.res_scale;
+        // this thread's 8 channels (c = tid & 7 for every chunk): s and g in registers once
+        float s8[8], g8[8];
+        {
+            const float* sv = gate + (4 + 2 * k) * 64 + (tid & 7) * 8;
+            const float4 s0 = *(const float4*)sv, s1 = *(const float4*)(sv + 4);
+            const float4 g0 = *(const float4*)(sv + 64), g1 = *(const float4*)(sv + 68);
+            s8[0] = s0.x, s8[1] = s0.y, s8[2] = s0.z, s8[3] = s0.w, s8[4] = s1.x, s8[5] = s1.y, s8[6] = s1.z, s8[7] = s1.w;
+            g8[0] = g0.x, g8[1] = g0.y, g8[2] = g0.z, g8[3] = g0.w, g8[4] = g1.x, g8[5] = g1.y, g8[6] = g1.z, g8[7] = g1.w;
+        }
+        int tq = tid;
+        asm volatile("" : "+v"(tq));
+#pragma unroll
+        for (int j = 0; j < HPT; ++j) {
+            if (j == HPT - 1 && wave >= 2) break;
+            const int i = tq + 512 * j, p = i >> 3, c = i & 7;
+            const int hr = p / XW, hc = p - hr * XW;
+            const int gh = h0 - 2 + hr, gw = w0 - 2 + hc;
+            const bool in = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            char* px = xh + hr * (XW * 128) + hcol(hc, c);
+            float xf[8], y[8];
+            unpack16<T>(*(const uint4*)px, xf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = in ? xf[e] * rs * s8[e] + g8[e] : 0.f;
+            const uint4 v = pack16<T>(y);
+            *(uint4*)px = v;
+            if (hc >= 16) *(uint4*)(eh + (hr * 4 + (hc - 16)) * 128 + ekey(hr, c)) = v;
+            const bool own = (unsigned)(hr - 2) < 16u && (unsigned)(hc - 2) < 16u;
+            const int off = own ? (((b * H + gh) * W + gw) * 64 + c * 8) * 2 : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), ors, off, 0, 0);
+        }
+    };
 
+    // the per-channel constants, loaded before the start-up DMA and written to LDS after its
+    // wait (read right after the DMA issue, their use made the compiler wait for the DMA too)
+    float cb1 = 0.f, cal = 0.f, cb2 = 0.f;
+    if (tid < 64) {
+        if (!BWD) cb1 = d.b1[tid];
+        if (!GC) cal = d.alpha[tid];   // (the group conv has no PReLU: d.alpha unset)
+        if (!BWD) cb2 = d.b2[tid];
+    }
+    // DEFER: the gate chain's operands (the SE weights, the first 16 tile partials of this
+    // wave's first tile) before the start-up DMA, so they return first
+    float f1e[2] = {0.f, 0.f}, f2e[2] = {0.f, 0.f}, v0e[16];
+    if constexpr (DEFER) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int i = tid + r * 512, c = i >> 4, j = i & 15;
+            f1e[r] = i < d.Cr * 64 ? d.pfc1[i] : 0.f;
+            f2e[r] = j < d.Cr ? d.pfc2[c * d.Cr + j] : 0.f;
+        }
+        const int b = (slot + (wave < nmine ? wave : 0) * nslot) / tpi;
+        const float* pp = d.pp + (size_t)b * tpi * 64 + lane;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v0e[u] = pp[(size_t)(u < tpi ? u : tpi - 1) * 64];
+    }
+    // SEB: the SE backward's operands of this wave's tile (wave k < nmine <= 6 handles tile k)
+    // go out before the start-up DMA, so they return first (vector memory returns in order)
+    float w2v[16], w1v[16], hv[16], sp[16], sv = 0.f, mv = 0.f;
+    if constexpr (SEB) {
+        if (wave < nmine) {
+            const int Cr = d.Cr, b = (slot + wave * nslot) / tpi;
+            const float* pp = d.pp + (size_t)b * tpi * 64 + lane;
+            // in order of use: the compiler's vmcnt for a load counts only its own later loads,
+            // so the last ~16 (w1v, mv: used after the wave sums) also wait for the DMA behind
+#pragma unroll
+            for (int u = 0; u < 16; ++u) sp[u] = pp[(size_t)(u < tpi ? u : tpi - 1) * 64];   // (unconditional: no early wait)
+            sv = A.se_s[(size_t)b * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w2v[j] = d.pfc2[lane * Cr + (j < Cr ? j : Cr - 1)];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) hv[j] = d.phid[(size_t)b * Cr + (j < Cr ? j : Cr - 1)];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w1v[j] = d.pfc1[(j < Cr ? j : Cr - 1) * 64 + lane];
+            mv = d.pmean[(size_t)b * 64 + lane];
+        }
+    }
     // ---- start-up: first taps and the first halo go out before anything else waits on memory
     uint4 tv0[HPT];
     issue_taps(0);
     issue_halo(slot);
     if constexpr (BWD) issue_z1(slot);
     if constexpr (DEFER) load_t(slot, tv0);
-    if (tid < 64) {
-        cst[tid] = BWD ? 0.f : d.b1[tid];
-        cst[64 + tid] = GC ? 0.f : d.alpha[tid];   // (the group conv has no PReLU: d.alpha unset)
-        cst[128 + tid] = BWD ? 0.f : d.b2[tid];
-    }
     if constexpr (DEFER) {
         // the gates of this block's tiles (<= MAXG): wave w handles tiles w, w + 8; lane c sums
         // the image's tile partials in tile order (every block computes identical values), then
@@ -393,16 +484,12 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
         // the first 16 tile partials of this wave's first tile go out before the SE weights'
         // round trip through LDS, so the two latencies overlap (one round trip, not two)
         float v0[16];
-        if (wave < nmine) {
-            const int b = (slot + wave * nslot) / tpi;
-            const float* pp = d.pp + (size_t)b * tpi * 64 + lane;
 #pragma unroll
-            for (int u = 0; u < 16; ++u) v0[u] = u < tpi ? pp[(size_t)u * 64] : 0.f;
-        }
-        for (int i = tid; i < 1024; i += 512) {
-            fcs[i] = i < Cr * 64 ? d.pfc1[i] : 0.f;          // [16][64], zero-padded hidden units
-            const int c = i >> 4, j = i & 15;
-            fcs[1024 + i] = j < Cr ? d.pfc2[c * Cr + j] : 0.f;   // [64][16]
+        for (int u = 0; u < 16; ++u) v0[u] = u < tpi ? v0e[u] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            fcs[tid + r * 512] = f1e[r];
+            fcs[1024 + tid + r * 512] = f2e[r];
         }
         __syncthreads();
         float* ws = (float*)(smem + O_PWS) + wave * 128;
@@ -454,14 +541,83 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
             }
         }
     }
+    if constexpr (SEB) {
+        // the SE backward of each of this block's tiles' images (<= 6 tiles: gate rows 4..15;
+        // rows 0..3 hold the slope partials): wave w handles tiles w (< 6), lane = channel c,
+        // in k_se_bwd_fused's order -- quarter sums over partials q, q+4, ..., their fixed-order
+        // combine, FC2^T by wave sums, FC1^T in hidden-unit order
+        // (nmine <= 6: wave k handles tile k; its operands were loaded before the start-up DMA)
+        const int Cr = d.Cr;
+        if (wave < nmine) {
+            const int k = wave;
+            const int t = slot + k * nslot, b = t / tpi;
+            const float* pp = d.pp + (size_t)b * tpi * 64 + lane;
+            // an opaque zero: the first sums cannot be hoisted above the start-up DMA (their
+            // wait would then hold the DMA issue back by a memory round trip)
+            float z0 = 0.f;
+            asm volatile("" : "+v"(z0));
+            float a4[4] = {z0, z0, z0, z0};
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (u < tpi) a4[u & 3] += sp[u];
+            for (int i0 = 16; i0 < tpi; i0 += 16) {
+                float v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = i0 + u < tpi ? pp[(size_t)(i0 + u) * 64] : 0.f;
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (i0 + u < tpi) a4[u & 3] += v[u];
+            }
+            const float a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+            const float dz = a * d.res_scale * sv * (1.f - sv);
+            float dh[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                dh[j] = 0.f;
+                dh[j] += w2v[j] * dz;
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) dh[j] += __shfl_xor(dh[j], o, 64);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) dh[j] = j < Cr && hv[j] > 0.f ? dh[j] : 0.f;
+            float ga = 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (j < Cr) ga += w1v[j] * dh[j];
+            gate[(4 + 2 * k) * 64 + lane] = sv;
+            gate[(5 + 2 * k) * 64 + lane] = ga * d.inv_hw;
+            if (t % tpi == 0) {                              // the FC weight-gradient rows, once per image
+                float* w2p = A.se_dw2p + (size_t)b * 64 * Cr;
+                float* w1p = A.se_dw1p + (size_t)b * 64 * Cr;
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (j < Cr) {
+                        w2p[lane * Cr + j] = dz * hv[j];
+                        w1p[j * 64 + lane] = dh[j] * mv;
+                    }
+            }
+        }
+    }
     RSTAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid < 64) {
+        cst[tid] = cb1;
+        cst[64 + tid] = cal;
+        cst[128 + tid] = cb2;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if constexpr (DEFER) {
         combine_halo(slot, 0, tv0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                         // a1 scratch and the halo image
+    }
+    if constexpr (SEB) {
+        se_halo(slot, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
     RSTAMP(1);
 
@@ -579,7 +735,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     // output stores this wave issues after the next tile's first taps (t and, for wave 0, the
     // tile's partial row; deferred: + the x_j chunks): the phase-0 wait leaves them in flight.
     // (Without DEFER the next halo's DMA is older than those taps: waited for as well.)
-    const int nst_tail = 4 + ((wave == 0 && d.part) ? 1 : 0) + (DEFER ? nch : 0);
+    const int nst_tail = 4 + ((wave == 0 && d.part) ? 1 : 0) + ((DEFER || SEB) ? nch : 0);
 
 #pragma unroll 1
     for (int k = 0; k < nmine; ++k) {
@@ -867,6 +1023,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
         if constexpr (DEFER) {
             if (next) combine_halo(t + nslot, k + 1, tv);
         }
+        if constexpr (SEB) {
+            if (next) se_halo(t + nslot, k + 1);
+        }
         if (k < 2) RSTAMP(15 + k * 14);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -880,15 +1039,15 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
 
 int g_cus = 0;
 
-template <typename T, bool DEFER, bool TRAIN, bool BWD = false, bool GC = false>
+template <typename T, bool DEFER, bool TRAIN, bool BWD = false, bool GC = false, bool SEB = false>
 void launch_rd(const RdArgs& a, int grid, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_rcab_d<T, DEFER, TRAIN, BWD, GC>,
+        (void)hipFuncSetAttribute((const void*)k_rcab_d<T, DEFER, TRAIN, BWD, GC, SEB>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, RD_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL((k_rcab_d<T, DEFER, TRAIN, BWD, GC>), dim3(grid), dim3(512), RD_LDS, s, a);
+    hipLaunchKernelGGL((k_rcab_d<T, DEFER, TRAIN, BWD, GC, SEB>), dim3(grid), dim3(512), RD_LDS, s, a);
 }
 
 template <typename T>
@@ -941,17 +1100,34 @@ extern "C" int fen_rcab_deferred(const fen_rcab_deferred_desc* d, void* stream) 
     return FEN_OK;
 }
 
+extern "C" int fen_rcab_bwd_se_supported(int dtype, int B, int H, int W, int C, int Cr) {
+    if (!fen_rcab_deferred_supported(dtype, B, H, W, C, Cr)) return 0;
+    const int ncu = rd_num_cus();
+    const int ntiles = B * (H / 16) * (W / 16);
+    const int grid = ntiles < ncu ? ntiles : ncu;
+    return (ntiles + grid - 1) / grid <= 6 && (H / 16) * (W / 16) <= 64 ? 1 : 0;
+}
+
 extern "C" int fen_rcab_bwd(const fen_rcab_bwd_desc* b, void* stream) {
     if (!b || !b->dt || !b->w2t || !b->w1t || !b->z1 || !b->alpha || !b->dz1 || !b->dalpha_part || !b->dx ||
         !b->dy)
         return FEN_EINVAL;
     if ((b->dot_t != nullptr) != (b->dot_part != nullptr)) return FEN_EINVAL;
-    if (!fen_rcab_deferred_supported(b->dtype, b->B, b->H, b->W, b->C, 16)) return FEN_EUNSUPPORTED;
+    const bool seb = b->se_part != nullptr;
+    if (seb && (!b->se_s || !b->se_mean || !b->se_hid || !b->se_w1 || !b->se_w2 || !b->se_dw1p || !b->se_dw2p))
+        return FEN_EINVAL;
+    const int Cr = seb ? b->se_Cr : 16;
+    if (!fen_rcab_deferred_supported(b->dtype, b->B, b->H, b->W, b->C, Cr)) return FEN_EUNSUPPORTED;
+    // SEB: <= 6 tiles per block (gate rows 4..15 hold their s, g), <= 64 tiles per image
+    if (seb && !fen_rcab_bwd_se_supported(b->dtype, b->B, b->H, b->W, b->C, Cr)) return FEN_EUNSUPPORTED;
+    const int ncu = rd_num_cus();
+    const int ntiles = b->B * (b->H / 16) * (b->W / 16);
+    const int grid = ntiles < ncu ? ntiles : ncu;
     RdArgs a{};
     fen_rcab_deferred_desc& d = a.d;
     d.dtype = b->dtype;
-    d.B = b->B, d.H = b->H, d.W = b->W, d.C = b->C, d.Cr = 16;
-    d.x = b->dt;
+    d.B = b->B, d.H = b->H, d.W = b->W, d.C = b->C, d.Cr = Cr;
+    d.x = seb ? b->dy : b->dt;                       // SEB: dt is built from dy's halo (and written)
     d.w1 = b->w2t;
     d.w2 = b->w1t;
     d.alpha = b->alpha;
@@ -962,12 +1138,27 @@ extern "C" int fen_rcab_bwd(const fen_rcab_bwd_desc* b, void* stream) {
     a.dpart = b->dalpha_part;
     a.dy = b->dy;
     a.dot_t = b->dot_t;
-    const int ncu = rd_num_cus();
-    const int ntiles = b->B * (b->H / 16) * (b->W / 16);
-    const int grid = ntiles < ncu ? ntiles : ncu;
+    if (seb) {
+        d.pp = b->se_part;
+        d.pfc1 = b->se_w1;
+        d.pfc2 = b->se_w2;
+        d.res_scale = b->se_res_scale;
+        d.inv_hw = 1.0f / (float)(b->H * b->W);
+        d.pmean = (float*)b->se_mean;
+        d.phid = (float*)b->se_hid;
+        d.xo = const_cast<void*>(b->dt);             // (an output in this mode)
+        a.se_s = b->se_s;
+        a.se_dw1p = b->se_dw1p;
+        a.se_dw2p = b->se_dw2p;
+    }
     hipStream_t s = (hipStream_t)stream;
-    if (b->dtype == FEN_F16) launch_rd<f16, false, false, true>(a, grid, s);
-    else launch_rd<bf16, false, false, true>(a, grid, s);
+    if (seb) {
+        if (b->dtype == FEN_F16) launch_rd<f16, false, false, true, false, true>(a, grid, s);
+        else launch_rd<bf16, false, false, true, false, true>(a, grid, s);
+    } else {
+        if (b->dtype == FEN_F16) launch_rd<f16, false, false, true>(a, grid, s);
+        else launch_rd<bf16, false, false, true>(a, grid, s);
+    }
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -62,6 +62,9 @@ class RcabBwdDesc(Structure):
         ("dt", c_void_p), ("w2t", c_void_p), ("z1", c_void_p), ("alpha", c_void_p), ("w1t", c_void_p),
         ("dy", c_void_p), ("dz1", c_void_p), ("dalpha_part", c_void_p), ("dx", c_void_p),
         ("dot_t", c_void_p), ("dot_part", c_void_p),
+        ("se_part", c_void_p), ("se_s", c_void_p), ("se_mean", c_void_p), ("se_hid", c_void_p),
+        ("se_w1", c_void_p), ("se_w2", c_void_p), ("se_dw1p", c_void_p), ("se_dw2p", c_void_p),
+        ("se_res_scale", c_float), ("se_Cr", c_int),
     ]
 
 
@@ -80,6 +83,7 @@ _SIGS = {
     "fen_wgrad_multi_work_floats": (c_size_t, [c_int, c_void_p]),
     "fen_wgrad3x3_multi": (c_int, [c_int, c_void_p, c_void_p]),
     "fen_rcab_deferred_supported": (c_int, [c_int] * 6),
+    "fen_rcab_bwd_se_supported": (c_int, [c_int] * 6),
     "fen_rcab_deferred": (c_int, [POINTER(RcabDeferredDesc), c_void_p]),
     "fen_rcab_bwd": (c_int, [POINTER(RcabBwdDesc), c_void_p]),
     "fen_rcab_group_end": (c_int, [POINTER(RcabDeferredDesc)] + [c_void_p] * 5),

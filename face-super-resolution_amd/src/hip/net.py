@@ -188,6 +188,10 @@ RCAB_BWD_FUSED = os.environ.get("FEN_RCAB_BWD", "fused") != "pair"
 # sum(dy * t) of the SE backward from the producing dgrad's epilogue (FEN_EPI_DOT) instead of
 # a fen_pool_dot pass over dy and t (FEN_SE_DOT=pass: the separate pass)
 DOT_FUSED = os.environ.get("FEN_SE_DOT", "fused") != "pass"
+# the SE backward folded into the fused RCAB backward launch where its envelope holds (the DOT
+# partials from dy's producer, <= 6 tiles per CU): 'fold' (default) or a separate
+# fen_se_bwd_fused launch (FEN_SE_IN_BWD=launch)
+SE_IN_BWD = os.environ.get("FEN_SE_IN_BWD", "fold") != "launch"
 WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
 
 
@@ -483,7 +487,8 @@ class Backward:
         s, ctx, Wt, p, G = self.s, self.ctx, self.Wt, self.Wt.p, self.G
         B, H, W, C = dy.shape
         HW = H * W
-        if self._dot is not None:
+        dot_part = self._dot is not None
+        if dot_part:
             part, npart = self._dot          # sum dy*t per tile, from dy's producer
             self._dot = None
         else:
@@ -500,7 +505,13 @@ class Backward:
         dt = ctx.scratch(f"bw_dt{rot}", dy.shape)
         se_args = (npart, 1.0 / HW, s.res_scale, ptr(part), ptr(sv["mean"]), ptr(sv["hid"]), ptr(sv["s"]),
                    ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]))
-        if SE_BWD_FUSED and C <= 64 and npart <= 64 and C * s.Cr <= 4096:
+        fused = (RCAB_BWD_FUSED and not extra_res and ctx.code != L.F32
+                 and ctx.lib.fen_rcab_deferred_supported(ctx.code, B, H, W, C, s.Cr))
+        # the SE backward folded into the fused launch (dt built on its dy halo in LDS)
+        seb = fused and SE_IN_BWD and dot_part and ctx.lib.fen_rcab_bwd_se_supported(ctx.code, B, H, W, C, s.Cr)
+        if seb:
+            pass                             # fen_rcab_bwd below writes dt, dw1p, dw2p
+        elif SE_BWD_FUSED and C <= 64 and npart <= 64 and C * s.Cr <= 4096:
             # SE backward + dt in one launch (same arithmetic as the pair below)
             ctx.emit("se_bwd_fused", ctx.lib.fen_se_bwd_fused, ctx.code, B, HW, C, s.Cr, *se_args, ptr(dy), None,
                      ptr(dw1p), ptr(dw2p), ptr(dt))
@@ -516,13 +527,16 @@ class Backward:
         T = tiles(H, W)
         dal = ctx.scratch("bw_dal" + pre, (B * T, C), torch.float32)
         dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
-        if (RCAB_BWD_FUSED and not extra_res and ctx.code != L.F32
-                and ctx.lib.fen_rcab_deferred_supported(ctx.code, B, H, W, C, s.Cr)):
+        if fused:
             d = L.RcabBwdDesc()
             d.dtype, d.B, d.H, d.W, d.C = ctx.code, B, H, W, C
             d.dt, d.w2t, d.z1 = ptr(dt), ptr(Wt.packed(pre + "conv2", 2)), ptr(sv["z1"])
             d.alpha, d.w1t, d.dy = ptr(p[pre + "prelu.weight"]), ptr(Wt.packed(pre + "conv1", 2)), ptr(dy)
             d.dz1, d.dalpha_part, d.dx = ptr(dz1), ptr(dal), ptr(dx)
+            if seb:
+                d.se_part, d.se_s, d.se_mean, d.se_hid = ptr(part), ptr(sv["s"]), ptr(sv["mean"]), ptr(sv["hid"])
+                d.se_w1, d.se_w2 = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
+                d.se_dw1p, d.se_dw2p, d.se_res_scale, d.se_Cr = ptr(dw1p), ptr(dw2p), s.res_scale, s.Cr
             dk = self._dot_conv(t_next, B, H, W, C)
             if dk:
                 d.dot_t, d.dot_part = ptr(dk["pre_in"]), ptr(dk["part"])

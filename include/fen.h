@@ -243,8 +243,25 @@ typedef struct {
     void* dx;                  /* out NHWC                                                      */
     const void* dot_t;         /* NULL or NHWC: the next RCAB's t (with dot_part)                */
     float* dot_part;           /* NULL or out [B*tiles][64]                                     */
+    /* The SE backward folded in (se_part != NULL; else these are ignored): dt is then an OUTPUT,
+     * dt = dy * se_res_scale * s + g with fen_se_bwd_fused's arithmetic (g from the FC chain
+     * over se_part), built on each tile's dy halo in LDS; the FC weight-gradient rows go to
+     * se_dw1p / se_dw2p exactly as fen_se_bwd_fused writes them.  <= 6 tiles per CU and <= 64
+     * tiles per image.  Replaces fen_se_bwd_fused + this launch (blocks.py:88-92,150-153).    */
+    const float* se_part;      /* sum over each tile of dy * t [B][tiles][64] (nparts = tiles)  */
+    const float* se_s;         /* saved gate s [B][64]                                           */
+    const float* se_mean;      /* saved pooled mean [B][64]                                      */
+    const float* se_hid;       /* saved hidden activations [B][Cr]                               */
+    const float* se_w1;        /* channel_attention.fc.0.weight [Cr][64]                         */
+    const float* se_w2;        /* channel_attention.fc.2.weight [64][Cr]                         */
+    float* se_dw1p;            /* out [B][Cr*64]                                                 */
+    float* se_dw2p;            /* out [B][64*Cr]                                                 */
+    float se_res_scale;        /* 0.2                                                            */
+    int se_Cr;                 /* <= 16                                                          */
 } fen_rcab_bwd_desc;
 int fen_rcab_bwd(const fen_rcab_bwd_desc* d, void* stream);
+/* 1 when fen_rcab_bwd takes the folded SE backward (se_part) at this shape, else 0            */
+int fen_rcab_bwd_se_supported(int dtype, int B, int H, int W, int C, int Cr);
 
 /* trainer.py:416-421 LR synthesis: bicubic x0.25, align_corners=False, NCHW fp32          */
 int fen_bicubic_down4(int B, int C, int H, int W, const float* hr, float* lr, void* stream);

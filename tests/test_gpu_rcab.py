@@ -207,6 +207,63 @@ def test_rcab_bwd_fused(prec, B, H, W, dot):
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("B,H,W", [(2, 32, 48), (3, 64, 64), (32, 64, 64), (40, 64, 64)])
+def test_rcab_bwd_se_fold(prec, B, H, W):
+    """fen_rcab_bwd with the SE backward folded in (se_part set: dt built on each tile's dy halo)
+    against fen_se_bwd_fused followed by the plain fen_rcab_bwd on the same inputs: dt, the FC
+    weight-gradient rows, dz1, dx, the slope and DOT partials all bit-identical (same arithmetic
+    in the same order).  B = 40 puts 3 tiles on a block (the in-loop fold of tiles 2 and 3)."""
+    from src.hip import lib as L
+    from src.hip.net import Weights, tiles
+    from src.hip.program import Ctx, ptr
+    dtype = DT[prec]
+    g = torch.Generator().manual_seed(11)
+    C, Cr = 64, 16
+    T = tiles(H, W)
+    ctx = Ctx(dtype, DEV)
+    if not ctx.lib.fen_rcab_bwd_se_supported(ctx.code, B, H, W, C, Cr):
+        pytest.skip("outside the folded envelope on this device")
+    w1 = torch.randn(C, C, 3, 3, generator=g) * 0.06
+    w2 = torch.randn(C, C, 3, 3, generator=g) * 0.06
+    Wt = Weights({"c1.weight": w1.to(DEV), "c2.weight": w2.to(DEV)}, dtype, DEV)
+    nh = lambda t: t.permute(0, 2, 3, 1).contiguous().to(DEV, dtype)
+    z1, dy, tn = (nh(torch.randn(B, C, H, W, generator=g)) for _ in range(3))
+    alpha = (torch.rand(C, generator=g) * 0.5).to(DEV)
+    part = (torch.randn(B * T, C, generator=g) * 3).to(DEV)
+    sg = torch.sigmoid(torch.randn(B, C, generator=g)).to(DEV)
+    mean = torch.randn(B, C, generator=g).to(DEV)
+    hid = torch.randn(B, Cr, generator=g).clamp_min(0).to(DEV)      # some units exactly 0
+    fc1 = (torch.randn(Cr, C, generator=g) * 0.2).to(DEV)
+    fc2 = (torch.randn(C, Cr, generator=g) * 0.2).to(DEV)
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for fold in (False, True):
+        dt = ctx.alloc((B, H, W, C))
+        dw1p = ctx.alloc((B, Cr * C), torch.float32)
+        dw2p = ctx.alloc((B, Cr * C), torch.float32)
+        dz1, dx = ctx.alloc((B, H, W, C)), ctx.alloc((B, H, W, C))
+        dal, dotp = ctx.alloc((B * T, C), torch.float32), ctx.alloc((B * T, C), torch.float32)
+        if not fold:
+            L.check(ctx.lib.fen_se_bwd_fused(ctx.code, B, H * W, C, Cr, T, 1.0 / (H * W), 0.2, ptr(part), ptr(mean),
+                                             ptr(hid), ptr(sg), ptr(fc1), ptr(fc2), ptr(dy), None, ptr(dw1p),
+                                             ptr(dw2p), ptr(dt), stream), "se_bwd_fused")
+        d = L.RcabBwdDesc()
+        d.dtype, d.B, d.H, d.W, d.C = ctx.code, B, H, W, C
+        d.dt, d.w2t, d.z1, d.alpha = ptr(dt), ptr(Wt.packed("c2", 2)), ptr(z1), ptr(alpha)
+        d.w1t, d.dy, d.dz1, d.dalpha_part, d.dx = ptr(Wt.packed("c1", 2)), ptr(dy), ptr(dz1), ptr(dal), ptr(dx)
+        d.dot_t, d.dot_part = ptr(tn), ptr(dotp)
+        if fold:
+            d.se_part, d.se_s, d.se_mean, d.se_hid = ptr(part), ptr(sg), ptr(mean), ptr(hid)
+            d.se_w1, d.se_w2, d.se_dw1p, d.se_dw2p = ptr(fc1), ptr(fc2), ptr(dw1p), ptr(dw2p)
+            d.se_res_scale, d.se_Cr = 0.2, Cr
+        L.check(ctx.lib.fen_rcab_bwd(d, stream), "rcab_bwd")
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (dt, dw1p, dw2p, dz1, dx, dal, dotp)])
+    for name, a_, b_ in zip(("dt", "dw1p", "dw2p", "dz1", "dx", "dalpha", "dot"), outs[0], outs[1]):
+        assert torch.equal(a_, b_), name
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("B,H,W,train", [(2, 32, 32, False), (17, 64, 64, True), (1, 48, 80, False),
                                           (32, 64, 64, False), (3, 16, 16, True)])
 def test_group_end_fused(prec, B, H, W, train):
