@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_conv_first4(int B, int Ci, int H, int W
 // ~27 x 64 VALU FMAs per pixel (VALU bound at ~47 TFLOP/s on VGG conv1_1, 64 x 256^2).
 constexpr int CFM16_BLOCKS = 2048;
 template <typename T, int MB>
-__global__ __launch_bounds__(256) void k_conv_first_m16(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
+__global__ __launch_bounds__(256, MB <= 4 ? 5 : 1) void k_conv_first_m16(int B, int Ci, int H, int W, int C, const float* __restrict__ x,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
                                                        T* __restrict__ y, const float* __restrict__ in_mean,
                                                        const float* __restrict__ in_istd, float act) {
@@ -180,25 +180,22 @@ __global__ __launch_bounds__(256) void k_conv_first_m16(int B, int Ci, int H, in
         }
     }
     // activation operand: lane reads halo offset boff[j] (+ the pixel's), or the constant
-    int boff[8];
-    float bconst[8];
+    int boff[8];                                             // -1: the bias column (1), -2: padding (0)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int k = 8 * q + j;
-        boff[j] = k < K ? (k / 9) * 324 + ((k % 9) / 3) * 18 + (k % 3) : -1;
-        bconst[j] = k == 27 ? 1.f : 0.f;
+        boff[j] = k < K ? (k / 9) * 324 + ((k % 9) / 3) * 18 + (k % 3) : (k == 27 ? -1 : -2);
     }
     // halo element i = tid + 256u: its channel is fixed per lane, so the normalisation is too;
     // loads are unconditional (clamped addresses, out-of-image elements zeroed at the LDS write)
     // so the prefetch stays in flight under the tile's MFMAs and stores
-    float xv[4], mu[4], is[4];
-    unsigned inb = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int ci = min((tid + u * 256) / 324, Ci - 1);
-        mu[u] = in_mean ? in_mean[ci] : 0.f;
-        is[u] = in_istd ? in_istd[ci] : 1.f;
+    __shared__ float nrm[2][3];                              // per-channel mean, 1/std
+    if (tid < 3) {
+        nrm[0][tid] = in_mean && tid < Ci ? in_mean[tid] : 0.f;
+        nrm[1][tid] = in_istd && tid < Ci ? in_istd[tid] : 1.f;
     }
+    float xv[4];
+    unsigned inb = 0;
     auto load = [&](int t) {
         const int b = t / (th * tw), tt = t - b * th * tw;
         const int h0 = (tt / tw) << 4, w0 = (tt % tw) << 4;
@@ -223,7 +220,10 @@ __global__ __launch_bounds__(256) void k_conv_first_m16(int B, int Ci, int H, in
         __syncthreads();                                     // the previous tile's reads are done
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (tid + u * 256 < 972) xs[tid + u * 256] = (inb >> u) & 1 ? (xv[u] - mu[u]) * is[u] : 0.f;
+            if (tid + u * 256 < 972) {
+                const int ci = (tid + u * 256) / 324;
+                xs[tid + u * 256] = (inb >> u) & 1 ? (xv[u] - nrm[0][ci]) * nrm[1][ci] : 0.f;
+            }
         __syncthreads();
         if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);   // the next tile, in flight
         // ragged edges: rows past H and columns past W recompute the last valid row / column, and
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_conv_first_m16(int B, int Ci, int H, in
             f16x8 bhi, blo;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float v = boff[j] >= 0 ? xs[boff[j] + r * 18 + cc] : bconst[j];
+                const float v = boff[j] >= 0 ? xs[boff[j] + r * 18 + cc] : (boff[j] == -1 ? 1.f : 0.f);
                 const f16 h = (f16)v;
                 bhi[j] = h;
                 blo[j] = (f16)(v - (float)h);
