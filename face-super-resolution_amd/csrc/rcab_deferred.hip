@@ -917,8 +917,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
                     const size_t o = ((size_t)(b * H + h0 + wr * 4 + n) * W + w0 + c16) * 64 + wc * 32 + m * 16 + 4 * q;
                     rv[m][n] = *(const uint2*)((const char*)A.dy + o * 2);
                     if (A.dot_t) dv[m][n] = *(const uint2*)((const char*)A.dot_t + o * 2);
+                    else if (A.gres) dv[m][n] = *(const uint2*)((const char*)A.gres + o * 2);   // 2nd residual
                 }
-            nhalo += A.dot_t ? 16 : 8;
+            nhalo += (A.dot_t || A.gres) ? 16 : 8;
         }
         if (k < 2) RSTAMP(10 + k * 14);
         // ================= conv2: phases 3..5 =================
@@ -961,6 +962,11 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
                                              hi16<T>(dv[m][n].y)};
 #pragma unroll
                         for (int r = 0; r < 4; ++r) ps[m][r] += rnd16<T>(acc2[m][n][r]) * tn[r];
+                    } else if (A.gres) {                       // a second residual (no DOT)
+                        acc2[m][n][0] += lo16<T>(dv[m][n].x);
+                        acc2[m][n][1] += hi16<T>(dv[m][n].x);
+                        acc2[m][n][2] += lo16<T>(dv[m][n].y);
+                        acc2[m][n][3] += hi16<T>(dv[m][n].y);
                     }
                 }
             }
@@ -1108,6 +1114,7 @@ extern "C" int fen_rcab_bwd(const fen_rcab_bwd_desc* b, void* stream) {
         !b->dy)
         return FEN_EINVAL;
     if ((b->dot_t != nullptr) != (b->dot_part != nullptr)) return FEN_EINVAL;
+    if (b->dres && b->dot_t) return FEN_EINVAL;       // the second residual takes the DOT operand's slot
     const bool seb = b->se_part != nullptr;
     if (seb && (!b->se_s || !b->se_mean || !b->se_hid || !b->se_w1 || !b->se_w2 || !b->se_dw1p || !b->se_dw2p))
         return FEN_EINVAL;
@@ -1133,6 +1140,7 @@ extern "C" int fen_rcab_bwd(const fen_rcab_bwd_desc* b, void* stream) {
     a.dpart = b->dalpha_part;
     a.dy = b->dy;
     a.dot_t = b->dot_t;
+    a.gres = b->dres;
     if (seb) {
         d.pp = b->se_part;
         d.pfc1 = b->se_w1;

@@ -64,7 +64,7 @@ class RcabBwdDesc(Structure):
         ("dot_t", c_void_p), ("dot_part", c_void_p),
         ("se_part", c_void_p), ("se_s", c_void_p), ("se_mean", c_void_p), ("se_hid", c_void_p),
         ("se_w1", c_void_p), ("se_w2", c_void_p), ("se_dw1p", c_void_p), ("se_dw2p", c_void_p),
-        ("se_res_scale", c_float), ("se_Cr", c_int),
+        ("se_res_scale", c_float), ("se_Cr", c_int), ("dres", c_void_p),
     ]
 
 

@@ -192,6 +192,10 @@ DOT_FUSED = os.environ.get("FEN_SE_DOT", "fused") != "pass"
 # partials from dy's producer, <= 6 tiles per CU): 'fold' (default) or a separate
 # fen_se_bwd_fused launch (FEN_SE_IN_BWD=launch)
 SE_IN_BWD = os.environ.get("FEN_SE_IN_BWD", "fold") != "launch"
+# a group's first RCAB (dx also carries the group's output gradient) on the fused backward too,
+# the second residual in the DOT operand's slot (FEN_RCAB_BWD_RES=1).  Measured 8.838 vs
+# 8.826 ms per training step against the two-launch pair (3 same-box reps): off by default
+BWD_RES_FUSED = os.environ.get("FEN_RCAB_BWD_RES", "0") == "1"
 WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
 
 
@@ -505,7 +509,10 @@ class Backward:
         dt = ctx.scratch(f"bw_dt{rot}", dy.shape)
         se_args = (npart, 1.0 / HW, s.res_scale, ptr(part), ptr(sv["mean"]), ptr(sv["hid"]), ptr(sv["s"]),
                    ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"]))
-        fused = (RCAB_BWD_FUSED and not extra_res and ctx.code != L.F32
+        # (one extra residual -- a group's first RCAB -- rides in the DOT operand's slot)
+        fused = (RCAB_BWD_FUSED and len(extra_res) <= (1 if BWD_RES_FUSED else 0)
+                 and not (extra_res and t_next is not None)
+                 and ctx.code != L.F32
                  and ctx.lib.fen_rcab_deferred_supported(ctx.code, B, H, W, C, s.Cr))
         # the SE backward folded into the fused launch (dt built on its dy halo in LDS)
         seb = fused and SE_IN_BWD and dot_part and ctx.lib.fen_rcab_bwd_se_supported(ctx.code, B, H, W, C, s.Cr)
@@ -533,6 +540,8 @@ class Backward:
             d.dt, d.w2t, d.z1 = ptr(dt), ptr(Wt.packed(pre + "conv2", 2)), ptr(sv["z1"])
             d.alpha, d.w1t, d.dy = ptr(p[pre + "prelu.weight"]), ptr(Wt.packed(pre + "conv1", 2)), ptr(dy)
             d.dz1, d.dalpha_part, d.dx = ptr(dz1), ptr(dal), ptr(dx)
+            if extra_res:
+                d.dres = ptr(extra_res[0])
             if seb:
                 d.se_part, d.se_s, d.se_mean, d.se_hid = ptr(part), ptr(sv["s"]), ptr(sv["mean"]), ptr(sv["hid"])
                 d.se_w1, d.se_w2 = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])

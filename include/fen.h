@@ -258,6 +258,8 @@ typedef struct {
     float* se_dw2p;            /* out [B][64*Cr]                                                 */
     float se_res_scale;        /* 0.2                                                            */
     int se_Cr;                 /* <= 16                                                          */
+    const void* dres;          /* NULL or NHWC: a second residual added to dx (a ResidualGroup's
+                                  first RCAB: the group's output gradient); not with dot_t        */
 } fen_rcab_bwd_desc;
 int fen_rcab_bwd(const fen_rcab_bwd_desc* d, void* stream);
 /* 1 when fen_rcab_bwd takes the folded SE backward (se_part) at this shape, else 0            */

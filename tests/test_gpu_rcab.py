@@ -145,12 +145,13 @@ def _round(x, dtype):
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("B,H,W,dot", [(2, 32, 32, True), (17, 64, 64, True), (1, 48, 80, False), (1, 16, 16, True),
-                                        (32, 64, 64, True)])
+                                        (32, 64, 64, True), (3, 32, 48, "res"), (32, 64, 64, "res")])
 def test_rcab_bwd_fused(prec, B, H, W, dot):
     """fen_rcab_bwd (the RCAB backward's conv2^T -> PReLU' -> conv1^T + dy in one launch, + the
     next RCAB's DOT partials) vs a torch fp32 restatement on the same rounded operands:
     g2 = conv2^T(dt), dz1 = g2 * PReLU'(z1), dalpha per tile = sum g2 * z1 * (z1 <= 0),
-    dx = conv1^T(dz1 as stored) + dy, DOT per tile = sum dx (as stored) * t_next.
+    dx = conv1^T(dz1 as stored) + dy, DOT per tile = sum dx (as stored) * t_next; dot = "res":
+    a second residual (dres, a group's first RCAB) added to dx instead of the DOT.
     rel-L2 <= 3e-3 (bf16) / 1e-3 (fp16) on dz1 and dx; 5e-3 / 2e-3 on the partial sums (a
     wrong tap, halo row, edge fragment or tile shows up as O(1))."""
     import torch.nn.functional as F
@@ -175,6 +176,8 @@ def test_rcab_bwd_fused(prec, B, H, W, dot):
     dal_ref = (g2 * z1 * (z1 <= 0)).view(B, C, H // 16, 16, W // 16, 16).sum((3, 5))
     dal_ref = dal_ref.permute(0, 2, 3, 1).reshape(B * tiles(H, W), C)
     dx_ref = F.conv_transpose2d(_round(dz1_ref, dtype), w1r, padding=1) + dy
+    if dot == "res":                                   # a group's first RCAB: + the group's dy
+        dx_ref = dx_ref + tn
     dot_ref = (_round(dx_ref, dtype) * tn).view(B, C, H // 16, 16, W // 16, 16).sum((3, 5))
     dot_ref = dot_ref.permute(0, 2, 3, 1).reshape(B * tiles(H, W), C)
 
@@ -192,7 +195,9 @@ def test_rcab_bwd_fused(prec, B, H, W, dot):
     d.dtype, d.B, d.H, d.W, d.C = ctx.code, B, H, W, C
     d.dt, d.w2t, d.z1, d.alpha = ptr(dtd), ptr(Wt.packed("c2", 2)), ptr(z1d), ptr(ad)
     d.w1t, d.dy, d.dz1, d.dalpha_part, d.dx = ptr(Wt.packed("c1", 2)), ptr(dyd), ptr(dz1), ptr(dal), ptr(dx)
-    if dot:
+    if dot == "res":
+        d.dres = ptr(tnd)
+    elif dot:
         d.dot_t, d.dot_part = ptr(tnd), ptr(dotp)
     L.check(ctx.lib.fen_rcab_bwd(d, torch.cuda.current_stream().cuda_stream), "rcab_bwd")
     torch.cuda.synchronize()
@@ -202,7 +207,7 @@ def test_rcab_bwd_fused(prec, B, H, W, dot):
     assert rel(nc(dz1), dz1_ref) <= tol
     assert rel(nc(dx), dx_ref) <= tol
     assert rel(dal.cpu(), dal_ref) <= tolp
-    if dot:
+    if dot is True:
         assert rel(dotp.cpu(), dot_ref) <= tolp
 
 
