@@ -387,9 +387,6 @@ __global__ __launch_bounds__(512, 1) void k_rcab_d(const RdArgs A) {
     // SEB: dt = dy * rs * s + g over the DMA'd dy halo image in place (+ the edge copy; zero
     // outside the image), the tile's own dt out (nch buffer stores per wave, as combine_halo)
     auto se_halo = [&](int t, int k) {
-#ifdef FEN_SEB_NOHALO
-        return;                                              // timing diagnostic only (wrong results)
-#endif
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const float rs = d.res_scale;

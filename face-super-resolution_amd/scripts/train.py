@@ -13,6 +13,7 @@ import os
 import random
 import sys
 from pathlib import Path
+from typing import Optional
 
 PKG = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(PKG))
@@ -40,6 +41,20 @@ def set_seed(seed: int) -> None:
     torch.manual_seed(seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
+
+
+def resolve_precision(cli: Optional[str], tr_cfg: dict) -> str:
+    """The compute precision.  The reference's `training.mixed_precision` (default true,
+    scripts/train.py:300) means torch.cuda.amp fp16 autocast + GradScaler (trainer.py:18,227,460),
+    which the HIP path does not restate: with it set, the precision must be chosen explicitly
+    (--precision fp32 | bf16) rather than silently training in a different arithmetic.  The
+    stage configs set mixed_precision: false -> fp32, the reference's own arithmetic."""
+    if cli is not None:
+        return cli
+    if tr_cfg.get("mixed_precision", True):
+        raise ValueError("training.mixed_precision is true (the reference's fp16 autocast + GradScaler, not "
+                         "restated on the HIP path): pass --precision fp32 or --precision bf16 explicitly")
+    return "fp32"
 
 
 def create_model(model_type: str, config: dict, precision: str):
@@ -81,7 +96,7 @@ def main(argv=None):
     ap.add_argument("--overfit-test", action="store_true")
     ap.add_argument("--device", type=str, default="cuda")
     ap.add_argument("--no-wandb", action="store_true")
-    ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--precision", type=str, default=None, choices=["fp32", "bf16"])
     ap.add_argument("--synthetic", type=int, default=0)
     args = ap.parse_args(argv)
 
@@ -110,8 +125,9 @@ def main(argv=None):
     val_loader = get_dataloader(data_root, "val", batch_size, data_cfg.get("num_workers", 4), hr_patch_size=hr_size,
                                 synthetic=max(args.synthetic // 8, batch_size) if args.synthetic else 0)
 
-    model = create_model(model_type, config, args.precision)
-    discriminator, gan_loss = create_gan(config, args.precision)
+    precision = resolve_precision(args.precision, tr_cfg)
+    model = create_model(model_type, config, precision)
+    discriminator, gan_loss = create_gan(config, precision)
     gan = loss_cfg.get("gan", {})
     pw = args.perceptual_weight if args.perceptual_weight is not None else loss_cfg.get("perceptual_weight", 0.01)
     loss_fn = create_loss_function(l1_weight=loss_cfg.get("l1_weight", 1.0), perceptual_weight=pw,
@@ -140,8 +156,6 @@ def main(argv=None):
         use_wandb=False, device=args.device, gan_weight=gan.get("weight", 0.0), gan_type=gan.get("type", "vanilla"),
         d_learning_rate=gan.get("d_lr", 1e-4), d_weight_decay=gan.get("d_weight_decay", 0.0),
         d_updates_per_g=gan.get("d_updates_per_g", 1), gan_start_epoch=gan.get("start_epoch", 0))
-    if tcfg.accumulation_steps != 1:
-        raise NotImplementedError("accumulation_steps > 1 is not supported by the fused step (the stage configs use 1)")
     trainer = Trainer(model, train_loader, val_loader, loss_fn, tcfg, discriminator=discriminator, gan_loss=gan_loss)
     if args.resume:
         trainer.load_checkpoint(args.resume, weights_only=args.fine_tune)

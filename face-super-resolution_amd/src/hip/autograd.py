@@ -49,7 +49,14 @@ class LiveWeights(Weights):
         if k in self.packs and old != stamp:
             if old[0] == stamp[0]:
                 # updated in place (an optimizer step bumps every parameter's version): re-pack
-                # every known copy in ONE fen_pack_multi launch, instead of one launch per use
+                # every known copy in ONE fen_pack_multi launch, instead of one launch per use.
+                # A copy whose parameter was re-homed since it was packed (flatten_params) packs
+                # from the current storage: the job table is rebuilt from the live parameters
+                for kk in self.packs:
+                    ww = self.params[kk[0] + ".weight"]
+                    if self._src[kk].data_ptr() != ww.data_ptr():
+                        self._src[kk] = ww.detach()
+                        self._dirty = True
                 self.pack()
                 for kk in self.packs:
                     ww = self.params[kk[0] + ".weight"]

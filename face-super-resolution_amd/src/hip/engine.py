@@ -46,7 +46,7 @@ class FENEngine:
                  device="cuda", loss_weight: float = 1.0, clip: float = 0.5, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, process_group=None,
                  perceptual: Optional[dict] = None, ssim_weight: float = 0.0, exchange=None,
-                 adam_state=None):
+                 adam_state=None, accumulation_steps: int = 1):
         """perceptual (training only): the stage configs' VGG19 term (perceptual.py:144-169) as
         dict(weight=, layers=, criterion=, normalize=, params={'features.i.weight': ...},
         layer_weights=None); its gradient joins the fused L1 gradient in dL/dsr.  ssim_weight
@@ -56,7 +56,9 @@ class FENEngine:
         pair); the loss gradients are pre-scaled by its `world`.  adam_state (training only): an
         (exp_avg, exp_avg_sq, scal) triple over the parameter arena to update (the Trainer's one
         generator optimizer state, shared by every engine and its module-path optimizer), else
-        a fresh one."""
+        a fresh one.  accumulation_steps (training only): the loss gradients are divided by it
+        (reference trainer.py:477); `step(update=False)` then runs forward + backward without
+        the update, as the reference's non-stepping batches do."""
         if train and dtype == torch.float16:
             raise NotImplementedError("fp16 is an inference precision on the HIP backend (train in bf16 or fp32)")
         self.spec = NetSpec.from_config(model.config)
@@ -125,11 +127,13 @@ class FENEngine:
                 off += p.numel()
             self.exchange = self._exchange_factory(self.flat_g)
             self.world = self.exchange.world
+            self.accum = max(1, int(accumulation_steps))
+            gdiv = self.world * self.accum        # the loss gradients' pre-scale (DP mean, accumulation)
             self.scal[3] = lr
             self.loss = torch.zeros(1, device=self.device)
             ctx.emit("bicubic_down4", ctx.lib.fen_bicubic_down4, B, s.out_ch, self.H, self.W, ptr(self.hr),
                      ptr(self.x))
-            self.l1_scale = loss_weight / (B * s.out_ch * self.H * self.W * self.world)
+            self.l1_scale = loss_weight / (B * s.out_ch * self.H * self.W * gdiv)
             self._build_forward(training=True)
             self._build_backward()
             self._build_update()
@@ -152,7 +156,7 @@ class FENEngine:
             lp = self.saved_tail["loss_part"]
             colsum(ctx, lp, lp.shape[0], 1, self.loss, scale=1.0 / (self.B * s.out_ch * self.H * self.W))
             if self.vgg is not None:
-                self.vgg.build(self.x2, self.loss_perc, self.saved_tail["dout"], grad_scale=1.0 / self.world)
+                self.vgg.build(self.x2, self.loss_perc, self.saved_tail["dout"], grad_scale=1.0 / (self.world * self.accum))
             if self.ssim_weight:
                 self._build_ssim()
 
@@ -168,7 +172,7 @@ class FENEngine:
         per = ctx.scratch("ssim_img", (B,), torch.float32)
         n = B * C * H * W
         ctx.emit("ssim", ctx.lib.fen_ssim, ctx.code, B, C, H, W, ptr(self.out), ptr(self.hr), ptr(self.ssim_win), 11,
-                 0.01 ** 2, 0.03 ** 2, ptr(part), ptr(self.saved_tail["dout"]), -self.ssim_weight / (n * self.world), 2)
+                 0.01 ** 2, 0.03 ** 2, ptr(part), ptr(self.saved_tail["dout"]), -self.ssim_weight / (n * self.world * self.accum), 2)
         ctx.emit("ssim_img", ctx.lib.fen_colsum, rows, B, ptr(part), 1.0 / (C * H * W), ptr(per), 0)
         ctx.emit("ssim_mean", ctx.lib.fen_colsum, B, 1, ptr(per), 1.0 / B, ptr(self.ssim_val), 0)
 
@@ -209,13 +213,16 @@ class FENEngine:
         self.ctx.run()
         return self.out
 
-    def step(self, hr: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def step(self, hr: Optional[torch.Tensor] = None, update: bool = True) -> torch.Tensor:
         """One training step on HR [B,3,H,W]: LR synthesis, fwd, L1 (+ perceptual), bwd,
-        all-reduce, clip, AdamW.  Returns the (device) total loss of this rank's shard."""
+        all-reduce, clip, AdamW (the last three skipped without `update`: a non-stepping batch
+        under accumulation).  Returns the (device) total loss of this rank's shard."""
         if hr is not None:
             self.hr.copy_(hr)
         self.ctx.run()
         self.exchange.wait()
+        if not update:
+            return self.total_loss()
         self.upd.run()
         self.Wt.pack()
         from ..training.optim import bump_versions

@@ -529,7 +529,10 @@ class Backward:
                      ptr(g), ptr(dt))
         self.cs.add(dw1p, B, s.Cr * C, G[ca + "0.weight"])
         self.cs.add(dw2p, B, s.Cr * C, G[ca + "2.weight"])
-        self.wb.add(sv["a1"], dt, B, H, W, C, C, G[pre + "conv2.weight"], G[pre + "conv2.bias"])
+        # conv2's weight gradient reads dt: queued only once dt's producer is emitted (with the
+        # SE fold that is fen_rcab_bwd below -- an add may flush the batch at once)
+        if not seb:
+            self.wb.add(sv["a1"], dt, B, H, W, C, C, G[pre + "conv2.weight"], G[pre + "conv2.bias"])
         dz1 = ctx.scratch(f"bw_dz1{rot}", dy.shape)
         T = tiles(H, W)
         dal = ctx.scratch("bw_dal" + pre, (B * T, C), torch.float32)
@@ -550,6 +553,8 @@ class Backward:
             if dk:
                 d.dot_t, d.dot_part = ptr(dk["pre_in"]), ptr(dk["part"])
             ctx.emit("rcab_bwd", ctx.lib.fen_rcab_bwd, byref(d))
+            if seb:
+                self.wb.add(sv["a1"], dt, B, H, W, C, C, G[pre + "conv2.weight"], G[pre + "conv2.bias"])
             self.cs.add(dal, B * T, C, G[pre + "prelu.weight"])
             self.wb.add(sv["x"], dz1, B, H, W, C, C, G[pre + "conv1.weight"], G[pre + "conv1.bias"])
             if flush:

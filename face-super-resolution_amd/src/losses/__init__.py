@@ -3,9 +3,10 @@
 The stage-1 generator step's loss is L1 (combined.py:38-47) + the VGG19 perceptual term
 (perceptual.py, stage1_psnr_config.yaml:40-50).  L1 is fused into the conv_last epilogue
 (sign(sr-hr)/N written by the kernel, fen_conv_desc.hr); the perceptual term runs on the
-HIP VGG path (src/hip/vgg.py) and its gradient joins L1's in the same dL/dsr buffer.  SSIM
-/ MS-SSIM / L2 / Charbonnier are not built yet: asking for them raises
-instead of silently training something else.
+HIP VGG path (src/hip/vgg.py) and its gradient joins L1's in the same dL/dsr buffer; the
+stage-2 SSIM term (ssim_loss.py:174-226) runs on the HIP SSIM kernel (src/losses/ssim.py,
+fused into the engine's dL/dsr as well).  MS-SSIM / L2 / Charbonnier are outside the built
+path: asking for them raises instead of silently training something else.
 """
 from __future__ import annotations
 

@@ -178,9 +178,7 @@ class Trainer:
             self.gan_loss = gan_loss.to(self.device) if gan_loss is not None else GANLoss(self.config.gan_type)
             self.optimizer_d = torch.optim.AdamW(self.discriminator.parameters(), lr=self.config.d_learning_rate,
                                                  weight_decay=self.config.d_weight_decay)
-            if self._capture_gan():
-                for g in self.optimizer_d.param_groups:   # its step counts live on the device
-                    g["capturable"] = True
+            self._make_d_capturable()
         self._gan_graph: Optional[dict] = None
         self._gan_eager_left = 2
         self.early_stopping = EarlyStopping(self.config.early_stopping_patience, self.config.early_stopping_mode)
@@ -219,7 +217,7 @@ class Trainer:
                             dtype=dtype, train=True, device=self.device, loss_weight=self.fused_l1,
                             clip=self.config.gradient_clip, lr=self.lr, weight_decay=self.config.weight_decay,
                             perceptual=self.fused_perceptual, ssim_weight=self.fused_ssim,
-                            adam_state=self.adam_state)
+                            adam_state=self.adam_state, accumulation_steps=self._accum())
             self._engines[key] = eng
         return self._engines[key]
 
@@ -229,15 +227,18 @@ class Trainer:
             return hr.chunk(self.world)[self.rank]
         return hr
 
-    def _generic_step(self, hr: torch.Tensor) -> torch.Tensor:
-        """Any other content loss: module autograd path + RCCL grad all-reduce + fused AdamW."""
+    def _generic_step(self, hr: torch.Tensor, update: bool = True) -> torch.Tensor:
+        """Any other content loss: module autograd path + RCCL grad all-reduce + fused AdamW
+        (only on the accumulation step, `update`; the loss is divided by accumulation_steps as
+        trainer.py:477 does)."""
         lr = bicubic_down4(hr)
         sr = self.model(lr)
         loss = self._content(sr, hr)
         for p in self.model.parameters():
             p.grad = None
-        (loss / self.world).backward()
-        self._apply_generic_update()
+        (loss / (self.world * self._accum())).backward()
+        if update:
+            self._apply_generic_update()
         return loss.detach()
 
     def _content(self, sr: torch.Tensor, hr: torch.Tensor) -> torch.Tensor:
@@ -248,7 +249,7 @@ class Trainer:
         out = self.loss_fn(sr, hr)
         return out[0] if isinstance(out, tuple) else out
 
-    def _gan_step(self, hr: torch.Tensor) -> torch.Tensor:
+    def _gan_step(self, hr: torch.Tensor, update: bool = True) -> torch.Tensor:
         """One stage-3 iteration (trainer.py:424-485): d_updates_per_g discriminator updates on
         real vs detached fake, then the generator on content + gan_weight x adversarial loss.
         Both networks run on the HIP path through their module autograd."""
@@ -271,21 +272,41 @@ class Trainer:
         loss = content + self.config.gan_weight * gl(D(sr), True)
         for p in self.model.parameters():
             p.grad = None
-        (loss / self.world).backward()
-        self._apply_generic_update()
+        (loss / (self.world * self._accum())).backward()
+        if update:
+            self._apply_generic_update()
         return loss.detach()
 
     def _capture_gan(self) -> bool:
-        return bool(self.config.capture_gan_step) and self.world == 1 and torch.cuda.is_available()
+        return (bool(self.config.capture_gan_step) and self.world == 1 and torch.cuda.is_available()
+                and self._accum() == 1)
 
-    def _gan_iteration(self, hr: torch.Tensor) -> torch.Tensor:
+    def _make_d_capturable(self) -> None:
+        """The captured GAN iteration steps optimizer_d inside the graph: its param groups need
+        `capturable` and its per-parameter step counts on the device as float32.  Also after
+        load_state_dict, which restores the saved groups' flag (False in checkpoints of the
+        reference trainer, of a DP run or of a run without capture) and CPU step counts."""
+        if not self._capture_gan():
+            return
+        for g in self.optimizer_d.param_groups:
+            g["capturable"] = True
+        for st in self.optimizer_d.state.values():
+            if "step" in st:
+                v = st["step"]
+                st["step"] = (v.to(self.device, torch.float32) if torch.is_tensor(v)
+                              else torch.tensor(float(v), dtype=torch.float32, device=self.device))
+
+    def _accum(self) -> int:
+        return max(1, int(self.config.accumulation_steps))
+
+    def _gan_iteration(self, hr: torch.Tensor, update: bool = True) -> torch.Tensor:
         """_gan_step, eagerly or (config.capture_gan_step) replayed from a hipGraph: the first
         two iterations run eagerly (lazy initialisation, allocator warm-up), the third is
         captured and every later one copies its batch into the captured input and replays.
         The update kernels write the parameters behind torch's version counters, so both
         networks' counters are bumped after a replay (the module path then re-packs)."""
         if not self._capture_gan():
-            return self._gan_step(hr)
+            return self._gan_step(hr, update)
         key = (tuple(hr.shape), float(self.lr), tuple(float(g["lr"]) for g in self.optimizer_d.param_groups),
                self.config.d_updates_per_g)
         st = self._gan_graph
@@ -328,20 +349,28 @@ class Trainer:
 
     # ------------------------------------------------------------------ loops
     def _train_epoch(self) -> Dict[str, float]:
+        """trainer.py:390-550.  accumulation_steps = k as the reference runs it: every batch
+        zeroes the generator's gradients (trainer.py:457) and back-propagates loss / k
+        (477-485); every k-th batch clips and steps (488-503) -- so the step sees the last
+        batch's gradient / k -- and counts a global step; the tracked loss is the undivided
+        one (508)."""
         self.model.train()
         total, n = 0.0, 0
-        for batch in self.train_loader:
+        k = self._accum()
+        for bi, batch in enumerate(self.train_loader):
             hr = self._shard(batch["hr"]).to(self.device, non_blocking=True)
+            update = (bi + 1) % k == 0
             if self.use_gan and self.current_epoch >= self.config.gan_start_epoch:
-                loss = self._gan_iteration(hr)
+                loss = self._gan_iteration(hr, update)
             elif self.fused_l1 is not None:
                 B, _, H, W = hr.shape
                 eng = self.engine(B, H, W)
                 eng.set_lr(self.lr)
-                loss = eng.step(hr)
+                loss = eng.step(hr, update=update)
             else:
-                loss = self._generic_step(hr)
-            self.global_step += 1
+                loss = self._generic_step(hr, update)
+            if update:
+                self.global_step += 1
             total += float(loss)  # per-step host sync, as trainer.py:508
             n += 1
         if self.world > 1:
@@ -475,6 +504,7 @@ class Trainer:
             self.discriminator.load_state_dict(ckpt["discriminator_state_dict"])
             if ckpt.get("optimizer_d_state_dict"):
                 self.optimizer_d.load_state_dict(ckpt["optimizer_d_state_dict"])
+                self._make_d_capturable()
 
 
 def overfit_test(model: nn.Module, dataloader, loss_fn: nn.Module, num_images: int = 10,

@@ -23,6 +23,7 @@ Fixtures:
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [g1 g2 ... g9]
 """
+import copy
 import os
 import sys
 import tempfile
@@ -194,8 +195,82 @@ def g9():
     np.savez_compressed(os.path.join(OUT, "g9_full64.npz"), **d)
 
 
+# g10: tensors kept whole (the rest of the 5.1 M parameters are pinned by projections): the
+# first and last RCAB, every group conv, the upsampler, conv_first, conv_last, conv_after_body
+G10_FULL = ("conv_first.", "residual_groups.0.blocks.0.", "residual_groups.5.blocks.9.",
+            "conv_after_body.", "upsample.", "conv_last.") + tuple(f"residual_groups.{g}.conv." for g in range(6))
+G10_NPROJ = 4
+
+
+def g10_full(name):
+    return name.startswith(G10_FULL)
+
+
+def g10_proj(index, arr):
+    """G10_NPROJ seeded Gaussian projections of a tensor (float64) -- regenerated identically by
+    the GPU test from (index, numel)."""
+    r = np.random.default_rng(1000 + index).standard_normal((G10_NPROJ, arr.size))
+    return r @ arr.astype(np.float64).ravel()
+
+
+def g10():
+    """Training at the north-star shape: g9's network, batch and HR (6x10, 64x64 -> 256x256,
+    B=2).  The L1 gradient of every parameter in train mode (reference autograd, fp32, and the
+    same in float64 as the accuracy yardstick), and the parameters after one reference
+    Trainer._train_epoch step (trainer.py:458-503: AdamW lr 1e-4, clip 0.5).  Whole tensors
+    for G10_FULL, seeded projections + norms for every tensor."""
+    sys.path.insert(0, OUT)
+    from smooth import smooth_images_u8
+    torch.manual_seed(0)
+    model = FaceEnhanceNet(num_channels=64, num_groups=6, blocks_per_group=10, reduction_ratio=4, scale_factor=4)
+    d = init_stats(model)
+    perturb_conv_last(model, 1)
+    hr_u8 = smooth_images_u8(2, 256, 256, 11)
+    hr = torch.from_numpy(hr_u8.astype(np.float32) / np.float32(255.0))
+    lr = F.interpolate(hr, scale_factor=0.25, mode="bicubic", align_corners=False)
+    d["hr_u8"] = hr_u8
+    names = [k for k, _ in model.named_parameters()]
+    d["names"] = np.array(names)
+    pre = {k: p.detach().clone() for k, p in model.named_parameters()}
+
+    def grads(m, x, y):
+        m.train()
+        m.zero_grad()
+        loss = F.l1_loss(m(x), y)
+        loss.backward()
+        return float(loss), {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+    loss32, g32 = grads(model, lr, hr)
+    m64 = copy.deepcopy(model).double()
+    loss64, g64 = grads(m64, lr.double(), hr.double())
+    d["l1_loss"], d["l1_loss_f64"] = np.array(loss32), np.array(loss64)
+    for i, k in enumerate(names):
+        a32, a64 = g32[k].numpy(), g64[k].numpy()
+        d["gproj/" + k] = g10_proj(i, a32)
+        d["gproj64/" + k] = g10_proj(i, a64)
+        d["gnorm/" + k] = np.array(np.linalg.norm(a32.astype(np.float64)))
+        d["gerr64/" + k] = np.array(np.linalg.norm(a32.astype(np.float64) - a64))   # the reference's own fp32 error
+        if g10_full(k):
+            d["g/" + k] = a32
+    model.zero_grad()
+    import src.training.trainer as T  # reference
+    with tempfile.TemporaryDirectory() as tmp:
+        cfg = T.TrainerConfig(learning_rate=1e-4, weight_decay=0.0, gradient_clip=0.5,
+                              use_amp=False, use_wandb=False, device="cpu", checkpoint_dir=tmp)
+        tr = T.Trainer(model, [{"hr": hr}], [{"hr": hr}], _L1(), cfg)
+        m = tr._train_epoch()
+    d["step_loss"] = np.array(float(m["loss"]))
+    for i, (k, p) in enumerate(model.named_parameters()):
+        delta = (p.detach() - pre[k]).numpy()
+        d["sproj/" + k] = g10_proj(i, delta)
+        d["snorm/" + k] = np.array(np.linalg.norm(delta.astype(np.float64)))
+        if g10_full(k):
+            d["s/" + k] = p.detach().numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "g10_train64.npz"), **d)
+
+
 ALL = {
-    "g1": g1, "g2": g2, "g3": g3,
+    "g1": g1, "g2": g2, "g3": g3, "g10": g10,
     "g4": lambda: g_net("g4_full.npz", lambda: FaceEnhanceNet(num_channels=64, num_groups=6, blocks_per_group=10,
                                                               reduction_ratio=4, scale_factor=4), (1, 3, 32, 32), 4),
     "g5": lambda: g_net("g5_c128.npz", lambda: FaceEnhanceNet(num_channels=128, num_groups=10, blocks_per_group=20,

@@ -125,7 +125,7 @@ def test_full_networks_vs_reference(golden, name, ctor, precision):
         # 0.0084, fp16 0.0014 dB on g4), plus a per-pixel bound, 6e-3 on [0,1] outputs.  The
         # 128-channel x8 net (config 5, which the reference runs in fp16) carries body
         # activations of O(1e3): fp16 0.0051 dB (gate 0.01), bf16 0.0105 dB (gate 0.02, bf16's
-        # weight rounding alone: tools/numerics_bf16.py).
+        # weight rounding alone: test_oracle.py::test_bf16_weight_rounding_alone_exceeds_001db).
         tol = 0.01
         if name == "g5_c128.npz" and precision == "bf16":
             tol = 0.02
@@ -171,3 +171,45 @@ def test_engine_train_step_matches_reference(g1):
     for k, v in m.state_dict().items():
         d = np.abs(v.cpu().numpy() - g1["s/" + k]).max()
         assert d <= 2e-5, (k, d)
+
+
+@pytest.mark.parametrize("order", ["junk_first", "hr_first"])
+def test_trainer_accumulation_matches_reference(g1, tmp_path, order):
+    """accumulation_steps = 2 on the fused engine, as the reference's loop runs it
+    (trainer.py:457-503): batch 1 runs forward + backward and no update, batch 2 back-propagates
+    loss / 2 and steps on that gradient alone (the reference zeroes the gradients every batch).
+    AdamW's first step is invariant to the 1/2 (m/sqrt(v)), so with G1's batch last the
+    parameters land on the reference's single-step parameters (g1 s/); with it first they do
+    not.  The gradient the update consumed is half the G1 gradient (power-of-two scale)."""
+    import torch.nn as nn
+    from src.training import Trainer, TrainerConfig
+    m = _config1()
+    m.load_state_dict(_sd(g1))
+    hr = torch.from_numpy(g1["hr"])
+    junk = torch.rand(hr.shape, generator=torch.Generator().manual_seed(99))
+    batches = [junk, hr] if order == "junk_first" else [hr, junk]
+    cfg = TrainerConfig(learning_rate=1e-4, weight_decay=0.0, gradient_clip=0.5, accumulation_steps=2,
+                        use_wandb=False, scheduler_type="none", checkpoint_dir=str(tmp_path))
+    tr = Trainer(m, [{"hr": b} for b in batches], None, loss_fn=nn.L1Loss(), config=cfg)
+    seen = []
+    eng = tr.engine(2, 128, 128)
+    run = eng.upd.run
+
+    def upd_run(*a):
+        seen.append(eng.flat_g.detach().clone())
+        return run(*a)
+    eng.upd.run = upd_run
+    tr._train_epoch()
+    torch.cuda.synchronize()
+    assert tr.global_step == 1 and len(seen) == 1
+    worst = max(float(np.abs(v.cpu().numpy() - g1["s/" + k]).max()) for k, v in m.state_dict().items())
+    if order == "junk_first":
+        assert worst <= 2e-5, worst
+        off = 0
+        for k, p in m.named_parameters():
+            g = seen[0][off:off + p.numel()].view_as(p).cpu().double()
+            ref = torch.from_numpy(g1["g/" + k]).double() / 2
+            off += p.numel()
+            assert float((g - ref).norm() / max(ref.norm(), 1e-30)) <= 1e-4, k
+    else:
+        assert worst >= 1e-4, worst

@@ -1,0 +1,127 @@
+"""Training parity at the north-star shape (BASELINE.json: 6x10 RCAB, 64 ch, 64x64 -> 256x256)
+against the reference's own training step (tests/golden/g10_train64.npz, made by importing the
+reference: g9's network, batch and HR).
+
+The golden holds, for every one of the 444 parameters, the L1 gradient (train mode, reference
+autograd, fp32) as four seeded Gaussian projections plus its norm -- whole tensors for the first
+and last RCAB, every group conv, the upsampler, conv_first, conv_after_body and conv_last --
+and the same for the parameter change of one reference Trainer._train_epoch step (AdamW lr 1e-4,
+clip 0.5, trainer.py:458-503).  Checks, through the graph engine FENEngine(train=True):
+
+  * B=2, fp32: whole tensors rel-L2 <= 1e-4; every tensor's projections within 2e-4 * |g|
+    (a projection of an error vector e is ~N(0, |e|^2): 2e-4 |g| ~ rel 1e-4); post-step
+    parameters max |d| <= 2e-5 (|update| ~ lr = 1e-4 per element).  The reference's own fp32
+    gradients sit within 2.5e-5 rel of its float64 run (gerr64 in the golden).
+  * B=32 (the golden's 2 images tiled 16x, the bench's batch): the mean-L1 gradient is the
+    B=2 one.  fp32 at the same bounds; bf16 -- the production kernels (the deferred RCAB's
+    training form, the SE-folded fused RCAB backward, the group end, the batched weight
+    gradients) at 2-3 tiles per block -- at the bf16 whole-network bound below.
+"""
+import numpy as np
+import pytest
+import torch
+
+from src_models_seed import full_ctor, seeded_model
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+NPROJ = 4
+# bf16 whole-network gradient bound: test_gpu_net.py's G1 bound (8e-2 rel-L2; L1's sign gradient
+# flips where |sr - hr| is below bf16 resolution, and 16-bit activations through 60 RCABs).
+BF16_REL = 8e-2
+
+
+@pytest.fixture(scope="module")
+def g10(golden):
+    return golden("g10_train64.npz")
+
+
+def _proj(index, arr):
+    """tests/golden/make_golden.py:g10_proj, regenerated from (index, numel)."""
+    r = np.random.default_rng(1000 + index).standard_normal((NPROJ, arr.size))
+    return r @ arr.astype(np.float64).ravel()
+
+
+def _engine(g, B, dtype):
+    from src.hip.engine import FENEngine
+    m = seeded_model(full_ctor("fp32" if dtype == torch.float32 else "bf16"), g)
+    eng = FENEngine(m, batch=B, lr_hw=(64, 64), dtype=dtype, train=True, clip=0.5, lr=1e-4)
+    hr = torch.from_numpy(g["hr_u8"].astype(np.float32) / np.float32(255.0))
+    eng.hr.copy_(hr.repeat(B // 2, 1, 1, 1).to(DEV))
+    return m, eng
+
+
+def _grads(eng):
+    eng.ctx.run()
+    eng.exchange.wait()
+    torch.cuda.synchronize()
+    return {k: v.detach().cpu() for k, v in eng.grads.items()}
+
+
+def _check_grads(g, grads, whole_tol, proj_tol):
+    bad = {}
+    names = list(g["names"])
+    worst = 0.0
+    for i, k in enumerate(names):
+        a = grads[k].numpy()
+        n = float(g["gnorm/" + k])
+        if "g/" + k in g:
+            ref = g["g/" + k].astype(np.float64)
+            rel = float(np.linalg.norm(a - ref) / max(np.linalg.norm(ref), 1e-30))
+            worst = max(worst, rel)
+            if not rel <= whole_tol:
+                bad[k] = ("whole", rel)
+        dp = float(np.abs(_proj(i, a) - g["gproj/" + k]).max()) / max(n, 1e-30)
+        dn = abs(float(np.linalg.norm(a.astype(np.float64))) - n) / max(n, 1e-30)
+        worst = max(worst, dp / 2)
+        if not (dp <= proj_tol and dn <= proj_tol / 2):
+            bad[k] = ("proj", dp, dn)
+    print(f"worst rel {worst:.2e}")
+    assert not bad, dict(list(bad.items())[:12])
+
+
+@pytest.mark.parametrize("B", [2, 32])
+def test_train64_fp32(g10, B):
+    m, eng = _engine(g10, B, torch.float32)
+    pre = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    grads = _grads(eng)
+    loss = float(eng.loss)
+    assert abs(loss - float(g10["l1_loss"])) <= 1e-6, loss
+    _check_grads(g10, grads, 1e-4, 2e-4)
+    # the update of the captured step: sumsq -> clip 0.5 -> AdamW (trainer.py:490-503)
+    eng.upd.run()
+    torch.cuda.synchronize()
+    bad = {}
+    for i, (k, p) in enumerate(m.named_parameters()):
+        post = p.detach().cpu()
+        if "s/" + k in g10:
+            d = float(np.abs(post.numpy() - g10["s/" + k]).max())
+            if not d <= 2e-5:
+                bad[k] = ("whole", d)
+        delta = (post - pre[k]).numpy()
+        n = float(g10["snorm/" + k])
+        dp = float(np.abs(_proj(i, delta) - g10["sproj/" + k]).max()) / max(n, 1e-30)
+        if not dp <= 1e-3:
+            bad[k] = ("proj", dp)
+    assert not bad, dict(list(bad.items())[:12])
+
+
+def test_train64_bf16_batch32(g10):
+    """The bench's training configuration (bf16, B=32): every gradient within the bf16
+    whole-network bound of the reference's, and the step moves every parameter like the
+    reference's step (AdamW's first step is ~lr * sign(g): projection agreement of the
+    update within 0.25 of its norm -- sign flips where |g| is below bf16 resolution)."""
+    m, eng = _engine(g10, 32, torch.bfloat16)
+    pre = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    grads = _grads(eng)
+    assert abs(float(eng.loss) - float(g10["l1_loss"])) <= 5e-4 * float(g10["l1_loss"])
+    _check_grads(g10, grads, BF16_REL, 2 * BF16_REL)
+    eng.upd.run()
+    torch.cuda.synchronize()
+    worst = 0.0
+    for i, (k, p) in enumerate(m.named_parameters()):
+        delta = (p.detach().cpu() - pre[k]).numpy()
+        n = float(g10["snorm/" + k])
+        worst = max(worst, float(np.abs(_proj(i, delta) - g10["sproj/" + k]).max()) / max(n, 1e-30))
+    print(f"bf16 step: worst projection error {worst:.3f} of |delta|")
+    assert worst <= 0.25, worst

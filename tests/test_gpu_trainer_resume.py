@@ -133,3 +133,34 @@ def test_fused_then_gan_then_resume_is_one_adamw(tmp_path, monkeypatch):
         r2.step(rec.grads[0][1])
         _close(tr2.model._fen_flat, r2, f"first step after resume ({first})")
         assert int(tr2._optimizer_state()["state"][0]["step"]) == 5
+
+
+def test_gan_capture_after_resume_from_noncapturable_optimizer_d(tmp_path):
+    """A stage-3 checkpoint whose optimizer_d was saved with capturable=False and CPU step counts
+    (the reference trainer's, a DP run's or a capture_gan_step=False run's) resumes into a
+    capturing trainer: the restored param groups are made capturable again, so the third GAN
+    iteration after the resume captures optimizer_d.step() and the later ones replay it."""
+    from src.models import VGGStyleDiscriminator
+    torch.manual_seed(3)
+    D = VGGStyleDiscriminator(input_size=128, precision="fp32")
+    tr = _trainer(_gen(1), D, tmp_path, gan_start=0)
+    tr.config.capture_gan_step = False
+    for g in tr.optimizer_d.param_groups:
+        g["capturable"] = False
+    tr.train_loader = _batches(1, 20)
+    tr._train_epoch()
+    torch.cuda.synchronize()
+    osd = tr.optimizer_d.state_dict()
+    assert not osd["param_groups"][0]["capturable"]
+    tr._save_checkpoint("noncap.pth")
+    torch.manual_seed(4)
+    tr2 = _trainer(_gen(7), VGGStyleDiscriminator(input_size=128, precision="fp32"), tmp_path, gan_start=0)
+    tr2.load_checkpoint(str(tmp_path / "noncap.pth"))
+    assert all(g["capturable"] for g in tr2.optimizer_d.param_groups)
+    assert all(st["step"].is_cuda for st in tr2.optimizer_d.state.values())
+    tr2.train_loader = _batches(4, 21)          # 2 eager, then capture, then a replay
+    tr2._train_epoch()
+    torch.cuda.synchronize()
+    assert tr2._gan_graph is not None
+    flat = tr2.model._fen_flat
+    assert bool(torch.isfinite(flat).all())

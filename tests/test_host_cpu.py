@@ -196,3 +196,52 @@ def test_train_cli_builds_gan_for_stage3():
     assert not any(isinstance(m, torch.nn.BatchNorm2d) for m in d.modules())
     assert ts.create_gan({"loss": {"gan": {"weight": 0.0}}}, "fp32") == (None, None)
     assert ts.create_gan({}, "fp32") == (None, None)
+
+
+def test_train_cli_mixed_precision_needs_explicit_precision():
+    """training.mixed_precision: true (the reference's fp16 autocast + GradScaler; its default when
+    the key is absent, scripts/train.py:300) is refused unless --precision is given; the stage
+    configs' false means fp32."""
+    ts = _train_script()
+    with pytest.raises(ValueError, match="mixed_precision"):
+        ts.resolve_precision(None, {"mixed_precision": True})
+    with pytest.raises(ValueError, match="mixed_precision"):
+        ts.resolve_precision(None, {})
+    assert ts.resolve_precision(None, {"mixed_precision": False}) == "fp32"
+    assert ts.resolve_precision("bf16", {"mixed_precision": True}) == "bf16"
+    assert ts.resolve_precision("fp32", {}) == "fp32"
+
+
+def test_trainer_accumulation_schedule():
+    """accumulation_steps = k as the reference runs it (trainer.py:457-508): every batch runs
+    forward + backward (loss / k), only every k-th batch updates and counts a global step, and the
+    tracked loss is the undivided one.  The step paths are stand-ins here (no GPU); the GPU test
+    test_gpu_module.py::test_trainer_accumulation_matches_reference pins the arithmetic."""
+    from src.training.trainer import Trainer, TrainerConfig
+
+    class FakeEngine:
+        def __init__(self):
+            self.calls = []
+
+        def set_lr(self, lr):
+            pass
+
+        def step(self, hr, update=True):
+            self.calls.append(update)
+            return torch.tensor(float(hr.sum()))
+
+    for k, nb in ((1, 4), (3, 7), (2, 6)):
+        tr = object.__new__(Trainer)
+        tr.config = TrainerConfig(accumulation_steps=k, use_wandb=False)
+        tr.rank, tr.world, tr.device = 0, 1, torch.device("cpu")
+        tr.use_gan, tr.fused_l1, tr.global_step, tr.current_epoch = False, 1.0, 0, 0
+        eng = FakeEngine()
+        tr.engine = lambda B, H, W: eng
+        tr.optimizer = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=1e-4)
+        tr.train_loader = [{"hr": torch.full((1, 3, 4, 4), float(i))} for i in range(nb)]
+        m = tr.model = torch.nn.Identity()
+        m = m.train()
+        out = tr._train_epoch()
+        assert eng.calls == [(i + 1) % k == 0 for i in range(nb)], (k, eng.calls)
+        assert tr.global_step == nb // k
+        assert abs(out["loss"] - sum(48.0 * i for i in range(nb)) / nb) < 1e-9
