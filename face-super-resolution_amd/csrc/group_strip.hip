@@ -1,0 +1,628 @@
+// One ResidualGroup as ONE persistent launch, its activations resident on the CUs
+// (reference src/models/blocks.py:161-189: NB x RCAB blocks.py:135-153 with ChannelAttention
+// blocks.py:83-92, then the group conv + the group's skip).
+//
+// Decomposition.  An image of H x 64 pixels is cut into S = H / 8 strips of 8 rows; one
+// 512-thread block (one CU: 158 KB of LDS) owns one strip for the whole group, wave w = row w
+// of the strip, all 64 channels (64 pixels x 64 channels per wave: 16 accumulator tiles of
+// v_mfma_f32_16x16x32_{f16,bf16}).  Between RCABs nothing of the strip leaves the CU:
+//   * x_j (the RCAB input) stays in registers in the accumulator layout (32 VGPRs), t_j
+//     (conv2's output) in the accumulators themselves; x_{j+1} = x_j + rs * s_j * t_j is
+//     computed in registers;
+//   * the LDS image (10 rows x 66 columns x 128 B: the strip, one halo row above and below,
+//     a zero column each side) holds x_j during conv1 and a1 = PReLU(conv1) during conv2
+//     (every conv runs on the strip's own rows only: no halo recompute);
+//   * the running conv's 9 filter taps (73.7 KB) are resident in LDS; the next conv's taps
+//     stream in by LDS-DMA as the phases free their slots (kh = 1 after the first phase, the
+//     rest after the conv).
+// What crosses CUs, per RCAB and strip: the SE pool partial (64 floats) and the strip's first
+// and last rows of x_j, t_j (the neighbours build their halo rows of x_{j+1} from them) and of
+// a1 (the neighbours' conv2 halo rows): <= 48 KB, stored write-through (sc1) and read with
+// sc1 loads after the producer's signal -- MI355X_MICROARCH.md, inter-workgroup visibility,
+// table row 1: sc1 payload stores -> every storing wave's vmcnt(0) -> barrier -> one lane
+// signals; one lane polls with sc1 loads; the polling wave loads after its poll matched, the
+// others after a barrier it joins.
+//   * the image's strips meet once per RCAB (the gate needs the mean over the whole image):
+//     one agent-scope counter per image, +1 per strip and RCAB;
+//   * neighbours meet once more inside the RCAB (a1's halo rows): a flag per strip = j + 1.
+// Blocks take their strip from a ticket counter in start order, so an image's strips are
+// always blocks that are already running: a block only ever waits on running blocks (no
+// co-residency assumption; other work on the GPU delays, never deadlocks).  Every wait is
+// bounded (the workspace's error word is set instead of hanging).  The last block to finish
+// resets the counters for the next launch (graph-replayable).
+//
+// Precision: 16-bit activations (fp16 / bf16) and weights, fp32 accumulation; x_{j+1}, a1
+// and the output rounded to the 16-bit format exactly where the per-launch chain
+// (rcab_deferred.hip) rounds them (t rounded before the gate product, as if stored).
+#include "fen_common.h"
+
+namespace {
+
+constexpr int SR = 8;                         // rows per strip = waves per block
+constexpr int SW = 64;                        // strip width = image width
+constexpr int IC = SW + 2;                    // LDS image columns (zero column each side)
+constexpr int IROW = IC * 128;                // 8448 B per LDS image row
+constexpr int IMG_BYTES = (SR + 2) * IROW;    // 84480
+constexpr int TAPB = 64 * 128;                // one filter tap [64 co][64 ci]
+constexpr int O_IMG = 0;
+constexpr int O_FILT = O_IMG + IMG_BYTES;     // 9 tap slots, slot = kh * 3 + kw
+constexpr int O_RED = O_FILT + 9 * TAPB;      // [8 waves][64] f32 pool partials
+constexpr int O_CST = O_RED + 8 * 64 * 4;     // b1 [64], alpha [64], b2 [64] (group conv: bias in b2)
+constexpr int O_GATE = O_CST + 3 * 64 * 4;    // [64] f32: rs * s of the last RCAB
+constexpr int O_SCR = O_GATE + 64 * 4;        // mean [64], ticket word
+constexpr int GS_LDS = O_SCR + 80 * 4;
+static_assert(GS_LDS <= 163840, "LDS budget");
+static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignment");
+
+constexpr int ROWB = SW * 128;                // one strip row, 8 KB
+constexpr int SPIN_MAX = 1 << 20;             // polls (~1.5 us each) before a wait gives up
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+// workspace: control words, counters, pool partials, boundary rows
+struct Ws {
+    size_t cnt, flg, part, bx, bt, ba, total;
+};
+__host__ __device__ inline Ws ws_layout(int B, int S) {
+    Ws L;
+    size_t o = 256;                          // [0] ticket [1] done [2] error
+    L.cnt = o;  o += (size_t)B * 128;        // one counter per image, own 128-B line
+    L.flg = o;  o += (size_t)B * S * 128;    // one a1 flag per strip, own line
+    L.part = o; o += (size_t)B * 2 * S * 64 * 4;
+    o = (o + 255) & ~(size_t)255;
+    const size_t rows = (size_t)B * S * 2 * 2 * ROWB;   // [img][strip][parity][side] rows
+    L.bx = o; o += rows;
+    L.bt = o; o += rows;
+    L.ba = o; o += rows;
+    L.total = o;
+    return L;
+}
+
+struct GsArgs {
+    int B, H, S, NB, Cr;
+    float res_scale, inv_hw;
+    const void* x;                            // group input  [B][H][64][64] NHWC
+    void* y;                                  // group output [B][H][64][64]
+    const void* w[2 * FEN_GS_MAXNB + 1];      // packed taps: conv1_0, conv2_0, ..., group conv
+    const float* bias[2 * FEN_GS_MAXNB + 1];
+    const float* alpha[FEN_GS_MAXNB];
+    const float* fc1[FEN_GS_MAXNB];           // [Cr][64]
+    const float* fc2[FEN_GS_MAXNB];           // [64][Cr]
+    float* s_out[FEN_GS_MAXNB];               // optional gates s [B][64] (attention maps)
+    char* work;
+};
+
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// 4 consecutive channels (acc element order) <-> one 8-B word pair
+template <typename T>
+__device__ __forceinline__ uint2 pk4(float a, float b, float c, float d) {
+    return make_uint2(pack2<T>(a, b), pack2<T>(c, d));
+}
+
+// lanes q and q^1 (same pixel) trade one 4-channel half so each holds 8 consecutive channels:
+// lo = the lane's channels of m-block 2mp, hi = of m-block 2mp + 1; the result is chunk
+// chunk_of(mp, q) of the pixel
+__device__ __forceinline__ uint4 pair16(uint2 lo, uint2 hi, bool odd) {
+    const uint2 snd = odd ? lo : hi;
+    uint2 rcv;
+    rcv.x = (unsigned)__shfl_xor((int)snd.x, 16, 64);
+    rcv.y = (unsigned)__shfl_xor((int)snd.y, 16, 64);
+    return odd ? make_uint4(rcv.x, rcv.y, hi.x, hi.y) : make_uint4(lo.x, lo.y, rcv.x, rcv.y);
+}
+__device__ __forceinline__ int chunk_of(int mp, int q) { return 4 * mp + ((q & 1) ? 2 : 0) + (q >> 1); }
+
+// bounded poll of an agent-scope counter (sc1 loads): true if it reached `target`
+__device__ __forceinline__ bool poll_ge(const int* p, int target) {
+    for (int it = 0; it < SPIN_MAX; ++it) {
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+
+__device__ __forceinline__ void vm_wait_n(int n) {
+    switch (n) {
+#define GS_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+        GS_VMC(1) GS_VMC(2) GS_VMC(3) GS_VMC(4) GS_VMC(5) GS_VMC(6) GS_VMC(7) GS_VMC(8) GS_VMC(9) GS_VMC(10)
+        GS_VMC(11) GS_VMC(12) GS_VMC(13) GS_VMC(14) GS_VMC(15) GS_VMC(16)
+#undef GS_VMC
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// one phase of a conv: the 3 taps (kh, 0..2) on the wave's output row; B fragments from LDS
+// image row (wave + kh) at column shift kw, A fragments from tap slot kh * 3 + kw.  Six
+// (tap, k-half) steps, the next step's fragments read during the current step's 16 MFMAs.
+template <typename T>
+__device__ __forceinline__ void conv_phase(f32x4 (&acc)[4][4], const char* img, const char* filt, int kh, int wave,
+                                           int q, int c16) {
+    asm volatile("" : "+v"(q), "+v"(c16));   // opaque lane coordinates: addresses per phase
+    const char* rowp = img + (wave + kh) * IROW;
+    const char* slot0 = filt + kh * 3 * TAPB;
+    uint4 A[2][4], Bf[2][4];
+    // the swizzle keys depend on the lane only (16 m and 16 p leave them unchanged): one base
+    // address per step, m and p as immediate offsets
+    auto load = [&](int s, uint4 (&a)[4], uint4 (&b)[4]) {
+        const int kw = s >> 1, chunk = (s & 1) * 4 + q;
+        const char* ab = slot0 + kw * TAPB + c16 * 128 + ((chunk ^ ((c16 >> 1) & 7)) << 4);
+        const char* bb = rowp + (c16 + kw) * 128 + ((chunk ^ ((c16 + kw) & 7)) << 4);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a[m] = *(const uint4*)(ab + m * 2048);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) b[p] = *(const uint4*)(bb + p * 2048);
+    };
+    load(0, A[0], Bf[0]);
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        if (s + 1 < 6) load(s + 1, A[(s + 1) & 1], Bf[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) mma16<T>(acc[m][p], A[s & 1][m], Bf[s & 1][p]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* img = smem + O_IMG;
+    char* filt = smem + O_FILT;
+    float* red = (float*)(smem + O_RED);
+    float* cst = (float*)(smem + O_CST);
+    float* gate = (float*)(smem + O_GATE);
+    float* scr = (float*)(smem + O_SCR);
+    int* tick_lds = (int*)(scr + 64);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = wave_id();
+    // lane coordinates; re-derived from an opaque copy of the lane id at the top of every
+    // chain step, so per-lane addresses are recomputed per step instead of being hoisted out
+    // of the chain loop (they would live through the convs, the register peak, and spill)
+    int q = lane >> 4, c16 = lane & 15;
+    bool odd = q & 1;
+    const int B = A.B, H = A.H, S = A.S, NB = A.NB;
+    const Ws L = ws_layout(B, S);
+    int* ctl = (int*)A.work;
+
+    // ---- the strip: a ticket in start order (an image's strips are running blocks)
+    if (tid == 0) *tick_lds = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // zero the LDS image (halo rows of edge strips and the zero columns stay zero)
+    for (int i = tid; i < IMG_BYTES / 16; i += 512) *(uint4*)(img + i * 16) = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const int ticket = __builtin_amdgcn_readfirstlane(*tick_lds);
+    const int im = ticket / S, strip = ticket - im * S;
+    const int r0 = strip * SR;
+    const bool has_up = strip > 0, has_dn = strip + 1 < S;
+    // waves 0 / 7 own the strip's boundary rows (publish them, fetch the neighbours')
+    const bool bwave = (wave == 0 && has_up) || (wave == SR - 1 && has_dn);
+    const int side = wave == 0 ? 0 : 1;                    // this wave's boundary side
+    const int nb_strip = wave == 0 ? strip - 1 : strip + 1;  // the neighbour it reads from
+
+    const size_t act_bytes = (size_t)B * H * SW * 128;
+    const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc((void*)A.work, 0, (int)L.total, 0x00020000);
+    int* cnt = (int*)(A.work + L.cnt) + im * 32;
+    int* flg = (int*)(A.work + L.flg);
+    auto rowoff = [&](size_t base, int s_, int par, int sd) -> int {
+        return (int)(base + ((size_t)((im * S + s_) * 2 + par) * 2 + sd) * ROWB);
+    };
+
+    // ---- filter taps by LDS-DMA: tap k of conv `ci` into slot k (this wave's 1-KB piece)
+    auto issue_taps = [&](int ci, int k0, int n) {     // taps k0 .. k0 + n - 1
+        const i32x4 wr = make_rsrc(A.w[ci], 9u * 64u * 128u);
+        int ll = lane;
+        asm volatile("" : "+v"(ll));
+        const int s = wave * 64 + ll, r = s >> 3, pc = s & 7;
+        const int v0 = (r * 64 + ((pc ^ ((r >> 1) & 7)) * 8)) * 2;
+        for (int k = k0; k < k0 + n; ++k)
+            dma16(wr, __builtin_amdgcn_readfirstlane(lds_addr(filt + k * TAPB + wave * 1024)), v0 + k * TAPB);
+    };
+    auto issue_kh1 = [&](int ci) { issue_taps(ci, 3, 3); };
+    auto issue_kh02 = [&](int ci) {
+        issue_taps(ci, 0, 3);
+        issue_taps(ci, 6, 3);
+    };
+
+    // ---- per-lane helpers on the accumulator layout: lane (q, c16) holds channels
+    // 16m + 4q + i (i = 0..3) of pixel 16p + c16 of the wave's row
+    uint2 xr[4][4];                                         // x_j, packed 16-bit
+    auto px_off = [&](int row, int p) -> size_t {           // byte offset of (image row, pixel 16p + c16)
+        return ((size_t)(im * H + row) * SW + 16 * p + c16) * 128;
+    };
+    auto write_row_lds = [&](int lrow, const uint2 (&v)[4][4]) {
+        int qq = q, cc = c16;
+        asm volatile("" : "+v"(qq), "+v"(cc));              // addresses per use, not hoisted
+        const int key = (cc + 1) & 7;
+        char* rb = img + lrow * IROW + (cc + 1) * 128 + (qq & 1) * 8;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            char* mb = rb + (((2 * m + (qq >> 1)) ^ key) << 4);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) *(uint2*)(mb + p * 2048) = v[m][p];
+        }
+    };
+    // a strip row (accumulator layout) out as 16-B chunks through `rs` at byte offset `base`
+    auto store_row = [&](__amdgpu_buffer_rsrc_t rs, int base, const uint2 (&v)[4][4], int aux) {
+        int qq = q, cc = c16;
+        asm volatile("" : "+v"(qq), "+v"(cc));
+        const int lb = base + cc * 128 + chunk_of(0, qq) * 16;
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int mp = 0; mp < 2; ++mp) {
+                const uint4 u = pair16(v[2 * mp][p], v[2 * mp + 1][p], odd);
+                const int off = lb + p * 2048 + mp * 64;
+                if (aux) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 16);
+                else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 0);
+            }
+    };
+    // a boundary row (16-B chunks, lane handles chunks lane + 64 k) -> LDS image row lrow
+    auto halo_to_lds = [&](int lrow, const uint4 (&v)[8]) {
+        int ll = lane;
+        asm volatile("" : "+v"(ll));
+        char* hb = img + lrow * IROW + hcol((ll >> 3) + 1, ll & 7);   // pixel + 8 k keeps the key
+#pragma unroll
+        for (int k = 0; k < 8; ++k) *(uint4*)(hb + k * 1024) = v[k];
+    };
+
+    // ================= start-up: conv1_0's taps, x_0, constants =================
+    issue_taps(0, 0, 9);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, (int)act_bytes, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+            xr[m][p] = *(const uint2*)((const char*)A.x + px_off(r0 + wave, p) + (16 * m + 4 * q) * 2);
+    uint4 hv[8];
+    if (bwave) {
+        const int row = wave == 0 ? r0 - 1 : r0 + SR;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = lane + 64 * k;
+            hv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xrs, (int)(((size_t)(im * H + row) * SW) * 128) + i * 16, 0, 0));
+        }
+    }
+    float cv = 0.f;
+    if (wave == 2) cv = A.bias[0][lane];
+    if (wave == 3) cv = A.alpha[0][lane];
+    if (wave == 4) cv = A.bias[1][lane];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
+    write_row_lds(wave + 1, xr);
+    if (bwave) halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
+
+    // ================= the chain: RCAB j = 0 .. NB-1, then the group conv =================
+    f32x4 acc[4][4];
+    const int khP2 = wave == 0 ? 2 : 0, khP3 = 2 - khP2;   // wave 0's upper halo row is read last
+    bool ok = true;
+    for (int j = 0; j <= NB; ++j) {
+        const bool gc = j == NB;
+        const int par = j & 1;
+        {
+            int ll = lane;
+            asm volatile("" : "+v"(ll));
+            q = ll >> 4, c16 = ll & 15, odd = q & 1;
+        }
+        if (j > 0) {
+            // ---- every strip of the image finished RCAB j-1 (partials, t/x rows published)
+            if (tid == 0) ok = ok && poll_ge(cnt, S * j);     // (after a timeout: no more waiting)
+            __syncthreads();
+            const int pp = (j - 1) & 1;
+            if (wave == 1) {
+                // the gate of RCAB j-1 (blocks.py:83-92): mean over the image from the S strip
+                // partials in strip order, FC1 -> ReLU -> FC2 -> sigmoid
+                // FC1 rows jj >= Cr read past fc1's end: 0, so hid_jj = 0 and FC2's columns
+                // k >= Cr (finite values of the next rows, or 0 past the end) drop out
+                const int Cr = A.Cr, jj = lane & 15, qq = lane >> 4;
+                const __amdgpu_buffer_rsrc_t f1r =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)A.fc1[j - 1], 0, Cr * 64 * 4, 0x00020000);
+                const __amdgpu_buffer_rsrc_t f2r =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)A.fc2[j - 1], 0, Cr * 64 * 4, 0x00020000);
+                float w1v[16], w2v[16], pv[16];
+#pragma unroll
+                for (int k4 = 0; k4 < 16; k4 += 4) {
+                    const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                    f1r, (jj * 64 + 16 * qq + k4) * 4, 0, 0));
+                    w1v[k4] = a.x, w1v[k4 + 1] = a.y, w1v[k4 + 2] = a.z, w1v[k4 + 3] = a.w;
+                }
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    w2v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(f2r, (lane * Cr + k) * 4, 0, 0));
+                // strips past S read past the buffer's end: 0 (range-checked buffer loads)
+                const int pbase = (int)(L.part + ((size_t)(im * 2 + pp) * S) * 64 * 4) + lane * 4;
+                const int pend = (int)(L.part + ((size_t)(im * 2 + pp) * S + S) * 64 * 4);
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    const int off = pbase + s * 256;
+                    pv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, off < pend ? off : 0x7ffffff0, 0, 16));
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                float msum = 0.f;
+#pragma unroll
+                for (int s = 0; s < 16; ++s) msum += pv[s];
+                const float mean = msum * A.inv_hw;
+                scr[lane] = mean;
+                float h = 0.f;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) h += w1v[k] * scr[16 * qq + k];
+                h += __shfl_xor(h, 16, 64);
+                h += __shfl_xor(h, 32, 64);
+                const float hid = fmaxf(h, 0.f);
+                float z = 0.f;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) z += w2v[k] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hid), k));
+                const float sg = 1.f / (1.f + expf(-z));
+                gate[lane] = sg * A.res_scale;
+                if (strip == 0 && A.s_out[j - 1]) A.s_out[j - 1][im * 64 + lane] = sg;
+            }
+            if (wave >= 2 && wave <= 4) {                   // the constants of this conv's epilogue
+                const float* src = gc ? (wave == 4 ? A.bias[2 * NB] : nullptr)
+                                      : (wave == 2 ? A.bias[2 * j] : wave == 3 ? A.alpha[j] : A.bias[2 * j + 1]);
+                cv = src ? src[lane] : 0.f;
+            }
+            uint4 nx[8], nt[8];
+            if (bwave) {                                    // the neighbour's x_{j-1}, t_{j-1} row
+                const int ox = rowoff(L.bx, nb_strip, pp, 1 - side), ot = rowoff(L.bt, nb_strip, pp, 1 - side);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int i = lane + 64 * k;
+                    nx[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ox + i * 16, 0, 16));
+                    nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + i * 16, 0, 16));
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (also this conv's taps, long issued)
+            if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
+            __syncthreads();
+            // ---- x_j = x_{j-1} + rs * s * t_{j-1} (t as stored: rounded), own row in registers
+            float g[4][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float4 gv = *(const float4*)(gate + 16 * m + 4 * q);
+                g[m][0] = gv.x, g[m][1] = gv.y, g[m][2] = gv.z, g[m][3] = gv.w;
+            }
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const float x0 = lo16<T>(xr[m][p].x), x1 = hi16<T>(xr[m][p].x);
+                    const float x2 = lo16<T>(xr[m][p].y), x3 = hi16<T>(xr[m][p].y);
+                    xr[m][p] = pk4<T>(rnd16<T>(acc[m][p][0]) * g[m][0] + x0, rnd16<T>(acc[m][p][1]) * g[m][1] + x1,
+                                      rnd16<T>(acc[m][p][2]) * g[m][2] + x2, rnd16<T>(acc[m][p][3]) * g[m][3] + x3);
+                }
+            write_row_lds(wave + 1, xr);
+            if (bwave) {                                    // the halo row of x_j, same arithmetic
+                const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
+                const float4 gb = *(const float4*)(gate + (lane & 7) * 8 + 4);
+                const float g8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    float xf[8], tf[8], yv[8];
+                    unpack16<T>(nx[k], xf);
+                    unpack16<T>(nt[k], tf);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) yv[e] = tf[e] * g8[e] + xf[e];
+                    hv[k] = pack16<T>(yv);
+                }
+                halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
+            }
+        }
+        // x_j's boundary rows for the neighbours (their halo rows of x_{j+1})
+        if (!gc && bwave) store_row(wsr, rowoff(L.bx, strip, par, side), xr, 16);
+
+        // ================= conv1 (or the group conv): 3 phases =================
+        const int ci = gc ? 2 * NB : 2 * j;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();                                    // image + constants; this conv's taps landed
+        conv_phase<T>(acc, img, filt, 1, wave, q, c16);
+        __syncthreads();                                    // kh = 1 slots free
+        if (!gc) issue_kh1(ci + 1);
+        conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
+        conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
+        if (gc) {
+            // ---- out = conv + bias + the group input (blocks.py:188-189): its own rows read
+            // again here (once per launch; kept out of the conv's register peak)
+            uint2 x0r[4][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    x0r[m][p] = *(const uint2*)((const char*)A.x + px_off(r0 + wave, p) + (16 * m + 4 * q) * 2);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint2 ov[4][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float4 bb = *(const float4*)(cst + 128 + 16 * m + 4 * q);
+                const float bia[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    float v[4];
+                    v[0] = acc[m][p][0] + bia[0] + lo16<T>(x0r[m][p].x);
+                    v[1] = acc[m][p][1] + bia[1] + hi16<T>(x0r[m][p].x);
+                    v[2] = acc[m][p][2] + bia[2] + lo16<T>(x0r[m][p].y);
+                    v[3] = acc[m][p][3] + bia[3] + hi16<T>(x0r[m][p].y);
+                    ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
+                }
+            }
+            const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(A.y, 0, (int)act_bytes, 0x00020000);
+            store_row(yrs, (int)((size_t)(im * H + r0 + wave) * SW * 128), ov, 0);
+            break;
+        }
+        __syncthreads();                                    // everyone done with x_j in LDS; all slots free
+        issue_kh02(ci + 1);
+        // ---- conv1 epilogue: a1 = PReLU(conv1 + b1) -> LDS (own row), boundary rows out
+        {
+            uint2 av[4][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float4 bb = *(const float4*)(cst + 16 * m + 4 * q);
+                const float4 aa = *(const float4*)(cst + 64 + 16 * m + 4 * q);
+                const float bia[4] = {bb.x, bb.y, bb.z, bb.w}, alp[4] = {aa.x, aa.y, aa.z, aa.w};
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    float v[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[i] = prelu_f(acc[m][p][i] + bia[i], alp[i]);
+                    av[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
+                }
+            }
+            write_row_lds(wave + 1, av);
+            if (bwave) store_row(wsr, rowoff(L.ba, strip, par, side), av, 16);
+        }
+        // ================= conv2 =================
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
+        vm_wait_n(6 + (bwave ? 8 : 0));                     // conv2's kh = 1 taps (older than the rest)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();                                    // a1 image (own rows) complete
+        conv_phase<T>(acc, img, filt, 1, wave, q, c16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv2's other taps; the a1 boundary stores
+        __syncthreads();
+        if (tid == 0)                                       // a1's boundary rows of RCAB j are out
+            __hip_atomic_store(flg + (im * S + strip) * 32, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        issue_kh1(j + 1 < NB ? ci + 2 : 2 * NB);
+        conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
+        if (bwave) {
+            // the neighbour's a1 row -> this wave's private halo row (only this wave reads it)
+            ok = ok && poll_ge(flg + (im * S + nb_strip) * 32, j + 1);
+            const int oa = rowoff(L.ba, nb_strip, par, 1 - side);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                hv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, oa + (lane + 64 * k) * 16, 0, 16));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
+        // ---- conv2 epilogue: t = conv2 + b2 (kept in the accumulators), pool partials
+        float ps[4][4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 bb = *(const float4*)(cst + 128 + 16 * m + 4 * q);
+            const float bia[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float s = 0.f;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    acc[m][p][i] += bia[i];
+                    s += acc[m][p][i];
+                }
+                ps[m][i] = s;
+            }
+        }
+        __syncthreads();                                    // every wave done with the a1 image, slots free
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float s = group16_sum(ps[m][i]);
+                if (c16 == 0) red[wave * 64 + 16 * m + 4 * q + i] = s;
+            }
+        if (bwave) {                                        // t_j's boundary row (as stored: rounded)
+            uint2 tv[4][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) tv[m][p] = pk4<T>(acc[m][p][0], acc[m][p][1], acc[m][p][2], acc[m][p][3]);
+            store_row(wsr, rowoff(L.bt, strip, par, side), tv, 16);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (wave == 0) {                                    // the strip's partial, rows in order
+            float s = 0.f;
+#pragma unroll
+            for (int w = 0; w < SR; ++w) s += red[w * 64 + lane];
+            const int off = (int)(L.part + ((size_t)(im * 2 + par) * S + strip) * 64 * 4) + lane * 4;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), wsr, off, 0, 16);
+        }
+        // the next conv's remaining taps (its kh = 1 taps went out at phase 2)
+        issue_kh02(j + 1 < NB ? ci + 2 : 2 * NB);
+        // every storing wave's stores (t row, partial) done before the signal
+        vm_wait_n(6);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- the last block out resets the counters for the next launch
+    if (!ok) __hip_atomic_fetch_or(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int nblk = B * S;
+        if (__hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
+            for (int b = 0; b < B; ++b)
+                __hip_atomic_store((int*)(A.work + L.cnt) + b * 32, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int i = 0; i < B * S; ++i) __hip_atomic_store(flg + i * 32, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+int g_gs_cus = 0;
+int gs_num_cus() {
+    if (g_gs_cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_gs_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_gs_cus <= 0) g_gs_cus = 256;
+    }
+    return g_gs_cus;
+}
+
+template <typename T>
+void launch_gs(const GsArgs& a, int grid, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_group_strip<T>, hipFuncAttributeMaxDynamicSharedMemorySize, GS_LDS);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_group_strip<T>, dim3(grid), dim3(512), GS_LDS, s, a);
+}
+
+}  // namespace
+
+extern "C" int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int nb) {
+    if ((dtype != FEN_BF16 && dtype != FEN_F16) || C != 64 || W != SW || H <= 0 || H % SR || H / SR > 16 || B <= 0 ||
+        Cr <= 0 || Cr > 16 || nb <= 0 || nb > FEN_GS_MAXNB)
+        return 0;
+    if ((size_t)B * H * W * 128 >= (size_t)0x7fff0000) return 0;      // 32-bit buffer offsets
+    if (ws_layout(B, H / SR).total >= (size_t)0x7fff0000) return 0;
+    return 1;
+}
+
+extern "C" size_t fen_group_strip_work_bytes(int B, int H) { return ws_layout(B, H / SR).total; }
+
+extern "C" int fen_group_strip(const fen_group_strip_desc* d, void* stream) {
+    if (!d || !d->x || !d->y || !d->work) return FEN_EINVAL;
+    if (!fen_group_strip_supported(d->dtype, d->B, d->H, d->W, d->C, d->Cr, d->nb)) return FEN_EUNSUPPORTED;
+    if (d->work_bytes < fen_group_strip_work_bytes(d->B, d->H)) return FEN_EINVAL;
+    GsArgs a{};
+    a.B = d->B, a.H = d->H, a.S = d->H / SR, a.NB = d->nb, a.Cr = d->Cr;
+    a.res_scale = d->res_scale, a.inv_hw = 1.0f / (float)(d->H * d->W);
+    a.x = d->x, a.y = d->y, a.work = (char*)d->work;
+    for (int j = 0; j < d->nb; ++j) {
+        if (!d->w1[j] || !d->b1[j] || !d->alpha[j] || !d->w2[j] || !d->b2[j] || !d->fc1[j] || !d->fc2[j])
+            return FEN_EINVAL;
+        a.w[2 * j] = d->w1[j], a.bias[2 * j] = d->b1[j];
+        a.w[2 * j + 1] = d->w2[j], a.bias[2 * j + 1] = d->b2[j];
+        a.alpha[j] = d->alpha[j], a.fc1[j] = d->fc1[j], a.fc2[j] = d->fc2[j], a.s_out[j] = d->s_out[j];
+    }
+    if (!d->wg || !d->bg) return FEN_EINVAL;
+    a.w[2 * d->nb] = d->wg, a.bias[2 * d->nb] = d->bg;
+    const int grid = d->B * (d->H / SR);
+    (void)gs_num_cus();
+    hipStream_t s = (hipStream_t)stream;
+    if (d->dtype == FEN_F16) launch_gs<f16>(a, grid, s);
+    else launch_gs<bf16>(a, grid, s);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}

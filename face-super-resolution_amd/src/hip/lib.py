@@ -68,6 +68,20 @@ class RcabBwdDesc(Structure):
     ]
 
 
+GS_MAXNB = 20   # FEN_GS_MAXNB
+
+
+class GroupStripDesc(Structure):
+    _fields_ = [
+        ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("Cr", c_int), ("nb", c_int),
+        ("res_scale", c_float), ("x", c_void_p), ("y", c_void_p),
+        ("w1", c_void_p * GS_MAXNB), ("b1", c_void_p * GS_MAXNB), ("alpha", c_void_p * GS_MAXNB),
+        ("w2", c_void_p * GS_MAXNB), ("b2", c_void_p * GS_MAXNB), ("fc1", c_void_p * GS_MAXNB),
+        ("fc2", c_void_p * GS_MAXNB), ("s_out", c_void_p * GS_MAXNB),
+        ("wg", c_void_p), ("bg", c_void_p), ("work", c_void_p), ("work_bytes", c_size_t),
+    ]
+
+
 class WgradDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
@@ -87,6 +101,9 @@ _SIGS = {
     "fen_rcab_deferred": (c_int, [POINTER(RcabDeferredDesc), c_void_p]),
     "fen_rcab_bwd": (c_int, [POINTER(RcabBwdDesc), c_void_p]),
     "fen_rcab_group_end": (c_int, [POINTER(RcabDeferredDesc)] + [c_void_p] * 5),
+    "fen_group_strip_supported": (c_int, [c_int] * 7),
+    "fen_group_strip_work_bytes": (c_size_t, [c_int, c_int]),
+    "fen_group_strip": (c_int, [POINTER(GroupStripDesc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
     "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),

@@ -58,6 +58,10 @@ RCAB_MODE = os.environ.get("FEN_RCAB", "deferred")
 # a ResidualGroup's end on the deferred path: the last RCAB's gate + residual and the group conv
 # in one fen_rcab_group_end launch ('fused', default) or fen_se_fused + fen_conv3x3 ('split')
 GROUP_END_FUSED = os.environ.get("FEN_GROUP_END", "fused") != "split"
+# inference: a whole ResidualGroup as ONE persistent strip-resident launch (fen_group_strip,
+# group_strip.hip) where its envelope holds (16-bit, 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP=0
+# selects the per-RCAB deferred launches
+GROUP_STRIP = os.environ.get("FEN_GROUP_STRIP", "1") != "0"
 # RCAB backward: the SE backward and its apply as one fen_se_bwd_fused launch (default) or
 # the fen_se_bwd + fen_se_bwd_apply pair (FEN_SE_BWD=pair; shapes outside the fused
 # kernel's envelope always take the pair)
@@ -391,11 +395,50 @@ class Forward:
                  ptr(prev["s"]), ptr(prev["t"]), s.res_scale, ptr(prev["x"]), ptr(y))
         return y, saved
 
+    def _strip_ok(self, x) -> bool:
+        B, H, W, C = x.shape
+        return (GROUP_STRIP and not self.save and self.s.NB > 0 and
+                bool(self.ctx.lib.fen_group_strip_supported(self.ctx.code, B, H, W, C, self.s.Cr, self.s.NB)))
+
+    def _group_strip(self, x: torch.Tensor, pre: str, names: Sequence[str], y: torch.Tensor) -> dict:
+        """The whole group in one fen_group_strip launch (inference): y = conv(chain(x)) + b + x."""
+        s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
+        B, H, W, C = x.shape
+        d = L.GroupStripDesc()
+        d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.nb = ctx.code, B, H, W, C, s.Cr, s.NB
+        d.res_scale = float(s.res_scale)
+        d.x, d.y = ptr(x), ptr(y)
+        blocks = []
+        for b in range(s.NB):
+            q = f"{pre}blocks.{b}."
+            ca = q + "channel_attention.fc."
+            d.w1[b], d.b1[b] = ptr(Wt.packed(q + "conv1", 0)), ptr(p[q + "conv1.bias"])
+            d.alpha[b] = ptr(p[q + "prelu.weight"])
+            d.w2[b], d.b2[b] = ptr(Wt.packed(q + "conv2", 0)), ptr(p[q + "conv2.bias"])
+            d.fc1[b], d.fc2[b] = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
+            sg = None
+            if self.attn is not None:
+                sg = ctx.alloc((B, C), torch.float32)
+                self.attn[names[b]] = sg
+                d.s_out[b] = ptr(sg)
+            blocks.append(dict(s=sg))
+        d.wg, d.bg = ptr(Wt.packed(pre + "conv", 0)), ptr(p[pre + "conv.bias"])
+        nbytes = int(ctx.lib.fen_group_strip_work_bytes(B, H))
+        work = ctx.persistent_zeros(f"group_strip/{B}x{H}", nbytes)
+        d.work, d.work_bytes = ptr(work), nbytes
+        ctx.emit("group_strip", ctx.lib.fen_group_strip, byref(d))
+        ctx.keep(d)
+        return dict(blocks=blocks, x=x, x_last=None)
+
     def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None, pre: Optional[str] = None):
         """ResidualGroup (blocks.py:185-189) -> (y, saved)."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
         pre = f"residual_groups.{g}." if pre is None else pre
+        if self._strip_ok(x):
+            y = out if out is not None and out.data_ptr() != x.data_ptr() else ctx.alloc(x.shape)
+            names = [f"group{g}_rcab{b}" for b in range(s.NB)]
+            return y, self._group_strip(x, pre, names, y)
         if self._deferred_ok(x) and s.NB > 0:
             pres = [f"{pre}blocks.{b}." for b in range(s.NB)]
             names = [f"group{g}_rcab{b}" for b in range(s.NB)]

@@ -75,6 +75,18 @@ class Ctx:
             self._scratch[key] = buf
         return buf[:n].view(tuple(shape))
 
+    def persistent_zeros(self, tag: str, nbytes: int) -> torch.Tensor:
+        """A zero-initialised byte buffer that outlives this context (kept in the shared state of
+        the eager contexts, or in the program): self-resetting sync workspaces."""
+        key = f"pz:{tag}"
+        buf = self._shared.get(key)
+        if buf is None or buf.numel() < nbytes:
+            if buf is not None:
+                self._hold.append(buf)
+            buf = torch.zeros(int(nbytes), dtype=torch.uint8, device=self.device)
+            self._shared[key] = buf
+        return buf
+
     def keep(self, obj) -> None:
         """Keep a host object (e.g. a ctypes job table) alive as long as the program."""
         self._hold.append(obj)

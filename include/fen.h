@@ -222,6 +222,41 @@ int fen_rcab_deferred(const fen_rcab_deferred_desc* d, void* stream);
 int fen_rcab_group_end(const fen_rcab_deferred_desc* d, const void* w, const float* bias, const void* res,
                        void* out, void* stream);
 
+/* A whole ResidualGroup in ONE persistent launch (ResidualGroup.forward, blocks.py:185-189:
+ * nb x RCAB.forward blocks.py:135-153 with ChannelAttention blocks.py:83-92, then the group
+ * conv and the group's skip), inference.  Each image is cut into H/8 strips of 8 rows x 64
+ * columns; one block (one CU) keeps its strip resident (x_j in registers, x_j / a1 and the
+ * running conv's filter in LDS) for all nb RCABs; the strips of an image exchange only the SE
+ * pool partials and their first / last rows (sc1 hand-offs through `work`).  y may not alias x.
+ * 16-bit NHWC, C = 64, W = 64, H a multiple of 8 (<= 128), Cr <= 16, nb <= FEN_GS_MAXNB.
+ * `work`: fen_group_strip_work_bytes(B, H) bytes, ZEROED once before the first launch; the
+ * kernel leaves its counters at zero (graph-replayable), and sets the int at byte 8 to nonzero
+ * if a hand-off wait timed out (then the output is invalid).  Grid = B * H/8 blocks, taken in
+ * start order (no co-residency assumption).                                                 */
+#define FEN_GS_MAXNB 20
+typedef struct {
+    int dtype;                 /* FEN_BF16 or FEN_F16                                          */
+    int B, H, W, C, Cr, nb;
+    float res_scale;           /* 0.2                                                          */
+    const void* x;             /* group input NHWC [B,H,64,64]                                 */
+    void* y;                   /* group output NHWC (conv(chain(x)) + bias + x)                */
+    const void* w1[FEN_GS_MAXNB];      /* per RCAB: conv1 packed mode 0 [9][64][64]           */
+    const float* b1[FEN_GS_MAXNB];
+    const float* alpha[FEN_GS_MAXNB];  /* PReLU [64]                                           */
+    const void* w2[FEN_GS_MAXNB];      /* conv2 packed mode 0                                  */
+    const float* b2[FEN_GS_MAXNB];
+    const float* fc1[FEN_GS_MAXNB];    /* channel_attention.fc.0.weight [Cr][64]               */
+    const float* fc2[FEN_GS_MAXNB];    /* channel_attention.fc.2.weight [64][Cr]               */
+    float* s_out[FEN_GS_MAXNB];        /* optional: each RCAB's gate s [B][64] (or NULL)       */
+    const void* wg;            /* the group conv, packed mode 0                                */
+    const float* bg;
+    void* work;
+    size_t work_bytes;
+} fen_group_strip_desc;
+int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
+size_t fen_group_strip_work_bytes(int B, int H);
+int fen_group_strip(const fen_group_strip_desc* d, void* stream);
+
 /* The RCAB backward's two data gradients in one launch (autograd of blocks.py:145-147):
  *   dz1 = conv2^T(dt) * PReLU'(z1),  dalpha_part[b][tile][c] = sum over the tile of
  *   conv2^T(dt) * z1 * (z1 <= 0),  dx = conv1^T(dz1) + dy,

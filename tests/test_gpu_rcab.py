@@ -385,7 +385,7 @@ def test_rcab_bwd_se_fold_vs_oracle(prec, B, H, W):
     tol, tolp = (3e-3, 5e-3) if prec == "bf16" else (1e-3, 2e-3)
     rel = lambda a_, b_: float((a_.double() - b_.double()).norm() / b_.double().norm())
     nc = lambda t: t.float().cpu().permute(0, 3, 1, 2)
-    assert rel(nc(dt), dt_ref) <= tol / 2
+    assert rel(nc(dt), dt_ref) <= tol      # one 16-bit rounding of dt (bf16: ~1.7e-3 rel-L2)
     # the FC weight-gradient rows: the per-image rows for every image (summed by the caller)
     assert rel(dw2p.cpu().view(B, C, Cr), dw2_ref) <= 1e-4
     assert rel(dw1p.cpu().view(B, Cr, C), dw1_ref) <= 1e-4
