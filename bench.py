@@ -21,11 +21,11 @@ Also reported (field "train"): the stage-1 generator training step (bicubic /4 L
 synthesis, forward, L1, backward, RCCL gradient all-reduce over xGMI for N>1, clip,
 AdamW) at batch 32 per GPU -- the DP path of the north star.
 
-roofline: the dominant kernel is the deferred-gate RCAB k_rcab_d (the previous RCAB's SE gate
-  and scaled residual applied to the input halo, conv1 -> PReLU -> conv2 -> tile sums, 64 ch,
-  64x64, B=32): algorithmic FLOPs per launch = 2 convs x 2 * 32*64*64 px * 64 co * 576 (= 9 taps
-  * 64 ci) = 19.33 GFLOP, timed live here with HIP events on the launch stream; peak = 2500
-  TFLOP/s fp16 / bf16 dense.
+roofline: the dominant kernel is k_group_strip (group_strip.hip): one ResidualGroup -- 10 fused
+  RCABs (conv1 -> PReLU -> conv2 -> SE gate -> scaled residual) + the group conv + skip, 64 ch,
+  64x64, B=32 -- as one persistent launch; algorithmic FLOPs per launch = 21 convs x 2 *
+  32*64*64 px * 64 co * 576 (= 9 taps * 64 ci) = 203 GFLOP (9.66 per conv, 19.33 per RCAB),
+  timed live here with HIP events on the launch stream; peak = 2500 TFLOP/s fp16 / bf16 dense.
 pcie_inclusive: the same forward with the batch handed over as NCHW fp32 pinned host buffers
 (H2D of the LR batch, graph replay, D2H of the SR batch, serial on one stream) -- reported
 beside `value`, never as it.
@@ -109,10 +109,16 @@ def timed(fn, steps, warmup, world):
 
 
 def dominant_op(engine):
-    """The launch the roofline is quoted on: an RCAB of the chain (fen_rcab_deferred: gate of
-    the previous RCAB applied to its input, conv1 + PReLU + conv2 + tile sums; one with a
-    deferred input, i.e. not a group's first), else the RCAB conv1 (64->64, 64x64, B=32) of
-    the per-op path."""
+    """The launch the roofline is quoted on: a whole ResidualGroup (fen_group_strip: NB fused
+    RCABs -- conv1 + PReLU + conv2 + SE gate + scaled residual each -- and the group conv, one
+    persistent launch; algorithmic FLOPs = (2 NB + 1) 64->64 convs), else an RCAB of the per-RCAB
+    chain (fen_rcab_deferred), else the RCAB conv1 (64->64, 64x64, B=32) of the per-op path."""
+    for op in engine.ctx.ops:
+        if op[0] == "group_strip":
+            d = op[2][0]._obj
+            conv = 2.0 * d.B * d.H * d.W * 64 * 576
+            return op, "k_group_strip (a ResidualGroup in one launch: %d x [conv1+PReLU+conv2+SE gate+residual] + " \
+                       "group conv + skip, 64ch %dx%d, B=%d)" % (d.nb, d.H, d.W, d.B), (2 * d.nb + 1) * conv
     for op in engine.ctx.ops:
         if op[0] == "rcab_deferred":
             d = op[2][0]._obj
@@ -409,7 +415,8 @@ def main():
         "roofline": {"bound": "mfma", "kernel": kern_label,
                      "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "kernel_ms": round(kern_ms, 5),
-                     "flop_per_launch": kern_flop, "traffic": load_traffic(kern_label)},
+                     "flop_per_launch": kern_flop, "traffic": load_traffic(kern_label),
+                     "per_rcab_us_equiv": round(kern_ms * 1e3 * RCAB_CONV_FLOP * 2 / kern_flop, 3)},
     }
     out["pcie_inclusive"] = time_pcie_inclusive(eng, x, args.steps, args.warmup, world)
     del eng

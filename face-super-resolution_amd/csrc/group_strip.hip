@@ -50,7 +50,15 @@ constexpr int O_RED = O_FILT + 9 * TAPB;      // [8 waves][64] f32 pool partials
 constexpr int O_CST = O_RED + 8 * 64 * 4;     // b1 [64], alpha [64], b2 [64] (group conv: bias in b2)
 constexpr int O_GATE = O_CST + 3 * 64 * 4;    // [64] f32: rs * s of the last RCAB
 constexpr int O_SCR = O_GATE + 64 * 4;        // mean [64], ticket word
+#ifdef FEN_STAMPS
+// diagnostic build only (tools/stamp_strip.py): s_memrealtime stamps of waves 0 and 1 in LDS,
+// copied to the workspace's tail at the end; no stamp executes in the product build
+constexpr int NSTAMP = 96;
+constexpr int O_STAMP = O_SCR + 80 * 4;
+constexpr int GS_LDS = O_STAMP + 2 * NSTAMP * 4;
+#else
 constexpr int GS_LDS = O_SCR + 80 * 4;
+#endif
 static_assert(GS_LDS <= 163840, "LDS budget");
 static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignment");
 
@@ -58,6 +66,19 @@ constexpr int ROWB = SW * 128;                // one strip row, 8 KB
 constexpr int SPIN_MAX = 1 << 20;             // polls (~1.5 us each) before a wait gives up
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+#ifdef FEN_STAMPS
+#define GSTAMP(i)                                                                              \
+    do {                                                                                       \
+        unsigned long long _rt;                                                                \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt)::"memory");        \
+        if (wave < 2 && lane == 0 && (i) < NSTAMP) stamp_lds[wave * NSTAMP + (i)] = (unsigned)_rt; \
+    } while (0)
+#else
+#define GSTAMP(i) \
+    do {          \
+    } while (0)
+#endif
 
 // workspace: control words, counters, pool partials, boundary rows
 struct Ws {
@@ -74,6 +95,9 @@ __host__ __device__ inline Ws ws_layout(int B, int S) {
     L.bx = o; o += rows;
     L.bt = o; o += rows;
     L.ba = o; o += rows;
+#ifdef FEN_STAMPS
+    o += (size_t)B * S * 2 * NSTAMP * 4;            // [block ticket][wave 0, 1][NSTAMP] u32
+#endif
     L.total = o;
     return L;
 }
@@ -175,6 +199,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     float* gate = (float*)(smem + O_GATE);
     float* scr = (float*)(smem + O_SCR);
     int* tick_lds = (int*)(scr + 64);
+#ifdef FEN_STAMPS
+    unsigned* stamp_lds = (unsigned*)(smem + O_STAMP);
+#endif
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = wave_id();
@@ -193,6 +220,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     for (int i = tid; i < IMG_BYTES / 16; i += 512) *(uint4*)(img + i * 16) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     const int ticket = __builtin_amdgcn_readfirstlane(*tick_lds);
+    GSTAMP(0);
     const int im = ticket / S, strip = ticket - im * S;
     const int r0 = strip * SR;
     const bool has_up = strip > 0, has_dn = strip + 1 < S;
@@ -293,6 +321,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
     write_row_lds(wave + 1, xr);
     if (bwave) halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
+    GSTAMP(1);
 
     // ================= the chain: RCAB j = 0 .. NB-1, then the group conv =================
     f32x4 acc[4][4];
@@ -308,8 +337,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         }
         if (j > 0) {
             // ---- every strip of the image finished RCAB j-1 (partials, t/x rows published)
+            GSTAMP(2 + 8 * j);
             if (tid == 0) ok = ok && poll_ge(cnt, S * j);     // (after a timeout: no more waiting)
             __syncthreads();
+            GSTAMP(3 + 8 * j);
             const int pp = (j - 1) & 1;
             if (wave == 1) {
                 // the gate of RCAB j-1 (blocks.py:83-92): mean over the image from the S strip
@@ -419,12 +450,14 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
 #pragma unroll
             for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GSTAMP(4 + 8 * j);
         __syncthreads();                                    // image + constants; this conv's taps landed
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);
         __syncthreads();                                    // kh = 1 slots free
         if (!gc) issue_kh1(ci + 1);
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
+        GSTAMP(5 + 8 * j);
         if (gc) {
             // ---- out = conv + bias + the group input (blocks.py:188-189): its own rows read
             // again here (once per launch; kept out of the conv's register peak)
@@ -482,6 +515,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
         vm_wait_n(6 + (bwave ? 8 : 0));                     // conv2's kh = 1 taps (older than the rest)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GSTAMP(6 + 8 * j);
         __syncthreads();                                    // a1 image (own rows) complete
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv2's other taps; the a1 boundary stores
@@ -501,7 +535,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
+        GSTAMP(7 + 8 * j);
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
+        GSTAMP(8 + 8 * j);
         // ---- conv2 epilogue: t = conv2 + b2 (kept in the accumulators), pool partials
         float ps[4][4];
 #pragma unroll
@@ -550,7 +586,16 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         vm_wait_n(6);
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        GSTAMP(9 + 8 * j);
     }
+    GSTAMP(NSTAMP - 1);
+#ifdef FEN_STAMPS
+    __syncthreads();
+    if (wave < 2) {
+        unsigned* dst = (unsigned*)(A.work + L.ba + (size_t)B * S * 2 * 2 * ROWB) + ((size_t)ticket * 2 + wave) * NSTAMP;
+        for (int i = lane; i < NSTAMP; i += 64) dst[i] = stamp_lds[wave * NSTAMP + i];
+    }
+#endif
     // ---- the last block out resets the counters for the next launch
     if (!ok) __hip_atomic_fetch_or(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
