@@ -39,7 +39,7 @@ namespace {
         asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"                 \
                      : "=s"(_rt), "=s"(_mt)::"memory");                                       \
         __builtin_amdgcn_sched_barrier(0);                                                    \
-        if ((threadIdx.x & 63) == 0 && (i) < 16) {                                            \
+        if (d.loss_part && (threadIdx.x & 63) == 0 && (i) < 16) {    /* never through NULL */    \
             unsigned long long* _p =                                                          \
                 (unsigned long long*)d.loss_part + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 32; \
             _p[2 * (i)] = _rt;                                                                \

@@ -50,8 +50,8 @@ constexpr int O_RED = O_FILT + 9 * TAPB;      // [8 waves][64] f32 pool partials
 constexpr int O_CST = O_RED + 8 * 64 * 4;     // b1 [64], alpha [64], b2 [64] (group conv: bias in b2)
 constexpr int O_GATE = O_CST + 3 * 64 * 4;    // [64] f32: rs * s of the last RCAB
 constexpr int O_SCR = O_GATE + 64 * 4;        // mean [64], ticket word
-#ifdef FEN_STAMPS
-// diagnostic build only (tools/stamp_strip.py): s_memrealtime stamps of waves 0 and 1 in LDS,
+#ifdef FEN_GS_STAMPS
+// diagnostic build only (-DFEN_GS_STAMPS, `make gsstamp`, tools/stamp_strip.py): s_memrealtime stamps of waves 0 and 1 in LDS,
 // copied to the workspace's tail at the end; no stamp executes in the product build
 constexpr int NSTAMP = 96;
 constexpr int O_STAMP = O_SCR + 80 * 4;
@@ -67,7 +67,7 @@ constexpr int SPIN_MAX = 1 << 20;             // polls (~1.5 us each) before a w
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
-#ifdef FEN_STAMPS
+#ifdef FEN_GS_STAMPS
 #define GSTAMP(i)                                                                              \
     do {                                                                                       \
         unsigned long long _rt;                                                                \
@@ -95,7 +95,7 @@ __host__ __device__ inline Ws ws_layout(int B, int S) {
     L.bx = o; o += rows;
     L.bt = o; o += rows;
     L.ba = o; o += rows;
-#ifdef FEN_STAMPS
+#ifdef FEN_GS_STAMPS
     o += (size_t)B * S * 2 * NSTAMP * 4;            // [block ticket][wave 0, 1][NSTAMP] u32
 #endif
     L.total = o;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     float* gate = (float*)(smem + O_GATE);
     float* scr = (float*)(smem + O_SCR);
     int* tick_lds = (int*)(scr + 64);
-#ifdef FEN_STAMPS
+#ifdef FEN_GS_STAMPS
     unsigned* stamp_lds = (unsigned*)(smem + O_STAMP);
 #endif
 
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         GSTAMP(9 + 8 * j);
     }
     GSTAMP(NSTAMP - 1);
-#ifdef FEN_STAMPS
+#ifdef FEN_GS_STAMPS
     __syncthreads();
     if (wave < 2) {
         unsigned* dst = (unsigned*)(A.work + L.ba + (size_t)B * S * 2 * 2 * ROWB) + ((size_t)ticket * 2 + wave) * NSTAMP;

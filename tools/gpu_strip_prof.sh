@@ -3,7 +3,7 @@
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof3
-FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_stamp.so timeout -k 10 200 python tools/stamp_strip.py > gpurun_out/prof3/stamps.txt 2>&1
+FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so timeout -k 10 200 python tools/stamp_strip.py > gpurun_out/prof3/stamps.txt 2>&1
 echo "stamps rc=$?"; cat gpurun_out/prof3/stamps.txt | tail -25
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3/inf -o run --output-format csv -- \
     python bench.py --no-train --no-stress --no-cpu-baseline > gpurun_out/prof3/inf_bench.log 2>&1

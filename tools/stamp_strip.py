@@ -1,7 +1,7 @@
 """Phase timeline of k_group_strip from the diagnostic stamp build (s_memrealtime, 100 MHz).
 
-    make -C face-super-resolution_amd/csrc stamp
-    FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_stamp.so python tools/stamp_strip.py
+    make -C face-super-resolution_amd/csrc gsstamp
+    FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so python tools/stamp_strip.py
 
 Runs the inference engine (fp16, B=32, 64x64) a few times and reads the last group launch's
 stamps from the workspace tail: waves 0 and 1 of every block, 96 slots.  Per RCAB j the slots are
