@@ -53,9 +53,9 @@ constexpr int O_SCR = O_GATE + 64 * 4;        // mean [64], ticket word
 #ifdef FEN_GS_STAMPS
 // diagnostic build only (-DFEN_GS_STAMPS, `make gsstamp`, tools/stamp_strip.py): s_memrealtime stamps of waves 0 and 1 in LDS,
 // copied to the workspace's tail at the end; no stamp executes in the product build
-constexpr int NSTAMP = 96;
+constexpr int NSTAMP = 100;
 constexpr int O_STAMP = O_SCR + 80 * 4;
-constexpr int GS_LDS = O_STAMP + 2 * NSTAMP * 4;
+constexpr int GS_LDS = O_STAMP + 8 * NSTAMP * 2;
 #else
 constexpr int GS_LDS = O_SCR + 80 * 4;
 #endif
@@ -72,7 +72,7 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     do {                                                                                       \
         unsigned long long _rt;                                                                \
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt)::"memory");        \
-        if (wave < 2 && lane == 0 && (i) < NSTAMP) stamp_lds[wave * NSTAMP + (i)] = (unsigned)_rt; \
+        if (lane == 0 && (i) < NSTAMP) stamp_lds[wave * NSTAMP + (i)] = (unsigned short)((unsigned)_rt - t_start); \
     } while (0)
 #else
 #define GSTAMP(i) \
@@ -86,17 +86,17 @@ struct Ws {
 };
 __host__ __device__ inline Ws ws_layout(int B, int S) {
     Ws L;
-    size_t o = 256;                          // [0] ticket [1] done [2] error
-    L.cnt = o;  o += (size_t)B * 128;        // one counter per image, own 128-B line
-    L.flg = o;  o += (size_t)B * S * 128;    // one a1 flag per strip, own line
-    L.part = o; o += (size_t)B * 2 * S * 64 * 4;
+    size_t o = 256;                          // [0] ticket [1] done [2] error [3] launch epoch
+    L.cnt = o;
+    L.flg = o;  o += (size_t)B * S * 4 * 128;  // per (strip, side, kind) a flag on its own line
+    L.part = o; o += (size_t)B * 2 * S * 64 * 8;   // [img][parity][strip][64] {tag, value} granules
     o = (o + 255) & ~(size_t)255;
     const size_t rows = (size_t)B * S * 2 * 2 * ROWB;   // [img][strip][parity][side] rows
     L.bx = o; o += rows;
     L.bt = o; o += rows;
     L.ba = o; o += rows;
 #ifdef FEN_GS_STAMPS
-    o += (size_t)B * S * 2 * NSTAMP * 4;            // [block ticket][wave 0, 1][NSTAMP] u32
+    o += (size_t)B * S * 8 * NSTAMP * 2;            // [block ticket][wave][NSTAMP] u16 (10 ns ticks)
 #endif
     L.total = o;
     return L;
@@ -136,11 +136,11 @@ __device__ __forceinline__ uint4 pair16(uint2 lo, uint2 hi, bool odd) {
 }
 __device__ __forceinline__ int chunk_of(int mp, int q) { return 4 * mp + ((q & 1) ? 2 : 0) + (q >> 1); }
 
-// bounded poll of an agent-scope counter (sc1 loads): true if it reached `target`
-__device__ __forceinline__ bool poll_ge(const int* p, int target) {
+// bounded poll of an agent-scope flag (sc1 loads): true once it holds `tag`
+__device__ __forceinline__ bool poll_eq(const unsigned* p, unsigned tag) {
     for (int it = 0; it < SPIN_MAX; ++it) {
-        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-        __builtin_amdgcn_s_sleep(2);
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag) return true;
+        __builtin_amdgcn_s_sleep(1);
     }
     return false;
 }
@@ -200,39 +200,61 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     float* scr = (float*)(smem + O_SCR);
     int* tick_lds = (int*)(scr + 64);
 #ifdef FEN_GS_STAMPS
-    unsigned* stamp_lds = (unsigned*)(smem + O_STAMP);
+    unsigned short* stamp_lds = (unsigned short*)(smem + O_STAMP);
 #endif
 
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
     const int wave = wave_id();
     // lane coordinates; re-derived from an opaque copy of the lane id at the top of every
     // chain step, so per-lane addresses are recomputed per step instead of being hoisted out
     // of the chain loop (they would live through the convs, the register peak, and spill)
     int q = lane >> 4, c16 = lane & 15;
     bool odd = q & 1;
-    const int B = A.B, H = A.H, S = A.S, NB = A.NB;
+    const int B = A.B, H = A.H, NB = A.NB;
+    int S = A.S;
     const Ws L = ws_layout(B, S);
     int* ctl = (int*)A.work;
 
-    // ---- the strip: a ticket in start order (an image's strips are running blocks)
-    if (tid == 0) *tick_lds = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- the strip: a ticket in start order (an image's strips are running blocks); the
+    // launch's epoch (tags of this launch's hand-offs: never equal to an earlier launch's)
+    if (tid == 0) {
+        tick_lds[0] = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tick_lds[1] = __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef FEN_GS_STAMPS
+        unsigned long long t0;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+        tick_lds[2] = (int)(unsigned)t0;
+#endif
+    }
     // zero the LDS image (halo rows of edge strips and the zero columns stay zero)
     for (int i = tid; i < IMG_BYTES / 16; i += 512) *(uint4*)(img + i * 16) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    const int ticket = __builtin_amdgcn_readfirstlane(*tick_lds);
+    const int ticket = __builtin_amdgcn_readfirstlane(tick_lds[0]);
+    const unsigned epoch = (unsigned)__builtin_amdgcn_readfirstlane(tick_lds[1]);
+    auto tag_of = [&](int j) -> unsigned { return (epoch << 8) | (unsigned)(j + 1); };
+#ifdef FEN_GS_STAMPS
+    const unsigned t_start = (unsigned)__builtin_amdgcn_readfirstlane(tick_lds[2]);   // the block's clock origin
+#endif
     GSTAMP(0);
-    const int im = ticket / S, strip = ticket - im * S;
-    const int r0 = strip * SR;
+    int im = ticket / S, strip = ticket - im * S;
+    int r0 = strip * SR;
     const bool has_up = strip > 0, has_dn = strip + 1 < S;
     // waves 0 / 7 own the strip's boundary rows (publish them, fetch the neighbours')
     const bool bwave = (wave == 0 && has_up) || (wave == SR - 1 && has_dn);
     const int side = wave == 0 ? 0 : 1;                    // this wave's boundary side
     const int nb_strip = wave == 0 ? strip - 1 : strip + 1;  // the neighbour it reads from
+    // x_{j+1}'s halo rows are built by two waves per side (half a row each: 4 of the 8 chunks
+    // per lane): waves 0, 2 the upper row, waves 7, 5 the lower one
+    const int hs = (wave == 0 || wave == 2) ? 0 : (wave == 5 || wave == SR - 1) ? 1 : -1;
+    const bool hwave = hs == 0 ? has_up : hs == 1 ? has_dn : false;
+    const int hk0 = (wave == 0 || wave == SR - 1) ? 0 : 4;
 
     const size_t act_bytes = (size_t)B * H * SW * 128;
     const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc((void*)A.work, 0, (int)L.total, 0x00020000);
-    int* cnt = (int*)(A.work + L.cnt) + im * 32;
-    int* flg = (int*)(A.work + L.flg);
+    unsigned* flg = (unsigned*)(A.work + L.flg);
+    // one flag word per (strip, side, kind), own 128-B line: kind 0 = a1 row, 1 = x / t rows
+    auto flag_of = [&](int s_, int sd, int kind) -> unsigned* { return flg + (((im * S + s_) * 2 + sd) * 2 + kind) * 32; };
     auto rowoff = [&](size_t base, int s_, int par, int sd) -> int {
         return (int)(base + ((size_t)((im * S + s_) * 2 + par) * 2 + sd) * ROWB);
     };
@@ -294,6 +316,11 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) *(uint4*)(hb + k * 1024) = v[k];
     };
+    auto load_row = [&](int off, uint4 (&v)[8]) {           // sc1: a handed-off row
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, off + (lane + 64 * k) * 16, 0, 16));
+    };
 
     // ================= start-up: conv1_0's taps, x_0, constants =================
     issue_taps(0, 0, 9);
@@ -303,8 +330,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
 #pragma unroll
         for (int p = 0; p < 4; ++p)
             xr[m][p] = *(const uint2*)((const char*)A.x + px_off(r0 + wave, p) + (16 * m + 4 * q) * 2);
-    uint4 hv[8];
     if (bwave) {
+        uint4 hv[8];
         const int row = wave == 0 ? r0 - 1 : r0 + SR;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -312,6 +339,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             hv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                                   xrs, (int)(((size_t)(im * H + row) * SW) * 128) + i * 16, 0, 0));
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
     }
     float cv = 0.f;
     if (wave == 2) cv = A.bias[0][lane];
@@ -320,39 +349,41 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
     write_row_lds(wave + 1, xr);
-    if (bwave) halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
     GSTAMP(1);
 
     // ================= the chain: RCAB j = 0 .. NB-1, then the group conv =================
-    f32x4 acc[4][4];
+    uint2 tr[4][4];                                         // t_j as stored (16-bit), for the next combine
     const int khP2 = wave == 0 ? 2 : 0, khP3 = 2 - khP2;   // wave 0's upper halo row is read last
     bool ok = true;
     for (int j = 0; j <= NB; ++j) {
         const bool gc = j == NB;
         const int par = j & 1;
+        const int sb = 2 + 9 * j;                           // this step's stamp slots
         {
+            // opaque per step: what is computed from these is recomputed here, not hoisted
             int ll = lane;
-            asm volatile("" : "+v"(ll));
-            q = ll >> 4, c16 = ll & 15, odd = q & 1;
+            asm volatile("" : "+v"(ll), "+s"(im), "+s"(strip), "+s"(S), "+s"(r0));
+            lane = ll, q = ll >> 4, c16 = ll & 15, odd = q & 1;
         }
         if (j > 0) {
-            // ---- every strip of the image finished RCAB j-1 (partials, t/x rows published)
-            GSTAMP(2 + 8 * j);
-            if (tid == 0) ok = ok && poll_ge(cnt, S * j);     // (after a timeout: no more waiting)
-            __syncthreads();
-            GSTAMP(3 + 8 * j);
+            GSTAMP(sb);
             const int pp = (j - 1) & 1;
+            const unsigned tg = tag_of(j - 1);
             if (wave == 1) {
                 // the gate of RCAB j-1 (blocks.py:83-92): mean over the image from the S strip
-                // partials in strip order, FC1 -> ReLU -> FC2 -> sigmoid
-                // FC1 rows jj >= Cr read past fc1's end: 0, so hid_jj = 0 and FC2's columns
-                // k >= Cr (finite values of the next rows, or 0 past the end) drop out
+                // partials, each an 8-B {tag, value} granule (the data is the flag: sc1 loads
+                // swept until every tag is this RCAB's), summed in strip order; FC1 -> ReLU ->
+                // FC2 -> sigmoid.  FC1 rows jj >= Cr read past fc1's end: 0, so hid_jj = 0 and
+                // FC2's columns k >= Cr (finite values of the next rows, or 0 past the end) drop out
+                // (the weight pointers made opaque here: buffer loads are speculatable, and
+                // hoisted out of this wave's branch they held 32 VGPRs in every wave)
                 const int Cr = A.Cr, jj = lane & 15, qq = lane >> 4;
-                const __amdgpu_buffer_rsrc_t f1r =
-                    __builtin_amdgcn_make_buffer_rsrc((void*)A.fc1[j - 1], 0, Cr * 64 * 4, 0x00020000);
-                const __amdgpu_buffer_rsrc_t f2r =
-                    __builtin_amdgcn_make_buffer_rsrc((void*)A.fc2[j - 1], 0, Cr * 64 * 4, 0x00020000);
-                float w1v[16], w2v[16], pv[16];
+                const float* f1p = A.fc1[j - 1];
+                const float* f2p = A.fc2[j - 1];
+                asm volatile("" : "+s"(f1p), "+s"(f2p));
+                const __amdgpu_buffer_rsrc_t f1r = __builtin_amdgcn_make_buffer_rsrc((void*)f1p, 0, Cr * 64 * 4, 0x00020000);
+                const __amdgpu_buffer_rsrc_t f2r = __builtin_amdgcn_make_buffer_rsrc((void*)f2p, 0, Cr * 64 * 4, 0x00020000);
+                float w1v[16], w2v[16];
 #pragma unroll
                 for (int k4 = 0; k4 < 16; k4 += 4) {
                     const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -362,18 +393,34 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
 #pragma unroll
                 for (int k = 0; k < 16; ++k)
                     w2v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(f2r, (lane * Cr + k) * 4, 0, 0));
-                // strips past S read past the buffer's end: 0 (range-checked buffer loads)
-                const int pbase = (int)(L.part + ((size_t)(im * 2 + pp) * S) * 64 * 4) + lane * 4;
-                const int pend = (int)(L.part + ((size_t)(im * 2 + pp) * S + S) * 64 * 4);
+                const unsigned long long* pg =
+                    (const unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + pp) * S) * 64 + lane;
+                // every granule load in flight at once, no branch per strip: strips past S re-read
+                // strip 0 and drop out of the sum and the check
+                float pv[16];
+                bool got = false;
+                for (int it = 0; it < SPIN_MAX && ok; ++it) {
+                    unsigned long long gv[16];
 #pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    const int off = pbase + s * 256;
-                    pv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wsr, off < pend ? off : 0x7ffffff0, 0, 16));
+                    for (int s_ = 0; s_ < 16; ++s_)
+                        gv[s_] = __hip_atomic_load(pg + (s_ < S ? s_ : 0) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned bad = 0u;
+#pragma unroll
+                    for (int s_ = 0; s_ < 16; ++s_) {
+                        const bool in = s_ < S;
+                        pv[s_] = in ? __uint_as_float((unsigned)gv[s_]) : 0.f;
+                        bad |= (unsigned)(in & ((unsigned)(gv[s_] >> 32) != tg));
+                    }
+                    if (__all(bad == 0u)) {
+                        got = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                ok = ok && got;
                 float msum = 0.f;
 #pragma unroll
-                for (int s = 0; s < 16; ++s) msum += pv[s];
+                for (int s_ = 0; s_ < 16; ++s_) msum += pv[s_];
                 const float mean = msum * A.inv_hw;
                 scr[lane] = mean;
                 float h = 0.f;
@@ -394,19 +441,39 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                                       : (wave == 2 ? A.bias[2 * j] : wave == 3 ? A.alpha[j] : A.bias[2 * j + 1]);
                 cv = src ? src[lane] : 0.f;
             }
-            uint4 nx[8], nt[8];
-            if (bwave) {                                    // the neighbour's x_{j-1}, t_{j-1} row
-                const int ox = rowoff(L.bx, nb_strip, pp, 1 - side), ot = rowoff(L.bt, nb_strip, pp, 1 - side);
+            uint4 nx[4], nt[4];
+            if (hwave) {
+                // the neighbour's x_{j-1}, t_{j-1} rows (this wave's half), after its flag (its
+                // storing wave drained them, then signalled): this wave polls and loads (row 1)
+                const int ns = hs == 0 ? strip - 1 : strip + 1;
+                ok = ok && poll_eq(flag_of(ns, 1 - hs, 1), tg);
+                const int ox = rowoff(L.bx, ns, pp, 1 - hs) + (lane + 64 * hk0) * 16;
+                const int ot = rowoff(L.bt, ns, pp, 1 - hs) + (lane + 64 * hk0) * 16;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int i = lane + 64 * k;
-                    nx[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ox + i * 16, 0, 16));
-                    nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + i * 16, 0, 16));
+                for (int k = 0; k < 4; ++k) {
+                    nx[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ox + k * 1024, 0, 16));
+                    nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + k * 1024, 0, 16));
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (also this conv's taps, long issued)
             if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
             __syncthreads();
+            GSTAMP(sb + 1);
+            if (hwave) {                                    // its half of x_j's halo row, same arithmetic
+                const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
+                const float4 gb = *(const float4*)(gate + (lane & 7) * 8 + 4);
+                const float g8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+                char* hb = img + (hs == 0 ? 0 : SR + 1) * IROW + hcol((lane >> 3) + 1, lane & 7) + hk0 * 1024;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float xf[8], tf[8], yv[8];
+                    unpack16<T>(nx[k], xf);
+                    unpack16<T>(nt[k], tf);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) yv[e] = tf[e] * g8[e] + xf[e];
+                    *(uint4*)(hb + k * 1024) = pack16<T>(yv);
+                }
+            }
             // ---- x_j = x_{j-1} + rs * s * t_{j-1} (t as stored: rounded), own row in registers
             float g[4][4];
 #pragma unroll
@@ -418,46 +485,34 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             for (int m = 0; m < 4; ++m)
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
+                    __builtin_amdgcn_sched_barrier(0);
                     const float x0 = lo16<T>(xr[m][p].x), x1 = hi16<T>(xr[m][p].x);
                     const float x2 = lo16<T>(xr[m][p].y), x3 = hi16<T>(xr[m][p].y);
-                    xr[m][p] = pk4<T>(rnd16<T>(acc[m][p][0]) * g[m][0] + x0, rnd16<T>(acc[m][p][1]) * g[m][1] + x1,
-                                      rnd16<T>(acc[m][p][2]) * g[m][2] + x2, rnd16<T>(acc[m][p][3]) * g[m][3] + x3);
+                    xr[m][p] = pk4<T>(lo16<T>(tr[m][p].x) * g[m][0] + x0, hi16<T>(tr[m][p].x) * g[m][1] + x1,
+                                      lo16<T>(tr[m][p].y) * g[m][2] + x2, hi16<T>(tr[m][p].y) * g[m][3] + x3);
                 }
             write_row_lds(wave + 1, xr);
-            if (bwave) {                                    // the halo row of x_j, same arithmetic
-                const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
-                const float4 gb = *(const float4*)(gate + (lane & 7) * 8 + 4);
-                const float g8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    float xf[8], tf[8], yv[8];
-                    unpack16<T>(nx[k], xf);
-                    unpack16<T>(nt[k], tf);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) yv[e] = tf[e] * g8[e] + xf[e];
-                    hv[k] = pack16<T>(yv);
-                }
-                halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
-            }
         }
         // x_j's boundary rows for the neighbours (their halo rows of x_{j+1})
         if (!gc && bwave) store_row(wsr, rowoff(L.bx, strip, par, side), xr, 16);
 
         // ================= conv1 (or the group conv): 3 phases =================
         const int ci = gc ? 2 * NB : 2 * j;
+        f32x4 acc[4][4];                                    // conv1 (group conv), then conv2
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        GSTAMP(4 + 8 * j);
+        GSTAMP(sb + 2);
         __syncthreads();                                    // image + constants; this conv's taps landed
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);
+        GSTAMP(sb + 3);
         __syncthreads();                                    // kh = 1 slots free
         if (!gc) issue_kh1(ci + 1);
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
-        GSTAMP(5 + 8 * j);
+        GSTAMP(sb + 4);
         if (gc) {
             // ---- out = conv + bias + the group input (blocks.py:188-189): its own rows read
             // again here (once per launch; kept out of the conv's register peak)
@@ -515,29 +570,28 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
         vm_wait_n(6 + (bwave ? 8 : 0));                     // conv2's kh = 1 taps (older than the rest)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        GSTAMP(6 + 8 * j);
+        GSTAMP(sb + 5);
         __syncthreads();                                    // a1 image (own rows) complete
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);
+        GSTAMP(sb + 6);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv2's other taps; the a1 boundary stores
-        __syncthreads();
-        if (tid == 0)                                       // a1's boundary rows of RCAB j are out
-            __hip_atomic_store(flg + (im * S + strip) * 32, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a1's boundary row is out: its storing wave signals for itself (one lane, after its drain)
+        if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 0), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();                                    // every wave's pieces of those taps landed
         issue_kh1(j + 1 < NB ? ci + 2 : 2 * NB);
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
+        GSTAMP(sb + 7);
         if (bwave) {
             // the neighbour's a1 row -> this wave's private halo row (only this wave reads it)
-            ok = ok && poll_ge(flg + (im * S + nb_strip) * 32, j + 1);
-            const int oa = rowoff(L.ba, nb_strip, par, 1 - side);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                hv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, oa + (lane + 64 * k) * 16, 0, 16));
+            ok = ok && poll_eq(flag_of(nb_strip, 1 - side, 0), tag_of(j));
+            uint4 hv[8];
+            load_row(rowoff(L.ba, nb_strip, par, 1 - side), hv);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
-        GSTAMP(7 + 8 * j);
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
-        GSTAMP(8 + 8 * j);
+        GSTAMP(sb + 8);
         // ---- conv2 epilogue: t = conv2 + b2 (kept in the accumulators), pool partials
         float ps[4][4];
 #pragma unroll
@@ -555,7 +609,6 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 ps[m][i] = s;
             }
         }
-        __syncthreads();                                    // every wave done with the a1 image, slots free
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -563,53 +616,52 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 const float s = group16_sum(ps[m][i]);
                 if (c16 == 0) red[wave * 64 + 16 * m + 4 * q + i] = s;
             }
-        if (bwave) {                                        // t_j's boundary row (as stored: rounded)
-            uint2 tv[4][4];
+        // t_j as stored (rounded; the accumulators are free from here)
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 4; ++m)
 #pragma unroll
-                for (int p = 0; p < 4; ++p) tv[m][p] = pk4<T>(acc[m][p][0], acc[m][p][1], acc[m][p][2], acc[m][p][3]);
-            store_row(wsr, rowoff(L.bt, strip, par, side), tv, 16);
-        }
+            for (int p = 0; p < 4; ++p) tr[m][p] = pk4<T>(acc[m][p][0], acc[m][p][1], acc[m][p][2], acc[m][p][3]);
+        if (bwave) store_row(wsr, rowoff(L.bt, strip, par, side), tr, 16);   // t_j's boundary row
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (wave == 0) {                                    // the strip's partial, rows in order
+        __syncthreads();                                    // partials in LDS; the a1 image and all slots free
+        if (wave == 0) {
+            // the strip's partial, rows in order, as {tag, value} granules (one 8-B sc1 store each)
             float s = 0.f;
 #pragma unroll
             for (int w = 0; w < SR; ++w) s += red[w * 64 + lane];
-            const int off = (int)(L.part + ((size_t)(im * 2 + par) * S + strip) * 64 * 4) + lane * 4;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), wsr, off, 0, 16);
+            unsigned long long* pg = (unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + par) * S + strip) * 64 + lane;
+            __hip_atomic_store(pg, ((unsigned long long)tag_of(j) << 32) | __float_as_uint(s), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
         // the next conv's remaining taps (its kh = 1 taps went out at phase 2)
         issue_kh02(j + 1 < NB ? ci + 2 : 2 * NB);
-        // every storing wave's stores (t row, partial) done before the signal
-        vm_wait_n(6);
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        GSTAMP(9 + 8 * j);
+        if (bwave) {
+            // x_j's and t_j's boundary rows are out: drained (older than the 6 DMAs), then
+            // this wave signals for itself
+            vm_wait_n(6);
+            if (lane == 0) __hip_atomic_store(flag_of(strip, side, 1), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     GSTAMP(NSTAMP - 1);
-#ifdef FEN_GS_STAMPS
-    __syncthreads();
-    if (wave < 2) {
-        unsigned* dst = (unsigned*)(A.work + L.ba + (size_t)B * S * 2 * 2 * ROWB) + ((size_t)ticket * 2 + wave) * NSTAMP;
-        for (int i = lane; i < NSTAMP; i += 64) dst[i] = stamp_lds[wave * NSTAMP + i];
-    }
-#endif
-    // ---- the last block out resets the counters for the next launch
+    // ---- the last block out advances the epoch and resets the ticket counters for the next launch
     if (!ok) __hip_atomic_fetch_or(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         const int nblk = B * S;
         if (__hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
-            for (int b = 0; b < B; ++b)
-                __hip_atomic_store((int*)(A.work + L.cnt) + b * 32, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int i = 0; i < B * S; ++i) __hip_atomic_store(flg + i * 32, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+#ifdef FEN_GS_STAMPS
+    __syncthreads();
+    {
+        unsigned short* dst = (unsigned short*)(A.work + L.ba + (size_t)B * S * 2 * 2 * ROWB) + (size_t)ticket * 8 * NSTAMP;
+        for (int i = tid; i < 8 * NSTAMP; i += 512) dst[i] = stamp_lds[i];
+    }
+#endif
 }
 
 int g_gs_cus = 0;
