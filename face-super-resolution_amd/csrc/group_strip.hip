@@ -124,17 +124,35 @@ __device__ __forceinline__ uint2 pk4(float a, float b, float c, float d) {
     return make_uint2(pack2<T>(a, b), pack2<T>(c, d));
 }
 
-// lanes q and q^1 (same pixel) trade one 4-channel half so each holds 8 consecutive channels:
-// lo = the lane's channels of m-block 2mp, hi = of m-block 2mp + 1; the result is chunk
-// chunk_of(mp, q) of the pixel
-__device__ __forceinline__ uint4 pair16(uint2 lo, uint2 hi, bool odd) {
-    const uint2 snd = odd ? lo : hi;
-    uint2 rcv;
-    rcv.x = (unsigned)__shfl_xor((int)snd.x, 16, 64);
-    rcv.y = (unsigned)__shfl_xor((int)snd.y, 16, 64);
-    return odd ? make_uint4(rcv.x, rcv.y, hi.x, hi.y) : make_uint4(lo.x, lo.y, rcv.x, rcv.y);
+// lanes q and q^1 (same pixel: rows 2k, 2k+1 of 16 lanes) trade one 4-channel half so each
+// holds 8 consecutive channels: lo = the lane's channels of m-block 2mp, hi = of m-block
+// 2mp + 1; the result is chunk chunk_of(mp, q) of the pixel.  v_permlane16_swap swaps the odd
+// rows of its first operand with the even rows of its second: even rows keep lo and receive
+// the odd partner's lo, odd rows keep hi and receive the even partner's hi (no LDS round trip)
+__device__ __forceinline__ uint4 pair16(uint2 lo, uint2 hi) {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+    return make_uint4(a[0], b[0], a[1], b[1]);
 }
 __device__ __forceinline__ int chunk_of(int mp, int q) { return 4 * mp + ((q & 1) ? 2 : 0) + (q >> 1); }
+
+// sum over the 8 lanes l ^ 8k (the lanes of one l & 7): row_ror:8 (lane ^ 8 in a row of 16),
+// then the row-pair and half swaps; a fixed tree, bit-identical in all 8 lanes
+__device__ __forceinline__ float sum_lanes_x8(float v) {
+    v += dpp_f<0x128>(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// P += sum_e bcast_e(v) * w[e], bcast_e = lane e of the lane's row of 16 (DPP row_newbcast)
+template <int E>
+__device__ __forceinline__ void bcast8_fma_(float& P, float v, const float (&w)[8]) {
+    P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + E, 0xf, 0xf, false)) * w[E];
+    if constexpr (E < 7) bcast8_fma_<E + 1>(P, v, w);
+}
+__device__ __forceinline__ void bcast8_fma(float& P, float v, const float (&w)[8]) { bcast8_fma_<0>(P, v, w); }
 
 // bounded poll of an agent-scope flag (sc1 loads): true once it holds `tag`
 __device__ __forceinline__ bool poll_eq(const unsigned* p, unsigned tag) {
@@ -210,7 +228,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     // chain step, so per-lane addresses are recomputed per step instead of being hoisted out
     // of the chain loop (they would live through the convs, the register peak, and spill)
     int q = lane >> 4, c16 = lane & 15;
-    bool odd = q & 1;
+#ifdef GS_PRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);   // A/B variant: the SIMDs' younger waves first
+#endif
     const int B = A.B, H = A.H, NB = A.NB;
     int S = A.S;
     const Ws L = ws_layout(B, S);
@@ -302,7 +322,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         for (int p = 0; p < 4; ++p)
 #pragma unroll
             for (int mp = 0; mp < 2; ++mp) {
-                const uint4 u = pair16(v[2 * mp][p], v[2 * mp + 1][p], odd);
+                const uint4 u = pair16(v[2 * mp][p], v[2 * mp + 1][p]);
                 const int off = lb + p * 2048 + mp * 64;
                 if (aux) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 16);
                 else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 0);
@@ -349,9 +369,17 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
     write_row_lds(wave + 1, xr);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();                                        // conv1_0's taps (every wave's pieces) landed
     GSTAMP(1);
 
     // ================= the chain: RCAB j = 0 .. NB-1, then the group conv =================
+    // Per RCAB, five barriers: B_X (conv1's image complete), B_E (conv1 done), B_Y (a1 image
+    // complete), B_Z (the strip's pool partial complete), B_G (the gate known).  Phase 1 of each
+    // conv reads the wave's own row only and runs without a barrier.  The gate's pool partial
+    // is computed from a1 before conv2's phases 2-3 (the conv is linear: sum over the strip's
+    // pixels of conv2(a1) = W2 applied to a1's per-channel sums, less the columns / rows a tap
+    // reads past the image's edge), so the image's strips exchange it while conv2 still runs.
     uint2 tr[4][4];                                         // t_j as stored (16-bit), for the next combine
     const int khP2 = wave == 0 ? 2 : 0, khP3 = 2 - khP2;   // wave 0's upper halo row is read last
     bool ok = true;
@@ -363,117 +391,14 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             // opaque per step: what is computed from these is recomputed here, not hoisted
             int ll = lane;
             asm volatile("" : "+v"(ll), "+s"(im), "+s"(strip), "+s"(S), "+s"(r0));
-            lane = ll, q = ll >> 4, c16 = ll & 15, odd = q & 1;
+            lane = ll, q = ll >> 4, c16 = ll & 15;
         }
+        const int ci = gc ? 2 * NB : 2 * j;
+        GSTAMP(sb);
+        uint4 nx[4], nt[4];
         if (j > 0) {
-            GSTAMP(sb);
-            const int pp = (j - 1) & 1;
-            const unsigned tg = tag_of(j - 1);
-            if (wave == 1) {
-                // the gate of RCAB j-1 (blocks.py:83-92): mean over the image from the S strip
-                // partials, each an 8-B {tag, value} granule (the data is the flag: sc1 loads
-                // swept until every tag is this RCAB's), summed in strip order; FC1 -> ReLU ->
-                // FC2 -> sigmoid.  FC1 rows jj >= Cr read past fc1's end: 0, so hid_jj = 0 and
-                // FC2's columns k >= Cr (finite values of the next rows, or 0 past the end) drop out
-                // (the weight pointers made opaque here: buffer loads are speculatable, and
-                // hoisted out of this wave's branch they held 32 VGPRs in every wave)
-                const int Cr = A.Cr, jj = lane & 15, qq = lane >> 4;
-                const float* f1p = A.fc1[j - 1];
-                const float* f2p = A.fc2[j - 1];
-                asm volatile("" : "+s"(f1p), "+s"(f2p));
-                const __amdgpu_buffer_rsrc_t f1r = __builtin_amdgcn_make_buffer_rsrc((void*)f1p, 0, Cr * 64 * 4, 0x00020000);
-                const __amdgpu_buffer_rsrc_t f2r = __builtin_amdgcn_make_buffer_rsrc((void*)f2p, 0, Cr * 64 * 4, 0x00020000);
-                float w1v[16], w2v[16];
-#pragma unroll
-                for (int k4 = 0; k4 < 16; k4 += 4) {
-                    const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                    f1r, (jj * 64 + 16 * qq + k4) * 4, 0, 0));
-                    w1v[k4] = a.x, w1v[k4 + 1] = a.y, w1v[k4 + 2] = a.z, w1v[k4 + 3] = a.w;
-                }
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    w2v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(f2r, (lane * Cr + k) * 4, 0, 0));
-                const unsigned long long* pg =
-                    (const unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + pp) * S) * 64 + lane;
-                // every granule load in flight at once, no branch per strip: strips past S re-read
-                // strip 0 and drop out of the sum and the check
-                float pv[16];
-                bool got = false;
-                for (int it = 0; it < SPIN_MAX && ok; ++it) {
-                    unsigned long long gv[16];
-#pragma unroll
-                    for (int s_ = 0; s_ < 16; ++s_)
-                        gv[s_] = __hip_atomic_load(pg + (s_ < S ? s_ : 0) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    unsigned bad = 0u;
-#pragma unroll
-                    for (int s_ = 0; s_ < 16; ++s_) {
-                        const bool in = s_ < S;
-                        pv[s_] = in ? __uint_as_float((unsigned)gv[s_]) : 0.f;
-                        bad |= (unsigned)(in & ((unsigned)(gv[s_] >> 32) != tg));
-                    }
-                    if (__all(bad == 0u)) {
-                        got = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                ok = ok && got;
-                float msum = 0.f;
-#pragma unroll
-                for (int s_ = 0; s_ < 16; ++s_) msum += pv[s_];
-                const float mean = msum * A.inv_hw;
-                scr[lane] = mean;
-                float h = 0.f;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) h += w1v[k] * scr[16 * qq + k];
-                h += __shfl_xor(h, 16, 64);
-                h += __shfl_xor(h, 32, 64);
-                const float hid = fmaxf(h, 0.f);
-                float z = 0.f;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) z += w2v[k] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hid), k));
-                const float sg = 1.f / (1.f + expf(-z));
-                gate[lane] = sg * A.res_scale;
-                if (strip == 0 && A.s_out[j - 1]) A.s_out[j - 1][im * 64 + lane] = sg;
-            }
-            if (wave >= 2 && wave <= 4) {                   // the constants of this conv's epilogue
-                const float* src = gc ? (wave == 4 ? A.bias[2 * NB] : nullptr)
-                                      : (wave == 2 ? A.bias[2 * j] : wave == 3 ? A.alpha[j] : A.bias[2 * j + 1]);
-                cv = src ? src[lane] : 0.f;
-            }
-            uint4 nx[4], nt[4];
-            if (hwave) {
-                // the neighbour's x_{j-1}, t_{j-1} rows (this wave's half), after its flag (its
-                // storing wave drained them, then signalled): this wave polls and loads (row 1)
-                const int ns = hs == 0 ? strip - 1 : strip + 1;
-                ok = ok && poll_eq(flag_of(ns, 1 - hs, 1), tg);
-                const int ox = rowoff(L.bx, ns, pp, 1 - hs) + (lane + 64 * hk0) * 16;
-                const int ot = rowoff(L.bt, ns, pp, 1 - hs) + (lane + 64 * hk0) * 16;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    nx[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ox + k * 1024, 0, 16));
-                    nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + k * 1024, 0, 16));
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (also this conv's taps, long issued)
-            if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
-            __syncthreads();
-            GSTAMP(sb + 1);
-            if (hwave) {                                    // its half of x_j's halo row, same arithmetic
-                const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
-                const float4 gb = *(const float4*)(gate + (lane & 7) * 8 + 4);
-                const float g8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
-                char* hb = img + (hs == 0 ? 0 : SR + 1) * IROW + hcol((lane >> 3) + 1, lane & 7) + hk0 * 1024;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    float xf[8], tf[8], yv[8];
-                    unpack16<T>(nx[k], xf);
-                    unpack16<T>(nt[k], tf);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) yv[e] = tf[e] * g8[e] + xf[e];
-                    *(uint4*)(hb + k * 1024) = pack16<T>(yv);
-                }
-            }
+            issue_kh02(ci);                                 // this conv's kh = 0, 2 taps (slots free since B_G)
+            if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;   // read after B_E / B_Z
             // ---- x_j = x_{j-1} + rs * s * t_{j-1} (t as stored: rounded), own row in registers
             float g[4][4];
 #pragma unroll
@@ -495,24 +420,57 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         }
         // x_j's boundary rows for the neighbours (their halo rows of x_{j+1})
         if (!gc && bwave) store_row(wsr, rowoff(L.bx, strip, par, side), xr, 16);
+        if (j > 0 && hwave) {
+            // the neighbour's x_{j-1}, t_{j-1} rows (this wave's half), after its flag (its
+            // storing wave drained them, then signalled): this wave polls and loads (row 1);
+            // the loads land during phase 1
+            const int pp = (j - 1) & 1;
+            const int ns = hs == 0 ? strip - 1 : strip + 1;
+            ok = ok && poll_eq(flag_of(ns, 1 - hs, 1), tag_of(j - 1));
+            const int ox = rowoff(L.bx, ns, pp, 1 - hs) + (lane + 64 * hk0) * 16;
+            const int ot = rowoff(L.bt, ns, pp, 1 - hs) + (lane + 64 * hk0) * 16;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                nx[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ox + k * 1024, 0, 16));
+                nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + k * 1024, 0, 16));
+            }
+        }
 
         // ================= conv1 (or the group conv): 3 phases =================
-        const int ci = gc ? 2 * NB : 2 * j;
         f32x4 acc[4][4];                                    // conv1 (group conv), then conv2
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
+        // phase 1 (kh = 1) reads the wave's own row only: no barrier.  Its taps are visible since
+        // B_G (or the start-up barrier); a wave whose combine is short starts its MFMAs while its
+        // SIMD partner still builds halo rows
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        GSTAMP(sb + 2);
-        __syncthreads();                                    // image + constants; this conv's taps landed
+        GSTAMP(sb + 1);
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);
-        GSTAMP(sb + 3);
-        __syncthreads();                                    // kh = 1 slots free
+        GSTAMP(sb + 2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this conv's taps; the halo rows
+        if (j > 0 && hwave) {                               // its half of x_j's halo row, same arithmetic
+            const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
+            const float4 gb = *(const float4*)(gate + (lane & 7) * 8 + 4);
+            const float g8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+            char* hb = img + (hs == 0 ? 0 : SR + 1) * IROW + hcol((lane >> 3) + 1, lane & 7) + hk0 * 1024;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float xf[8], tf[8], yv[8];
+                unpack16<T>(nx[k], xf);
+                unpack16<T>(nt[k], tf);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) yv[e] = tf[e] * g8[e] + xf[e];
+                *(uint4*)(hb + k * 1024) = pack16<T>(yv);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __syncthreads();                                    // B_X: every image row written; kh = 1 slots free
         if (!gc) issue_kh1(ci + 1);
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
-        GSTAMP(sb + 4);
+        GSTAMP(sb + 3);
         if (gc) {
             // ---- out = conv + bias + the group input (blocks.py:188-189): its own rows read
             // again here (once per launch; kept out of the conv's register peak)
@@ -542,9 +500,11 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             store_row(yrs, (int)((size_t)(im * H + r0 + wave) * SW * 128), ov, 0);
             break;
         }
-        __syncthreads();                                    // everyone done with x_j in LDS; all slots free
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's pieces of conv2's kh = 1 taps
+        __syncthreads();                                    // B_E: x_j's reads done (all slots free); those taps visible
         issue_kh02(ci + 1);
-        // ---- conv1 epilogue: a1 = PReLU(conv1 + b1) -> LDS (own row), boundary rows out
+        // ---- conv1 epilogue: a1 = PReLU(conv1 + b1) -> LDS (own row), boundary rows out; the
+        // row's per-channel sums of a1 (fp32, before the 16-bit rounding conv2 reads) -> red[wave]
         {
             uint2 av[4][4];
 #pragma unroll
@@ -552,12 +512,20 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 const float4 bb = *(const float4*)(cst + 16 * m + 4 * q);
                 const float4 aa = *(const float4*)(cst + 64 + 16 * m + 4 * q);
                 const float bia[4] = {bb.x, bb.y, bb.z, bb.w}, alp[4] = {aa.x, aa.y, aa.z, aa.w};
+                float rs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
                     float v[4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) v[i] = prelu_f(acc[m][p][i] + bia[i], alp[i]);
                     av[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) rs[i] += v[i];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float s = group16_sum(rs[i]);
+                    if (c16 == 0) red[wave * 64 + 16 * m + 4 * q + i] = s;
                 }
             }
             write_row_lds(wave + 1, av);
@@ -568,19 +536,84 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
-        vm_wait_n(6 + (bwave ? 8 : 0));                     // conv2's kh = 1 taps (older than the rest)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GSTAMP(sb + 4);
+        conv_phase<T>(acc, img, filt, 1, wave, q, c16);     // own a1 row only: no barrier
         GSTAMP(sb + 5);
-        __syncthreads();                                    // a1 image (own rows) complete
-        conv_phase<T>(acc, img, filt, 1, wave, q, c16);
-        GSTAMP(sb + 6);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv2's other taps; the a1 boundary stores
         // a1's boundary row is out: its storing wave signals for itself (one lane, after its drain)
         if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 0), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();                                    // every wave's pieces of those taps landed
+        __syncthreads();                                    // B_Y: a1 image and row sums complete; conv2's taps visible
+        {
+            // ---- the strip's pool partial of t_j (blocks.py:89 AdaptiveAvgPool of conv2's
+            // output, less the bias): sum over the strip's output pixels of conv2(a1) =
+            // sum_{ci, tap} W2[tap][co][ci] * u[ci][tap], u = the sum of a1[ci] over the input
+            // pixels the tap reads -- the strip's a1 sum, less column 0 (kw = 2) / column W-1
+            // (kw = 0), less the image's row 0 (kh = 2; strip 0's first row) / row H-1 (kh = 0;
+            // the last strip's last row), whose inputs lie past the image's edge.  Wave w takes
+            // channels ci = 8w .. 8w+7: lane (r, c) reads row r's sums of channel 8w + c and
+            // both edge pixels (from the LDS image), the sums over the 8 rows by lane exchanges;
+            // then lane co accumulates W2[tap][co][8w .. 8w+7] * u (fixed order) into red, in
+            // the slots this wave alone read (a permutation: co -> [co >> 3][8w + (co & 7)])
+            int ll = lane;
+            asm volatile("" : "+v"(ll));
+            const int r = ll >> 3, c = ll & 7, cw = 8 * wave + c;
+            const float rsum = red[r * 64 + cw];
+            const char* rb = img + (r + 1) * IROW + 2 * c;
+            const float p0 = lo16<T>((unsigned)*(const unsigned short*)(rb + hcol(1, wave)));
+            const float pl = lo16<T>((unsigned)*(const unsigned short*)(rb + hcol(SW, wave)));
+            // every lane of channel c: the strip's sums less column W-1 (kw = 0), -, less column 0 (kw = 2)
+            const float tt = sum_lanes_x8(rsum), c0 = sum_lanes_x8(p0), cl = sum_lanes_x8(pl);
+            const float bs[3] = {tt - cl, tt, tt - c0};
+            // lane co: sum_c sum_kw bs[kw](c) * sum_kh W2[kh][kw][co][8w + c]; bs of channel c from
+            // lane c of the lane's row of 16 (row_newbcast)
+            const char* wb = filt + ll * 128 + ((wave ^ ((ll >> 1) & 7)) << 4);
+            float P = 0.f;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                float w0[8], w1[8], w2[8];
+                unpack16<T>(*(const uint4*)(wb + kw * TAPB), w0);
+                unpack16<T>(*(const uint4*)(wb + (3 + kw) * TAPB), w1);
+                unpack16<T>(*(const uint4*)(wb + (6 + kw) * TAPB), w2);
+                float ws[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ws[e] = w0[e] + w1[e] + w2[e];
+                bcast8_fma(P, bs[kw], ws);
+            }
+            if (strip == 0 || strip == S - 1) {
+                // the image's first / last row: the taps that read past the top (kh = 2) / bottom
+                // (kh = 0) edge drop that row's terms.  Row 0's sums sit in lanes 0..7, row 7's in 56..63
+                const float ev[3] = {rsum - pl, rsum, rsum - p0};
+#pragma unroll
+                for (int side_ = 0; side_ < 2; ++side_) {
+                    if (side_ == 0 ? strip != 0 : strip != S - 1) continue;
+                    const int kh = side_ == 0 ? 2 : 0, l0 = side_ == 0 ? 0 : 56;
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        float wk[8];
+                        unpack16<T>(*(const uint4*)(wb + (3 * kh + kw) * TAPB), wk);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            P -= wk[e] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ev[kw]), l0 + e));
+                    }
+                }
+            }
+            red[(ll >> 3) * 64 + 8 * wave + (ll & 7)] = P;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();                                    // B_Z: the partial's eight channel slices in red; kh = 1 slots free
         issue_kh1(j + 1 < NB ? ci + 2 : 2 * NB);
+        if (wave == 3) {
+            // the strip's partial as {tag, value} granules (one 8-B sc1 store each), slices in order
+            float s = 0.f;
+#pragma unroll
+            for (int w = 0; w < SR; ++w) s += red[(lane >> 3) * 64 + 8 * w + (lane & 7)];
+            unsigned long long* pg = (unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + par) * S + strip) * 64 + lane;
+            __hip_atomic_store(pg, ((unsigned long long)tag_of(j) << 32) | __float_as_uint(s), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        GSTAMP(sb + 6);
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
-        GSTAMP(sb + 7);
         if (bwave) {
             // the neighbour's a1 row -> this wave's private halo row (only this wave reads it)
             ok = ok && poll_eq(flag_of(nb_strip, 1 - side, 0), tag_of(j));
@@ -591,56 +624,97 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
-        GSTAMP(sb + 8);
-        // ---- conv2 epilogue: t = conv2 + b2 (kept in the accumulators), pool partials
-        float ps[4][4];
+        GSTAMP(sb + 7);
+        // ---- conv2 epilogue: t_j = conv2 + b2 as stored (rounded), kept for the next combine
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const float4 bb = *(const float4*)(cst + 128 + 16 * m + 4 * q);
-            const float bia[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float s = 0.f;
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    acc[m][p][i] += bia[i];
-                    s += acc[m][p][i];
-                }
-                ps[m][i] = s;
-            }
+            for (int p = 0; p < 4; ++p)
+                tr[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
         }
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float s = group16_sum(ps[m][i]);
-                if (c16 == 0) red[wave * 64 + 16 * m + 4 * q + i] = s;
-            }
-        // t_j as stored (rounded; the accumulators are free from here)
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int p = 0; p < 4; ++p) tr[m][p] = pk4<T>(acc[m][p][0], acc[m][p][1], acc[m][p][2], acc[m][p][3]);
         if (bwave) store_row(wsr, rowoff(L.bt, strip, par, side), tr, 16);   // t_j's boundary row
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();                                    // partials in LDS; the a1 image and all slots free
-        if (wave == 0) {
-            // the strip's partial, rows in order, as {tag, value} granules (one 8-B sc1 store each)
-            float s = 0.f;
+        if (wave == 1) {
+            // the gate of RCAB j (blocks.py:83-92): mean over the image from the S strip
+            // partials, each an 8-B {tag, value} granule (the data is the flag: sc1 loads
+            // swept until every tag is this RCAB's), summed in strip order, + b2; FC1 -> ReLU
+            // -> FC2 -> sigmoid.  FC1 rows jj >= Cr read past fc1's end: 0, so hid_jj = 0 and
+            // FC2's columns k >= Cr (finite values of the next rows, or 0 past the end) drop out
+            // (the weight pointers made opaque here: buffer loads are speculatable, and
+            // hoisted out of this wave's branch they held 32 VGPRs in every wave)
+            const int Cr = A.Cr, jj = lane & 15, qq = lane >> 4;
+            const float* f1p = A.fc1[j];
+            const float* f2p = A.fc2[j];
+            const float* b2p = A.bias[2 * j + 1];
+            asm volatile("" : "+s"(f1p), "+s"(f2p), "+s"(b2p));
+            const __amdgpu_buffer_rsrc_t f1r = __builtin_amdgcn_make_buffer_rsrc((void*)f1p, 0, Cr * 64 * 4, 0x00020000);
+            const __amdgpu_buffer_rsrc_t f2r = __builtin_amdgcn_make_buffer_rsrc((void*)f2p, 0, Cr * 64 * 4, 0x00020000);
+            float w1v[16], w2v[16];
 #pragma unroll
-            for (int w = 0; w < SR; ++w) s += red[w * 64 + lane];
-            unsigned long long* pg = (unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + par) * S + strip) * 64 + lane;
-            __hip_atomic_store(pg, ((unsigned long long)tag_of(j) << 32) | __float_as_uint(s), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            for (int k4 = 0; k4 < 16; k4 += 4) {
+                const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                f1r, (jj * 64 + 16 * qq + k4) * 4, 0, 0));
+                w1v[k4] = a.x, w1v[k4 + 1] = a.y, w1v[k4 + 2] = a.z, w1v[k4 + 3] = a.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                w2v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(f2r, (lane * Cr + k) * 4, 0, 0));
+            const float b2v = b2p[lane];
+            const unsigned tg = tag_of(j);
+            const unsigned long long* pg =
+                (const unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + par) * S) * 64 + lane;
+            // every granule load in flight at once, no branch per strip: strips past S re-read
+            // strip 0 and drop out of the sum and the check
+            float msum = 0.f;
+            bool got = false;
+            for (int it = 0; it < SPIN_MAX && ok; ++it) {
+                unsigned long long gv[16];
+#pragma unroll
+                for (int s_ = 0; s_ < 16; ++s_)
+                    gv[s_] = __hip_atomic_load(pg + (s_ < S ? s_ : 0) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                unsigned bad = 0u;
+                float ms = 0.f;                             // in strip order
+#pragma unroll
+                for (int s_ = 0; s_ < 16; ++s_) {
+                    const bool in = s_ < S;
+                    ms += in ? __uint_as_float((unsigned)gv[s_]) : 0.f;
+                    bad |= (unsigned)(in & ((unsigned)(gv[s_] >> 32) != tg));
+                }
+                msum = ms;
+                if (__all(bad == 0u)) {
+                    got = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            ok = ok && got;
+            const float mean = msum * A.inv_hw + b2v;
+            scr[lane] = mean;
+            float h = 0.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) h += w1v[k] * scr[16 * qq + k];
+            h += __shfl_xor(h, 16, 64);
+            h += __shfl_xor(h, 32, 64);
+            const float hid = fmaxf(h, 0.f);
+            float z = 0.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) z += w2v[k] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hid), k));
+            const float sg = 1.f / (1.f + expf(-z));
+            gate[lane] = sg * A.res_scale;
+            if (strip == 0 && A.s_out[j]) A.s_out[j][im * 64 + lane] = sg;
         }
-        // the next conv's remaining taps (its kh = 1 taps went out at phase 2)
-        issue_kh02(j + 1 < NB ? ci + 2 : 2 * NB);
-        if (bwave) {
-            // x_j's and t_j's boundary rows are out: drained (older than the 6 DMAs), then
-            // this wave signals for itself
-            vm_wait_n(6);
-            if (lane == 0) __hip_atomic_store(flag_of(strip, side, 1), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wave >= 2 && wave <= 4) {                       // the next conv's epilogue constants
+            const bool ng = j + 1 == NB;
+            const float* src = ng ? (wave == 4 ? A.bias[2 * NB] : nullptr)
+                                  : (wave == 2 ? A.bias[2 * j + 2] : wave == 3 ? A.alpha[j + 1] : A.bias[2 * j + 3]);
+            cv = src ? src[lane] : 0.f;
         }
+        // x_j's and t_j's boundary rows out: drained, then the storing wave signals for itself
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 1), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GSTAMP(sb + 8);
+        __syncthreads();                                    // B_G: the gate in LDS; conv2's reads done (all slots free)
     }
     GSTAMP(NSTAMP - 1);
     // ---- the last block out advances the epoch and resets the ticket counters for the next launch

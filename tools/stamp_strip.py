@@ -5,10 +5,10 @@
 
 Runs the inference engine (fp16, B=32, 64x64) a few times and reads the last group launch's
 stamps from the workspace tail: every wave of every block, 100 u16 slots (10 ns ticks from the
-block's start).  Per RCAB j the slots 2+9j .. 10+9j are: sync start, gate barrier passed, conv1
-start (before its first barrier), conv1 phase 1 done, conv1 done, conv2 start (before its first
-barrier), conv2 phase 1 done, phase 2 done (before the a1 halo fetch), conv2 done.  Prints the
-medians over blocks and RCABs 1..9 of each segment, per wave (us).
+block's start).  Per RCAB j the slots 2+9j .. 10+9j are: step start (gate barrier passed), conv1
+phase 1 start (combine done), phase 1 done, conv1 done, conv2 phase 1 start (a1 epilogue done),
+its phase 1 done, phase 2 start (pool partial published), conv2 done, gate barrier reached.
+Prints the medians over blocks and RCABs 1..9 of each segment, per wave (us).
 """
 import os
 import sys
@@ -23,8 +23,8 @@ import torch  # noqa: E402
 from bench import bench_batch, build_model  # noqa: E402
 
 NSTAMP = 100
-SEG = ["sync+gate", "combine", "conv1 p1", "conv1 p2-3", "a1 epilogue", "conv2 p1", "conv2 p2",
-       "conv2 p3", "epilogue2"]
+SEG = ["combine", "conv1 p1", "halo+c1 p2-3", "a1 epilogue", "conv2 p1", "pool partial", "conv2 p2-3",
+       "epi2+gate", "B_G wait"]
 
 
 def main():
@@ -58,8 +58,8 @@ def main():
     tot = st[:, :, 2 + 9 * 10] - st[:, :, 2 + 9 * 1]
     print(f"RCAB 1..9 total per RCAB: {med(tot) / 9:.2f} us")
     g = 2 + 9 * 10
-    print(f"group end: sync+gate {med(st[:, :, g + 1] - st[:, :, g]):.2f}  combine {med(st[:, :, g + 2] - st[:, :, g + 1]):.2f}  "
-          f"conv {med(st[:, :, g + 4] - st[:, :, g + 2]):.2f}  out {med(st[:, 0, NSTAMP - 1] - st[:, 0, g + 4]):.2f}")
+    print(f"group end: combine {med(st[:, :, g + 1] - st[:, :, g]):.2f}  conv {med(st[:, :, g + 3] - st[:, :, g + 1]):.2f}  "
+          f"out {med(st[:, 0, NSTAMP - 1] - st[:, 0, g + 3]):.2f}")
 
 
 if __name__ == "__main__":
