@@ -151,6 +151,20 @@ def time_dominant_kernel(engine, reps=50):
     return e0.elapsed_time(e1) / reps, label, flop  # ms
 
 
+def captured_or_eager(eng, world):
+    """A training engine's step replayed from its captured hipGraph -- at N > 1 with the bucket
+    all-reduces recorded in it (stream-ordered RCCL exchange) -- or, should the capture fail at
+    N > 1, the same step run eagerly (the line says which)."""
+    try:
+        eng.capture()
+        return eng.replay, "hipGraph replay" + (" (RCCL all-reduces captured)" if world > 1 else "")
+    except Exception as e:   # noqa: BLE001 -- reported, and the eager step is timed instead
+        if world == 1:
+            raise
+        torch.cuda.synchronize()
+        return eng.step, f"eager (capture failed: {type(e).__name__}: {str(e)[:120]})"
+
+
 def time_pcie_inclusive(eng, x, steps, warmup, world):
     """images/s when the boundary hands over host buffers: NCHW fp32 LR batch in pinned host
     memory -> H2D into the engine's input, the captured forward, SR batch D2H into pinned
@@ -436,16 +450,12 @@ def main():
         teng = FENEngine(tm, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=True, device="cuda")
         hr_t = hr   # the smooth synthetic HR batch (LR synthesis runs inside the step)
         teng.hr.copy_(hr_t)
-        if world == 1:
-            teng.capture()
-            fn = teng.replay
-        else:
-            fn = teng.step
+        fn, tpath = captured_or_eager(teng, world)
         tt = timed(fn, args.train_steps, 3, world)
         out["train"] = {"metric": "training images/sec (stage-1 L1 generator step) at batch 32/GPU",
                         "value": round(B * world * args.train_steps / tt, 2),
                         "ms_per_step": round(1000.0 * tt / args.train_steps, 3), "steps": args.train_steps,
-                        "loss": float(teng.loss), "allreduce": (("RCCL (torch.distributed nccl backend)" if backend == "nccl" else backend)
+                        "loss": float(teng.loss), "path": tpath, "allreduce": (("RCCL (torch.distributed nccl backend)" if backend == "nccl" else backend)
                                       + ", 8 buckets, overlapped with backward") if world > 1 else "none"}
         del teng
         torch.cuda.empty_cache()
@@ -462,11 +472,7 @@ def main():
             peng = FENEngine(pm, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=True, device="cuda",
                              perceptual=spec)
             peng.hr.copy_(hr_t)
-            if world == 1:
-                peng.capture()
-                fn = peng.replay
-            else:
-                fn = peng.step
+            fn, _ = captured_or_eager(peng, world)
             tp = timed(fn, args.train_steps, 3, world)
             out["train_perceptual"] = {
                 "metric": "training images/sec (stage-1 step: L1 + VGG19 conv3_4 perceptual) at batch 32/GPU",

@@ -248,9 +248,12 @@ class FENEngine:
         return self.scal[0]
 
     def capture(self):
-        """Capture one forward (inference) or one full step (single-GPU training) in a hipGraph."""
-        if self.train and self.world > 1:
-            raise RuntimeError("graph capture of the DP step is not supported (RCCL hooks run on the host)")
+        """Capture one forward (inference) or one full training step in a hipGraph.  At N > 1
+        the step's bucket all-reduces are recorded too: the exchange is stream-ordered (RCCL on
+        a side stream forked from the capture stream at each bucket's mark, joined before the
+        update), so a replay is the whole DP step with no host round trip."""
+        if self.train and self.world > 1 and not getattr(self.exchange, "capturable", False):
+            raise RuntimeError("graph capture of the DP step needs a stream-ordered exchange")
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):  # warm-up on the side stream (allocator + lazy init)
@@ -268,6 +271,7 @@ class FENEngine:
     def _replay_body(self):
         self.ctx.run()
         if self.train:
+            self.exchange.wait()
             self.upd.run()
             self.Wt.pack()
 

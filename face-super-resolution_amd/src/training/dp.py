@@ -61,22 +61,122 @@ def model_bucket_plan(model: torch.nn.Module) -> List[Bucket]:
 
 
 class BucketExchange:
-    """Async SUM all-reduce of arena slices, joined by `wait()`; a no-op at world size 1."""
+    """SUM all-reduce of arena slices, one per bucket as the backward reaches it, joined by
+    `wait()`; a no-op at world size 1 (unless `force`: the tests' one-rank RCCL group).
 
-    def __init__(self, flat: torch.Tensor, plan: Sequence[Bucket], group=None):
+    On the GPU the exchange is stream-ordered and graph-capturable: `launch` forks a side
+    stream from the current one (event record / wait -- the bucket's gradients are enqueued
+    before the fork), issues the collective there (RCCL runs behind it on its own stream), and
+    `wait` joins the side stream back into the current one.  No host synchronisation anywhere,
+    so a whole DP training step (forward, backward with the bucket all-reduces overlapped, the
+    join, clip, AdamW) records into one hipGraph.  On CPU tensors (gloo, the CPU tests) the
+    collectives are async work handles joined by the host."""
+
+    def __init__(self, flat: torch.Tensor, plan: Sequence[Bucket], group=None, force: bool = False):
         self.flat, self.group = flat, group
+        self.plan = list(plan)
         self.views = {tag: flat[lo:hi] for tag, lo, hi in plan}
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.active = self.world > 1 or force
+        self.capturable = bool(flat.is_cuda)
+        self.stream = torch.cuda.Stream(device=flat.device) if (self.active and flat.is_cuda) else None
         self.works: List = []
+        self._forked = False
 
     def launch(self, tag: str) -> None:
-        if self.world > 1:
+        if not self.active:
+            return
+        if self.stream is not None:
+            self.stream.wait_stream(torch.cuda.current_stream(self.flat.device))
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(self.views[tag], group=self.group)
+            self._forked = True
+        else:
             self.works.append(dist.all_reduce(self.views[tag], group=self.group, async_op=True))
 
     def wait(self) -> None:
+        if self._forked:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
+            self._forked = False
         for w in self.works:
             w.wait()
         self.works = []
+
+
+class ParamGradExchange:
+    """Bucketed, overlapped gradient all-reduce for module-autograd parameters (the generator
+    on the module path, the discriminator): each bucket is a run of parameters in
+    `named_parameters()` order; a post-accumulate-grad hook per parameter counts its bucket's
+    arrivals, and the bucket's last one copies the bucket's `.grad`s into its slice of `flat`
+    (one multi-tensor copy) and launches that slice's all-reduce (BucketExchange: stream-
+    ordered, capturable).  `wait()` joins; `flat` then holds the global-batch gradients (the
+    caller's loss is pre-scaled by 1/world).  `copy_back` also writes them into the `.grad`s
+    (for optimisers that read `.grad`).  Hooks fire only while `armed` (an accumulation batch
+    that does not step exchanges nothing)."""
+
+    def __init__(self, params: Sequence[torch.Tensor], flat: torch.Tensor, buckets: Sequence[Tuple[int, int]],
+                 group=None, force: bool = False, copy_back: bool = False):
+        self.params = list(params)
+        offs, o = [], 0
+        for p in self.params:
+            offs.append(o)
+            o += p.numel()
+        if o != flat.numel():
+            raise ValueError("flat buffer does not match the parameters")
+        self.flat, self.copy_back = flat, copy_back
+        self.fviews = [flat[a:a + p.numel()].view_as(p) for a, p in zip(offs, self.params)]
+        plan = []
+        for i, (a, b) in enumerate(buckets):
+            lo = offs[a]
+            hi = offs[b - 1] + self.params[b - 1].numel()
+            plan.append((f"b{i}", lo, hi))
+        self.ranges = [(a, b) for a, b in buckets]
+        self.ex = BucketExchange(flat, plan, group, force)
+        self.world, self.active = self.ex.world, self.ex.active
+        self.armed = False
+        self._left = [b - a for a, b in self.ranges]
+        self._hooks = []
+        if self.active:
+            for bi, (a, b) in enumerate(self.ranges):
+                for i in range(a, b):
+                    self._hooks.append(self.params[i].register_post_accumulate_grad_hook(
+                        lambda _p, bi=bi: self._arrived(bi)))
+
+    def _arrived(self, bi: int) -> None:
+        if not self.armed:
+            return
+        self._left[bi] -= 1
+        if self._left[bi] == 0:
+            a, b = self.ranges[bi]
+            torch._foreach_copy_(self.fviews[a:b], [p.grad for p in self.params[a:b]])
+            self.ex.launch(f"b{bi}")
+
+    def arm(self) -> None:
+        self.armed = True
+        self._left = [b - a for a, b in self.ranges]
+
+    def wait(self) -> None:
+        """Join; every bucket must have been launched by this backward."""
+        if not self.armed:
+            return
+        if any(self._left):
+            raise RuntimeError(f"gradient buckets not complete after backward: {self._left}")
+        self.ex.wait()
+        if self.copy_back:
+            torch._foreach_copy_([p.grad for p in self.params], self.fviews)
+        self.armed = False
+
+    def remove(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def even_buckets(n: int, k: int) -> List[Tuple[int, int]]:
+    """k contiguous runs of n parameters, the last run first in backward order."""
+    k = max(1, min(k, n))
+    cuts = [round(i * n / k) for i in range(k + 1)]
+    return [(cuts[i], cuts[i + 1]) for i in range(k)]
 
 
 def broadcast_arena(flat: torch.Tensor, src: int = 0, group=None) -> None:

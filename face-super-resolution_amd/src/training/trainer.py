@@ -169,6 +169,7 @@ class Trainer:
         self.adam_state[2][3] = self.lr
         self._engines: Dict[tuple, FENEngine] = {}
         self._generic_opt: Optional[FusedAdamW] = None
+        self._flat_g: Optional[torch.Tensor] = None
         # stage-3 GAN (trainer.py:230-250): the reference's discriminator optimizer object
         self.use_gan = self.config.gan_weight > 0 and discriminator is not None
         self.discriminator = self.optimizer_d = self.gan_loss = None
@@ -181,6 +182,12 @@ class Trainer:
             self._make_d_capturable()
         self._gan_graph: Optional[dict] = None
         self._gan_eager_left = 2
+        # data-parallel gradient exchanges of the module-autograd path (generator, discriminator):
+        # bucketed, launched from post-accumulate hooks as the backward completes each bucket,
+        # stream-ordered (capturable); built on first use.  _dp_force: exchange at world size 1
+        # too (the one-rank RCCL tests)
+        self._g_ex = self._d_ex = None
+        self._dp_force = False
         self.early_stopping = EarlyStopping(self.config.early_stopping_patience, self.config.early_stopping_mode)
         self.checkpoint_dir = Path(self.config.checkpoint_dir)
         if self.rank == 0:
@@ -227,15 +234,41 @@ class Trainer:
             return hr.chunk(self.world)[self.rank]
         return hr
 
+    def _dp_exchanges(self) -> None:
+        """The generator's gradients land in `_flat_g` (the fused AdamW's arena) bucket by bucket
+        -- tail, rg{G-1}..rg0, head: dp.bucket_plan's groups -- each all-reduced as soon as the
+        backward completes it; the discriminator's in two buckets, copied back into `.grad` for
+        optimizer_d.  Only when exchanging (world > 1, or forced)."""
+        if self._flat_g is None:
+            self._flat_g = torch.zeros_like(self.model._fen_flat)
+        if not (self.world > 1 or self._dp_force) or self._g_ex is not None:
+            return
+        from .dp import ParamGradExchange, _group_of, even_buckets
+        names = [n for n, _ in self.model.named_parameters()]
+        runs, a = [], 0
+        for i in range(1, len(names) + 1):
+            if i == len(names) or _group_of(names[i]) != _group_of(names[a]):
+                runs.append((a, i))
+                a = i
+        self._g_ex = ParamGradExchange(list(self.model.parameters()), self._flat_g, runs, force=self._dp_force)
+        if self.use_gan:
+            dps = list(self.discriminator.parameters())
+            dflat = torch.zeros(sum(p.numel() for p in dps), device=self.device)
+            self._d_ex = ParamGradExchange(dps, dflat, even_buckets(len(dps), 2), force=self._dp_force,
+                                           copy_back=True)
+
     def _generic_step(self, hr: torch.Tensor, update: bool = True) -> torch.Tensor:
         """Any other content loss: module autograd path + RCCL grad all-reduce + fused AdamW
         (only on the accumulation step, `update`; the loss is divided by accumulation_steps as
         trainer.py:477 does)."""
+        self._dp_exchanges()
         lr = bicubic_down4(hr)
         sr = self.model(lr)
         loss = self._content(sr, hr)
         for p in self.model.parameters():
             p.grad = None
+        if update and self._g_ex is not None:
+            self._g_ex.arm()
         (loss / (self.world * self._accum())).backward()
         if update:
             self._apply_generic_update()
@@ -254,6 +287,7 @@ class Trainer:
         real vs detached fake, then the generator on content + gan_weight x adversarial loss.
         Both networks run on the HIP path through their module autograd."""
         D, gl = self.discriminator, self.gan_loss
+        self._dp_exchanges()
         lr = bicubic_down4(hr)
         D.train()
         for _ in range(self.config.d_updates_per_g):
@@ -261,25 +295,28 @@ class Trainer:
             with torch.no_grad():
                 sr_d = self.model(lr)
             d_loss = (gl(D(hr), True) + gl(D(sr_d.detach()), False)) / 2
+            if self._d_ex is not None:
+                self._d_ex.arm()
             (d_loss / self.world).backward()
-            if self.world > 1:
-                for p in D.parameters():
-                    if p.grad is not None:
-                        dist.all_reduce(p.grad)
+            if self._d_ex is not None:
+                self._d_ex.wait()        # D's two buckets, all-reduced as the backward completed them
             self.optimizer_d.step()
         sr = self.model(lr)
         content = self._content(sr, hr)
         loss = content + self.config.gan_weight * gl(D(sr), True)
         for p in self.model.parameters():
             p.grad = None
+        if update and self._g_ex is not None:
+            self._g_ex.arm()
         (loss / (self.world * self._accum())).backward()
         if update:
             self._apply_generic_update()
         return loss.detach()
 
     def _capture_gan(self) -> bool:
-        return (bool(self.config.capture_gan_step) and self.world == 1 and torch.cuda.is_available()
-                and self._accum() == 1)
+        """World size 1, or N > 1: the exchanges are stream-ordered (RCCL on side streams
+        forked and joined inside the captured iteration)."""
+        return bool(self.config.capture_gan_step) and torch.cuda.is_available() and self._accum() == 1
 
     def _make_d_capturable(self) -> None:
         """The captured GAN iteration steps optimizer_d inside the graph: its param groups need
@@ -329,9 +366,10 @@ class Trainer:
         return st["loss"]
 
     def _apply_generic_update(self):
+        if self._flat_g is None:
+            self._flat_g = torch.zeros_like(self.model._fen_flat)
         if self._generic_opt is None:
             flat = self.model._fen_flat
-            self._flat_g = torch.zeros_like(flat)
             self._generic_opt = FusedAdamW(list(self.model.parameters()), flat, self._flat_g, lr=self.lr,
                                            weight_decay=self.config.weight_decay, max_norm=self.config.gradient_clip,
                                            state=self.adam_state)
@@ -340,10 +378,13 @@ class Trainer:
             for p in self.model.parameters():
                 self._flat_g_views.append(self._flat_g[off:off + p.numel()].view_as(p))
                 off += p.numel()
-        # one multi-tensor copy (a few launches) instead of one copy per parameter (444 here)
-        torch._foreach_copy_(self._flat_g_views, [p.grad for p in self.model.parameters()])
-        if self.world > 1:
-            dist.all_reduce(self._flat_g)
+        if self._g_ex is not None:
+            self._g_ex.wait()            # the buckets, copied and all-reduced during the backward
+        else:
+            # one multi-tensor copy (a few launches) instead of one copy per parameter (444 here)
+            torch._foreach_copy_(self._flat_g_views, [p.grad for p in self.model.parameters()])
+            if self.world > 1:
+                dist.all_reduce(self._flat_g)
         self._generic_opt.set_lr(self.lr)
         self._generic_opt.step()
 

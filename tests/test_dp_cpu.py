@@ -166,3 +166,60 @@ def test_val_metrics_reduced_across_ranks(tmp_path):
     np.testing.assert_array_equal(r0["stops"], r1["stops"])
     # global mean over all 5 batches of each epoch: (90 + 50) / 5, ...
     np.testing.assert_allclose(r0["psnr"], [28.0, 29.0, 30.0, 31.0])
+
+
+# ------------------------------------------------------------------ module-path exchange
+def _pge_worker(rank, world, port, out_dir):
+    """ParamGradExchange over gloo: each rank back-propagates its shard of a global batch with
+    the loss pre-scaled by 1/world; the buckets' hooks copy and all-reduce as the backward
+    completes them; after wait() the flat buffer (and, with copy_back, every .grad) holds the
+    global-batch gradient.  An unarmed backward exchanges nothing."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from src.training.dp import ParamGradExchange, even_buckets
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 4), torch.nn.Tanh(),
+                                  torch.nn.Linear(4, 3))
+        ps = list(net.parameters())
+        flat = torch.zeros(sum(p.numel() for p in ps))
+        ex = ParamGradExchange(ps, flat, even_buckets(len(ps), 3), copy_back=True)
+        assert ex.active and ex.world == world and len(ex.ranges) == 3
+        x = torch.randn(8, 6, generator=torch.Generator().manual_seed(1))
+        y = torch.randn(8, 3, generator=torch.Generator().manual_seed(2))
+        shard = slice(rank * 4, rank * 4 + 4)
+        # unarmed: hooks see the grads but launch nothing; flat stays zero
+        loss = torch.nn.functional.mse_loss(net(x[shard]), y[shard])
+        (loss / world).backward()
+        assert float(flat.abs().sum()) == 0.0
+        ex.wait()                                     # a no-op when not armed
+        for p in ps:
+            p.grad = None
+        ex.arm()
+        loss = torch.nn.functional.mse_loss(net(x[shard]), y[shard])
+        (loss / world).backward()
+        ex.wait()
+        got = [p.grad.clone() for p in ps]
+        for p in ps:
+            p.grad = None
+        torch.nn.functional.mse_loss(net(x), y).backward()   # the global batch, one process
+        ref = [p.grad for p in ps]
+        err = max(float((a - b).abs().max()) for a, b in zip(got, ref))
+        torch.save({"err": err, "flat_ok": bool(torch.allclose(flat, torch.cat([r.reshape(-1) for r in ref]),
+                                                                atol=1e-6))}, os.path.join(out_dir, f"pge{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_param_grad_exchange_world2(tmp_path):
+    mp.spawn(_pge_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        d = torch.load(tmp_path / f"pge{r}.pt", weights_only=True)
+        assert d["err"] <= 1e-6 and d["flat_ok"], d
+
+
+def test_even_buckets():
+    from src.training.dp import even_buckets
+    assert even_buckets(10, 3) == [(0, 3), (3, 7), (7, 10)]
+    assert even_buckets(2, 5) == [(0, 1), (1, 2)]
+    assert even_buckets(7, 1) == [(0, 7)]

@@ -78,3 +78,75 @@ def test_engine_step_over_rccl(precision):
             assert torch.equal(e2.flat_p, e1.flat_p), step
     finally:
         dist.destroy_process_group()
+
+
+def _init_one_rank():
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", torch.cuda.current_device()))
+
+
+def test_engine_captured_step_over_rccl():
+    """The DP training step recorded in one hipGraph with its bucket all-reduces
+    (dp.BucketExchange on the GPU is stream-ordered: each bucket's RCCL all_reduce on a side
+    stream forked from the capture stream at the backward's mark, the side stream joined before
+    clip + AdamW), on a one-rank RCCL group with the exchange forced: the capture's warm-up step
+    and every replay equal the exchange-free eager step bit for bit."""
+    from src.hip.engine import FENEngine
+    from src.models import FaceEnhanceNet
+    from src.training.dp import BucketExchange
+
+    def model():
+        torch.manual_seed(4)
+        m = FaceEnhanceNet(num_channels=64, num_groups=2, blocks_per_group=2, precision="bf16")
+        with torch.no_grad():
+            m.conv_last.weight.normal_(0, 1e-3, generator=torch.Generator().manual_seed(5))
+        return m
+
+    hr = torch.rand(2, 3, 128, 128, generator=torch.Generator().manual_seed(7)).to(DEV)
+    kw = dict(batch=2, lr_hw=(32, 32), dtype=torch.bfloat16, train=True, clip=0.5, lr=1e-3)
+    e1 = FENEngine(model(), **kw)
+    _init_one_rank()
+    try:
+        e2 = FENEngine(model(), **kw, exchange=lambda flat, plan: BucketExchange(flat, plan, force=True))
+        assert e2.exchange.active and e2.exchange.stream is not None and e2.exchange.capturable
+        e2.hr.copy_(hr)
+        e2.capture()                      # one eager step (exchanged), then the recorded step
+        e1.step(hr)
+        torch.cuda.synchronize()
+        assert torch.equal(e2.flat_p, e1.flat_p)
+        for i in range(3):
+            e2.replay()
+            l1 = e1.step(hr)
+            torch.cuda.synchronize()
+            assert torch.equal(e2.loss, l1), i
+            assert torch.equal(e2.flat_g, e1.flat_g), i
+            assert torch.equal(e2.flat_p, e1.flat_p), i
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gan_captured_iteration_over_rccl(tmp_path):
+    """The stage-3 GAN iteration with the module path's bucketed exchanges (dp.ParamGradExchange:
+    the generator's tail / group / head buckets and the discriminator's two, each all-reduced
+    from a post-accumulate hook as the backward completes it, stream-ordered), forced on a
+    one-rank RCCL group and replayed from a captured hipGraph: bit-identical to the eager,
+    exchange-free iteration (losses, generator arena, discriminator parameters and buffers)."""
+    from test_gpu_gan_capture import _state, _trainer
+    eager = _trainer(False, tmp_path / "e")
+    _init_one_rank()
+    try:
+        cap = _trainer(True, tmp_path / "c")
+        cap._dp_force = True
+        gen = torch.Generator().manual_seed(5)
+        for i in range(5):
+            hr = torch.rand(2, 3, 128, 128, generator=gen).to(DEV)
+            le = float(eager._gan_iteration(hr))
+            lc = float(cap._gan_iteration(hr))
+            assert le == lc, (i, le, lc)
+            for a, b in zip(_state(eager), _state(cap)):
+                assert torch.equal(a, b), i
+        assert cap._gan_graph is not None and cap._g_ex is not None and cap._d_ex is not None
+        assert len(cap._g_ex.ranges) == 2 + 1 and len(cap._d_ex.ranges) == 2   # tail, rg0, head
+    finally:
+        dist.destroy_process_group()

@@ -114,11 +114,26 @@ def test_train64_fp32(g10, B):
     assert not bad, dict(list(bad.items())[:12])
 
 
+def _adamw_first_step(p, g, lr=1e-4, clip=0.5, b1=0.9, b2=0.999, eps=1e-8):
+    """The reference's update (trainer.py:490-503: clip_grad_norm_ 0.5, AdamW step 1, no weight
+    decay) in float64 on the given arena: what the step must do with the gradients it has."""
+    n = np.sqrt(sum(float((v.astype(np.float64) ** 2).sum()) for v in g.values()))
+    coef = min(1.0, clip / (n + 1e-6))
+    out = {}
+    for k, v in g.items():
+        gc = v.astype(np.float64) * coef
+        m, vv = (1 - b1) * gc, (1 - b2) * gc * gc
+        out[k] = p[k].astype(np.float64) - lr * (m / (1 - b1)) / (np.sqrt(vv / (1 - b2)) + eps)
+    return out
+
+
 def test_train64_bf16_batch32(g10):
     """The bench's training configuration (bf16, B=32): every gradient within the bf16
-    whole-network bound of the reference's, and the step moves every parameter like the
-    reference's step (AdamW's first step is ~lr * sign(g): projection agreement of the
-    update within 0.25 of its norm -- sign flips where |g| is below bf16 resolution)."""
+    whole-network bound of the reference's; the step is the reference's clip + AdamW applied
+    to those gradients (float64 replay, max |d| <= 2e-6 = 2 % of lr).  (The update itself is
+    not compared with the reference's: AdamW's first step is ~lr * sign(g), and where |g| is
+    below bf16 resolution the sign is noise -- whole tensors of the deepest layers move by a
+    different +-lr pattern.  The fp32 test pins the step against the reference.)"""
     m, eng = _engine(g10, 32, torch.bfloat16)
     pre = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
     grads = _grads(eng)
@@ -127,10 +142,7 @@ def test_train64_bf16_batch32(g10):
     _check_grads(g10, grads, BF16_REL, BF16_PROJ)
     eng.upd.run()
     torch.cuda.synchronize()
-    worst = 0.0
-    for i, (k, p) in enumerate(m.named_parameters()):
-        delta = (p.detach().cpu() - pre[k]).numpy()
-        n = float(g10["snorm/" + k])
-        worst = max(worst, float(np.abs(_proj(i, delta) - g10["sproj/" + k]).max()) / max(n, 1e-30))
-    print(f"bf16 step: worst projection error {worst:.3f} of |delta|")
-    assert worst <= 0.25, worst
+    want = _adamw_first_step({k: v.numpy() for k, v in pre.items()}, {k: v.numpy() for k, v in grads.items()})
+    worst = max(float(np.abs(p.detach().cpu().numpy() - want[k]).max()) for k, p in m.named_parameters())
+    print(f"bf16 step vs the float64 replay of clip + AdamW on its gradients: max |d| {worst:.2e}")
+    assert worst <= 2e-6, worst
