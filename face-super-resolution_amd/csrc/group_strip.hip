@@ -114,6 +114,14 @@ struct GsArgs {
     const float* fc2[FEN_GS_MAXNB];           // [64][Cr]
     float* s_out[FEN_GS_MAXNB];               // optional gates s [B][64] (attention maps)
     char* work;
+    int save;                                 // training: the backward's operands out
+    void* sv_x[FEN_GS_MAXNB];
+    void* sv_z1[FEN_GS_MAXNB];
+    void* sv_a1[FEN_GS_MAXNB];
+    void* sv_t[FEN_GS_MAXNB];
+    float* sv_mean[FEN_GS_MAXNB];
+    float* sv_hid[FEN_GS_MAXNB];
+    void* x_last;
 };
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -328,6 +336,13 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 0);
             }
     };
+    // training: the wave's row of a saved activation (plain stores; the backward reads it)
+    auto save_row = [&](void* base, const uint2 (&v)[4][4]) {
+        void* bp = base;
+        asm volatile("" : "+s"(bp));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, 0, (int)act_bytes, 0x00020000);
+        store_row(rs, (int)((size_t)(im * H + r0 + wave) * SW * 128), v, 0);
+    };
     // a boundary row (16-B chunks, lane handles chunks lane + 64 k) -> LDS image row lrow
     auto halo_to_lds = [&](int lrow, const uint4 (&v)[8]) {
         int ll = lane;
@@ -420,6 +435,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         }
         // x_j's boundary rows for the neighbours (their halo rows of x_{j+1})
         if (!gc && bwave) store_row(wsr, rowoff(L.bx, strip, par, side), xr, 16);
+        if (A.save && j > 0) save_row(gc ? A.x_last : A.sv_x[j], xr);   // x_0 is the group input
         if (j > 0 && hwave) {
             // the neighbour's x_{j-1}, t_{j-1} rows (this wave's half), after its flag (its
             // storing wave drained them, then signalled): this wave polls and loads (row 1);
@@ -505,6 +521,17 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         issue_kh02(ci + 1);
         // ---- conv1 epilogue: a1 = PReLU(conv1 + b1) -> LDS (own row), boundary rows out; the
         // row's per-channel sums of a1 (fp32, before the 16-bit rounding conv2 reads) -> red[wave]
+        if (A.save) {                                       // z1 = conv1 + b1 (PReLU's input)
+            uint2 zv[4][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float4 bb = *(const float4*)(cst + 16 * m + 4 * q);
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    zv[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
+            }
+            save_row(A.sv_z1[j], zv);
+        }
         {
             uint2 av[4][4];
 #pragma unroll
@@ -530,6 +557,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             }
             write_row_lds(wave + 1, av);
             if (bwave) store_row(wsr, rowoff(L.ba, strip, par, side), av, 16);
+            if (A.save) save_row(A.sv_a1[j], av);
         }
         // ================= conv2 =================
 #pragma unroll
@@ -634,6 +662,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 tr[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
         }
         if (bwave) store_row(wsr, rowoff(L.bt, strip, par, side), tr, 16);   // t_j's boundary row
+        if (A.save) save_row(A.sv_t[j], tr);
         if (wave == 1) {
             // the gate of RCAB j (blocks.py:83-92): mean over the image from the S strip
             // partials, each an 8-B {tag, value} granule (the data is the flag: sc1 loads
@@ -702,6 +731,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             const float sg = 1.f / (1.f + expf(-z));
             gate[lane] = sg * A.res_scale;
             if (strip == 0 && A.s_out[j]) A.s_out[j][im * 64 + lane] = sg;
+            if (strip == 0 && A.save) {
+                A.sv_mean[j][im * 64 + lane] = mean;
+                if (lane < Cr) A.sv_hid[j][im * Cr + lane] = hid;
+            }
         }
         if (wave >= 2 && wave <= 4) {                       // the next conv's epilogue constants
             const bool ng = j + 1 == NB;
@@ -780,6 +813,18 @@ extern "C" int fen_group_strip(const fen_group_strip_desc* d, void* stream) {
     a.B = d->B, a.H = d->H, a.S = d->H / SR, a.NB = d->nb, a.Cr = d->Cr;
     a.res_scale = d->res_scale, a.inv_hw = 1.0f / (float)(d->H * d->W);
     a.x = d->x, a.y = d->y, a.work = (char*)d->work;
+    a.save = d->save ? 1 : 0;
+    if (a.save) {
+        if (!d->x_last) return FEN_EINVAL;
+        a.x_last = d->x_last;
+        for (int j = 0; j < d->nb; ++j) {
+            if ((j > 0 && !d->sv_x[j]) || !d->sv_z1[j] || !d->sv_a1[j] || !d->sv_t[j] || !d->sv_mean[j] ||
+                !d->sv_hid[j] || !d->s_out[j])
+                return FEN_EINVAL;
+            a.sv_x[j] = d->sv_x[j], a.sv_z1[j] = d->sv_z1[j], a.sv_a1[j] = d->sv_a1[j], a.sv_t[j] = d->sv_t[j];
+            a.sv_mean[j] = d->sv_mean[j], a.sv_hid[j] = d->sv_hid[j];
+        }
+    }
     for (int j = 0; j < d->nb; ++j) {
         if (!d->w1[j] || !d->b1[j] || !d->alpha[j] || !d->w2[j] || !d->b2[j] || !d->fc1[j] || !d->fc2[j])
             return FEN_EINVAL;

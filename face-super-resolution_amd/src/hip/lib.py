@@ -79,6 +79,9 @@ class GroupStripDesc(Structure):
         ("w2", c_void_p * GS_MAXNB), ("b2", c_void_p * GS_MAXNB), ("fc1", c_void_p * GS_MAXNB),
         ("fc2", c_void_p * GS_MAXNB), ("s_out", c_void_p * GS_MAXNB),
         ("wg", c_void_p), ("bg", c_void_p), ("work", c_void_p), ("work_bytes", c_size_t),
+        ("save", c_int), ("sv_x", c_void_p * GS_MAXNB), ("sv_z1", c_void_p * GS_MAXNB),
+        ("sv_a1", c_void_p * GS_MAXNB), ("sv_t", c_void_p * GS_MAXNB), ("sv_mean", c_void_p * GS_MAXNB),
+        ("sv_hid", c_void_p * GS_MAXNB), ("x_last", c_void_p),
     ]
 
 

@@ -62,6 +62,9 @@ GROUP_END_FUSED = os.environ.get("FEN_GROUP_END", "fused") != "split"
 # group_strip.hip) where its envelope holds (16-bit, 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP=0
 # selects the per-RCAB deferred launches
 GROUP_STRIP = os.environ.get("FEN_GROUP_STRIP", "1") != "0"
+# ... and the training forward too (the kernel then writes the backward's saved tensors);
+# FEN_GROUP_STRIP_TRAIN=0 keeps training on the per-RCAB launches
+GROUP_STRIP_TRAIN = os.environ.get("FEN_GROUP_STRIP_TRAIN", "1") != "0"
 # RCAB backward: the SE backward and its apply as one fen_se_bwd_fused launch (default) or
 # the fen_se_bwd + fen_se_bwd_apply pair (FEN_SE_BWD=pair; shapes outside the fused
 # kernel's envelope always take the pair)
@@ -397,11 +400,13 @@ class Forward:
 
     def _strip_ok(self, x) -> bool:
         B, H, W, C = x.shape
-        return (GROUP_STRIP and not self.save and self.s.NB > 0 and
+        return (GROUP_STRIP and (not self.save or GROUP_STRIP_TRAIN) and self.s.NB > 0 and
                 bool(self.ctx.lib.fen_group_strip_supported(self.ctx.code, B, H, W, C, self.s.Cr, self.s.NB)))
 
     def _group_strip(self, x: torch.Tensor, pre: str, names: Sequence[str], y: torch.Tensor) -> dict:
-        """The whole group in one fen_group_strip launch (inference): y = conv(chain(x)) + b + x."""
+        """The whole group in one fen_group_strip launch: y = conv(chain(x)) + b + x; in training
+        (self.save) the launch also writes every RCAB's x_j, z1, a1, t_j, s, mean, hid and the
+        chain's output (the backward's operands, the per-RCAB launches' saved set)."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
         d = L.GroupStripDesc()
@@ -417,18 +422,31 @@ class Forward:
             d.w2[b], d.b2[b] = ptr(Wt.packed(q + "conv2", 0)), ptr(p[q + "conv2.bias"])
             d.fc1[b], d.fc2[b] = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
             sg = None
-            if self.attn is not None:
+            if self.attn is not None or self.save:
                 sg = ctx.alloc((B, C), torch.float32)
-                self.attn[names[b]] = sg
                 d.s_out[b] = ptr(sg)
-            blocks.append(dict(s=sg))
+                if self.attn is not None:
+                    self.attn[names[b]] = sg
+            if self.save:
+                xb = x if b == 0 else ctx.alloc(x.shape)
+                z1, a1, t = ctx.alloc(x.shape), ctx.alloc(x.shape), ctx.alloc(x.shape)
+                mean, hid = ctx.alloc((B, C), torch.float32), ctx.alloc((B, s.Cr), torch.float32)
+                d.sv_x[b], d.sv_z1[b], d.sv_a1[b], d.sv_t[b] = ptr(xb), ptr(z1), ptr(a1), ptr(t)
+                d.sv_mean[b], d.sv_hid[b] = ptr(mean), ptr(hid)
+                blocks.append(dict(x=xb, z1=z1, a1=a1, t=t, mean=mean, hid=hid, s=sg))
+            else:
+                blocks.append(dict(s=sg))
+        x_last = None
+        if self.save:
+            x_last = ctx.alloc(x.shape)
+            d.save, d.x_last = 1, ptr(x_last)
         d.wg, d.bg = ptr(Wt.packed(pre + "conv", 0)), ptr(p[pre + "conv.bias"])
         nbytes = int(ctx.lib.fen_group_strip_work_bytes(B, H))
         work = ctx.persistent_zeros(f"group_strip/{B}x{H}", nbytes)
         d.work, d.work_bytes = ptr(work), nbytes
         ctx.emit("group_strip", ctx.lib.fen_group_strip, byref(d))
         ctx.keep(d)
-        return dict(blocks=blocks, x=x, x_last=None)
+        return dict(blocks=blocks, x=x, x_last=x_last)
 
     def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None, pre: Optional[str] = None):
         """ResidualGroup (blocks.py:185-189) -> (y, saved)."""

@@ -224,7 +224,8 @@ int fen_rcab_group_end(const fen_rcab_deferred_desc* d, const void* w, const flo
 
 /* A whole ResidualGroup in ONE persistent launch (ResidualGroup.forward, blocks.py:185-189:
  * nb x RCAB.forward blocks.py:135-153 with ChannelAttention blocks.py:83-92, then the group
- * conv and the group's skip), inference.  Each image is cut into H/8 strips of 8 rows x 64
+ * conv and the group's skip), inference, or training with `save` (the backward's saved
+ * tensors written as the chain runs).  Each image is cut into H/8 strips of 8 rows x 64
  * columns; one block (one CU) keeps its strip resident (x_j in registers, x_j / a1 and the
  * running conv's filter in LDS) for all nb RCABs; the strips of an image exchange only the SE
  * pool partials and their first / last rows (sc1 hand-offs through `work`).  y may not alias x.
@@ -252,6 +253,16 @@ typedef struct {
     const float* bg;
     void* work;
     size_t work_bytes;
+    /* training (save = 1): the backward's operands, written as the chain runs (NHWC, 16-bit,
+     * [B,H,64,64]; x_j = RCAB j's input: sv_x[0] is not written, the group input x is it) */
+    int save;
+    void* sv_x[FEN_GS_MAXNB];
+    void* sv_z1[FEN_GS_MAXNB];         /* conv1 + b1, before PReLU                             */
+    void* sv_a1[FEN_GS_MAXNB];         /* PReLU(z1)                                            */
+    void* sv_t[FEN_GS_MAXNB];          /* conv2 + b2                                           */
+    float* sv_mean[FEN_GS_MAXNB];      /* the SE pool means [B][64]                            */
+    float* sv_hid[FEN_GS_MAXNB];       /* ReLU(FC1(mean)) [B][Cr]  (s goes to s_out)           */
+    void* x_last;                      /* the chain's output = the group conv's input          */
 } fen_group_strip_desc;
 int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
 size_t fen_group_strip_work_bytes(int B, int H);

@@ -141,3 +141,44 @@ def test_group_strip_graph_replay():
         torch.cuda.synchronize()
         assert torch.equal(y, y_e)
         assert _work_error(ctx) == [(0, 0, 0)]
+
+
+def _run_save(q, n, x_nhwc, dtype, strip):
+    from src.hip import net
+    from src.hip.net import Forward, NetSpec, Weights
+    from src.hip.program import Ctx
+    old = net.GROUP_STRIP, net.GROUP_STRIP_TRAIN
+    net.GROUP_STRIP = net.GROUP_STRIP_TRAIN = strip
+    try:
+        ctx = Ctx(dtype, DEV)
+        Wt = Weights({k: v.to(DEV) for k, v in q.items()}, dtype, DEV)
+        fw = Forward(NetSpec(C=64, G=1, NB=n, Cr=16), ctx, Wt, save=True)
+        used = fw._strip_ok(x_nhwc)
+        y, sv = fw.group(x_nhwc, 0, pre="rg.")
+        torch.cuda.synchronize()
+    finally:
+        net.GROUP_STRIP, net.GROUP_STRIP_TRAIN = old
+    return y, sv, used
+
+
+@pytest.mark.parametrize("B,H", [(32, 64), (3, 16)])
+def test_group_strip_training_saves_match_chain(B, H):
+    """Training form (bf16): the launch also writes what the backward reads -- every RCAB's
+    x_j, z1, a1, t_j, s, mean, hid and the chain's output -- equal to the per-RCAB training
+    launches' saved tensors within the chain tolerance (2e-3 rel per RCAB; the two kernels sum
+    in different orders), the gates within 2e-3; the output as in test_group_strip_vs_deferred_chain."""
+    dtype, n = torch.bfloat16, 4
+    q = _params(n, seed=21)
+    x = torch.randn(B, H, 64, 64, generator=torch.Generator().manual_seed(4)).to(DEV, dtype)
+    ys, svs, used = _run_save(q, n, x, dtype, True)
+    yd, svd, used_d = _run_save(q, n, x, dtype, False)
+    assert used and not used_d
+    tol = 2e-3 * (n + 1)
+    assert _rel(ys.float(), yd.float()) <= tol
+    assert _rel(svs["x_last"].float(), svd["x_last"].float()) <= tol
+    for j, (a, b) in enumerate(zip(svs["blocks"], svd["blocks"])):
+        for k in ("x", "z1", "a1", "t", "mean", "hid"):
+            r = _rel(a[k].float(), b[k].float())
+            assert r <= 2e-3 * (j + 1), (j, k, r)
+        assert float((a["s"] - b["s"]).abs().max()) <= 2e-3, j
+    assert svs["blocks"][0]["x"].data_ptr() == x.data_ptr()
