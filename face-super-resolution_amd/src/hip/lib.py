@@ -85,6 +85,19 @@ class GroupStripDesc(Structure):
     ]
 
 
+class GroupStripBwdDesc(Structure):
+    _fields_ = [
+        ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("Cr", c_int), ("nb", c_int),
+        ("res_scale", c_float), ("dy", c_void_p), ("dx", c_void_p), ("dres", c_void_p), ("wgt", c_void_p),
+        ("w1t", c_void_p * GS_MAXNB), ("w2t", c_void_p * GS_MAXNB), ("alpha", c_void_p * GS_MAXNB),
+        ("fc1", c_void_p * GS_MAXNB), ("fc2", c_void_p * GS_MAXNB), ("z1", c_void_p * GS_MAXNB),
+        ("t", c_void_p * GS_MAXNB), ("s", c_void_p * GS_MAXNB), ("mean", c_void_p * GS_MAXNB),
+        ("hid", c_void_p * GS_MAXNB), ("dt", c_void_p * GS_MAXNB), ("dz1", c_void_p * GS_MAXNB),
+        ("dalpha_part", c_void_p * GS_MAXNB), ("dw1p", c_void_p * GS_MAXNB), ("dw2p", c_void_p * GS_MAXNB),
+        ("work", c_void_p), ("work_bytes", c_size_t),
+    ]
+
+
 class WgradDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
@@ -107,6 +120,9 @@ _SIGS = {
     "fen_group_strip_supported": (c_int, [c_int] * 7),
     "fen_group_strip_work_bytes": (c_size_t, [c_int, c_int]),
     "fen_group_strip": (c_int, [POINTER(GroupStripDesc), c_void_p]),
+    "fen_group_strip_bwd_supported": (c_int, [c_int] * 7),
+    "fen_group_strip_bwd_work_bytes": (c_size_t, [c_int, c_int]),
+    "fen_group_strip_bwd": (c_int, [POINTER(GroupStripBwdDesc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
     "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),

@@ -204,6 +204,10 @@ SE_IN_BWD = os.environ.get("FEN_SE_IN_BWD", "fold") != "launch"
 # 8.826 ms per training step against the two-launch pair (3 same-box reps): off by default
 BWD_RES_FUSED = os.environ.get("FEN_RCAB_BWD_RES", "0") == "1"
 WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
+# a ResidualGroup's whole backward (group conv^T, every RCAB's SE backward, conv2^T, PReLU',
+# conv1^T) as ONE strip-resident fen_group_strip_bwd launch where its envelope holds (16-bit,
+# 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP_BWD=0 selects the per-RCAB launches
+GROUP_STRIP_BWD = os.environ.get("FEN_GROUP_STRIP_BWD", "1") != "0"
 
 
 class WgradBatch:
@@ -635,11 +639,69 @@ class Backward:
         self.wb.flush()
         self.cs.flush()
 
+    def _strip_bwd_ok(self, sv: dict, dy: torch.Tensor, extra_res: Sequence) -> bool:
+        B, H, W, C = dy.shape
+        blocks = sv.get("blocks") or []
+        return (GROUP_STRIP_BWD and self.s.NB > 0 and len(extra_res) <= 1 and self.ctx.code != L.F32
+                and len(blocks) == self.s.NB and all(b.get("z1") is not None for b in blocks)
+                and bool(self.ctx.lib.fen_group_strip_bwd_supported(self.ctx.code, B, H, W, C, self.s.Cr, self.s.NB)))
+
+    def _group_strip_bwd(self, sv: dict, dy: torch.Tensor, pre: str, extra_res: Sequence, dx_out) -> torch.Tensor:
+        """The group's backward in one fen_group_strip_bwd launch (data gradients, SE backward,
+        dt / dz1 for the weight gradients), then its weight gradients (8 per fen_wgrad3x3_multi
+        launch) and the PReLU / SE column sums."""
+        s, ctx, Wt, p, G = self.s, self.ctx, self.Wt, self.Wt.p, self.G
+        B, H, W, C = dy.shape
+        d = L.GroupStripBwdDesc()
+        d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.nb = ctx.code, B, H, W, C, s.Cr, s.NB
+        d.res_scale = float(s.res_scale)
+        dx = dx_out if dx_out is not None else ctx.alloc(dy.shape)
+        d.dy, d.dx = ptr(dy), ptr(dx)
+        if extra_res:
+            d.dres = ptr(extra_res[0])
+        d.wgt = ptr(Wt.packed(pre + "conv", 2))
+        outs = []
+        for b in range(s.NB):
+            q = f"{pre}blocks.{b}."
+            ca = q + "channel_attention.fc."
+            blk = sv["blocks"][b]
+            d.w1t[b], d.w2t[b] = ptr(Wt.packed(q + "conv1", 2)), ptr(Wt.packed(q + "conv2", 2))
+            d.alpha[b] = ptr(p[q + "prelu.weight"])
+            d.fc1[b], d.fc2[b] = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
+            d.z1[b], d.t[b] = ptr(blk["z1"]), ptr(blk["t"])
+            d.s[b], d.mean[b], d.hid[b] = ptr(blk["s"]), ptr(blk["mean"]), ptr(blk["hid"])
+            o = dict(dt=ctx.scratch(f"gsb_dt{b}", dy.shape), dz1=ctx.scratch(f"gsb_dz1{b}", dy.shape),
+                     dal=ctx.scratch(f"gsb_dal{b}", (B * H, C), torch.float32),
+                     dw1p=ctx.scratch(f"gsb_dw1p{b}", (B, s.Cr * C), torch.float32),
+                     dw2p=ctx.scratch(f"gsb_dw2p{b}", (B, s.Cr * C), torch.float32))
+            d.dt[b], d.dz1[b], d.dalpha_part[b] = ptr(o["dt"]), ptr(o["dz1"]), ptr(o["dal"])
+            d.dw1p[b], d.dw2p[b] = ptr(o["dw1p"]), ptr(o["dw2p"])
+            outs.append(o)
+        nbytes = int(ctx.lib.fen_group_strip_bwd_work_bytes(B, H))
+        work = ctx.persistent_zeros(f"group_strip_bwd/{B}x{H}", nbytes)
+        d.work, d.work_bytes = ptr(work), nbytes
+        ctx.emit("group_strip_bwd", ctx.lib.fen_group_strip_bwd, byref(d))
+        ctx.keep(d)
+        self.wb.add(sv["x_last"], dy, B, H, W, C, C, G[pre + "conv.weight"], G[pre + "conv.bias"])
+        for b in reversed(range(s.NB)):
+            q = f"{pre}blocks.{b}."
+            ca = q + "channel_attention.fc."
+            blk, o = sv["blocks"][b], outs[b]
+            self.wb.add(blk["a1"], o["dt"], B, H, W, C, C, G[q + "conv2.weight"], G[q + "conv2.bias"])
+            self.wb.add(blk["x"], o["dz1"], B, H, W, C, C, G[q + "conv1.weight"], G[q + "conv1.bias"])
+            self.cs.add(o["dal"], B * H, C, G[q + "prelu.weight"])
+            self.cs.add(o["dw1p"], B, s.Cr * C, G[ca + "0.weight"])
+            self.cs.add(o["dw2p"], B, s.Cr * C, G[ca + "2.weight"])
+        self.flush()
+        return dx
+
     def group(self, sv: dict, dy: torch.Tensor, g: int, extra_res: Sequence = (), dx_out=None,
               pre: Optional[str] = None) -> torch.Tensor:
         s, ctx, Wt = self.s, self.ctx, self.Wt
         B, H, W, C = dy.shape
         pre = f"residual_groups.{g}." if pre is None else pre
+        if self._strip_bwd_ok(sv, dy, extra_res):
+            return self._group_strip_bwd(sv, dy, pre, extra_res, dx_out)
         self._wg(pre + "conv", sv["x_last"], dy, B, H, W, C, C)
         d = ctx.scratch("bw_rg_in", dy.shape)
         blocks = sv["blocks"]

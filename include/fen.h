@@ -268,6 +268,49 @@ int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int
 size_t fen_group_strip_work_bytes(int B, int H);
 int fen_group_strip(const fen_group_strip_desc* d, void* stream);
 
+/* The backward of a whole ResidualGroup in ONE persistent launch (autograd of
+ * ResidualGroup.forward blocks.py:185-189 and of each RCAB blocks.py:135-153 /
+ * ChannelAttention blocks.py:83-92), on the saved tensors of a training fen_group_strip:
+ *   d = conv_g^T(dy);  for j = nb-1 .. 0:  SE backward (a = sum over the image of d * t_j),
+ *   dt_j = d * res_scale * s_j + g_j,  dz1_j = conv2_j^T(dt_j) * PReLU'(z1_j),
+ *   d += conv1_j^T(dz1_j);  dx = d + dy (+ dres).
+ * Writes dt_j and dz1_j (the conv2 / conv1 weight gradients' dy operands: run
+ * fen_wgrad3x3_multi on (a1_j, dt_j), (x_j, dz1_j) and (x_last, dy) afterwards),
+ * dalpha_part_j [B*H][64] (sum over each image row of conv2^T(dt) * z1 * [z1 <= 0]: column sums
+ * give prelu.weight's gradient), dw1p_j [B][Cr][64] and dw2p_j [B][64][Cr] (per-image SE weight
+ * gradients: column sums over B).  Same strips, envelope and hand-off scheme as
+ * fen_group_strip (its own `work`, fen_group_strip_bwd_work_bytes, ZEROED once).  w*t / wgt are
+ * the mode-2 (transposed) packs.  dx may not alias dy or dres.                                */
+typedef struct {
+    int dtype;                 /* FEN_BF16 or FEN_F16                                          */
+    int B, H, W, C, Cr, nb;
+    float res_scale;
+    const void* dy;            /* the group output's gradient NHWC [B,H,64,64]                 */
+    void* dx;                  /* the group input's gradient                                   */
+    const void* dres;          /* optional second residual gradient added to dx (or NULL)      */
+    const void* wgt;           /* the group conv, packed mode 2                                */
+    const void* w1t[FEN_GS_MAXNB];     /* per RCAB: conv1 packed mode 2                        */
+    const void* w2t[FEN_GS_MAXNB];     /* conv2 packed mode 2                                  */
+    const float* alpha[FEN_GS_MAXNB];
+    const float* fc1[FEN_GS_MAXNB];    /* [Cr][64]                                             */
+    const float* fc2[FEN_GS_MAXNB];    /* [64][Cr]                                             */
+    const void* z1[FEN_GS_MAXNB];      /* saved: conv1 + b1                                    */
+    const void* t[FEN_GS_MAXNB];       /* saved: conv2 + b2                                    */
+    const float* s[FEN_GS_MAXNB];      /* saved gates [B][64]                                  */
+    const float* mean[FEN_GS_MAXNB];   /* saved pool means [B][64]                             */
+    const float* hid[FEN_GS_MAXNB];    /* saved ReLU(FC1(mean)) [B][Cr]                        */
+    void* dt[FEN_GS_MAXNB];            /* out: dL/dt NHWC                                      */
+    void* dz1[FEN_GS_MAXNB];           /* out: dL/dz1 NHWC                                     */
+    float* dalpha_part[FEN_GS_MAXNB];  /* out: [B*H][64]                                       */
+    float* dw1p[FEN_GS_MAXNB];         /* out: [B][Cr][64]                                     */
+    float* dw2p[FEN_GS_MAXNB];         /* out: [B][64][Cr]                                     */
+    void* work;
+    size_t work_bytes;
+} fen_group_strip_bwd_desc;
+int fen_group_strip_bwd_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
+size_t fen_group_strip_bwd_work_bytes(int B, int H);
+int fen_group_strip_bwd(const fen_group_strip_bwd_desc* d, void* stream);
+
 /* The RCAB backward's two data gradients in one launch (autograd of blocks.py:145-147):
  *   dz1 = conv2^T(dt) * PReLU'(z1),  dalpha_part[b][tile][c] = sum over the tile of
  *   conv2^T(dt) * z1 * (z1 <= 0),  dx = conv1^T(dz1) + dy,
