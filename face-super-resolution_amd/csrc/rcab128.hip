@@ -1,0 +1,414 @@
+// 128-channel RCAB convs (BASELINE configs[4]: FaceEnhanceNet with num_channels = 128, Cr = 32,
+// reference src/models/blocks.py:105-153 (RCAB), blocks.py:83-92 (ChannelAttention),
+// blocks.py:185-189 (ResidualGroup)), one persistent launch per conv with the RCAB's elementwise
+// work folded into its prologue / epilogue:
+//   mode 1 (conv1):      in  = x_j = x_{j-1} + rs * s_{j-1} * t_{j-1}   (deferred gate; or x_j)
+//                        out = a1 = PReLU(conv1(x_j) + b1)   (+ x_j's own tile, for the next RCAB)
+//   mode 2 (conv2):      in  = a1;  out = t_j = conv2(a1) + b2  + per-tile channel sums of t_j
+//   mode 3 (group conv): in  = the chain's output (deferred gate as mode 1); out = conv + b + res
+// The gate s_{j-1} of an image (mean over its tiles' sums -> FC1 -> ReLU -> FC2 -> sigmoid) is
+// recomputed by every block in its prologue from the producer's tile sums: the kernel boundary is
+// the per-image hand-off, no block ever waits on another (any grid, graph-replayable).
+//
+// Tile = 4 rows x 64 px x 128 output channels; one 512-thread block per CU walks tiles
+// (grid = min(tiles, CUs); the stress config's 128x128 B=4 is exactly one tile per CU), wave w =
+// (row w >> 1, output-channel half w & 1): 64 px x 64 co, 16 accumulator tiles of
+// v_mfma_f32_16x16x32_{f16,bf16}, the group-strip kernel's per-wave shape.  LDS:
+//   * the input image: 6 rows (tile + halo) x 66 columns x 256 B (128 ch), 99 KB; 16-B chunk c
+//     of column col at chunk c ^ (col & 15) (16 consecutive columns at one chunk -> 16 distinct
+//     slots of the 256-B bank row);
+//   * a 3-slot filter ring: a slot = one (tap, 64-input-channel half) = [128 co][64 ci], 16 KB,
+//     filled by LDS-DMA two steps ahead (18 steps per conv, one barrier each).  128x128x9 filters
+//     (295 KB) do not fit beside the image.
+// Precision: 16-bit operands, fp32 accumulation; x_j, a1, t rounded to the 16-bit format where
+// the per-op path (conv + fen_se_fused) rounds them.
+#include "fen_common.h"
+
+namespace {
+
+constexpr int TR = 4, TW = 64, CC = 128;
+constexpr int ICOL = TW + 2;                 // 66 image columns
+constexpr int PXB = CC * 2;                  // 256 B per pixel
+constexpr int IROW = ICOL * PXB;             // 16896 B per image row
+constexpr int IMG = (TR + 2) * IROW;         // 101376 B = 99 DMA pieces
+constexpr int NUNIT = IMG / 16;              // 6336 16-B units
+constexpr int NPIECE = IMG / 1024;           // 99
+constexpr int SLOT = CC * 128;               // [128 co][64 ci] 16-bit
+constexpr int NSLOT = 3;
+constexpr int NSTEP = 18;                    // 9 taps x 2 input-channel halves
+constexpr int O_RING = IMG;
+constexpr int O_CST = O_RING + NSLOT * SLOT; // bias [128], alpha [128]
+constexpr int O_GATE = O_CST + 2 * CC * 4;   // rs * s [128]
+constexpr int O_RED = O_GATE + CC * 4;       // [4][128] f32
+constexpr int O_SCR = O_RED + 4 * CC * 4;    // mean [128], hid [32]
+constexpr int LDS128 = O_SCR + (CC + 32) * 4;
+static_assert(LDS128 <= 163840, "LDS budget");
+static_assert(IMG % 1024 == 0, "whole DMA pieces");
+constexpr unsigned OOB = 0x80000000u;        // a buffer offset past every tensor: loads return 0
+
+struct K128 {
+    int B, H, W, Cr;
+    float res_scale, inv_hw;
+    const void* x;        // conv input (mode 2: a1), or x_{j-1} with tp
+    const void* tp;       // t_{j-1} (deferred gate) or NULL
+    const float* pp;      // tile sums of t_{j-1} [B][tiles][128]
+    const float* pfc1;    // [Cr][128]
+    const float* pfc2;    // [128][Cr]
+    float* ps;            // s_{j-1} [B][128] copy or NULL
+    void* xo;             // x_j out or NULL
+    const void* w;        // packed mode 0 [9][128][128]
+    const float* bias;
+    const float* alpha;
+    const void* res;      // mode 3
+    void* y;
+    void* z1;             // mode 1, optional
+    float* part;          // mode 2
+};
+
+template <typename T>
+__device__ __forceinline__ uint2 pk4(float a, float b, float c, float d) {
+    return make_uint2(pack2<T>(a, b), pack2<T>(c, d));
+}
+// lanes q and q ^ 1 trade a 4-channel half so each holds 8 consecutive channels (chunk_of)
+__device__ __forceinline__ uint4 pair16(uint2 lo, uint2 hi) {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo.x, hi.x, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(lo.y, hi.y, false, false);
+    return make_uint4(a[0], b[0], a[1], b[1]);
+}
+__device__ __forceinline__ int chunk_of(int mp, int q) { return 4 * mp + ((q & 1) ? 2 : 0) + (q >> 1); }
+
+template <typename T, int MODE, bool COMB>
+__global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* img = smem;
+    char* ring = smem + O_RING;
+    float* cst = (float*)(smem + O_CST);
+    float* gate = (float*)(smem + O_GATE);
+    float* red = (float*)(smem + O_RED);
+    float* scr = (float*)(smem + O_SCR);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = wave_id();
+    const int wr = wave >> 1, wh = wave & 1;          // the wave's output row and channel half
+    const int B = A.B, H = A.H, W = A.W;
+    const int tpr = W / TW, tpi = (H / TR) * tpr, ntiles = B * tpi;
+    const unsigned act_bytes = (unsigned)((size_t)B * H * W * PXB);
+    const i32x4 wrs = make_rsrc(A.w, 9u * CC * CC * 2u);
+
+    // filter step s = (tap s >> 1, input half s & 1) into ring slot s % 3: this wave's 2 pieces
+    auto issue_step = [&](int s) {
+        const int tap = s >> 1, ch = s & 1;
+        char* slot = ring + (s % NSLOT) * SLOT;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int piece = 2 * wave + k;
+            int ll = lane;
+            asm volatile("" : "+v"(ll));
+            const int u = piece * 64 + ll, r = u >> 3, pc = u & 7;
+            const int lc = pc ^ ((r >> 1) & 7);
+            dma16(wrs, __builtin_amdgcn_readfirstlane(lds_addr(slot + piece * 1024)),
+                  ((tap * CC + r) * CC + ch * 64 + lc * 8) * 2);
+        }
+    };
+
+    int prev_b = -1;
+    for (int tile = xcd_block(); tile < ntiles; tile += gridDim.x) {
+        const int b = tile / tpi, rem = tile - b * tpi;
+        const int r0 = (rem / tpr) * TR, w0 = (rem % tpr) * TW;
+        issue_step(0);
+        issue_step(1);
+        if (tid < CC) {
+            cst[tid] = A.bias[tid];
+            if (MODE == 1) cst[CC + tid] = A.alpha[tid];
+        }
+        // ---------------- the input image ----------------
+        if constexpr (COMB) {
+            // x_j = x_{j-1} + rs * s * t_{j-1} over the tile + halo: x and t chunks in flight while
+            // the gate is computed
+            constexpr int KU = (NUNIT + 511) / 512;   // 13
+            const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, (int)act_bytes, 0x00020000);
+            const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc((void*)A.tp, 0, (int)act_bytes, 0x00020000);
+            uint4 xv[KU], tv[KU];
+            unsigned offs[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                const int u = tid + 512 * k;
+                const int lrow = u / (ICOL * 16), rr = u - lrow * (ICOL * 16);
+                const int col = rr >> 4, pc = rr & 15, lc = pc ^ (col & 15);
+                const int gh = r0 - 1 + lrow, gw = w0 - 1 + col;
+                const bool ok = u < NUNIT && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+                offs[k] = ok ? (unsigned)((((size_t)b * H + gh) * W + gw) * PXB + lc * 16) : OOB;
+                xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)offs[k], 0, 0));
+                tv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trs, (int)offs[k], 0, 0));
+            }
+            if (b != prev_b) {
+                // the gate of image b (blocks.py:83-92): mean of t_{j-1} from its tile sums
+                // (fixed order: tiles g, g + 4, ... per quarter, quarters in order)
+                {
+                    const int c = tid & (CC - 1), g = tid >> 7;
+                    const float* pb = A.pp + (size_t)b * tpi * CC + c;
+                    float sacc = 0.f;
+                    for (int k = g; k < tpi; k += 4) sacc += pb[(size_t)k * CC];
+                    red[g * CC + c] = sacc;
+                }
+                __syncthreads();
+                if (tid < CC) scr[tid] = ((red[tid] + red[CC + tid]) + (red[2 * CC + tid] + red[3 * CC + tid])) * A.inv_hw;
+                __syncthreads();
+                {
+                    // FC1 + ReLU: row k = tid >> 4 (k < Cr), 8 channels per lane, summed over the row of 16 lanes
+                    const int k = tid >> 4, j8 = (tid & 15) * 8;
+                    float h = 0.f;
+                    if (k < A.Cr) {
+                        const float* w1 = A.pfc1 + (size_t)k * CC + j8;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) h += w1[e] * scr[j8 + e];
+                    }
+                    h = group16_sum(h);
+                    if ((tid & 15) == 0 && k < 32) scr[CC + k] = fmaxf(h, 0.f);
+                }
+                __syncthreads();
+                if (tid < CC) {
+                    const float* w2 = A.pfc2 + (size_t)tid * A.Cr;
+                    float z = 0.f;
+                    for (int k = 0; k < A.Cr; ++k) z += w2[k] * scr[CC + k];
+                    const float sg = 1.f / (1.f + expf(-z));
+                    gate[tid] = sg * A.res_scale;
+                    if (A.ps && rem == 0) A.ps[(size_t)b * CC + tid] = sg;
+                }
+                prev_b = b;
+                __syncthreads();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            char* xo = (char*)A.xo;
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                const int u = tid + 512 * k;
+                if (u < NUNIT) {
+                    const int lrow = u / (ICOL * 16), rr = u - lrow * (ICOL * 16);
+                    const int col = rr >> 4, pc = rr & 15, lc = pc ^ (col & 15);
+                    const float4 ga = *(const float4*)(gate + lc * 8);
+                    const float4 gb = *(const float4*)(gate + lc * 8 + 4);
+                    const float g8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+                    float xf[8], tf[8], yv[8];
+                    unpack16<T>(xv[k], xf);
+                    unpack16<T>(tv[k], tf);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) yv[e] = tf[e] * g8[e] + xf[e];
+                    const uint4 o = pack16<T>(yv);
+                    *(uint4*)(img + u * 16) = o;
+                    // the tile's own x_j (not the halo: its owner writes it) for the next RCAB
+                    if (xo && lrow >= 1 && lrow <= TR && col >= 1 && col <= TW) *(uint4*)(xo + offs[k]) = o;
+                }
+            }
+        } else {
+            // plain input by LDS-DMA (zero padding: past-the-end offsets read 0)
+            const i32x4 xr = make_rsrc(A.x, act_bytes);
+            for (int k = 0; k < (NPIECE + 7) / 8; ++k) {
+                const int piece = wave + 8 * k;
+                if (piece >= NPIECE) break;
+                int ll = lane;
+                asm volatile("" : "+v"(ll));
+                const int u = piece * 64 + ll;
+                const int lrow = u / (ICOL * 16), rr = u - lrow * (ICOL * 16);
+                const int col = rr >> 4, pc = rr & 15, lc = pc ^ (col & 15);
+                const int gh = r0 - 1 + lrow, gw = w0 - 1 + col;
+                const bool ok = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+                const unsigned off = ok ? (unsigned)((((size_t)b * H + gh) * W + gw) * PXB + lc * 16) : OOB;
+                dma16(xr, __builtin_amdgcn_readfirstlane(lds_addr(img + piece * 1024)), (int)off);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+        // ---------------- the conv: 18 (tap, input-half) steps ----------------
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[m][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < NSTEP; ++s) {
+            if (s > 0) {
+                if (s + 1 < NSTEP) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();   // step s's pieces landed (every wave's); step s - 1's slot free
+            if (s + 2 < NSTEP) issue_step(s + 2);
+            const int tap = s >> 1, ch = s & 1, kh = tap / 3, kw = tap - 3 * kh;
+            int q = lane >> 4, c16 = lane & 15;
+            asm volatile("" : "+v"(q), "+v"(c16));
+            const char* ab = ring + (s % NSLOT) * SLOT + (64 * wh + c16) * 128;
+            const int ka = (c16 >> 1) & 7;
+            const int colb = c16 + kw, kb = colb & 15;
+            const char* bb = img + (wr + kh) * IROW + colb * PXB;
+            uint4 Af[2][4], Bf[2][4];
+            auto load = [&](int ks, uint4 (&a)[4], uint4 (&bv)[4]) {
+                const char* ap = ab + (((4 * ks + q) ^ ka) << 4);
+                const char* bp = bb + (((8 * ch + 4 * ks + q) ^ kb) << 4);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) a[m] = *(const uint4*)(ap + m * 2048);
+#pragma unroll
+                for (int p = 0; p < 4; ++p) bv[p] = *(const uint4*)(bp + p * 16 * PXB);
+            };
+            load(0, Af[0], Bf[0]);
+            load(1, Af[1], Bf[1]);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) mma16<T>(acc[m][p], Af[ks][m], Bf[ks][p]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+
+        // ---------------- epilogue: lane (q, c16) holds channels 64 wh + 16 m + 4 q + i of pixel
+        // w0 + 16 p + c16 in row r0 + wr ----------------
+        {
+            const int q = lane >> 4, c16 = lane & 15;
+            const size_t rowpx = ((size_t)b * H + r0 + wr) * W + w0 + c16;
+            char* yb = (char*)A.y + rowpx * PXB + 128 * wh + chunk_of(0, q) * 16;
+            uint2 ov[4][4];
+            if constexpr (MODE == 1) {
+                uint2 zv[4][4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int c0 = 64 * wh + 16 * m + 4 * q;
+                    const float4 bb4 = *(const float4*)(cst + c0);
+                    const float4 aa4 = *(const float4*)(cst + CC + c0);
+                    const float bia[4] = {bb4.x, bb4.y, bb4.z, bb4.w}, alp[4] = {aa4.x, aa4.y, aa4.z, aa4.w};
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        float z[4], v[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            z[i] = acc[m][p][i] + bia[i];
+                            v[i] = prelu_f(z[i], alp[i]);
+                        }
+                        zv[m][p] = pk4<T>(z[0], z[1], z[2], z[3]);
+                        ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
+                    }
+                }
+                if (A.z1) {
+                    char* zb = (char*)A.z1 + rowpx * PXB + 128 * wh + chunk_of(0, q) * 16;
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+#pragma unroll
+                        for (int mp = 0; mp < 2; ++mp)
+                            *(uint4*)(zb + p * 16 * PXB + mp * 64) = pair16(zv[2 * mp][p], zv[2 * mp + 1][p]);
+                }
+            } else if constexpr (MODE == 2) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int c0 = 64 * wh + 16 * m + 4 * q;
+                    const float4 bb4 = *(const float4*)(cst + c0);
+                    const float bia[4] = {bb4.x, bb4.y, bb4.z, bb4.w};
+                    float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        float v[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            v[i] = acc[m][p][i] + bia[i];
+                            rs[i] += v[i];
+                        }
+                        ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float sm = group16_sum(rs[i]);
+                        if (c16 == 0) red[wr * CC + c0 + i] = sm;
+                    }
+                }
+            } else {
+                const char* rb = (const char*)A.res + rowpx * PXB;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int c0 = 64 * wh + 16 * m + 4 * q;
+                    const float4 bb4 = *(const float4*)(cst + c0);
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        float rv[4];
+                        ld4<T>(rb + p * 16 * PXB + c0 * 2, rv);
+                        ov[m][p] = pk4<T>(acc[m][p][0] + bb4.x + rv[0], acc[m][p][1] + bb4.y + rv[1],
+                                          acc[m][p][2] + bb4.z + rv[2], acc[m][p][3] + bb4.w + rv[3]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int mp = 0; mp < 2; ++mp)
+                    *(uint4*)(yb + p * 16 * PXB + mp * 64) = pair16(ov[2 * mp][p], ov[2 * mp + 1][p]);
+        }
+        __syncthreads();   // the image and the ring are free for the next tile; red complete
+        if constexpr (MODE == 2) {
+            if (tid < CC)
+                A.part[((size_t)b * tpi + rem) * CC + tid] =
+                    (red[tid] + red[CC + tid]) + (red[2 * CC + tid] + red[3 * CC + tid]);
+        }
+    }
+}
+
+int g_c128_cus = 0;
+
+template <typename T, int MODE, bool COMB>
+void launch128(const K128& a, int grid, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_rcab128<T, MODE, COMB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS128);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_rcab128<T, MODE, COMB>), dim3(grid), dim3(512), LDS128, s, a);
+}
+
+template <typename T>
+void dispatch128(const K128& a, int mode, bool comb, int grid, hipStream_t s) {
+    if (mode == 1) comb ? launch128<T, 1, true>(a, grid, s) : launch128<T, 1, false>(a, grid, s);
+    else if (mode == 2) launch128<T, 2, false>(a, grid, s);
+    else comb ? launch128<T, 3, true>(a, grid, s) : launch128<T, 3, false>(a, grid, s);
+}
+
+}  // namespace
+
+extern "C" int fen_rcab_c128_supported(int dtype, int B, int H, int W, int C, int Cr) {
+    if ((dtype != FEN_BF16 && dtype != FEN_F16) || C != CC || B <= 0 || H <= 0 || W <= 0 || H % TR || W % TW ||
+        Cr <= 0 || Cr > 32)
+        return 0;
+    if ((size_t)B * H * W * PXB >= (size_t)0x7fff0000) return 0;      // 32-bit buffer offsets
+    return 1;
+}
+
+extern "C" int fen_rcab_c128_tiles(int H, int W) { return (H / TR) * (W / TW); }
+
+extern "C" int fen_rcab_c128(const fen_rcab_c128_desc* d, void* stream) {
+    if (!d || !d->x || !d->w || !d->bias || !d->y) return FEN_EINVAL;
+    if (!fen_rcab_c128_supported(d->dtype, d->B, d->H, d->W, d->C, d->Cr > 0 ? d->Cr : 1)) return FEN_EUNSUPPORTED;
+    const int mode = d->mode;
+    if (mode < 1 || mode > 3) return FEN_EINVAL;
+    const bool comb = d->tp != nullptr;
+    if (comb && (mode == 2 || !d->pp || !d->pfc1 || !d->pfc2 || d->Cr <= 0 || d->Cr > 32)) return FEN_EINVAL;
+    if (mode == 1 && !d->alpha) return FEN_EINVAL;
+    if (mode == 2 && !d->part) return FEN_EINVAL;
+    if (mode == 3 && !d->res) return FEN_EINVAL;
+    if (d->y == d->x || (comb && d->y == d->tp) || (d->xo && (d->xo == d->x || d->xo == d->tp))) return FEN_EINVAL;
+    K128 a{};
+    a.B = d->B, a.H = d->H, a.W = d->W, a.Cr = d->Cr;
+    a.res_scale = d->res_scale, a.inv_hw = 1.0f / (float)(d->H * d->W);
+    a.x = d->x, a.tp = d->tp, a.pp = d->pp, a.pfc1 = d->pfc1, a.pfc2 = d->pfc2, a.ps = d->ps;
+    a.xo = comb ? d->xo : nullptr;
+    a.w = d->w, a.bias = d->bias, a.alpha = d->alpha, a.res = d->res, a.y = d->y, a.z1 = d->z1, a.part = d->part;
+    if (g_c128_cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_c128_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_c128_cus <= 0) g_c128_cus = 256;
+    }
+    const int ntiles = d->B * (d->H / TR) * (d->W / TW);
+    const int grid = ntiles < g_c128_cus ? ntiles : g_c128_cus;
+    hipStream_t s = (hipStream_t)stream;
+    if (d->dtype == FEN_F16) dispatch128<f16>(a, mode, comb, grid, s);
+    else dispatch128<bf16>(a, mode, comb, grid, s);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}

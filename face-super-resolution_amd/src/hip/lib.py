@@ -98,6 +98,15 @@ class GroupStripBwdDesc(Structure):
     ]
 
 
+class RcabC128Desc(Structure):
+    _fields_ = [
+        ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("Cr", c_int), ("mode", c_int),
+        ("res_scale", c_float), ("x", c_void_p), ("tp", c_void_p), ("pp", c_void_p), ("pfc1", c_void_p),
+        ("pfc2", c_void_p), ("ps", c_void_p), ("xo", c_void_p), ("w", c_void_p), ("bias", c_void_p),
+        ("alpha", c_void_p), ("res", c_void_p), ("y", c_void_p), ("z1", c_void_p), ("part", c_void_p),
+    ]
+
+
 class WgradDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
@@ -123,6 +132,9 @@ _SIGS = {
     "fen_group_strip_bwd_supported": (c_int, [c_int] * 7),
     "fen_group_strip_bwd_work_bytes": (c_size_t, [c_int, c_int]),
     "fen_group_strip_bwd": (c_int, [POINTER(GroupStripBwdDesc), c_void_p]),
+    "fen_rcab_c128_supported": (c_int, [c_int] * 6),
+    "fen_rcab_c128_tiles": (c_int, [c_int] * 2),
+    "fen_rcab_c128": (c_int, [POINTER(RcabC128Desc), c_void_p]),
     "fen_conv_first_fwd": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_void_p]),
     "fen_conv_first_fwd_ex": (c_int, [c_int] * 6 + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),

@@ -65,6 +65,11 @@ GROUP_STRIP = os.environ.get("FEN_GROUP_STRIP", "1") != "0"
 # ... and the training forward too (the kernel then writes the backward's saved tensors);
 # FEN_GROUP_STRIP_TRAIN=0 keeps training on the per-RCAB launches
 GROUP_STRIP_TRAIN = os.environ.get("FEN_GROUP_STRIP_TRAIN", "1") != "0"
+# inference at 128 channels (BASELINE configs[4]): a ResidualGroup as 2 * nb + 1 fen_rcab_c128
+# launches (rcab128.hip: each RCAB's gate deferred into the next conv's input, its pool sums in
+# conv2's epilogue) where the envelope holds (16-bit, H % 4 == 0, W % 64 == 0, Cr <= 32);
+# FEN_RCAB_C128=0 selects the per-op launches
+RCAB_C128 = os.environ.get("FEN_RCAB_C128", "1") != "0"
 # RCAB backward: the SE backward and its apply as one fen_se_bwd_fused launch (default) or
 # the fen_se_bwd + fen_se_bwd_apply pair (FEN_SE_BWD=pair; shapes outside the fused
 # kernel's envelope always take the pair)
@@ -452,11 +457,78 @@ class Forward:
         ctx.keep(d)
         return dict(blocks=blocks, x=x, x_last=x_last)
 
+    def _c128_ok(self, x) -> bool:
+        B, H, W, C = x.shape
+        return (RCAB_C128 and not self.save and self.s.NB > 0 and
+                bool(self.ctx.lib.fen_rcab_c128_supported(self.ctx.code, B, H, W, C, self.s.Cr)))
+
+    def _group_c128(self, x: torch.Tensor, pre: str, names: Sequence[str], y: torch.Tensor) -> dict:
+        """The group on fen_rcab_c128 (inference): per RCAB j a conv1 launch that builds x_j from
+        x_{j-1} + rs * s_{j-1} * t_{j-1} while staging its input (writing x_j for the next
+        combine) and a conv2 launch (t_j + its tile sums); the group conv applies the last
+        gate the same way and adds the group's input."""
+        s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
+        B, H, W, C = x.shape
+        T = int(ctx.lib.fen_rcab_c128_tiles(H, W))
+        blocks = []
+        prev = None
+
+        def desc(mode, xin, w, bias, yout):
+            d = L.RcabC128Desc()
+            d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.mode = ctx.code, B, H, W, C, s.Cr, mode
+            d.res_scale = float(s.res_scale)
+            d.x, d.w, d.bias, d.y = ptr(xin), ptr(w), ptr(bias), ptr(yout)
+            return d
+
+        def gate_from(d, pv):
+            ca = pv["pre"] + "channel_attention.fc."
+            d.tp, d.pp = ptr(pv["t"]), ptr(pv["part"])
+            d.pfc1, d.pfc2 = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
+            if self.attn is not None:
+                sg = ctx.alloc((B, C), torch.float32)
+                self.attn[pv["name"]] = sg
+                d.ps = ptr(sg)
+                pv["blk"]["s"] = sg
+
+        for j in range(s.NB):
+            q = f"{pre}blocks.{j}."
+            a1 = ctx.scratch("c128_a1", x.shape)
+            if prev is None:
+                d = desc(1, x, Wt.packed(q + "conv1", 0), p[q + "conv1.bias"], a1)
+                xj = x
+            else:
+                xj = ctx.scratch(f"c128_x{j & 1}", x.shape)
+                d = desc(1, prev["x"], Wt.packed(q + "conv1", 0), p[q + "conv1.bias"], a1)
+                gate_from(d, prev)
+                d.xo = ptr(xj)
+            d.alpha = ptr(p[q + "prelu.weight"])
+            ctx.emit("rcab_c128_conv1", ctx.lib.fen_rcab_c128, byref(d))
+            ctx.keep(d)
+            t = ctx.scratch(f"c128_t{j & 1}", x.shape)
+            part = ctx.scratch(f"c128_p{j & 1}", (B * T, C), torch.float32)
+            d = desc(2, a1, Wt.packed(q + "conv2", 0), p[q + "conv2.bias"], t)
+            d.part = ptr(part)
+            ctx.emit("rcab_c128_conv2", ctx.lib.fen_rcab_c128, byref(d))
+            ctx.keep(d)
+            blk = dict(s=None)
+            blocks.append(blk)
+            prev = dict(pre=q, x=xj, t=t, part=part, name=names[j], blk=blk)
+        d = desc(3, prev["x"], Wt.packed(pre + "conv", 0), p[pre + "conv.bias"], y)
+        gate_from(d, prev)
+        d.res = ptr(x)
+        ctx.emit("rcab_c128_group_conv", ctx.lib.fen_rcab_c128, byref(d))
+        ctx.keep(d)
+        return dict(blocks=blocks, x=x, x_last=None)
+
     def group(self, x: torch.Tensor, g: int, out: Optional[torch.Tensor] = None, pre: Optional[str] = None):
         """ResidualGroup (blocks.py:185-189) -> (y, saved)."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
         pre = f"residual_groups.{g}." if pre is None else pre
+        if self._c128_ok(x):
+            y = out if out is not None and out.data_ptr() != x.data_ptr() else ctx.alloc(x.shape)
+            names = [f"group{g}_rcab{b}" for b in range(s.NB)]
+            return y, self._group_c128(x, pre, names, y)
         if self._strip_ok(x):
             y = out if out is not None and out.data_ptr() != x.data_ptr() else ctx.alloc(x.shape)
             names = [f"group{g}_rcab{b}" for b in range(s.NB)]

@@ -268,6 +268,43 @@ int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int
 size_t fen_group_strip_work_bytes(int B, int H);
 int fen_group_strip(const fen_group_strip_desc* d, void* stream);
 
+/* 128-channel RCAB convs (BASELINE configs[4]: num_channels = 128, Cr = 32; RCAB blocks.py:
+ * 135-153, ChannelAttention blocks.py:83-92, ResidualGroup blocks.py:185-189), one launch per
+ * conv with the RCAB's elementwise work folded in; replaces the per-op conv + fen_se_fused
+ * launches at C = 128.  With tp != NULL the input is built with the previous RCAB's gate
+ * (deferred as in fen_rcab_deferred): in = x + res_scale * s * tp, s from pp / pfc1 / pfc2
+ * (its per-image copy to ps when ps != NULL), in's own tiles to xo when xo != NULL.
+ *   mode 1 (conv1):      y = PReLU(conv(in) + bias; alpha)   (z1 = conv(in) + bias if z1 != NULL)
+ *   mode 2 (conv2):      y = conv(x) + bias; part = per-tile channel sums of y (fp32, before the
+ *                        16-bit rounding) [B][fen_rcab_c128_tiles(H, W)][128]  (tp must be NULL)
+ *   mode 3 (group conv): y = conv(in) + bias + res
+ * 16-bit NHWC [B,H,W,128]; H % 4 == 0, W % 64 == 0, Cr <= 32; w packed mode 0 [9][128][128].
+ * Every block is independent (any grid, graph-replayable, no workspace).  y may not alias x,
+ * tp; xo may not alias x, tp.                                                                   */
+typedef struct {
+    int dtype;                 /* FEN_BF16 or FEN_F16                                          */
+    int B, H, W, C, Cr;
+    int mode;                  /* 1, 2, 3 as above                                             */
+    float res_scale;           /* 0.2                                                          */
+    const void* x;             /* the conv input, or x_{j-1} with tp                           */
+    const void* tp;            /* t_{j-1} (deferred gate) or NULL                              */
+    const float* pp;           /* part of t_{j-1} (a mode-2 launch's)                          */
+    const float* pfc1;         /* RCAB j-1 channel_attention.fc.0.weight [Cr][128]             */
+    const float* pfc2;         /* RCAB j-1 channel_attention.fc.2.weight [128][Cr]             */
+    float* ps;                 /* s_{j-1} [B][128] copy or NULL                                */
+    void* xo;                  /* x_j = x + res_scale * s * tp out, or NULL                    */
+    const void* w;             /* packed mode 0                                                */
+    const float* bias;
+    const float* alpha;        /* mode 1: PReLU [128]                                          */
+    const void* res;           /* mode 3: the residual (the group's input)                     */
+    void* y;
+    void* z1;                  /* mode 1: optional pre-activation copy                         */
+    float* part;               /* mode 2                                                       */
+} fen_rcab_c128_desc;
+int fen_rcab_c128_supported(int dtype, int B, int H, int W, int C, int Cr);
+int fen_rcab_c128_tiles(int H, int W);
+int fen_rcab_c128(const fen_rcab_c128_desc* d, void* stream);
+
 /* The backward of a whole ResidualGroup in ONE persistent launch (autograd of
  * ResidualGroup.forward blocks.py:185-189 and of each RCAB blocks.py:135-153 /
  * ChannelAttention blocks.py:83-92), on the saved tensors of a training fen_group_strip:
