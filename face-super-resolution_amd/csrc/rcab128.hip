@@ -6,6 +6,9 @@
 //                        out = a1 = PReLU(conv1(x_j) + b1)   (+ x_j's own tile, for the next RCAB)
 //   mode 2 (conv2):      in  = a1;  out = t_j = conv2(a1) + b2  + per-tile channel sums of t_j
 //   mode 3 (group conv): in  = the chain's output (deferred gate as mode 1); out = conv + b + res
+//   mode 4 (upsampler stage, custom.py's conv(C -> 4C) + PixelShuffle(2) + PReLU): the 4C
+//                        outputs as 4 blocks of 128 (the shuffle-permuted mode-1 pack: block k =
+//                        sub-pixel (k >> 1, k & 1)), run one after another on the tile's image
 // The gate s_{j-1} of an image (mean over its tiles' sums -> FC1 -> ReLU -> FC2 -> sigmoid) is
 // recomputed by every block in its prologue from the producer's tile sums: the kernel boundary is
 // the per-image hand-off, no block ever waits on another (any grid, graph-replayable).
@@ -37,8 +40,8 @@ constexpr int SLOT = CC * 128;               // [128 co][64 ci] 16-bit
 constexpr int NSLOT = 3;
 constexpr int NSTEP = 18;                    // 9 taps x 2 input-channel halves
 constexpr int O_RING = IMG;
-constexpr int O_CST = O_RING + NSLOT * SLOT; // bias [128], alpha [128]
-constexpr int O_GATE = O_CST + 2 * CC * 4;   // rs * s [128]
+constexpr int O_CST = O_RING + NSLOT * SLOT; // bias [4][128] (mode 4: per output block), alpha [128]
+constexpr int O_GATE = O_CST + 5 * CC * 4;   // rs * s [128]
 constexpr int O_RED = O_GATE + CC * 4;       // [4][128] f32
 constexpr int O_SCR = O_RED + 4 * CC * 4;    // mean [128], hid [32]
 constexpr int LDS128 = O_SCR + (CC + 32) * 4;
@@ -64,6 +67,16 @@ struct K128 {
     void* z1;             // mode 1, optional
     float* part;          // mode 2
 };
+
+// s_waitcnt vmcnt(n) for the few counts the step loop needs
+__device__ __forceinline__ void vm_wait(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
 
 template <typename T>
 __device__ __forceinline__ uint2 pk4(float a, float b, float c, float d) {
@@ -93,12 +106,16 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
     const int B = A.B, H = A.H, W = A.W;
     const int tpr = W / TW, tpi = (H / TR) * tpr, ntiles = B * tpi;
     const unsigned act_bytes = (unsigned)((size_t)B * H * W * PXB);
-    const i32x4 wrs = make_rsrc(A.w, 9u * CC * CC * 2u);
+    constexpr int NCO = MODE == 4 ? 4 : 1;           // 128-channel output blocks per tile
+    constexpr int NG = NCO * NSTEP;                   // filter steps per tile
+    const i32x4 wrs = make_rsrc(A.w, 9u * NCO * CC * CC * 2u);
 
-    // filter step s = (tap s >> 1, input half s & 1) into ring slot s % 3: this wave's 2 pieces
-    auto issue_step = [&](int s) {
+    // filter step g = (output block g / 18; tap (g % 18) >> 1, input half g & 1) into ring slot
+    // g % 3: this wave's 2 pieces (packed [9][NCO * 128][128])
+    auto issue_step = [&](int g) {
+        const int cb = g / NSTEP, s = g - cb * NSTEP;
         const int tap = s >> 1, ch = s & 1;
-        char* slot = ring + (s % NSLOT) * SLOT;
+        char* slot = ring + (g % NSLOT) * SLOT;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int piece = 2 * wave + k;
@@ -107,7 +124,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
             const int u = piece * 64 + ll, r = u >> 3, pc = u & 7;
             const int lc = pc ^ ((r >> 1) & 7);
             dma16(wrs, __builtin_amdgcn_readfirstlane(lds_addr(slot + piece * 1024)),
-                  ((tap * CC + r) * CC + ch * 64 + lc * 8) * 2);
+                  (((tap * NCO + cb) * CC + r) * CC + ch * 64 + lc * 8) * 2);
         }
     };
 
@@ -118,8 +135,13 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
         issue_step(0);
         issue_step(1);
         if (tid < CC) {
-            cst[tid] = A.bias[tid];
-            if (MODE == 1) cst[CC + tid] = A.alpha[tid];
+            if constexpr (MODE == 4) {
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) cst[cb * CC + tid] = A.bias[4 * tid + cb];   // packed row -> co = 4c + cb
+            } else {
+                cst[tid] = A.bias[tid];
+            }
+            if (MODE == 1 || MODE == 4) cst[4 * CC + tid] = A.alpha[tid];
         }
         // ---------------- the input image ----------------
         if constexpr (COMB) {
@@ -219,23 +241,28 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-        // ---------------- the conv: 18 (tap, input-half) steps ----------------
+        // ---------------- per 128-channel output block: the conv's 18 (tap, input-half) steps
+        for (int cb = 0; cb < NCO; ++cb) {
         f32x4 acc[4][4];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int p = 0; p < 4; ++p) acc[m][p] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int s = 0; s < NSTEP; ++s) {
-            if (s > 0) {
-                if (s + 1 < NSTEP) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int g = cb * NSTEP + s;
+            if (g > 0) {
+                // step g's pieces: later issues in flight are step g + 1's (2) and, on a block's
+                // first two steps, the previous block's epilogue stores (8, mode 4)
+                int n = g + 1 < NG ? 2 : 0;
+                if (MODE == 4 && cb > 0 && s < 2) n += 8;
+                vm_wait(n);
             }
-            __syncthreads();   // step s's pieces landed (every wave's); step s - 1's slot free
-            if (s + 2 < NSTEP) issue_step(s + 2);
+            __syncthreads();   // step g's pieces landed (every wave's); step g - 1's slot free
+            if (g + 2 < NG) issue_step(g + 2);
             const int tap = s >> 1, ch = s & 1, kh = tap / 3, kw = tap - 3 * kh;
             int q = lane >> 4, c16 = lane & 15;
             asm volatile("" : "+v"(q), "+v"(c16));
-            const char* ab = ring + (s % NSLOT) * SLOT + (64 * wh + c16) * 128;
+            const char* ab = ring + (g % NSLOT) * SLOT + (64 * wh + c16) * 128;
             const int ka = (c16 >> 1) & 7;
             const int colb = c16 + kw, kb = colb & 15;
             const char* bb = img + (wr + kh) * IROW + colb * PXB;
@@ -274,7 +301,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
                 for (int m = 0; m < 4; ++m) {
                     const int c0 = 64 * wh + 16 * m + 4 * q;
                     const float4 bb4 = *(const float4*)(cst + c0);
-                    const float4 aa4 = *(const float4*)(cst + CC + c0);
+                    const float4 aa4 = *(const float4*)(cst + 4 * CC + c0);
                     const float bia[4] = {bb4.x, bb4.y, bb4.z, bb4.w}, alp[4] = {aa4.x, aa4.y, aa4.z, aa4.w};
 #pragma unroll
                     for (int p = 0; p < 4; ++p) {
@@ -319,6 +346,30 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
                         if (c16 == 0) red[wr * CC + c0 + i] = sm;
                     }
                 }
+            } else if constexpr (MODE == 4) {
+                // conv block cb = sub-pixel (cb >> 1, cb & 1) of PixelShuffle(2), then PReLU on the
+                // shuffled channel c (custom.py's upsampler stage): output [B][2H][2W][128]
+                const size_t opx = ((size_t)b * 2 * H + 2 * (r0 + wr) + (cb >> 1)) * (2 * W) + 2 * (w0 + c16) + (cb & 1);
+                char* ob = (char*)A.y + opx * PXB + 128 * wh + chunk_of(0, q) * 16;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int c0 = 64 * wh + 16 * m + 4 * q;
+                    const float4 bb4 = *(const float4*)(cst + cb * CC + c0);
+                    const float4 aa4 = *(const float4*)(cst + 4 * CC + c0);
+                    const float bia[4] = {bb4.x, bb4.y, bb4.z, bb4.w}, alp[4] = {aa4.x, aa4.y, aa4.z, aa4.w};
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        float v[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] = prelu_f(acc[m][p][i] + bia[i], alp[i]);
+                        ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+#pragma unroll
+                    for (int mp = 0; mp < 2; ++mp)
+                        *(uint4*)(ob + p * 32 * PXB + mp * 64) = pair16(ov[2 * mp][p], ov[2 * mp + 1][p]);
             } else {
                 const char* rb = (const char*)A.res + rowpx * PXB;
 #pragma unroll
@@ -334,12 +385,15 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
                     }
                 }
             }
+            if constexpr (MODE != 4) {
 #pragma unroll
-            for (int p = 0; p < 4; ++p)
+                for (int p = 0; p < 4; ++p)
 #pragma unroll
-                for (int mp = 0; mp < 2; ++mp)
-                    *(uint4*)(yb + p * 16 * PXB + mp * 64) = pair16(ov[2 * mp][p], ov[2 * mp + 1][p]);
+                    for (int mp = 0; mp < 2; ++mp)
+                        *(uint4*)(yb + p * 16 * PXB + mp * 64) = pair16(ov[2 * mp][p], ov[2 * mp + 1][p]);
+            }
         }
+        }   // output blocks
         __syncthreads();   // the image and the ring are free for the next tile; red complete
         if constexpr (MODE == 2) {
             if (tid < CC)
@@ -366,6 +420,7 @@ template <typename T>
 void dispatch128(const K128& a, int mode, bool comb, int grid, hipStream_t s) {
     if (mode == 1) comb ? launch128<T, 1, true>(a, grid, s) : launch128<T, 1, false>(a, grid, s);
     else if (mode == 2) launch128<T, 2, false>(a, grid, s);
+    else if (mode == 4) launch128<T, 4, false>(a, grid, s);
     else comb ? launch128<T, 3, true>(a, grid, s) : launch128<T, 3, false>(a, grid, s);
 }
 
@@ -385,10 +440,11 @@ extern "C" int fen_rcab_c128(const fen_rcab_c128_desc* d, void* stream) {
     if (!d || !d->x || !d->w || !d->bias || !d->y) return FEN_EINVAL;
     if (!fen_rcab_c128_supported(d->dtype, d->B, d->H, d->W, d->C, d->Cr > 0 ? d->Cr : 1)) return FEN_EUNSUPPORTED;
     const int mode = d->mode;
-    if (mode < 1 || mode > 3) return FEN_EINVAL;
+    if (mode < 1 || mode > 4) return FEN_EINVAL;
     const bool comb = d->tp != nullptr;
-    if (comb && (mode == 2 || !d->pp || !d->pfc1 || !d->pfc2 || d->Cr <= 0 || d->Cr > 32)) return FEN_EINVAL;
-    if (mode == 1 && !d->alpha) return FEN_EINVAL;
+    if (comb && (mode == 2 || mode == 4 || !d->pp || !d->pfc1 || !d->pfc2 || d->Cr <= 0 || d->Cr > 32)) return FEN_EINVAL;
+    if ((mode == 1 || mode == 4) && !d->alpha) return FEN_EINVAL;
+    if (mode == 4 && comb) return FEN_EINVAL;
     if (mode == 2 && !d->part) return FEN_EINVAL;
     if (mode == 3 && !d->res) return FEN_EINVAL;
     if (d->y == d->x || (comb && d->y == d->tp) || (d->xo && (d->xo == d->x || d->xo == d->tp))) return FEN_EINVAL;

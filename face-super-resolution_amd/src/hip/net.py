@@ -566,16 +566,38 @@ class Forward:
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = feat.shape
         fb = ctx.alloc(feat.shape) if self.save else ctx.scratch("tail_fb", feat.shape)
-        conv(ctx, feat, Wt.packed("conv_after_body", 0), B, H, W, C, C, bias=p["conv_after_body.bias"], y=fb,
-             res=(feat0,))
+
+        def c128(hh_, ww_) -> bool:   # the 128-channel kernels (inference)
+            return (RCAB_C128 and not self.save and
+                    bool(ctx.lib.fen_rcab_c128_supported(ctx.code, B, hh_, ww_, C, max(s.Cr, 1))))
+
+        def c128_launch(name, mode, x_, w_, bias_, y_, alpha_=None, res_=None):
+            d = L.RcabC128Desc()
+            d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.mode = ctx.code, B, x_.shape[1], x_.shape[2], C, max(s.Cr, 1), mode
+            d.res_scale = float(s.res_scale)
+            d.x, d.w, d.bias, d.y = ptr(x_), ptr(w_), ptr(bias_), ptr(y_)
+            d.alpha, d.res = ptr(alpha_), ptr(res_)
+            ctx.emit(name, ctx.lib.fen_rcab_c128, byref(d))
+            ctx.keep(d)
+
+        if c128(H, W):
+            c128_launch("c128_after_body", 3, feat, Wt.packed("conv_after_body", 0), p["conv_after_body.bias"], fb,
+                        res_=feat0)
+        else:
+            conv(ctx, feat, Wt.packed("conv_after_body", 0), B, H, W, C, C, bias=p["conv_after_body.bias"], y=fb,
+                 res=(feat0,))
         h, hh, ww = fb, H, W
         stages = []
         for st in range(s.n_stages):
             key = f"upsample.stages.{st}."
             a = ctx.alloc((B, 2 * hh, 2 * ww, C)) if self.save else ctx.scratch(f"up_a{st & 1}", (B, 2 * hh, 2 * ww, C))
             v = ctx.alloc((B, 2 * hh, 2 * ww, C)) if self.save else None
-            conv(ctx, h, Wt.packed(key + "conv", 1), B, hh, ww, C, 4 * C, bias=p[key + "conv.bias"],
-                 epi=L.EPI_PRELU | L.EPI_SHUFFLE, alpha=p[key + "prelu.weight"], y=a, y_pre=v)
+            if c128(hh, ww):
+                c128_launch("c128_upsample", 4, h, Wt.packed(key + "conv", 1), p[key + "conv.bias"], a,
+                            alpha_=p[key + "prelu.weight"])
+            else:
+                conv(ctx, h, Wt.packed(key + "conv", 1), B, hh, ww, C, 4 * C, bias=p[key + "conv.bias"],
+                     epi=L.EPI_PRELU | L.EPI_SHUFFLE, alpha=p[key + "prelu.weight"], y=a, y_pre=v)
             stages.append(dict(x=h, v=v, a=a, H=hh, W=ww))
             h, hh, ww = a, 2 * hh, 2 * ww
         if out is None:

@@ -278,13 +278,17 @@ int fen_group_strip(const fen_group_strip_desc* d, void* stream);
  *   mode 2 (conv2):      y = conv(x) + bias; part = per-tile channel sums of y (fp32, before the
  *                        16-bit rounding) [B][fen_rcab_c128_tiles(H, W)][128]  (tp must be NULL)
  *   mode 3 (group conv): y = conv(in) + bias + res
- * 16-bit NHWC [B,H,W,128]; H % 4 == 0, W % 64 == 0, Cr <= 32; w packed mode 0 [9][128][128].
+ *   mode 4 (upsampler stage): y = PReLU(PixelShuffle(2)(conv(x) + bias); alpha), y [B,2H,2W,128];
+ *                        w = the conv(128 -> 512) packed mode 1 [9][512][128] (shuffle-permuted
+ *                        rows), bias [512], alpha [128]  (tp must be NULL)
+ * 16-bit NHWC [B,H,W,128]; H % 4 == 0, W % 64 == 0, Cr <= 32; w packed mode 0 [9][128][128]
+ * (mode 4: as stated there).
  * Every block is independent (any grid, graph-replayable, no workspace).  y may not alias x,
  * tp; xo may not alias x, tp.                                                                   */
 typedef struct {
     int dtype;                 /* FEN_BF16 or FEN_F16                                          */
     int B, H, W, C, Cr;
-    int mode;                  /* 1, 2, 3 as above                                             */
+    int mode;                  /* 1 .. 4 as above                                              */
     float res_scale;           /* 0.2                                                          */
     const void* x;             /* the conv input, or x_{j-1} with tp                           */
     const void* tp;            /* t_{j-1} (deferred gate) or NULL                              */
