@@ -134,6 +134,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
         const int r0 = (rem / tpr) * TR, w0 = (rem % tpr) * TW;
         issue_step(0);
         issue_step(1);
+        issue_step(2);
         if (tid < CC) {
             if constexpr (MODE == 4) {
 #pragma unroll
@@ -164,38 +165,58 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
                 tv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trs, (int)offs[k], 0, 0));
             }
             if (b != prev_b) {
-                // the gate of image b (blocks.py:83-92): mean of t_{j-1} from its tile sums
-                // (fixed order: tiles g, g + 4, ... per quarter, quarters in order)
+                // the gate of image b (blocks.py:83-92): mean of t_{j-1} from its tile sums (fixed
+                // order: tiles g, g + 4, ... per quarter, quarters in order), FC1 -> ReLU -> FC2 ->
+                // sigmoid.  Every operand load is issued before the first reduction.
+                const int c = tid & (CC - 1), g = tid >> 7;
+                const int k1 = tid >> 4, j8 = (tid & 15) * 8;
+                // FC2 lane layout: channel c2 = tid >> 2, hidden units k8 .. k8 + 7 (a quad per channel)
+                const int c2 = tid >> 2, k8 = (tid & 3) * 8;
+                float w1[8], w2[8];
                 {
-                    const int c = tid & (CC - 1), g = tid >> 7;
+                    const float* w1p = A.pfc1 + (size_t)(k1 < A.Cr ? k1 : 0) * CC + j8;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) w1[e] = k1 < A.Cr ? w1p[e] : 0.f;
+                    const float* w2p = A.pfc2 + (size_t)c2 * A.Cr;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) w2[e] = k8 + e < A.Cr ? w2p[k8 + e] : 0.f;
+                }
+                {
                     const float* pb = A.pp + (size_t)b * tpi * CC + c;
-                    float sacc = 0.f;
-                    for (int k = g; k < tpi; k += 4) sacc += pb[(size_t)k * CC];
-                    red[g * CC + c] = sacc;
+                    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+                    int k = g;
+                    for (; k + 12 < tpi; k += 16) {
+                        s0 += pb[(size_t)k * CC];
+                        s1 += pb[(size_t)(k + 4) * CC];
+                        s2 += pb[(size_t)(k + 8) * CC];
+                        s3 += pb[(size_t)(k + 12) * CC];
+                    }
+                    for (; k < tpi; k += 4) s0 += pb[(size_t)k * CC];
+                    red[g * CC + c] = (s0 + s1) + (s2 + s3);
                 }
                 __syncthreads();
                 if (tid < CC) scr[tid] = ((red[tid] + red[CC + tid]) + (red[2 * CC + tid] + red[3 * CC + tid])) * A.inv_hw;
                 __syncthreads();
                 {
-                    // FC1 + ReLU: row k = tid >> 4 (k < Cr), 8 channels per lane, summed over the row of 16 lanes
-                    const int k = tid >> 4, j8 = (tid & 15) * 8;
+                    // FC1 + ReLU: row k1 = tid >> 4 (k1 < Cr), 8 channels per lane, summed over the row of 16 lanes
                     float h = 0.f;
-                    if (k < A.Cr) {
-                        const float* w1 = A.pfc1 + (size_t)k * CC + j8;
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) h += w1[e] * scr[j8 + e];
-                    }
+                    for (int e = 0; e < 8; ++e) h += w1[e] * scr[j8 + e];
                     h = group16_sum(h);
-                    if ((tid & 15) == 0 && k < 32) scr[CC + k] = fmaxf(h, 0.f);
+                    if ((tid & 15) == 0) scr[CC + k1] = fmaxf(h, 0.f);
                 }
                 __syncthreads();
-                if (tid < CC) {
-                    const float* w2 = A.pfc2 + (size_t)tid * A.Cr;
+                {
                     float z = 0.f;
-                    for (int k = 0; k < A.Cr; ++k) z += w2[k] * scr[CC + k];
-                    const float sg = 1.f / (1.f + expf(-z));
-                    gate[tid] = sg * A.res_scale;
-                    if (A.ps && rem == 0) A.ps[(size_t)b * CC + tid] = sg;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) z += w2[e] * scr[CC + k8 + e];
+                    z += dpp_f<0xB1>(z);                     // the quad's four partial sums
+                    z += dpp_f<0x4E>(z);
+                    if ((tid & 3) == 0) {
+                        const float sg = 1.f / (1.f + expf(-z));
+                        gate[c2] = sg * A.res_scale;
+                        if (A.ps && rem == 0) A.ps[(size_t)b * CC + c2] = sg;
+                    }
                 }
                 prev_b = b;
                 __syncthreads();
@@ -240,159 +261,165 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();   // the image, steps 0..2's filter slots and the constants visible
 
-        // ---------------- per 128-channel output block: the conv's 18 (tap, input-half) steps
-        for (int cb = 0; cb < NCO; ++cb) {
+        // ---------------- the conv: NG filter steps (per 128-channel output block 9 taps x 2
+        // input halves), each 2 k-halves of 16 MFMAs.  The barrier that publishes step g + 1's
+        // slot sits between step g's two k-halves (their fragments already in registers), and the
+        // same barrier frees step g's slot for the DMA of step g + 3: one barrier per step, its
+        // wait hidden behind MFMAs.  Each k-half's fragments are re-read (for the next step) as
+        // soon as its MFMAs are issued: 2 x 8 fragments live, no double buffer.
+        uint4 A0[4], B0[4], A1[4], B1[4];
+        auto load_half = [&](int g, int ks, uint4 (&a)[4], uint4 (&bv)[4]) {
+            const int s = g % NSTEP;
+            const int tap = s >> 1, ch = s & 1, kh = tap / 3, kw = tap - 3 * kh;
+            int q = lane >> 4, c16 = lane & 15;
+            asm volatile("" : "+v"(q), "+v"(c16));
+            const int colb = c16 + kw;
+            const char* ap = ring + (g % NSLOT) * SLOT + (64 * wh + c16) * 128 + (((4 * ks + q) ^ ((c16 >> 1) & 7)) << 4);
+            const char* bp = img + (wr + kh) * IROW + colb * PXB + (((8 * ch + 4 * ks + q) ^ (colb & 15)) << 4);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) a[m] = *(const uint4*)(ap + m * 2048);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) bv[p] = *(const uint4*)(bp + p * 16 * PXB);
+        };
+        // publish step g + 1 (this wave's pieces landed; every wave's after the barrier) and
+        // recycle step g's slot for step g + 3.  `extra`: epilogue stores issued after step
+        // g + 1's DMA (mode 4's output block boundary)
+        auto advance = [&](int g, int extra) {
+            vm_wait((g + 2 < NG ? 2 : 0) + extra);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step g done
+            __syncthreads();
+            if (g + 3 < NG) issue_step(g + 3);
+        };
+        load_half(0, 0, A0, B0);
+        load_half(0, 1, A1, B1);
         f32x4 acc[4][4];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int p = 0; p < 4; ++p) acc[m][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < NSTEP; ++s) {
-            const int g = cb * NSTEP + s;
-            if (g > 0) {
-                // step g's pieces: later issues in flight are step g + 1's (2) and, on a block's
-                // first two steps, the previous block's epilogue stores (8, mode 4)
-                int n = g + 1 < NG ? 2 : 0;
-                if (MODE == 4 && cb > 0 && s < 2) n += 8;
-                vm_wait(n);
-            }
-            __syncthreads();   // step g's pieces landed (every wave's); step g - 1's slot free
-            if (g + 2 < NG) issue_step(g + 2);
-            const int tap = s >> 1, ch = s & 1, kh = tap / 3, kw = tap - 3 * kh;
-            int q = lane >> 4, c16 = lane & 15;
-            asm volatile("" : "+v"(q), "+v"(c16));
-            const char* ab = ring + (g % NSLOT) * SLOT + (64 * wh + c16) * 128;
-            const int ka = (c16 >> 1) & 7;
-            const int colb = c16 + kw, kb = colb & 15;
-            const char* bb = img + (wr + kh) * IROW + colb * PXB;
-            uint4 Af[2][4], Bf[2][4];
-            auto load = [&](int ks, uint4 (&a)[4], uint4 (&bv)[4]) {
-                const char* ap = ab + (((4 * ks + q) ^ ka) << 4);
-                const char* bp = bb + (((8 * ch + 4 * ks + q) ^ kb) << 4);
-#pragma unroll
-                for (int m = 0; m < 4; ++m) a[m] = *(const uint4*)(ap + m * 2048);
-#pragma unroll
-                for (int p = 0; p < 4; ++p) bv[p] = *(const uint4*)(bp + p * 16 * PXB);
-            };
-            load(0, Af[0], Bf[0]);
-            load(1, Af[1], Bf[1]);
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
+        for (int cb = 0; cb < NCO; ++cb) {
+            for (int s = 0; s < NSTEP; ++s) {
+                const int g = cb * NSTEP + s;
+                const bool more = s < NSTEP - 1;
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) mma16<T>(acc[m][p], Af[ks][m], Bf[ks][p]);
+                    for (int p = 0; p < 4; ++p) mma16<T>(acc[m][p], A0[m], B0[p]);
                 __builtin_amdgcn_sched_barrier(0);
+                // a block's first step: the previous block's epilogue stores (8) went out after step
+                // g + 1's DMA
+                if (more) {
+                    advance(g, (MODE == 4 && cb > 0 && s == 0) ? 8 : 0);
+                    load_half(g + 1, 0, A0, B0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) mma16<T>(acc[m][p], A1[m], B1[p]);
+                __builtin_amdgcn_sched_barrier(0);
+                if (more) load_half(g + 1, 1, A1, B1);
             }
-        }
+            const int g = cb * NSTEP + NSTEP - 1;
 
-        // ---------------- epilogue: lane (q, c16) holds channels 64 wh + 16 m + 4 q + i of pixel
-        // w0 + 16 p + c16 in row r0 + wr ----------------
-        {
+            // ---------------- epilogue of output block cb: lane (q, c16) holds channels
+            // 64 wh + 16 m + 4 q + i of pixel w0 + 16 p + c16 in row r0 + wr; pairs of m-blocks
+            // become 16-B stores (pair16)
             const int q = lane >> 4, c16 = lane & 15;
             const size_t rowpx = ((size_t)b * H + r0 + wr) * W + w0 + c16;
-            char* yb = (char*)A.y + rowpx * PXB + 128 * wh + chunk_of(0, q) * 16;
-            uint2 ov[4][4];
-            if constexpr (MODE == 1) {
-                uint2 zv[4][4];
+            const int cho = 128 * wh + chunk_of(0, q) * 16;
+            float tsum[4][4];                                   // mode 2: the row's channel sums
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int c0 = 64 * wh + 16 * m + 4 * q;
-                    const float4 bb4 = *(const float4*)(cst + c0);
-                    const float4 aa4 = *(const float4*)(cst + 4 * CC + c0);
-                    const float bia[4] = {bb4.x, bb4.y, bb4.z, bb4.w}, alp[4] = {aa4.x, aa4.y, aa4.z, aa4.w};
+            for (int m = 0; m < 4; ++m)
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        float z[4], v[4];
+                for (int i = 0; i < 4; ++i) tsum[m][i] = 0.f;
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            z[i] = acc[m][p][i] + bia[i];
-                            v[i] = prelu_f(z[i], alp[i]);
-                        }
-                        zv[m][p] = pk4<T>(z[0], z[1], z[2], z[3]);
-                        ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
+            for (int mp = 0; mp < 2; ++mp) {
+                float bia[2][4], alp[2][4];
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    const int c0 = 64 * wh + 16 * (2 * mp + h2) + 4 * q;
+                    const float4 bb4 = *(const float4*)(cst + (MODE == 4 ? cb * CC : 0) + c0);
+                    bia[h2][0] = bb4.x, bia[h2][1] = bb4.y, bia[h2][2] = bb4.z, bia[h2][3] = bb4.w;
+                    if constexpr (MODE == 1 || MODE == 4) {
+                        const float4 aa4 = *(const float4*)(cst + 4 * CC + c0);
+                        alp[h2][0] = aa4.x, alp[h2][1] = aa4.y, alp[h2][2] = aa4.z, alp[h2][3] = aa4.w;
                     }
                 }
-                if (A.z1) {
-                    char* zb = (char*)A.z1 + rowpx * PXB + 128 * wh + chunk_of(0, q) * 16;
 #pragma unroll
-                    for (int p = 0; p < 4; ++p)
+                for (int p = 0; p < 4; ++p) {
+                    float v[2][4];
 #pragma unroll
-                        for (int mp = 0; mp < 2; ++mp)
-                            *(uint4*)(zb + p * 16 * PXB + mp * 64) = pair16(zv[2 * mp][p], zv[2 * mp + 1][p]);
-                }
-            } else if constexpr (MODE == 2) {
+                    for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int c0 = 64 * wh + 16 * m + 4 * q;
-                    const float4 bb4 = *(const float4*)(cst + c0);
-                    const float bia[4] = {bb4.x, bb4.y, bb4.z, bb4.w};
-                    float rs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        float v[4];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            v[i] = acc[m][p][i] + bia[i];
-                            rs[i] += v[i];
+                        for (int i = 0; i < 4; ++i) v[h2][i] = acc[2 * mp + h2][p][i] + bia[h2][i];
+                    if constexpr (MODE == 1) {
+                        if (A.z1) {
+                            char* zb = (char*)A.z1 + (rowpx + 16 * p) * PXB + cho + mp * 64;
+                            *(uint4*)zb = pair16(pk4<T>(v[0][0], v[0][1], v[0][2], v[0][3]),
+                                                 pk4<T>(v[1][0], v[1][1], v[1][2], v[1][3]));
                         }
-                        ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
                     }
+                    if constexpr (MODE == 2) {
+#pragma unroll
+                        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) tsum[2 * mp + h2][i] += v[h2][i];
+                    }
+                    if constexpr (MODE == 3) {
+                        float rv[2][4];
+#pragma unroll
+                        for (int h2 = 0; h2 < 2; ++h2)
+                            ld4<T>((const char*)A.res + (rowpx + 16 * p) * PXB + (64 * wh + 16 * (2 * mp + h2) + 4 * q) * 2,
+                                   rv[h2]);
+#pragma unroll
+                        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) v[h2][i] += rv[h2][i];
+                    }
+                    if constexpr (MODE == 1 || MODE == 4) {
+#pragma unroll
+                        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) v[h2][i] = prelu_f(v[h2][i], alp[h2][i]);
+                    }
+                    const uint4 o = pair16(pk4<T>(v[0][0], v[0][1], v[0][2], v[0][3]),
+                                           pk4<T>(v[1][0], v[1][1], v[1][2], v[1][3]));
+                    if constexpr (MODE == 4) {
+                        // conv block cb = sub-pixel (cb >> 1, cb & 1) of PixelShuffle(2), PReLU on
+                        // the shuffled channel (custom.py's upsampler stage): out [B][2H][2W][128]
+                        const size_t opx = ((size_t)b * 2 * H + 2 * (r0 + wr) + (cb >> 1)) * (2 * W) +
+                                           2 * (w0 + 16 * p + c16) + (cb & 1);
+                        *(uint4*)((char*)A.y + opx * PXB + cho + mp * 64) = o;
+                    } else {
+                        *(uint4*)((char*)A.y + (rowpx + 16 * p) * PXB + cho + mp * 64) = o;
+                    }
+                }
+            }
+            if constexpr (MODE == 2) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const float sm = group16_sum(rs[i]);
-                        if (c16 == 0) red[wr * CC + c0 + i] = sm;
+                        const float sm = group16_sum(tsum[m][i]);
+                        if (c16 == 0) red[wr * CC + 64 * wh + 16 * m + 4 * q + i] = sm;
                     }
-                }
-            } else if constexpr (MODE == 4) {
-                // conv block cb = sub-pixel (cb >> 1, cb & 1) of PixelShuffle(2), then PReLU on the
-                // shuffled channel c (custom.py's upsampler stage): output [B][2H][2W][128]
-                const size_t opx = ((size_t)b * 2 * H + 2 * (r0 + wr) + (cb >> 1)) * (2 * W) + 2 * (w0 + c16) + (cb & 1);
-                char* ob = (char*)A.y + opx * PXB + 128 * wh + chunk_of(0, q) * 16;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int c0 = 64 * wh + 16 * m + 4 * q;
-                    const float4 bb4 = *(const float4*)(cst + cb * CC + c0);
-                    const float4 aa4 = *(const float4*)(cst + 4 * CC + c0);
-                    const float bia[4] = {bb4.x, bb4.y, bb4.z, bb4.w}, alp[4] = {aa4.x, aa4.y, aa4.z, aa4.w};
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        float v[4];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) v[i] = prelu_f(acc[m][p][i] + bia[i], alp[i]);
-                        ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
-                    }
-                }
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int mp = 0; mp < 2; ++mp)
-                        *(uint4*)(ob + p * 32 * PXB + mp * 64) = pair16(ov[2 * mp][p], ov[2 * mp + 1][p]);
-            } else {
-                const char* rb = (const char*)A.res + rowpx * PXB;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int c0 = 64 * wh + 16 * m + 4 * q;
-                    const float4 bb4 = *(const float4*)(cst + c0);
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        float rv[4];
-                        ld4<T>(rb + p * 16 * PXB + c0 * 2, rv);
-                        ov[m][p] = pk4<T>(acc[m][p][0] + bb4.x + rv[0], acc[m][p][1] + bb4.y + rv[1],
-                                          acc[m][p][2] + bb4.z + rv[2], acc[m][p][3] + bb4.w + rv[3]);
-                    }
-                }
             }
-            if constexpr (MODE != 4) {
+            if (g + 1 < NG) {
+                // the next output block (mode 4): its first step's fragments; step g + 1's DMA is
+                // older than this block's 8 stores
+                advance(g, 8);
+                load_half(g + 1, 0, A0, B0);
+                load_half(g + 1, 1, A1, B1);
 #pragma unroll
-                for (int p = 0; p < 4; ++p)
+                for (int m = 0; m < 4; ++m)
 #pragma unroll
-                    for (int mp = 0; mp < 2; ++mp)
-                        *(uint4*)(yb + p * 16 * PXB + mp * 64) = pair16(ov[2 * mp][p], ov[2 * mp + 1][p]);
+                    for (int p = 0; p < 4; ++p) acc[m][p] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-        }
         }   // output blocks
         __syncthreads();   // the image and the ring are free for the next tile; red complete
         if constexpr (MODE == 2) {
