@@ -189,8 +189,8 @@ def conv_flop(cin, cout, h, w, k=3):
 
 def time_stress(steps=3, warmup=1, B=4, hw=128, precision="fp16"):
     """BASELINE configs[4]: the 128-ch / 10x20 RCAB x8 stress variant, inference, 128x128 ->
-    1024x1024 (x8 from a 128 input), in its stated fp16, on the
-    per-op kernels (the fused RCAB covers 64 ch only).  Algorithmic FLOPs: every 3x3 conv
+    1024x1024 (x8 from a 128 input), in its stated fp16; the body,
+    conv_after_body and the upsampler on fen_rcab_c128 (rcab128.hip).  Algorithmic FLOPs: every 3x3 conv
     (head, 400 RCAB convs, 10 group convs, conv_after_body, 3 upsampler stages, conv_last)."""
     from src.models import FaceEnhanceNet
     from src.hip.engine import FENEngine
