@@ -14,7 +14,7 @@ FC=$(find $D/fetch -name '*counter_collection.csv' | head -1)
 WC=$(find $D/write -name '*counter_collection.csv' | head -1)
 AF=$(grep algorithmic_bytes_fwd_train $D/fetch.log | awk '{print $2}')
 AB=$(grep algorithmic_bytes_bwd $D/fetch.log | awk '{print $2}')
-python tools/prof_summary.py pmc "$FC" "$WC" $D/pmc_k_group_strip_train.json "k_group_strip<" "$AF" \
+python tools/prof_summary.py pmc "$FC" "$WC" $D/pmc_k_group_strip_train.json "k_group_strip!bwd" "$AF" \
     "k_group_strip, training form (a ResidualGroup's forward + the backward's operands), bf16, B=32, 64x64x64"
 python tools/prof_summary.py pmc "$FC" "$WC" $D/pmc_k_group_strip_bwd.json "k_group_strip_bwd" "$AB" \
     "k_group_strip_bwd (a ResidualGroup's backward data gradients + SE backward), bf16, B=32, 64x64x64"
@@ -25,10 +25,12 @@ while read -r set; do
   f=$(find $D/sq$i -name '*counter_collection.csv' | head -1)
   python - "$f" <<'PY'
 import csv, sys, collections
-for key in ("k_group_strip<", "k_group_strip_bwd"):
+for key in ("k_group_strip!bwd", "k_group_strip_bwd"):
+    sub, _, excl = key.partition("!")
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(sys.argv[1])):
-        if key in r.get('Kernel_Name', ''):
+        n = r.get('Kernel_Name', '')
+        if sub in n and not (excl and excl in n):
             agg[r['Counter_Name']].append(float(r['Counter_Value']))
     for k, v in sorted(agg.items()):
         v = v[12:] or v      # drop the first two steps' launches (6 groups per step)

@@ -25,10 +25,16 @@ def stats(src, dst):
               f'{r["Name"][:100]}')
 
 
+def _match(name, key):
+    """key: substring, or 'sub!excl' (contains sub, not excl)."""
+    sub, _, excl = key.partition("!")
+    return sub in name and not (excl and excl in name)
+
+
 def _per_dispatch(path, counter, key):
     vals = []
     for r in csv.DictReader(open(path)):
-        if key in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if _match(r["Kernel_Name"], key) and r["Counter_Name"] == counter:
             vals.append(float(r["Counter_Value"]))
     return vals
 
