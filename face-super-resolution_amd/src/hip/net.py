@@ -209,6 +209,11 @@ SE_IN_BWD = os.environ.get("FEN_SE_IN_BWD", "fold") != "launch"
 # 8.826 ms per training step against the two-launch pair (3 same-box reps): off by default
 BWD_RES_FUSED = os.environ.get("FEN_RCAB_BWD_RES", "0") == "1"
 WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
+# ... on the strip backward (dt / dz1 are per-RCAB buffers, nothing rotates): a group's 21 weight
+# gradients in one launch pair (FEN_WGRAD_MAXJOBS = 32): each block reduces ~2.7x more tiles into
+# its slab, so 2.7x fewer fp32 slabs are written and re-read by the finalize, and 3 launch
+# fills / drains become 1 (FEN_WGRAD_STRIP_BATCH=8 gives the per-8 batches)
+WGRAD_STRIP_BATCH = max(1, min(32, int(os.environ.get("FEN_WGRAD_STRIP_BATCH", "32"))))
 # a ResidualGroup's whole backward (group conv^T, every RCAB's SE backward, conv2^T, PReLU',
 # conv1^T) as ONE strip-resident fen_group_strip_bwd launch where its envelope holds (16-bit,
 # 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP_BWD=0 selects the per-RCAB launches
@@ -776,16 +781,24 @@ class Backward:
         d.work, d.work_bytes = ptr(work), nbytes
         ctx.emit("group_strip_bwd", ctx.lib.fen_group_strip_bwd, byref(d))
         ctx.keep(d)
-        self.wb.add(sv["x_last"], dy, B, H, W, C, C, G[pre + "conv.weight"], G[pre + "conv.bias"])
+        wb = self.wb
+        size = getattr(wb, "size", None)
+        if size is not None:   # this group's weight gradients in one batch
+            wb.flush()
+            wb.size = WGRAD_STRIP_BATCH
+        wb.add(sv["x_last"], dy, B, H, W, C, C, G[pre + "conv.weight"], G[pre + "conv.bias"])
         for b in reversed(range(s.NB)):
             q = f"{pre}blocks.{b}."
             ca = q + "channel_attention.fc."
             blk, o = sv["blocks"][b], outs[b]
-            self.wb.add(blk["a1"], o["dt"], B, H, W, C, C, G[q + "conv2.weight"], G[q + "conv2.bias"])
-            self.wb.add(blk["x"], o["dz1"], B, H, W, C, C, G[q + "conv1.weight"], G[q + "conv1.bias"])
+            wb.add(blk["a1"], o["dt"], B, H, W, C, C, G[q + "conv2.weight"], G[q + "conv2.bias"])
+            wb.add(blk["x"], o["dz1"], B, H, W, C, C, G[q + "conv1.weight"], G[q + "conv1.bias"])
             self.cs.add(o["dal"], B * H, C, G[q + "prelu.weight"])
             self.cs.add(o["dw1p"], B, s.Cr * C, G[ca + "0.weight"])
             self.cs.add(o["dw2p"], B, s.Cr * C, G[ca + "2.weight"])
+        wb.flush()
+        if size is not None:
+            wb.size = size
         self.flush()
         return dx
 

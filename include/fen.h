@@ -112,7 +112,7 @@ int fen_wgrad3x3(const fen_wgrad_desc* d, void* stream);
  * descs' work fields are ignored).  Results equal fen_wgrad3x3 per job up to fp32
  * summation order (deterministic run to run).  The backward's conv1/conv2 weight gradients
  * of consecutive RCABs (autograd of blocks.py:135-153's convs; trainer.py:482-485).       */
-#define FEN_WGRAD_MAXJOBS 8
+#define FEN_WGRAD_MAXJOBS 32
 size_t fen_wgrad_multi_work_floats(int n, const fen_wgrad_desc* descs);
 int fen_wgrad3x3_multi(int n, const fen_wgrad_desc* descs, void* stream);
 

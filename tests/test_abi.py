@@ -71,14 +71,14 @@ def test_wgrad_multi_validation_without_gpu():
     import ctypes
     from src.hip import lib as L
     lib = L.load()
-    arr = (L.WgradDesc * 9)()
+    arr = (L.WgradDesc * 33)()                                    # FEN_WGRAD_MAXJOBS + 1
     for d in arr:
         d.dtype, d.B, d.H, d.W, d.Cin, d.Cout, d.cout_valid = L.BF16, 32, 64, 64, 64, 64, 64
         d.x = d.dy = d.dw = d.work = 16
     p = ctypes.cast(arr, ctypes.c_void_p)
     assert lib.fen_wgrad3x3_multi(0, p, None) == -1
-    assert lib.fen_wgrad3x3_multi(9, p, None) == -1
-    assert lib.fen_wgrad_multi_work_floats(9, p) == 0
+    assert lib.fen_wgrad3x3_multi(33, p, None) == -1
+    assert lib.fen_wgrad_multi_work_floats(33, p) == 0
     one = lib.fen_wgrad_work_floats(ctypes.byref(arr[0]))
     assert one == 256 * (64 * 64 * 9 + 64)
     assert lib.fen_wgrad_multi_work_floats(4, p) == one          # 4 jobs x 64 chunks
