@@ -473,30 +473,30 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         // a1's boundary row is out: its storing wave signals for itself (one lane, after its drain)
         if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 0), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();                                    // B_Y: a1 image and row sums complete; conv2's taps visible
-        {
-            // ---- the strip's pool partial of t_j (blocks.py:89 AdaptiveAvgPool of conv2's
-            // output, less the bias): sum over the strip's output pixels of conv2(a1) =
-            // sum_{ci, tap} W2[tap][co][ci] * u[ci][tap], u = the sum of a1[ci] over the input
-            // pixels the tap reads -- the strip's a1 sum, less column 0 (kw = 2) / column W-1
-            // (kw = 0), less the image's row 0 (kh = 2; strip 0's first row) / row H-1 (kh = 0;
-            // the last strip's last row), whose inputs lie past the image's edge.  Wave w takes
-            // channels ci = 8w .. 8w+7: lane (r, c) reads row r's sums of channel 8w + c and
-            // both edge pixels (from the LDS image), the sums over the 8 rows by lane exchanges;
-            // then lane co accumulates W2[tap][co][8w .. 8w+7] * u (fixed order) into red, in
-            // the slots this wave alone read (a permutation: co -> [co >> 3][8w + (co & 7)])
+        // ---- the strip's pool partial of t_j (blocks.py:89 AdaptiveAvgPool of conv2's output,
+        // less the bias): sum over the strip's output pixels of conv2(a1) = sum_{ci, tap}
+        // W2[tap][co][ci] * u[ci][tap], u = the sum of a1[ci] over the input pixels the tap reads
+        // -- the strip's a1 sum, less column 0 (kw = 2) / column W-1 (kw = 0), less the image's
+        // row 0 (kh = 2; strip 0's first row) / row H-1 (kh = 0; the last strip's last row),
+        // whose inputs lie past the image's edge.  Slice sl takes channels ci = 8 sl .. 8 sl + 7:
+        // lane (r, c) reads row r's sums of channel 8 sl + c and both edge pixels (from the LDS
+        // image), the sums over the 8 rows by lane exchanges; then lane co accumulates
+        // W2[tap][co][8 sl .. 8 sl + 7] * u (fixed order) into red, in the slots only this slice
+        // reads (a permutation: co -> [co >> 3][8 sl + (co & 7)]).
+        auto pool_slice = [&](int sl) {
             int ll = lane;
             asm volatile("" : "+v"(ll));
-            const int r = ll >> 3, c = ll & 7, cw = 8 * wave + c;
+            const int r = ll >> 3, c = ll & 7, cw = 8 * sl + c;
             const float rsum = red[r * 64 + cw];
             const char* rb = img + (r + 1) * IROW + 2 * c;
-            const float p0 = lo16<T>((unsigned)*(const unsigned short*)(rb + hcol(1, wave)));
-            const float pl = lo16<T>((unsigned)*(const unsigned short*)(rb + hcol(SW, wave)));
+            const float p0 = lo16<T>((unsigned)*(const unsigned short*)(rb + hcol(1, sl)));
+            const float pl = lo16<T>((unsigned)*(const unsigned short*)(rb + hcol(SW, sl)));
             // every lane of channel c: the strip's sums less column W-1 (kw = 0), -, less column 0 (kw = 2)
             const float tt = sum_lanes_x8(rsum), c0 = sum_lanes_x8(p0), cl = sum_lanes_x8(pl);
             const float bs[3] = {tt - cl, tt, tt - c0};
-            // lane co: sum_c sum_kw bs[kw](c) * sum_kh W2[kh][kw][co][8w + c]; bs of channel c from
+            // lane co: sum_c sum_kw bs[kw](c) * sum_kh W2[kh][kw][co][8 sl + c]; bs of channel c from
             // lane c of the lane's row of 16 (row_newbcast)
-            const char* wb = filt + ll * 128 + ((wave ^ ((ll >> 1) & 7)) << 4);
+            const char* wb = filt + ll * 128 + ((sl ^ ((ll >> 1) & 7)) << 4);
             float P = 0.f;
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
@@ -527,20 +527,22 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                     }
                 }
             }
-            red[(ll >> 3) * 64 + 8 * wave + (ll & 7)] = P;
-        }
+            red[(ll >> 3) * 64 + 8 * sl + (ll & 7)] = P;
+        };
+        // the strip's partial as {tag, value} granules (one 8-B sc1 store each), slices in order
+        auto publish_partial = [&]() {
+            float s_ = 0.f;
+#pragma unroll
+            for (int w = 0; w < SR; ++w) s_ += red[(lane >> 3) * 64 + 8 * w + (lane & 7)];
+            unsigned long long* pg = (unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + par) * S + strip) * 64 + lane;
+            __hip_atomic_store(pg, ((unsigned long long)tag_of(j) << 32) | __float_as_uint(s_), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        };
+        pool_slice(wave);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();                                    // B_Z: the partial's eight channel slices in red; kh = 1 slots free
         issue_kh1(j + 1 < NB ? ci + 2 : 2 * NB);
-        if (wave == 3) {
-            // the strip's partial as {tag, value} granules (one 8-B sc1 store each), slices in order
-            float s = 0.f;
-#pragma unroll
-            for (int w = 0; w < SR; ++w) s += red[(lane >> 3) * 64 + 8 * w + (lane & 7)];
-            unsigned long long* pg = (unsigned long long*)(A.work + L.part) + ((size_t)(im * 2 + par) * S + strip) * 64 + lane;
-            __hip_atomic_store(pg, ((unsigned long long)tag_of(j) << 32) | __float_as_uint(s), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (wave == 3) publish_partial();
         GSTAMP(sb + 6);
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
         if (bwave) {

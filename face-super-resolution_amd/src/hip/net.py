@@ -209,11 +209,10 @@ SE_IN_BWD = os.environ.get("FEN_SE_IN_BWD", "fold") != "launch"
 # 8.826 ms per training step against the two-launch pair (3 same-box reps): off by default
 BWD_RES_FUSED = os.environ.get("FEN_RCAB_BWD_RES", "0") == "1"
 WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
-# ... on the strip backward (dt / dz1 are per-RCAB buffers, nothing rotates): a group's 21 weight
-# gradients in one launch pair (FEN_WGRAD_MAXJOBS = 32): each block reduces ~2.7x more tiles into
-# its slab, so 2.7x fewer fp32 slabs are written and re-read by the finalize, and 3 launch
-# fills / drains become 1 (FEN_WGRAD_STRIP_BATCH=8 gives the per-8 batches)
-WGRAD_STRIP_BATCH = max(1, min(32, int(os.environ.get("FEN_WGRAD_STRIP_BATCH", "32"))))
+# ... on the strip backward: the group's 21 weight gradients in batches of FEN_WGRAD_STRIP_BATCH
+# (the group conv's first).  One 21-job launch (2.7x fewer fp32 slabs) measured slower: 7.12-7.14
+# vs 6.59-6.61 ms per stage-1 step at 8 (same box, 3 reps each)
+WGRAD_STRIP_BATCH = max(1, min(32, int(os.environ.get("FEN_WGRAD_STRIP_BATCH", "8"))))
 # a ResidualGroup's whole backward (group conv^T, every RCAB's SE backward, conv2^T, PReLU',
 # conv1^T) as ONE strip-resident fen_group_strip_bwd launch where its envelope holds (16-bit,
 # 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP_BWD=0 selects the per-RCAB launches
