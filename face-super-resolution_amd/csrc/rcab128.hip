@@ -112,6 +112,32 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
 
     // filter step g = (output block g / 18; tap (g % 18) >> 1, input half g & 1) into ring slot
     // g % 3: this wave's 2 pieces (packed [9][NCO * 128][128])
+    // the step loop's addresses from per-lane parts computed once per tile, after the staging
+    // (their registers are not live through it): the two DMA pieces' source offsets, the A
+    // (filter slot) and B (image, per kw) fragment offsets of k-half 0.  The chunk index
+    // 8 ch + 4 ks + q has ch, ks in bits the lane's q does not touch, and the row / column parts
+    // are multiples of 128 / 256 B, so the (ch, ks) forms are those XORed with (4 ks + 8 ch) << 4
+    int dlane0 = 0, dlane1 = 0, aoff0 = 0, boffA = 0, boffB = 0, boffC = 0;
+    auto lane_offsets = [&]() {
+        int ll = lane;
+        asm volatile("" : "+v"(ll));
+        const int u0 = (2 * wave) * 64 + ll, r0_ = u0 >> 3, r1_ = r0_ + 8, pc = u0 & 7;
+        dlane0 = (r0_ * CC + (pc ^ ((r0_ >> 1) & 7)) * 8) * 2;
+        dlane1 = (r1_ * CC + (pc ^ ((r1_ >> 1) & 7)) * 8) * 2;
+        const int q = ll >> 4, c16 = ll & 15;
+        aoff0 = (64 * wh + c16) * 128 + ((q ^ ((c16 >> 1) & 7)) << 4);
+        boffA = wr * IROW + c16 * PXB + ((q ^ (c16 & 15)) << 4);
+        boffB = wr * IROW + (c16 + 1) * PXB + ((q ^ ((c16 + 1) & 15)) << 4);
+        boffC = wr * IROW + (c16 + 2) * PXB + ((q ^ ((c16 + 2) & 15)) << 4);
+    };
+    auto issue_step_fast = [&](int g) {
+        const int cb = g / NSTEP, s = g - cb * NSTEP;
+        const int tap = s >> 1, ch = s & 1;
+        char* slot = ring + (g % NSLOT) * SLOT;
+        const int sbase = ((tap * NCO + cb) * CC * CC + ch * 64) * 2;
+        dma16(wrs, __builtin_amdgcn_readfirstlane(lds_addr(slot + (2 * wave) * 1024)), sbase + dlane0);
+        dma16(wrs, __builtin_amdgcn_readfirstlane(lds_addr(slot + (2 * wave + 1) * 1024)), sbase + dlane1);
+    };
     auto issue_step = [&](int g) {
         const int cb = g / NSTEP, s = g - cb * NSTEP;
         const int tap = s >> 1, ch = s & 1;
@@ -274,11 +300,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
         auto load_half = [&](int g, int ks, uint4 (&a)[4], uint4 (&bv)[4]) {
             const int s = g % NSTEP;
             const int tap = s >> 1, ch = s & 1, kh = tap / 3, kw = tap - 3 * kh;
-            int q = lane >> 4, c16 = lane & 15;
-            asm volatile("" : "+v"(q), "+v"(c16));
-            const int colb = c16 + kw;
-            const char* ap = ring + (g % NSLOT) * SLOT + (64 * wh + c16) * 128 + (((4 * ks + q) ^ ((c16 >> 1) & 7)) << 4);
-            const char* bp = img + (wr + kh) * IROW + colb * PXB + (((8 * ch + 4 * ks + q) ^ (colb & 15)) << 4);
+            const int bo = kw == 0 ? boffA : kw == 1 ? boffB : boffC;
+            const char* ap = ring + (g % NSLOT) * SLOT + (aoff0 ^ (ks << 6));
+            const char* bp = img + kh * IROW + (bo ^ ((4 * ks + 8 * ch) << 4));
 #pragma unroll
             for (int m = 0; m < 4; ++m) a[m] = *(const uint4*)(ap + m * 2048);
 #pragma unroll
@@ -291,8 +315,9 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
             vm_wait((g + 2 < NG ? 2 : 0) + extra);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of step g done
             __syncthreads();
-            if (g + 3 < NG) issue_step(g + 3);
+            if (g + 3 < NG) issue_step_fast(g + 3);
         };
+        lane_offsets();
         load_half(0, 0, A0, B0);
         load_half(0, 1, A1, B1);
         f32x4 acc[4][4];
