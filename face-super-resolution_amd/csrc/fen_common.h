@@ -307,9 +307,20 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
     return (unsigned)(size_t)(const lds_void*)p;
 }
 
-#define FEN_CHECK_LAUNCH()                                    \
-    do {                                                      \
-        if (hipGetLastError() != hipSuccess) return FEN_EHIP; \
+// hipGetLastError() also returns the last status of any HIP call made on this thread, so
+// hipErrorNotReady left by a host-side hipEventQuery/hipStreamQuery (torch's gloo hand-off polls
+// events between steps) is not a launch failure and is only consumed here.  A real failure is
+// kept for fen_last_hip_error().
+namespace fen_detail {
+extern thread_local int last_hip_error;
+}
+#define FEN_CHECK_LAUNCH()                                        \
+    do {                                                          \
+        hipError_t e_ = hipGetLastError();                        \
+        if (e_ != hipSuccess && e_ != hipErrorNotReady) {         \
+            fen_detail::last_hip_error = (int)e_;                 \
+            return FEN_EHIP;                                      \
+        }                                                         \
     } while (0)
 
 // conv_last fast path (conv_last.hip): bf16, Cin 64, Cout <= 4, x4 skip, H and W multiples of 16

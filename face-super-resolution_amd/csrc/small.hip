@@ -1772,6 +1772,15 @@ extern "C" int fen_scale(size_t n, float* y, float s, void* stream) {
     return FEN_OK;
 }
 
+namespace fen_detail {
+thread_local int last_hip_error = 0;
+}
+
+extern "C" const char* fen_last_hip_error(void) {
+    const int e = fen_detail::last_hip_error;
+    return e ? hipGetErrorString((hipError_t)e) : "none";
+}
+
 extern "C" const char* fen_status_string(int code) {
     switch (code) {
         case FEN_OK: return "FEN_OK";

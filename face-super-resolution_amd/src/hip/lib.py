@@ -183,6 +183,7 @@ _SIGS = {
     "fen_s2d_filter": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
+    "fen_last_hip_error": (ctypes.c_char_p, []),
     "fen_build_info": (ctypes.c_char_p, []),
 }
 
@@ -216,6 +217,8 @@ def load():
 def check(code: int, what: str = "") -> None:
     if code != 0:
         msg = load().fen_status_string(code).decode()
+        if code == -3:
+            msg += f" [{load().fen_last_hip_error().decode()}]"
         raise FenError(f"{what}: {msg} (status {code})")
 
 

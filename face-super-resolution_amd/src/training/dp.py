@@ -78,7 +78,8 @@ class BucketExchange:
         self.views = {tag: flat[lo:hi] for tag, lo, hi in plan}
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.active = self.world > 1 or force
-        self.capturable = bool(flat.is_cuda)
+        # gloo stages CUDA tensors through the host (not stream-ordered): only RCCL captures
+        self.capturable = bool(flat.is_cuda) and (not self.active or dist.get_backend(group) == "nccl")
         self.stream = torch.cuda.Stream(device=flat.device) if (self.active and flat.is_cuda) else None
         self.works: List = []
         self._forked = False

@@ -522,6 +522,8 @@ int fen_s2d_filter(int Cout, int C, const float* src, float* dst, int gather, vo
 int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const void* dy, void* out, void* stream);
 
 const char* fen_status_string(int code);
+/* hipGetErrorString() of the HIP error behind this thread's last FEN_EHIP, or "none". */
+const char* fen_last_hip_error(void);
 const char* fen_build_info(void);
 
 #ifdef __cplusplus
