@@ -379,7 +379,8 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            from src.training.dp import init_rccl
+            init_rccl(torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
     from src.hip.engine import FENEngine

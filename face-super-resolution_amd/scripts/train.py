@@ -104,7 +104,8 @@ def main(argv=None):
     if world > 1 and not dist.is_initialized():
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        from src.training.dp import init_rccl
+        init_rccl(torch.device("cuda", local))
     rank = dist.get_rank() if dist.is_initialized() else 0
 
     config = load_config(args.config) if Path(args.config).exists() else {}

@@ -263,7 +263,10 @@ class FENEngine:
             from ..training.optim import bump_versions
             bump_versions(self._model_params)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local capture: ProcessGroupNCCL's watchdog thread polls the warm-up step's
+        # collectives with hipEventQuery, which a global-mode capture forbids process-wide
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._replay_body()
         self.graph = g
         return g

@@ -26,6 +26,19 @@ import torch.distributed as dist
 Bucket = Tuple[str, int, int]  # (tag, lo, hi) element offsets into the flat arena
 
 
+def init_rccl(device: torch.device, **kw) -> None:
+    """`init_process_group("nccl")` for a graph-captured DP step.  ProcessGroupNCCL's event
+    cache hands a finished eager collective's HIP events to the next collective; when that one
+    is issued inside a capture, the event is re-recorded on a capturing stream while the
+    watchdog thread (or the flight recorder's stale entry) may still query it, and the query
+    fails with hipErrorCapturedEvent -- which the watchdog turns into an abort (seen once in
+    three runs of tests/test_gpu_rccl.py's captured GAN iteration).  Fresh events per
+    collective cost microseconds, and only on eager steps: a replayed graph creates none."""
+    import os
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    dist.init_process_group("nccl", device_id=device, **kw)
+
+
 def _group_of(name: str) -> str:
     if name.startswith("conv_first."):
         return "head"

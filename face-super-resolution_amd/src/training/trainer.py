@@ -355,7 +355,9 @@ class Trainer:
                 return self._gan_step(hr)
             static_hr = hr.detach().clone()
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            torch.cuda.synchronize()
+            # thread-local: the RCCL watchdog thread's event polls stay legal (FENEngine.capture)
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 loss = self._gan_step(static_hr)
             st = self._gan_graph = {"graph": graph, "hr": static_hr, "loss": loss, "key": key}
         st["hr"].copy_(hr)

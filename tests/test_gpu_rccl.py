@@ -12,6 +12,7 @@ import socket
 import pytest
 import torch
 import torch.distributed as dist
+from src.training.dp import init_rccl
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -60,7 +61,7 @@ def test_engine_step_over_rccl(precision):
     e1 = FENEngine(model(), batch=2, lr_hw=(32, 32), dtype=dt, train=True, clip=0.5, lr=1e-3)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", torch.cuda.current_device()))
+    init_rccl(torch.device("cuda", torch.cuda.current_device()), rank=0, world_size=1)
     try:
         assert dist.get_backend() == "nccl"
         log = []
@@ -83,7 +84,7 @@ def test_engine_step_over_rccl(precision):
 def _init_one_rank():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", torch.cuda.current_device()))
+    init_rccl(torch.device("cuda", torch.cuda.current_device()), rank=0, world_size=1)
 
 
 def test_engine_captured_step_over_rccl():
