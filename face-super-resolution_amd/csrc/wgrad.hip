@@ -529,6 +529,9 @@ int wgrad_geom(const fen_wgrad_desc* d, int njobs, int* nchunk, int* tpc, int* c
     const int yz = (d->Cout / *cot) * ((d->Cin + 63) / 64);
     int t = (ntiles * yz * njobs + 255) / 256;  // target ~256 blocks
     if (t < 1) t = 1;
+    // ... and never more: one block per CU, so a 257th block is a second wave of a whole chunk
+    // (5 jobs of 512 tiles at t = 10 would be 5 x 52 = 260 blocks; t = 11 gives 235)
+    while (njobs * yz * ((ntiles + t - 1) / t) > 256) ++t;
     *tpc = t;
     *nchunk = (ntiles + t - 1) / t;
     return FEN_OK;

@@ -210,9 +210,10 @@ SE_IN_BWD = os.environ.get("FEN_SE_IN_BWD", "fold") != "launch"
 BWD_RES_FUSED = os.environ.get("FEN_RCAB_BWD_RES", "0") == "1"
 WGRAD_BATCH = max(1, min(8, int(os.environ.get("FEN_WGRAD_BATCH", "8"))))
 # ... on the strip backward: the group's 21 weight gradients in batches of FEN_WGRAD_STRIP_BATCH
-# (the group conv's first).  One 21-job launch (2.7x fewer fp32 slabs) measured slower: 7.12-7.14
-# vs 6.59-6.61 ms per stage-1 step at 8 (same box, 3 reps each)
-WGRAD_STRIP_BATCH = max(1, min(32, int(os.environ.get("FEN_WGRAD_STRIP_BATCH", "8"))))
+# (the group conv's first), by default all 21 in one launch (252 blocks of 43 tiles, 3x fewer
+# fp32 slabs than batches of 8): 6.67-6.68 vs 6.87-6.90 ms per stage-1 step at 8 and 6.81 at 11
+# (same box, 3 reps each), once the launch geometry stopped spilling past 256 blocks
+WGRAD_STRIP_BATCH = max(1, min(32, int(os.environ.get("FEN_WGRAD_STRIP_BATCH", "21"))))
 # a ResidualGroup's whole backward (group conv^T, every RCAB's SE backward, conv2^T, PReLU',
 # conv1^T) as ONE strip-resident fen_group_strip_bwd launch where its envelope holds (16-bit,
 # 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP_BWD=0 selects the per-RCAB launches
