@@ -347,7 +347,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
     __builtin_amdgcn_s_barrier();
     for (int k = 0, t = t_begin; t < t_end; ++k, ++t) {
         const char* cur = smem + (k & 1) * Cfg::SLOT;
+#ifndef WG_NODMA   // diagnostic build: no next-tile loads (times the MFMA/LDS-read body alone)
         if (t + 1 < t_end) issue(t + 1, smem + ((k + 1) & 1) * Cfg::SLOT);
+#endif
         const char* hx = cur;
         const char* ty = cur + HALO_SLOT;
         uint4 A0[MC], B0[9], A1[MC], B1[9];
@@ -372,6 +374,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
             }
         };
         auto mma = [&](int s, const uint4 (&A)[MC], const uint4 (&Bf)[9]) {
+#ifdef WG_NOMMA     // diagnostic build: no MFMAs (times the loads alone)
+            return;
+#endif
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
