@@ -277,35 +277,61 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
     const i32x4 xr = make_rsrc(J.x[job], (unsigned)((size_t)d.B * H * W * Cin * 2));
     const i32x4 yr = make_rsrc(J.dy[job], (unsigned)((size_t)d.B * H * W * Cout * 2));
 
-    // every wave issues its share of the tile's 41 halo + TILE_DMA dy pieces
+    // every wave issues its share of the tile's 41 halo + TILE_DMA dy pieces: piece k of a
+    // wave is i = wave + NW k.  Its lanes' pixel (dr, dc) relative to the tile origin and byte
+    // offset from that origin's first channel are fixed for the block, worked out once here
+    // (dr = -1000 for the halo's padding lanes: always out of bounds); per tile a piece is a
+    // bounds test and an add (the integer divisions per piece and tile were most of the
+    // kernel's VALU)
+    constexpr int NPC = (HALO_DMA + Cfg::TILE_DMA + NW - 1) / NW;
+    int prel[NPC], ppos[NPC];
+#pragma unroll
+    for (int k = 0; k < NPC; ++k) {
+        const int i = wave + NW * k;
+        int dr = -1000, dc = 0, rel = 0;
+        if (i < HALO_DMA) {
+            const int s = i * 64 + lane, p = s >> 3, pos = s & 7;
+            const int hr = p / HALO, hc = p - hr * HALO;
+            const int c = pos ^ wkey(hc);
+            if (s < HP * 8) {
+                dr = hr - 1;
+                dc = hc - 1;
+            }
+            rel = ((dr * W + dc) * Cin + c * 8) * 2;
+        } else if (i < HALO_DMA + Cfg::TILE_DMA) {
+            const int s = (i - HALO_DMA) * 64 + lane;
+            int p, c;
+            if constexpr (COT == 64) {
+                p = s >> 3;
+                c = (s & 7) ^ wkey(p & 15);
+            } else {
+                p = pswap16(s >> 1);
+                c = s & 1;
+            }
+            dr = p >> 4;
+            dc = p & 15;
+            rel = ((dr * W + dc) * Cout + c * 8) * 2;
+        }
+        prel[k] = rel;
+        ppos[k] = (dr << 16) | (dc & 0xffff);
+    }
     auto issue = [&](int t, const char* slotp) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const unsigned hbase = lds_addr(slotp), ybase = lds_addr(slotp + HALO_SLOT);
-        for (int i = wave; i < HALO_DMA + Cfg::TILE_DMA; i += NW) {
-            if (i < HALO_DMA) {
-                const int s = i * 64 + lane, p = s >> 3, pos = s & 7;
-                const int hr = p / HALO, hc = p - hr * HALO;
-                const int c = pos ^ wkey(hc);
-                const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-                const bool in = s < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-                const int voff = in ? (((b * H + gh) * W + gw) * Cin + ci0 + c * 8) * 2 : 0x7ffffff0;
-                dma16(xr, __builtin_amdgcn_readfirstlane(hbase + i * 1024), voff);
-            } else {
-                const int j = i - HALO_DMA;
-                const int s = j * 64 + lane;
-                int p, c;
-                if constexpr (COT == 64) {
-                    p = s >> 3;
-                    c = (s & 7) ^ wkey(p & 15);
-                } else {
-                    p = pswap16(s >> 1);
-                    c = s & 1;
-                }
-                const int gh = h0 + (p >> 4), gw = w0 + (p & 15);
-                const bool in = gh < H && gw < W;
-                const int voff = in ? (((b * H + gh) * W + gw) * Cout + co0 + c * 8) * 2 : 0x7ffffff0;
-                dma16(yr, __builtin_amdgcn_readfirstlane(ybase + j * 1024), voff);
+        const int xb = (((b * H + h0) * W + w0) * Cin + ci0) * 2;
+        const int yb = (((b * H + h0) * W + w0) * Cout + co0) * 2;
+#pragma unroll
+        for (int k = 0; k < NPC; ++k) {
+            const int i = wave + NW * k;
+            if (i < HALO_DMA + Cfg::TILE_DMA) {
+                const int gh = h0 + (ppos[k] >> 16), gw = w0 + ((ppos[k] << 16) >> 16);
+                const bool in = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+                if (i < HALO_DMA)
+                    dma16(xr, __builtin_amdgcn_readfirstlane(hbase + i * 1024), in ? xb + prel[k] : 0x7ffffff0);
+                else
+                    dma16(yr, __builtin_amdgcn_readfirstlane(ybase + (i - HALO_DMA) * 1024),
+                          in ? yb + prel[k] : 0x7ffffff0);
             }
         }
     };
