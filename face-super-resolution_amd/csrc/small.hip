@@ -1202,47 +1202,93 @@ __global__ __launch_bounds__(1024) void k_colsum_multi(const ColJobs jobs) {
 }
 
 // Pack many conv weights in one launch: job k covers packed elements [e0[k], e0[k+1]).
+// Each job's range in the launch's index space is rounded up to whole 256-thread blocks, so a
+// block's job is block-uniform (one scalar search per block, not a dependent chain of e0
+// loads per thread) and the element math is 32-bit.
+constexpr unsigned PACK_RUN = 8;                  // consecutive packed elements per thread (one 16-B store)
+constexpr unsigned PACK_BLK = 256 * PACK_RUN;
 struct PackJobK {
     const float* w;
     void* out;
     int mode, Cout, Cin;
+    unsigned n;   // packed elements
 };
 template <typename T>
 __device__ __forceinline__ void pack_one(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out,
-                                         size_t i) {
+                                         unsigned i) {
     if (mode == 2) {  // [9][Cin_pad][Cout], row = ci, taps flipped
-        const int co = (int)(i % Cout);
-        const int ci = (int)((i / Cout) % ((Cin + 15) & ~15));
-        const int tap = (int)(i / ((size_t)Cout * ((Cin + 15) & ~15)));
+        const int co = (int)(i % (unsigned)Cout);
+        const int ci = (int)((i / (unsigned)Cout) % (unsigned)((Cin + 15) & ~15));
+        const int tap = (int)(i / ((unsigned)Cout * (unsigned)((Cin + 15) & ~15)));
         const int kh = 2 - tap / 3, kw = 2 - tap % 3;
         out[i] = fromf<T>(ci < Cin ? w[(((size_t)co * Cin + ci) * 3 + kh) * 3 + kw] : 0.f);
     } else {          // [9][Cout_pad][Cin], row = co (mode 1: shuffle-permuted rows)
         const int coutp = (Cout + 15) & ~15;
-        const int ci = (int)(i % Cin);
-        const int cp = (int)((i / Cin) % coutp);
-        const int tap = (int)(i / ((size_t)Cin * coutp));
+        const int ci = (int)(i % (unsigned)Cin);
+        const int cp = (int)((i / (unsigned)Cin) % (unsigned)coutp);
+        const int tap = (int)(i / ((unsigned)Cin * (unsigned)coutp));
         int co = cp;
         if (mode == 1) { const int Cq = Cout / 4; co = 4 * (cp % Cq) + cp / Cq; }
         out[i] = fromf<T>(cp < Cout ? w[(((size_t)co * Cin + ci) * 3 + tap / 3) * 3 + tap % 3] : 0.f);
     }
 }
+// PACK_RUN consecutive packed elements from i (a multiple of PACK_RUN): one index decomposition,
+// then the row / channel / tap counters stepped with carries
+template <typename T>
+__device__ __forceinline__ void pack_run(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out,
+                                         unsigned i) {
+    float v[PACK_RUN];
+    if (mode == 2) {
+        const unsigned cinp = (unsigned)((Cin + 15) & ~15);
+        unsigned co = i % (unsigned)Cout, ci = (i / (unsigned)Cout) % cinp, tap = i / ((unsigned)Cout * cinp);
+#pragma unroll
+        for (unsigned k = 0; k < PACK_RUN; ++k) {
+            const unsigned kh = 2 - tap / 3, kw = 2 - tap % 3;
+            v[k] = ci < (unsigned)Cin ? w[(((size_t)co * Cin + ci) * 3 + kh) * 3 + kw] : 0.f;
+            if (++co == (unsigned)Cout) {
+                co = 0;
+                if (++ci == cinp) { ci = 0; ++tap; }
+            }
+        }
+    } else {
+        const unsigned coutp = (unsigned)((Cout + 15) & ~15), Cq = (unsigned)Cout / 4;
+        unsigned ci = i % (unsigned)Cin, cp = (i / (unsigned)Cin) % coutp, tap = i / ((unsigned)Cin * coutp);
+#pragma unroll
+        for (unsigned k = 0; k < PACK_RUN; ++k) {
+            const unsigned co = mode == 1 ? 4 * (cp % Cq) + cp / Cq : cp;
+            v[k] = cp < (unsigned)Cout ? w[(((size_t)co * Cin + ci) * 3 + tap / 3) * 3 + tap % 3] : 0.f;
+            if (++ci == (unsigned)Cin) {
+                ci = 0;
+                if (++cp == coutp) { cp = 0; ++tap; }
+            }
+        }
+    }
+    if constexpr (sizeof(T) == 2) {
+        *(uint4*)(out + i) = pack16<T>(v);
+    } else {
+        *(uint4*)(out + i) = pack16<float>(v);
+        *(uint4*)(out + i + 4) = pack16<float>(v + 4);
+    }
+}
 template <typename T>
 __global__ void k_pack(int mode, int Cout, int Cin, const float* __restrict__ w, T* __restrict__ out, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) pack_one<T>(mode, Cout, Cin, w, out, i);
+    if (i < n) pack_one<T>(mode, Cout, Cin, w, out, (unsigned)i);
 }
 template <typename T>
 __global__ void k_pack_multi(int njobs, const PackJobK* __restrict__ jobs, const unsigned long long* __restrict__ e0,
                              unsigned long long total) {
-    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    int lo = 0, hi = njobs - 1;   // last job with e0 <= i
+    const unsigned long long b0 = (unsigned long long)blockIdx.x * PACK_BLK;   // block-uniform
+    if (b0 >= total) return;
+    int lo = 0, hi = njobs - 1;   // last job with e0 <= b0
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (e0[mid] <= i) lo = mid; else hi = mid - 1;
+        if (e0[mid] <= b0) lo = mid; else hi = mid - 1;
     }
     const PackJobK jb = jobs[lo];
-    pack_one<T>(jb.mode, jb.Cout, jb.Cin, jb.w, (T*)jb.out, (size_t)(i - e0[lo]));
+    // packed sizes are multiples of 16 (padded Cout / Cin rows): a run never straddles a job's end
+    const unsigned j = (unsigned)(b0 - e0[lo]) + threadIdx.x * PACK_RUN;
+    if (j < jb.n) pack_run<T>(jb.mode, jb.Cout, jb.Cin, jb.w, (T*)jb.out, j);
 }
 
 constexpr int SUMSQ_BLOCKS_MAX = 1024;
@@ -1664,9 +1710,11 @@ extern "C" int fen_pack_table(int dtype, int njobs, const fen_pack_job* jobs, vo
     for (int i = 0; i < njobs; ++i) {
         const fen_pack_job& j = jobs[i];
         if (!j.w || !j.out || j.mode < 0 || j.mode > 2 || (j.mode == 1 && j.Cout % 4)) return FEN_EINVAL;
-        pj[i] = PackJobK{j.w, j.out, j.mode, j.Cout, j.Cin};
+        const size_t n = fen_packed_elems(j.mode, j.Cout, j.Cin);
+        if (n >= (1ull << 31) || n % PACK_RUN) return FEN_EUNSUPPORTED;
+        pj[i] = PackJobK{j.w, j.out, j.mode, j.Cout, j.Cin, (unsigned)n};
         e0[i] = acc;
-        acc += fen_packed_elems(j.mode, j.Cout, j.Cin);
+        acc += (n + PACK_BLK - 1) / PACK_BLK * PACK_BLK;
     }
     e0[njobs] = acc;
     *total = (size_t)acc;
@@ -1677,7 +1725,7 @@ extern "C" int fen_pack_multi(int dtype, int njobs, const void* table_dev, size_
     if (njobs <= 0 || !table_dev || total == 0) return FEN_EINVAL;
     const PackJobK* pj = (const PackJobK*)table_dev;
     const unsigned long long* e0 = (const unsigned long long*)(pj + njobs);
-    const unsigned nb = (unsigned)((total + 255) / 256);
+    const unsigned nb = (unsigned)((total + PACK_BLK - 1) / PACK_BLK);   // 256 threads x PACK_RUN
     if (dtype == FEN_BF16)
         hipLaunchKernelGGL(k_pack_multi<bf16>, dim3(nb), dim3(256), 0, STREAM, njobs, pj, e0, (unsigned long long)total);
     else if (dtype == FEN_F16)

@@ -419,7 +419,7 @@ int fen_pack_conv_w(int dtype, int mode, int Cout, int Cin, const float* w, void
 size_t fen_packed_elems(int mode, int Cout, int Cin);
 /* Many packs in one launch (the re-pack after every optimizer step).  fen_pack_table fills a
  * host buffer of fen_pack_table_bytes(njobs) bytes (job table + element offsets, *total =
- * packed elements); the caller copies it to device memory once and replays fen_pack_multi. */
+ * the launch's index space: each job's packed elements rounded up to 256); the caller copies it to device memory once and replays fen_pack_multi. */
 typedef struct {
     const float* w;   /* OIHW fp32 source                                                     */
     void* out;        /* packed destination of dtype                                          */
