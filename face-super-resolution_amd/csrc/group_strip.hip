@@ -114,6 +114,8 @@ struct GsArgs {
     float* sv_mean[FEN_GS_MAXNB];
     float* sv_hid[FEN_GS_MAXNB];
     void* x_last;
+    int* status;                              // optional: a timed-out wait is reported here
+    int fault;                                // test-only: image 0 strip 1 skips one a1 flag
 };
 
 template <typename T>
@@ -471,7 +473,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         GSTAMP(sb + 5);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv2's other taps; the a1 boundary stores
         // a1's boundary row is out: its storing wave signals for itself (one lane, after its drain)
-        if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 0), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (bwave && lane == 0 && !(A.fault && ticket == 1 && j == 0 && side == 0))
+            __hip_atomic_store(flag_of(strip, side, 0), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();                                    // B_Y: a1 image and row sums complete; conv2's taps visible
         // ---- the strip's pool partial of t_j (blocks.py:89 AdaptiveAvgPool of conv2's output,
         // less the bias): sum over the strip's output pixels of conv2(a1) = sum_{ci, tap}
@@ -657,14 +660,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     if (!ok) __hip_atomic_fetch_or(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-        const int nblk = B * S;
-        if (__hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
-            __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (tid == 0) strip_finish(ctl, B * S, A.status, FEN_STATUS_GS_FWD);
 #ifdef FEN_GS_STAMPS
     __syncthreads();
     {
@@ -717,6 +713,7 @@ extern "C" int fen_group_strip(const fen_group_strip_desc* d, void* stream) {
     a.res_scale = d->res_scale, a.inv_hw = 1.0f / (float)(d->H * d->W);
     a.x = d->x, a.y = d->y, a.work = (char*)d->work;
     a.save = d->save ? 1 : 0;
+    a.status = d->status, a.fault = d->fault;
     if (a.save) {
         if (!d->x_last) return FEN_EINVAL;
         a.x_last = d->x_last;

@@ -80,6 +80,8 @@ struct GsbArgs {
     float* dw1p[FEN_GS_MAXNB];                // [B][Cr][64]
     float* dw2p[FEN_GS_MAXNB];                // [B][64][Cr]
     char* work;
+    int* status;                              // optional: a timed-out wait is reported here
+    int fault;                                // test-only: image 0 strip 1 skips one dz1 flag
 };
 
 template <typename T>
@@ -364,7 +366,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             conv_phase<T>(acc, img, filt, 1, wave, q, c16);     // own dz1 row only: no barrier
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv1^T's other taps; the dz1 boundary stores
-            if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 0), tag_of(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (bwave && lane == 0 && !(A.fault && ticket == 1 && k == 1 && side == 0))
+                __hip_atomic_store(flag_of(strip, side, 0), tag_of(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();                                // B_Y: dz1's image complete; kh = 1 slots free
             if (jr > 0) issue_kh1(ci + 2);                  // the next RCAB's conv2^T
             load_acc(jr > 0 ? A.t[jr - 1] : A.dy, tv);
@@ -548,14 +551,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
     if (!ok) __hip_atomic_fetch_or(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-        const int nblk = B * S;
-        if (__hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
-            __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (tid == 0) strip_finish(ctl, B * S, A.status, FEN_STATUS_GS_BWD);
 }
 
 template <typename T>
@@ -588,6 +584,7 @@ extern "C" int fen_group_strip_bwd(const fen_group_strip_bwd_desc* d, void* stre
     a.B = d->B, a.H = d->H, a.S = d->H / SR, a.NB = nb, a.Cr = d->Cr;
     a.res_scale = d->res_scale, a.inv_hw = 1.0f / (float)(d->H * d->W);
     a.dy = d->dy, a.dx = d->dx, a.dres = d->dres, a.work = (char*)d->work;
+    a.status = d->status, a.fault = d->fault;
     a.w[0] = d->wgt;
     for (int j = 0; j < nb; ++j) {
         if (!d->w1t[j] || !d->w2t[j] || !d->alpha[j] || !d->fc1[j] || !d->fc2[j] || !d->z1[j] || !d->t[j] ||

@@ -1829,6 +1829,26 @@ extern "C" const char* fen_last_hip_error(void) {
     return e ? hipGetErrorString((hipError_t)e) : "none";
 }
 
+extern "C" int fen_status_word(void** host, void** dev) {
+    if (!host || !dev) return FEN_EINVAL;
+    static void* words[64] = {};
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e == hipSuccess && (d < 0 || d >= 64)) return FEN_EUNSUPPORTED;
+    if (e == hipSuccess && !words[d]) {
+        e = hipHostMalloc(&words[d], 64, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) { for (int i = 0; i < 16; ++i) ((volatile int*)words[d])[i] = 0; }
+        else words[d] = nullptr;
+    }
+    if (e == hipSuccess) e = hipHostGetDevicePointer(dev, words[d], 0);
+    if (e != hipSuccess) {
+        fen_detail::last_hip_error = (int)e;
+        return FEN_EHIP;
+    }
+    *host = words[d];
+    return FEN_OK;
+}
+
 extern "C" const char* fen_status_string(int code) {
     switch (code) {
         case FEN_OK: return "FEN_OK";

@@ -64,6 +64,27 @@ __device__ __forceinline__ bool poll_eq(const unsigned* p, unsigned tag) {
     return false;
 }
 
+// End of a strip launch, thread 0 of every block after its `ok` went into ctl[2] (drained):
+// the last block out advances the launch epoch, resets the ticket counters for the next launch
+// and, when the caller passed a status word, moves the error word there (a vector store at
+// system scope: the word may be host-mapped pinned memory the host reads without a sync) and
+// clears it, so a later launch on the same workspace starts clean.
+// ctl: [0] ticket [1] done [2] error [3] launch epoch.
+__device__ __forceinline__ void strip_finish(int* ctl, int nblk, int* status, int status_bit) {
+    if (__hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
+        if (status) {
+            const int e = __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e) {
+                __hip_atomic_store(status, status_bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(ctl + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __device__ __forceinline__ void vm_wait_n(int n) {
     switch (n) {
 #define GS_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;

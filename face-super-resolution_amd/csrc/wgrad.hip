@@ -562,7 +562,9 @@ int wgrad_geom(const fen_wgrad_desc* d, int njobs, int* nchunk, int* tpc, int* c
     if (t < 1) t = 1;
     // ... and never more: one block per CU, so a 257th block is a second wave of a whole chunk
     // (5 jobs of 512 tiles at t = 10 would be 5 x 52 = 260 blocks; t = 11 gives 235)
-    while (njobs * yz * ((ntiles + t - 1) / t) > 256) ++t;
+    // Bounded: once t >= ntiles a job is one chunk, and njobs * yz > 256 simply runs more than
+    // one wave of blocks (the persistent form still sums each chunk into its own slab).
+    while (t < ntiles && njobs * yz * ((ntiles + t - 1) / t) > 256) ++t;
     *tpc = t;
     *nchunk = (ntiles + t - 1) / t;
     return FEN_OK;

@@ -80,6 +80,40 @@ def create_gan(config: dict, precision: str):
     return d, GANLoss(gan_type=gan.get("type", "vanilla"))
 
 
+def train_loader_kwargs(config: dict) -> dict:
+    """The train loader's augmentation keywords from the YAML, with the reference CLI's defaults
+    (scripts/train.py:174-191): augmentation.random_crop.hr_patch_size (128),
+    horizontal_flip (0.5), random_rotate90 (0.0), color_jitter.{probability 0.3, brightness 0.1,
+    contrast 0.1, saturation 0.0, hue 0.0}.  Every one reaches get_dataloader, which applies it
+    or raises (src/data)."""
+    aug = config.get("augmentation", {}) or {}
+    cj = aug.get("color_jitter", {}) or {}
+    known = {"horizontal_flip", "random_rotate90", "random_crop", "color_jitter"}
+    extra = sorted(set(aug) - known)
+    if extra:
+        raise ValueError(f"augmentation keys {extra} are not read by the reference's train.py either "
+                         "(scripts/train.py:174-191): remove them")
+    return dict(hr_patch_size=(aug.get("random_crop", {}) or {}).get("hr_patch_size", 128),
+                horizontal_flip=aug.get("horizontal_flip", 0.5), random_rotate90=aug.get("random_rotate90", 0.0),
+                color_jitter_prob=cj.get("probability", 0.3), brightness=cj.get("brightness", 0.1),
+                contrast=cj.get("contrast", 0.1), saturation=cj.get("saturation", 0.0), hue=cj.get("hue", 0.0))
+
+
+def build_loaders(config: dict, data_root: str, batch_size: int, synthetic: int = 0):
+    """Train / val loaders as the reference CLI builds them (scripts/train.py:171-198): the train
+    loader with the YAML's augmentation, the val loader with FFHQDataset's defaults (val mode:
+    full images, no augmentation)."""
+    data_cfg = config.get("data", {}) or {}
+    nw = data_cfg.get("num_workers", 4)
+    kw = train_loader_kwargs(config)
+    seed = (config.get("project", {}) or {}).get("seed", 42)
+    train = get_dataloader(data_root, "train", batch_size, nw, synthetic=synthetic, seed=seed, **kw)
+    val_syn = max(synthetic // 8, batch_size) if synthetic else 0
+    val = get_dataloader(data_root, "val", batch_size, nw, synthetic=val_syn, seed=seed,
+                         hr_patch_size=kw["hr_patch_size"] if synthetic else 128)
+    return train, val
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="Train Face Super-Resolution Model (MI355X)")
     ap.add_argument("--config", type=str, default="configs/config.yaml")
@@ -119,12 +153,7 @@ def main(argv=None):
     lr = args.lr or tr_cfg.get("optimizer", {}).get("lr", 1e-4)
     data_root = args.data_root or data_cfg.get("data_root", "data/processed")
     model_type = args.model or config.get("model", {}).get("type", "custom")
-    aug = config.get("augmentation", {})
-    hr_size = aug.get("random_crop", {}).get("hr_patch_size", data_cfg.get("hr_size", 256))
-    train_loader = get_dataloader(data_root, "train", batch_size, data_cfg.get("num_workers", 4), hr_patch_size=hr_size,
-                                  horizontal_flip=aug.get("horizontal_flip", 0.5), synthetic=args.synthetic)
-    val_loader = get_dataloader(data_root, "val", batch_size, data_cfg.get("num_workers", 4), hr_patch_size=hr_size,
-                                synthetic=max(args.synthetic // 8, batch_size) if args.synthetic else 0)
+    train_loader, val_loader = build_loaders(config, data_root, batch_size, args.synthetic)
 
     precision = resolve_precision(args.precision, tr_cfg)
     model = create_model(model_type, config, precision)

@@ -35,6 +35,7 @@ class DeviceHRLoader:
         if hr_patch_size % 2:
             raise ValueError("hr_patch_size must be even")
         self.images, self.B, self.P = images, batch_size, hr_patch_size
+        self.dataset = images           # the reference's `len(loader.dataset)` (scripts/train.py:200)
         self.flip_p, self.rot_p, self.color_p = horizontal_flip, random_rotate90, color_jitter_prob
         self.bri, self.con, self.sat = brightness, contrast, saturation
         self.rng = np.random.default_rng(seed)

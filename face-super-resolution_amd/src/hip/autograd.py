@@ -139,6 +139,7 @@ class GroupFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, rt: Runtime, attn, *params):
         _check_input(x)
+        L.check_strip_status()      # an earlier strip launch's timed-out wait raises here
         xh = to_nhwc(x, rt.dtype)
         W = rt.wt(x.device)
         c = rt.ctx(x.device)
@@ -150,6 +151,7 @@ class GroupFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         _check_grad(ctx.rt)
+        L.check_strip_status()
         rt, sv = ctx.rt, ctx.sv
         dyh = to_nhwc(dy, rt.dtype)
         c = rt.ctx(dy.device)

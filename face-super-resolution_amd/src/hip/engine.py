@@ -208,6 +208,7 @@ class FENEngine:
 
     def forward(self, x: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Inference: x NCHW fp32 [B,3,h,w] -> out NCHW fp32 [B,3,H,W] (eval: clamped)."""
+        L.check_strip_status()
         if x is not None:
             self.x.copy_(x)
         self.ctx.run()
@@ -217,6 +218,7 @@ class FENEngine:
         """One training step on HR [B,3,H,W]: LR synthesis, fwd, L1 (+ perceptual), bwd,
         all-reduce, clip, AdamW (the last three skipped without `update`: a non-stepping batch
         under accumulation).  Returns the (device) total loss of this rank's shard."""
+        L.check_strip_status()
         if hr is not None:
             self.hr.copy_(hr)
         self.ctx.run()
@@ -278,7 +280,14 @@ class FENEngine:
             self.upd.run()
             self.Wt.pack()
 
+    def check_status(self) -> None:
+        """Raise FenError if a strip launch of an earlier step reported a timed-out hand-off wait
+        (forward / step / replay check before they enqueue; call this after the last step, once
+        the stream has drained, to cover it too)."""
+        L.check_strip_status()
+
     def replay(self):
+        L.check_strip_status()
         self.graph.replay()
         if self.train:
             from ..training.optim import bump_versions

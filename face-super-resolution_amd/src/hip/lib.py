@@ -81,7 +81,7 @@ class GroupStripDesc(Structure):
         ("wg", c_void_p), ("bg", c_void_p), ("work", c_void_p), ("work_bytes", c_size_t),
         ("save", c_int), ("sv_x", c_void_p * GS_MAXNB), ("sv_z1", c_void_p * GS_MAXNB),
         ("sv_a1", c_void_p * GS_MAXNB), ("sv_t", c_void_p * GS_MAXNB), ("sv_mean", c_void_p * GS_MAXNB),
-        ("sv_hid", c_void_p * GS_MAXNB), ("x_last", c_void_p),
+        ("sv_hid", c_void_p * GS_MAXNB), ("x_last", c_void_p), ("status", c_void_p), ("fault", c_int),
     ]
 
 
@@ -94,7 +94,7 @@ class GroupStripBwdDesc(Structure):
         ("t", c_void_p * GS_MAXNB), ("s", c_void_p * GS_MAXNB), ("mean", c_void_p * GS_MAXNB),
         ("hid", c_void_p * GS_MAXNB), ("dt", c_void_p * GS_MAXNB), ("dz1", c_void_p * GS_MAXNB),
         ("dalpha_part", c_void_p * GS_MAXNB), ("dw1p", c_void_p * GS_MAXNB), ("dw2p", c_void_p * GS_MAXNB),
-        ("work", c_void_p), ("work_bytes", c_size_t),
+        ("work", c_void_p), ("work_bytes", c_size_t), ("status", c_void_p), ("fault", c_int),
     ]
 
 
@@ -182,6 +182,7 @@ _SIGS = {
     "fen_s2d2": (c_int, [c_int] * 5 + [c_void_p] * 2 + [c_int, c_void_p]),
     "fen_s2d_filter": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
+    "fen_status_word": (c_int, [POINTER(c_void_p), POINTER(c_void_p)]),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
     "fen_last_hip_error": (ctypes.c_char_p, []),
     "fen_build_info": (ctypes.c_char_p, []),
@@ -220,6 +221,44 @@ def check(code: int, what: str = "") -> None:
         if code == -3:
             msg += f" [{load().fen_last_hip_error().decode()}]"
         raise FenError(f"{what}: {msg} (status {code})")
+
+
+STATUS_GS_FWD, STATUS_GS_BWD = 1, 2   # FEN_STATUS_GS_*
+
+_status = {}
+
+
+def strip_status_ptr(device) -> int:
+    """Device address of this process's status word for `device` (fen_status_word: one int in
+    host-mapped coherent pinned memory): every fen_group_strip / fen_group_strip_bwd launch
+    reports a timed-out hand-off wait there (include/fen.h).  The host reads the word without
+    synchronising (`check_strip_status`), so a replayed hipGraph needs no extra node and the
+    fault-free path costs nothing."""
+    import torch
+    dev = torch.device(device)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ent = _status.get(key)
+    if ent is None:
+        hp, dp = c_void_p(), c_void_p()
+        with torch.cuda.device(key):
+            check(load().fen_status_word(ctypes.byref(hp), ctypes.byref(dp)), "status_word")
+        # the host reads it through ctypes: no torch op (and no sync) per check
+        ent = _status[key] = (int(dp.value), ctypes.c_int32.from_address(hp.value))
+    return ent[0]
+
+
+def check_strip_status() -> None:
+    """Raise FenError if a strip launch enqueued earlier reported a timed-out wait (its outputs,
+    and everything computed from them, are invalid), and clear the word.  A launch still in
+    flight is seen by a later check."""
+    for key, (_, word) in _status.items():
+        v = word.value
+        if v:
+            word.value = 0
+            kinds = [n for b, n in ((STATUS_GS_FWD, "fen_group_strip"), (STATUS_GS_BWD, "fen_group_strip_bwd"))
+                     if v & b]
+            raise FenError(f"{' / '.join(kinds) or 'strip kernel'} on cuda:{key}: a hand-off wait between "
+                           "strips timed out (another kernel held the CUs); that launch's outputs were invalid")
 
 
 def dtype_code(torch_dtype) -> int:

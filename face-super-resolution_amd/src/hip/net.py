@@ -218,6 +218,11 @@ WGRAD_STRIP_BATCH = max(1, min(32, int(os.environ.get("FEN_WGRAD_STRIP_BATCH", "
 # conv1^T) as ONE strip-resident fen_group_strip_bwd launch where its envelope holds (16-bit,
 # 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP_BWD=0 selects the per-RCAB launches
 GROUP_STRIP_BWD = os.environ.get("FEN_GROUP_STRIP_BWD", "1") != "0"
+# test-only fault injection for the strip kernels' bounded waits (fen_group_strip_desc.fault):
+# bit 0 = the forward launches, bit 1 = the backward launches skip one hand-off flag in one
+# strip, so its neighbour's wait times out and the launch reports through the status word
+# (lib.check_strip_status).  Read when a launch is built; 0 in production.
+GS_FAULT = 0
 
 
 class WgradBatch:
@@ -458,6 +463,7 @@ class Forward:
         nbytes = int(ctx.lib.fen_group_strip_work_bytes(B, H))
         work = ctx.persistent_zeros(f"group_strip/{B}x{H}", nbytes)
         d.work, d.work_bytes = ptr(work), nbytes
+        d.status, d.fault = L.strip_status_ptr(ctx.device), GS_FAULT & 1
         ctx.emit("group_strip", ctx.lib.fen_group_strip, byref(d))
         ctx.keep(d)
         return dict(blocks=blocks, x=x, x_last=x_last)
@@ -779,6 +785,7 @@ class Backward:
         nbytes = int(ctx.lib.fen_group_strip_bwd_work_bytes(B, H))
         work = ctx.persistent_zeros(f"group_strip_bwd/{B}x{H}", nbytes)
         d.work, d.work_bytes = ptr(work), nbytes
+        d.status, d.fault = L.strip_status_ptr(ctx.device), (GS_FAULT >> 1) & 1
         ctx.emit("group_strip_bwd", ctx.lib.fen_group_strip_bwd, byref(d))
         ctx.keep(d)
         wb = self.wb

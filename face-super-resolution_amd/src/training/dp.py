@@ -35,8 +35,31 @@ def init_rccl(device: torch.device, **kw) -> None:
     three runs of tests/test_gpu_rccl.py's captured GAN iteration).  Fresh events per
     collective cost microseconds, and only on eager steps: a replayed graph creates none."""
     import os
-    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    v = os.environ.get(EVENT_CACHE_VAR)
+    if v not in (None, "0"):
+        raise RuntimeError(f"{EVENT_CACHE_VAR}={v!r} is inherited from the environment; a captured DP "
+                           "step needs it off (ProcessGroupNCCL re-records cached events inside the "
+                           "capture). Unset it or set it to 0.")
+    os.environ[EVENT_CACHE_VAR] = "0"
     dist.init_process_group("nccl", device_id=device, **kw)
+
+
+EVENT_CACHE_VAR = "TORCH_NCCL_CUDA_EVENT_CACHE"
+
+
+def exchange_capturable(group=None) -> bool:
+    """Whether a collective on `group` may be recorded into a hipGraph: world size 1 (nothing
+    is exchanged), or RCCL with the event cache off (what `init_rccl` sets up).  gloo stages
+    CUDA tensors through the host, and a user's own `init_process_group('nccl')` with the
+    event cache on can abort the watchdog inside a capture (see `init_rccl`)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return True
+    return _rccl_capture_ok(group)
+
+
+def _rccl_capture_ok(group=None) -> bool:
+    import os
+    return dist.get_backend(group) == "nccl" and os.environ.get(EVENT_CACHE_VAR) == "0"
 
 
 def _group_of(name: str) -> str:
@@ -91,8 +114,9 @@ class BucketExchange:
         self.views = {tag: flat[lo:hi] for tag, lo, hi in plan}
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.active = self.world > 1 or force
-        # gloo stages CUDA tensors through the host (not stream-ordered): only RCCL captures
-        self.capturable = bool(flat.is_cuda) and (not self.active or dist.get_backend(group) == "nccl")
+        # gloo stages CUDA tensors through the host (not stream-ordered): only RCCL captures,
+        # and only with ProcessGroupNCCL's event cache off (init_rccl)
+        self.capturable = bool(flat.is_cuda) and (not self.active or _rccl_capture_ok(group))
         self.stream = torch.cuda.Stream(device=flat.device) if (self.active and flat.is_cuda) else None
         self.works: List = []
         self._forked = False

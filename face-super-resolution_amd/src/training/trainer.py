@@ -33,6 +33,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..hip.engine import FENEngine, flatten_params
+from ..hip.lib import check_strip_status
 from ..hip.program import Ctx, ptr
 from .dp import broadcast_arena
 from .optim import FusedAdamW, adamw_state, bump_versions, state_view
@@ -314,9 +315,16 @@ class Trainer:
         return loss.detach()
 
     def _capture_gan(self) -> bool:
-        """World size 1, or N > 1: the exchanges are stream-ordered (RCCL on side streams
-        forked and joined inside the captured iteration)."""
-        return bool(self.config.capture_gan_step) and torch.cuda.is_available() and self._accum() == 1
+        """World size 1, or N > 1 over RCCL with the event cache off (`dp.init_rccl`): the
+        exchanges are stream-ordered (RCCL on side streams forked and joined inside the captured
+        iteration).  gloo (host-staged) or a user's own `init_process_group('nccl')` with the
+        event cache on run the iteration eagerly."""
+        from .dp import _rccl_capture_ok
+        if not (bool(self.config.capture_gan_step) and torch.cuda.is_available() and self._accum() == 1):
+            return False
+        if self.world > 1 or getattr(self, "_dp_force", False):
+            return dist.is_available() and dist.is_initialized() and _rccl_capture_ok()
+        return True
 
     def _make_d_capturable(self) -> None:
         """The captured GAN iteration steps optimizer_d inside the graph: its param groups need
@@ -415,6 +423,7 @@ class Trainer:
             if update:
                 self.global_step += 1
             total += float(loss)  # per-step host sync, as trainer.py:508
+            check_strip_status()  # ... so a strip launch's timed-out wait raises at its own step
             n += 1
         if self.world > 1:
             t = torch.tensor([total, n], device=self.device, dtype=torch.float64)

@@ -263,7 +263,18 @@ typedef struct {
     float* sv_mean[FEN_GS_MAXNB];      /* the SE pool means [B][64]                            */
     float* sv_hid[FEN_GS_MAXNB];       /* ReLU(FC1(mean)) [B][Cr]  (s goes to s_out)           */
     void* x_last;                      /* the chain's output = the group conv's input          */
+    /* optional (NULL = off): where a timed-out hand-off wait is reported.  The launch's last
+     * block stores FEN_STATUS_GS_FWD there (a system-scope store: host-mapped pinned memory
+     * may be passed, read by the host without a sync) and clears the workspace's error word;
+     * the word is never cleared by the kernel -- the caller resets it after reading.  With
+     * status NULL the error word stays set in `work` (byte 8) instead.                        */
+    int* status;
+    int fault;                         /* test-only fault injection: nonzero = the block with
+                                          ticket 1 skips RCAB 0's a1 flag (its neighbour's wait
+                                          times out after ~1 s); 0 in production              */
 } fen_group_strip_desc;
+#define FEN_STATUS_GS_FWD 1            /* a fen_group_strip wait timed out (output invalid)     */
+#define FEN_STATUS_GS_BWD 2            /* a fen_group_strip_bwd wait timed out                  */
 int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
 size_t fen_group_strip_work_bytes(int B, int H);
 int fen_group_strip(const fen_group_strip_desc* d, void* stream);
@@ -347,6 +358,8 @@ typedef struct {
     float* dw2p[FEN_GS_MAXNB];         /* out: [B][64][Cr]                                     */
     void* work;
     size_t work_bytes;
+    int* status;                       /* as fen_group_strip_desc.status (FEN_STATUS_GS_BWD)   */
+    int fault;                         /* test-only: ticket 1 skips the first RCAB's dz1 flag  */
 } fen_group_strip_bwd_desc;
 int fen_group_strip_bwd_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
 size_t fen_group_strip_bwd_work_bytes(int B, int H);
@@ -520,6 +533,12 @@ int fen_s2d2(int dtype, int B, int H, int W, int C, const void* x, void* y, int 
  * zeros where no tap lands) and the OIHW gradient back from the phase-major one (gather = 1)  */
 int fen_s2d_filter(int Cout, int C, const float* src, float* dst, int gather, void* stream);
 int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const void* dy, void* out, void* stream);
+
+/* A status word for fen_group_strip / fen_group_strip_bwd `status`: one zeroed int in
+ * host-mapped, coherent pinned memory (hipHostMalloc, 64 B), allocated on the first call for
+ * the current device and kept for the process; *host is what the host reads (no sync needed),
+ * *dev what the kernels store to.  The only allocation the library makes.  0 or FEN_EHIP.  */
+int fen_status_word(void** host, void** dev);
 
 const char* fen_status_string(int code);
 /* hipGetErrorString() of the HIP error behind this thread's last FEN_EHIP, or "none". */

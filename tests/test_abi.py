@@ -87,6 +87,13 @@ def test_wgrad_multi_validation_without_gpu():
     arr[2].H = 64
     arr[3].x = None
     assert lib.fen_wgrad3x3_multi(4, p, None) == -1
+    arr[3].x = 16
+    # njobs x (Cout/64) x (Cin/64) > 256 even at one chunk per job: the launch geometry must
+    # terminate (one chunk per job, more than one wave of blocks) rather than spin on the host
+    for n, c in ((5, 512), (17, 256)):
+        for d in arr:
+            d.Cin = d.Cout = d.cout_valid = c
+        assert lib.fen_wgrad_multi_work_floats(n, p) == n * (c * c * 9 + c)
 
 
 def test_conv_dot_epilogue_validation_without_gpu():

@@ -67,6 +67,8 @@ def _run(q, n, x_nhwc, dtype, strip=True, record=False, ctx=None):
 
 
 def _work_error(ctx):
+    from src.hip import lib as L
+    L.check_strip_status()          # a timed-out wait is reported there (and cleared from `work`)
     bufs = [v for k, v in ctx._shared.items() if k.startswith("pz:group_strip")]
     assert bufs
     ints = [b[:256].view(torch.int32).cpu() for b in bufs]

@@ -100,6 +100,8 @@ def _oracle(q, n, x_nchw, dy_nchw, dtype, dres_nchw=None):
 
 
 def _work_error(ctx):
+    from src.hip import lib as L
+    L.check_strip_status()
     bufs = [v for k, v in ctx._shared.items() if k.startswith("pz:group_strip_bwd")]
     assert bufs
     ints = [b[:256].view(torch.int32).cpu() for b in bufs]

@@ -137,9 +137,16 @@ def test_data_sources(tmp_path):
     ds = SyntheticHRDataset(4, 32, seed=3)
     assert torch.equal(ds[1]["hr"], SyntheticHRDataset(4, 32, seed=3)[1]["hr"])
     assert ds[0]["hr"].shape == (3, 32, 32) and float(ds[0]["hr"].max()) <= 1.0
-    dl = get_dataloader(None, "train", batch_size=2, num_workers=0, hr_patch_size=32, synthetic=6)
+    dl = get_dataloader(None, "train", batch_size=2, num_workers=0, hr_patch_size=32, synthetic=6,
+                        color_jitter_prob=0.0, device="cpu")
     batches = list(dl)
     assert len(batches) == 3 and batches[0]["hr"].shape == (2, 3, 32, 32)
+    # colour jitter (the reference's default probability 0.3) runs on the GPU data path only:
+    # a source that cannot apply it raises instead of dropping it
+    with pytest.raises(ValueError, match="color_jitter"):
+        get_dataloader(None, "train", batch_size=2, num_workers=0, hr_patch_size=32, synthetic=6, device="cpu")
+    with pytest.raises(NotImplementedError):
+        get_dataloader(None, "train", batch_size=2, synthetic=6, return_filename=True)
     img = (np.arange(40 * 40 * 3) % 251).astype(np.uint8).reshape(40, 40, 3)
     for i in range(3):
         np.save(tmp_path / f"im{i}.npy", img)
@@ -148,10 +155,69 @@ def test_data_sources(tmp_path):
         get_dataloader(str(tmp_path / "missing"), "train", batch_size=2, num_workers=0, hr_patch_size=32)
     with pytest.raises(FileNotFoundError):
         get_dataloader(None, "val", batch_size=2, num_workers=0, hr_patch_size=32)
-    nd = NpyHRDataset(str(tmp_path), hr_patch_size=32)
+    # val / test: the full image, no augmentation (PairedTransform mode != 'train')
+    nd = NpyHRDataset(str(tmp_path), hr_patch_size=32, train=False)
     t = nd[0]["hr"]
-    assert t.shape == (3, 32, 32)
-    assert torch.allclose(t, torch.from_numpy(img[:32, :32]).permute(2, 0, 1).float() / 255.0)
+    assert t.shape == (3, 40, 40)
+    assert torch.allclose(t, torch.from_numpy(img).permute(2, 0, 1).float() / 255.0)
+    vl = get_dataloader(str(tmp_path), "val", batch_size=3, num_workers=0, device="cpu")
+    assert next(iter(vl))["hr"].shape == (3, 3, 40, 40)
+
+
+def test_train_transform_matches_reference_order(tmp_path):
+    """NpyHRDataset's train transform = PairedTransform.__call__ (transforms.py:188-216): a random
+    crop when the image is larger than the patch, then flip (p), then rot90 (p, k in 1..3), the
+    draws in that order from one generator -- restated here with numpy on the HWC array."""
+    from src.data import NpyHRDataset
+    r = np.random.default_rng(0)
+    imgs = [r.integers(0, 256, (48, 40, 3), dtype=np.uint8) for _ in range(4)]
+    for i, a in enumerate(imgs):
+        np.save(tmp_path / f"im{i}.npy", a)
+    ds = NpyHRDataset(str(tmp_path), hr_patch_size=32, horizontal_flip=0.5, random_rotate90=0.7, seed=5)
+    ref_rng = np.random.default_rng(5)
+    seen_flip = seen_rot = False
+    for rep in range(6):
+        for i, a in enumerate(imgs):
+            top = int(ref_rng.integers(0, 48 - 32 + 1))
+            left = int(ref_rng.integers(0, 40 - 32 + 1))
+            h = a[top:top + 32, left:left + 32]
+            if ref_rng.random() < 0.5:
+                h = np.fliplr(h)
+                seen_flip = True
+            if ref_rng.random() < 0.7:
+                h = np.rot90(h, int(ref_rng.integers(1, 4)))
+                seen_rot = True
+            want = torch.from_numpy(np.ascontiguousarray(h)).permute(2, 0, 1).float() / 255.0
+            assert torch.equal(ds[i]["hr"], want), (rep, i)
+    assert seen_flip and seen_rot
+
+
+def test_train_cli_passes_augmentation_to_loader(monkeypatch):
+    """scripts/train.py hands the YAML's augmentation block to the loader with the reference CLI's
+    defaults (scripts/train.py:174-191); an augmentation key it does not read is refused."""
+    ts = _train_script()
+    calls = []
+    monkeypatch.setattr(ts, "get_dataloader", lambda *a, **k: calls.append((a, k)) or object())
+    cfg = {"data": {"num_workers": 3}, "project": {"seed": 7},
+           "augmentation": {"horizontal_flip": 0.25, "random_rotate90": 0.5,
+                            "random_crop": {"hr_patch_size": 256, "lr_patch_size": 64},
+                            "color_jitter": {"probability": 0.4, "brightness": 0.2, "contrast": 0.15,
+                                             "saturation": 0.05, "hue": 0.02}}}
+    ts.build_loaders(cfg, "/data", 32)
+    (ta, tk), (va, vk) = calls
+    assert ta == ("/data", "train", 32, 3) and va == ("/data", "val", 32, 3)
+    for k, v in dict(hr_patch_size=256, horizontal_flip=0.25, random_rotate90=0.5, color_jitter_prob=0.4,
+                     brightness=0.2, contrast=0.15, saturation=0.05, hue=0.02, seed=7).items():
+        assert tk[k] == v, k
+    assert "color_jitter_prob" not in vk          # val: FFHQDataset's defaults, mode 'val' (no augmentation)
+    calls.clear()
+    ts.build_loaders({"augmentation": {"random_crop": {"hr_patch_size": 256}}}, "/data", 16)
+    tk = calls[0][1]
+    assert (tk["horizontal_flip"], tk["random_rotate90"], tk["color_jitter_prob"], tk["brightness"],
+            tk["contrast"], tk["saturation"]) == (0.5, 0.0, 0.3, 0.1, 0.1, 0.0)
+    assert ts.train_loader_kwargs({})["hr_patch_size"] == 128
+    with pytest.raises(ValueError, match="vertical_flip"):
+        ts.train_loader_kwargs({"augmentation": {"vertical_flip": 0.5}})
 
 
 def test_early_stopping_semantics():
