@@ -473,13 +473,14 @@ def main():
             peng = FENEngine(pm, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=True, device="cuda",
                              perceptual=spec)
             peng.hr.copy_(hr_t)
-            fn, _ = captured_or_eager(peng, world)
+            fn, ppath = captured_or_eager(peng, world)
             tp = timed(fn, args.train_steps, 3, world)
             out["train_perceptual"] = {
                 "metric": "training images/sec (stage-1 step: L1 + VGG19 conv3_4 perceptual) at batch 32/GPU",
                 "value": round(B * world * args.train_steps / tp, 2),
                 "ms_per_step": round(1000.0 * tp / args.train_steps, 3), "steps": args.train_steps,
-                "loss": float(peng.total_loss()), "vgg": "random-init VGG19 (no ImageNet weights offline)"}
+                "loss": float(peng.total_loss()), "vgg": "random-init VGG19 (no ImageNet weights offline)",
+                "path": ppath}
             del peng
             torch.cuda.empty_cache()
             # stage 2 (stage2_ssim_config.yaml:40-50): L1 x 1 + perceptual x 0.5 + (1 - SSIM) x 0.2
@@ -489,17 +490,13 @@ def main():
             seng = FENEngine(sm, batch=B, lr_hw=(64, 64), dtype=torch.bfloat16, train=True, device="cuda",
                              perceptual=spec2, ssim_weight=0.2)
             seng.hr.copy_(hr_t)
-            if world == 1:
-                seng.capture()
-                fn = seng.replay
-            else:
-                fn = seng.step
+            fn, spath = captured_or_eager(seng, world)
             ts = timed(fn, args.train_steps, 3, world)
             out["train_stage2"] = {
                 "metric": "training images/sec (stage-2 step: L1 + 0.5 perceptual + 0.2 (1 - SSIM)) at batch 32/GPU",
                 "value": round(B * world * args.train_steps / ts, 2),
                 "ms_per_step": round(1000.0 * ts / args.train_steps, 3), "steps": args.train_steps,
-                "loss": float(seng.total_loss())}
+                "loss": float(seng.total_loss()), "path": spath}
             if world == 1:
                 out["aux"] = {"ssim_loss_grad": time_ssim(seng)}
             del seng
@@ -522,6 +519,11 @@ def main():
         out["psnr_parity"] = dict(pp[prec], images=B, target="HR (smooth synthetic, uint8 levels)",
                                   ref="CPU oracle fp32 (pinned to the reference, tests/test_oracle.py)",
                                   tolerance_db=0.01, **{other: pp[other]})
+    # every strip launch of the timed regions reported through the status word: a timed-out
+    # hand-off wait (invalid outputs) fails the run here instead of passing as a number
+    from src.hip import lib as L
+    torch.cuda.synchronize()
+    L.check_strip_status()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
