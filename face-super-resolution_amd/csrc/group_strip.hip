@@ -106,7 +106,7 @@ struct GsArgs {
     const float* fc2[FEN_GS_MAXNB];           // [64][Cr]
     float* s_out[FEN_GS_MAXNB];               // optional gates s [B][64] (attention maps)
     char* work;
-    int save;                                 // training: the backward's operands out
+    int save;                                 // training: the backward's operands out (SAVE)
     void* sv_x[FEN_GS_MAXNB];
     void* sv_z1[FEN_GS_MAXNB];
     void* sv_a1[FEN_GS_MAXNB];
@@ -118,7 +118,7 @@ struct GsArgs {
     int fault;                                // test-only: image 0 strip 1 skips one a1 flag
 };
 
-template <typename T>
+template <typename T, bool SAVE>
 __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* img = smem + O_IMG;
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         }
         // x_j's boundary rows for the neighbours (their halo rows of x_{j+1})
         if (!gc && bwave) store_row(wsr, rowoff(L.bx, strip, par, side), xr, 16);
-        if (A.save && j > 0) save_row(gc ? A.x_last : A.sv_x[j], xr);   // x_0 is the group input
+        if (SAVE && j > 0) save_row(gc ? A.x_last : A.sv_x[j], xr);   // x_0 is the group input
         if (j > 0 && hwave) {
             // the neighbour's x_{j-1}, t_{j-1} rows (this wave's half), after its flag (its
             // storing wave drained them, then signalled): this wave polls and loads (row 1);
@@ -419,24 +419,13 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             store_row(yrs, (int)((size_t)(im * H + r0 + wave) * SW * 128), ov, 0);
             break;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's pieces of conv2's kh = 1 taps
-        __syncthreads();                                    // B_E: x_j's reads done (all slots free); those taps visible
-        issue_kh02(ci + 1);
         // ---- conv1 epilogue: a1 = PReLU(conv1 + b1) -> LDS (own row), boundary rows out; the
-        // row's per-channel sums of a1 (fp32, before the 16-bit rounding conv2 reads) -> red[wave]
-        if (A.save) {                                       // z1 = conv1 + b1 (PReLU's input)
-            uint2 zv[4][4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const float4 bb = *(const float4*)(cst + 16 * m + 4 * q);
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    zv[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
-            }
-            save_row(A.sv_z1[j], zv);
-        }
-        {
-            uint2 av[4][4];
+        // row's per-channel sums of a1 (fp32, before the 16-bit rounding conv2 reads) -> red[wave].
+        // It runs BEFORE the barrier B_E (only the LDS write of the a1 row must wait for every
+        // wave's conv1 reads of x_j): a wave that finished its phases early computes its epilogue
+        // while its SIMD partner still issues MFMAs, instead of idling at B_E (GS_LATE_EPI: after)
+        uint2 av[4][4];
+        auto a1_epilogue = [&]() {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const float4 bb = *(const float4*)(cst + 16 * m + 4 * q);
@@ -458,10 +447,31 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                     if (c16 == 0) red[wave * 64 + 16 * m + 4 * q + i] = s;
                 }
             }
-            write_row_lds(wave + 1, av);
-            if (bwave) store_row(wsr, rowoff(L.ba, strip, par, side), av, 16);
-            if (A.save) save_row(A.sv_a1[j], av);
+        };
+#ifndef GS_LATE_EPI
+        constexpr bool early = true;
+#else
+        constexpr bool early = false;
+#endif
+        if (early) a1_epilogue();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's pieces of conv2's kh = 1 taps
+        __syncthreads();                                    // B_E: x_j's reads done (all slots free); those taps visible
+        issue_kh02(ci + 1);
+        if (SAVE) {                                         // z1 = conv1 + b1 (PReLU's input)
+            uint2 zv[4][4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float4 bb = *(const float4*)(cst + 16 * m + 4 * q);
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    zv[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
+            }
+            save_row(A.sv_z1[j], zv);
         }
+        if (!early) a1_epilogue();
+        write_row_lds(wave + 1, av);
+        if (bwave) store_row(wsr, rowoff(L.ba, strip, par, side), av, 16);
+        if (SAVE) save_row(A.sv_a1[j], av);
         // ================= conv2 =================
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -568,7 +578,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 tr[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
         }
         if (bwave) store_row(wsr, rowoff(L.bt, strip, par, side), tr, 16);   // t_j's boundary row
-        if (A.save) save_row(A.sv_t[j], tr);
+        if (SAVE) save_row(A.sv_t[j], tr);
         if (wave == 1) {
             // the gate of RCAB j (blocks.py:83-92): mean over the image from the S strip
             // partials, each an 8-B {tag, value} granule (the data is the flag: sc1 loads
@@ -637,7 +647,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             const float sg = 1.f / (1.f + expf(-z));
             gate[lane] = sg * A.res_scale;
             if (strip == 0 && A.s_out[j]) A.s_out[j][im * 64 + lane] = sg;
-            if (strip == 0 && A.save) {
+            if (strip == 0 && SAVE) {
                 A.sv_mean[j][im * 64 + lane] = mean;
                 if (lane < Cr) A.sv_hid[j][im * Cr + lane] = hid;
             }
@@ -681,14 +691,15 @@ int gs_num_cus() {
     return g_gs_cus;
 }
 
-template <typename T>
+template <typename T, bool SAVE>
 void launch_gs(const GsArgs& a, int grid, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_group_strip<T>, hipFuncAttributeMaxDynamicSharedMemorySize, GS_LDS);
+        (void)hipFuncSetAttribute((const void*)k_group_strip<T, SAVE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  GS_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL(k_group_strip<T>, dim3(grid), dim3(512), GS_LDS, s, a);
+    hipLaunchKernelGGL((k_group_strip<T, SAVE>), dim3(grid), dim3(512), GS_LDS, s, a);
 }
 
 }  // namespace
@@ -737,8 +748,13 @@ extern "C" int fen_group_strip(const fen_group_strip_desc* d, void* stream) {
     const int grid = d->B * (d->H / SR);
     (void)gs_num_cus();
     hipStream_t s = (hipStream_t)stream;
-    if (d->dtype == FEN_F16) launch_gs<f16>(a, grid, s);
-    else launch_gs<bf16>(a, grid, s);
+    if (d->dtype == FEN_F16) {
+        if (a.save) launch_gs<f16, true>(a, grid, s);
+        else launch_gs<f16, false>(a, grid, s);
+    } else {
+        if (a.save) launch_gs<bf16, true>(a, grid, s);
+        else launch_gs<bf16, false>(a, grid, s);
+    }
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

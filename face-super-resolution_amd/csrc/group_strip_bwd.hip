@@ -322,12 +322,15 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
             conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();                                // B_E: dt's reads done (all slots free); taps visible
-            issue_kh02(ci + 1);
             // ---- dz1 = conv2^T(dt) * PReLU'(z1) -> LDS (own row), boundary row out, HBM; the
-            // row's dalpha partials sum conv2^T(dt) * z1 * [z1 <= 0] (blocks.py:146's PReLU)
+            // row's dalpha partials sum conv2^T(dt) * z1 * [z1 <= 0] (blocks.py:146's PReLU).
+            // Computed before B_E (only the LDS write must wait for every wave's dt reads): a wave
+            // done with its phases works while its SIMD partner still issues MFMAs
+#ifdef GSB_LATE_EPI
+            __syncthreads();                                // A/B variant: the epilogue after every wave's conv
+#endif
+            uint2 zd[4][4];
             {
-                uint2 zd[4][4];
                 float* dal = A.dal[jr];
                 asm volatile("" : "+s"(dal));
 #pragma unroll
@@ -354,10 +357,12 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                         *(float4*)(dal + (size_t)(im * H + r0 + wave) * 64 + 16 * m + 4 * q) =
                             make_float4(sv[0], sv[1], sv[2], sv[3]);
                 }
-                write_row_lds(wave + 1, zd);
-                if (bwave) store_row(wsr, rowoff(L.bz, strip, par, side), zd, 16);
-                save_row(A.dz1[jr], zd);
             }
+            __syncthreads();                                // B_E: dt's reads done (all slots free); taps visible
+            issue_kh02(ci + 1);
+            write_row_lds(wave + 1, zd);
+            if (bwave) store_row(wsr, rowoff(L.bz, strip, par, side), zd, 16);
+            save_row(A.dz1[jr], zd);
             // ================= conv1^T =================
 #pragma unroll
             for (int m = 0; m < 4; ++m)

@@ -13,9 +13,13 @@ clip 0.5, trainer.py:458-503).  Checks, through the graph engine FENEngine(train
     parameters max |d| <= 2e-5 (|update| ~ lr = 1e-4 per element).  The reference's own fp32
     gradients sit within 2.5e-5 rel of its float64 run (gerr64 in the golden).
   * B=32 (the golden's 2 images tiled 16x, the bench's batch): the mean-L1 gradient is the
-    B=2 one.  fp32 at the same bounds; bf16 -- the production kernels (the deferred RCAB's
-    training form, the SE-folded fused RCAB backward, the group end, the batched weight
-    gradients) at 2-3 tiles per block -- at the bf16 whole-network bound below.
+    B=2 one.  fp32 at the same bounds (the per-op / deferred-RCAB kernels: the strip kernels are
+    16-bit only); bf16 -- the production kernels: each ResidualGroup's forward as one
+    fen_group_strip launch (training form, saving the backward's operands), its backward as one
+    fen_group_strip_bwd launch, the batched weight gradients -- at the bf16 whole-network bound
+    below, and (test_train64_bf16_strip_vs_per_rcab) against the per-RCAB bf16 path (the
+    deferred RCAB's training form, the SE-folded fused RCAB backward, the group end) on the same
+    step at per-tensor bounds near their measured gap.
 """
 import numpy as np
 import pytest
@@ -146,3 +150,45 @@ def test_train64_bf16_batch32(g10):
     worst = max(float(np.abs(p.detach().cpu().numpy() - want[k]).max()) for k, p in m.named_parameters())
     print(f"bf16 step vs the float64 replay of clip + AdamW on its gradients: max |d| {worst:.2e}")
     assert worst <= 2e-6, worst
+
+
+def _bf16_grads_with(g, strip):
+    from src.hip import net
+    old = net.GROUP_STRIP_TRAIN, net.GROUP_STRIP_BWD
+    net.GROUP_STRIP_TRAIN = net.GROUP_STRIP_BWD = strip
+    try:
+        m, eng = _engine(g, 32, torch.bfloat16)
+        ops = [op[0] for op in eng.ctx.ops]
+        assert ("group_strip" in ops and "group_strip_bwd" in ops) == strip, ops[:8]
+        grads = _grads(eng)
+        return float(eng.loss), grads
+    finally:
+        net.GROUP_STRIP_TRAIN, net.GROUP_STRIP_BWD = old
+
+
+def test_train64_bf16_strip_vs_per_rcab(g10):
+    """The bench's bf16 B=32 step on the strip kernels against the same step on the per-RCAB
+    bf16 kernels (both round the same tensors to bf16 at the same points; the strip kernels sum
+    the SE pools and gradients over strips instead of 16x16 tiles).  Per tensor: rel-L2 <= 2e-2
+    for every gradient, and the whole arena <= 5e-3 (a wrong halo row, gate, slope or SE row in
+    either would be O(1) on its tensors); the measured gap is printed."""
+    ls, gs = _bf16_grads_with(g10, True)
+    lr_, gr = _bf16_grads_with(g10, False)
+    assert abs(ls - lr_) <= 1e-4 * abs(lr_), (ls, lr_)
+    num = den = 0.0
+    worst, wk, bad = 0.0, None, {}
+    for k, a in gs.items():
+        b = gr[k].double()
+        d = float((a.double() - b).norm())
+        n = float(b.norm())
+        num += d * d
+        den += n * n
+        e = d / max(n, 1e-30)
+        if e > worst:
+            worst, wk = e, k
+        if not e <= 2e-2:
+            bad[k] = e
+    whole = (num / den) ** 0.5
+    print(f"strip vs per-RCAB bf16 B=32: whole {whole:.2e}, worst {worst:.2e} ({wk})")
+    assert whole <= 5e-3, whole
+    assert not bad, dict(list(bad.items())[:10])
