@@ -40,7 +40,10 @@ __device__ __forceinline__ void hrow(const SsimWin& win, const float* p, const f
     }
 }
 
-template <bool GRAD, typename T>
+// CB > 1 (grad_mode 2, C <= CB): one block takes every channel of its tile in turn and adds the
+// gradients to the NHWC16 buffer once, 4 channels per 8-B (16-bit) / 16-B (fp32) read-modify-
+// write per pixel, instead of C blocks each rewriting one 2-byte channel of every pixel row.
+template <bool GRAD, typename T, int CB>
 __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const float* __restrict__ pred,
                                               const float* __restrict__ target, const SsimWin win, float C1,
                                               float C2, float* __restrict__ part, void* __restrict__ grad,
@@ -61,11 +64,22 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     float* st = sb + E2 * PS;
     float (*abc)[E1][E1 + 1] = (float (*)[E1][E1 + 1])sb;
     const int tid = threadIdx.x;
-    const int plane = blockIdx.z, b = plane / C, ch = plane % C;
     const int h0 = blockIdx.y * ST, w0 = blockIdx.x * ST;
     const int gy0 = h0 - O1 - SR, gx0 = w0 - O1 - SR;     // image coords of E2's (0, 0)
+    const int b = CB > 1 ? (int)blockIdx.z : (int)blockIdx.z / C;
+    float dacc[CB][CW2];                                  // CB > 1: this thread's gradients, per channel
+#pragma unroll
+    for (int k = 0; k < CB; ++k)
+#pragma unroll
+        for (int o = 0; o < CW2; ++o) dacc[k][o] = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < CB; ++cc) {
+    if (CB > 1 && cc >= C) break;
+    const int ch = CB > 1 ? cc : (int)blockIdx.z % C;
+    const int plane = b * C + ch;
     const float* pp = pred + (size_t)plane * H * W;
     const float* tp = target + (size_t)plane * H * W;
+    if (CB > 1 && cc > 0) __syncthreads();                // the previous channel's reads of sb / hp / red done
     for (int i = tid; i < E2 * E2; i += 256) {
         const int r = i / E2, c = i % E2, gy = gy0 + r, gx = gx0 + c;
         const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
@@ -174,7 +188,9 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
                 const size_t e = (size_t)gy * W + gx;
                 const float p = pp[e], t = tp[e];                // L2-hot: this block staged them
                 const float d = grad_scale * (m[0][o] + 2.f * p * m[1][o] + t * m[2][o]);
-                if (grad_mode == 1) {
+                if constexpr (CB > 1) {
+                    dacc[cc][o] = d;
+                } else if (grad_mode == 1) {
                     ((float*)grad)[(size_t)plane * H * W + e] = d;
                 } else {
                     T* q = (T*)grad + (((size_t)b * H + gy) * W + gx) * 16 + ch;
@@ -192,6 +208,36 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     if (tid == 0) {
         const int ntile = gridDim.x * gridDim.y;
         part[((size_t)ch * ntile + blockIdx.y * gridDim.x + blockIdx.x) * B + b] = red[0];
+    }
+    }   // channels
+    if constexpr (GRAD && CB > 1) {
+        // channels 0..3 of each pixel in one read-modify-write (channels >= C written back as read)
+        for (int i = tid; i < ST * NCH2; i += 256) {
+            const int c = i % ST, r0 = (i / ST) * CW2, gx = w0 + c;
+            if (gx >= W) continue;
+#pragma unroll
+            for (int o = 0; o < CW2; ++o) {
+                const int gy = h0 + r0 + o;
+                if (gy >= H) break;
+                T* q = (T*)grad + (((size_t)b * H + gy) * W + gx) * 16;
+                if constexpr (sizeof(T) == 2) {
+                    uint2 u = *(const uint2*)q;
+                    const T* v = (const T*)&u;
+                    T w4[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+                    for (int k = 0; k < CB && k < 4; ++k)
+                        if (k < C) w4[k] = fromf<T>(tof<T>(w4[k]) + dacc[k][o]);
+                    *(uint2*)q = *(const uint2*)w4;
+                } else {
+                    float4 u = *(const float4*)q;
+                    float* v = (float*)&u;
+#pragma unroll
+                    for (int k = 0; k < CB && k < 4; ++k)
+                        if (k < C) v[k] += dacc[k][o];
+                    *(float4*)q = u;
+                }
+            }
+        }
     }
 }
 
@@ -212,14 +258,25 @@ extern "C" int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred
     SsimWin w;
     for (int j = 0; j < 2 * SR + 1; ++j) w.g[j] = window1d[j];
     const dim3 grid((W + ST - 1) / ST, (H + ST - 1) / ST, B * C);
+    const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);      // CB: channels looped in the block
     if (grad_mode == 0) {
-        hipLaunchKernelGGL((k_ssim<false, float>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
+        hipLaunchKernelGGL((k_ssim<false, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
                            part, nullptr, 0.f, 0);
-    } else if (grad_mode == 1 || dtype == FEN_F32) {
-        hipLaunchKernelGGL((k_ssim<true, float>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
+    } else if (grad_mode == 1) {
+        hipLaunchKernelGGL((k_ssim<true, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
+                           part, grad, grad_scale, grad_mode);
+    } else if (C <= 3 && (dtype == FEN_F32 || dtype == FEN_BF16)) {
+        if (dtype == FEN_F32)
+            hipLaunchKernelGGL((k_ssim<true, float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
+                               C2, part, grad, grad_scale, grad_mode);
+        else
+            hipLaunchKernelGGL((k_ssim<true, bf16, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
+                               C2, part, grad, grad_scale, grad_mode);
+    } else if (dtype == FEN_F32) {
+        hipLaunchKernelGGL((k_ssim<true, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
                            part, grad, grad_scale, grad_mode);
     } else if (dtype == FEN_BF16) {
-        hipLaunchKernelGGL((k_ssim<true, bf16>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
+        hipLaunchKernelGGL((k_ssim<true, bf16, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
                            part, grad, grad_scale, grad_mode);
     } else {
         return FEN_EINVAL;

@@ -3,7 +3,7 @@
 # then (DPOV=1) the DP exchange overlap measurement
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_gpu_group_strip.py tests/test_gpu_group_strip_bwd.py tests/test_gpu_strip_status.py -m gpu -v -s -x --timeout 200 --timeout-method thread > gpurun_out/ab_tests.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_group_strip.py tests/test_gpu_group_strip_bwd.py tests/test_gpu_strip_status.py tests/test_gpu_ssim.py -m gpu -v -s -x --timeout 200 --timeout-method thread > gpurun_out/ab_tests.log 2>&1
 rc=$?; echo "strip tests rc=$rc"; grep -E "passed|failed|Error" gpurun_out/ab_tests.log | tail -4
 [ $rc -eq 0 ] || { tail -30 gpurun_out/ab_tests.log; exit 1; }
 libs="face-super-resolution_amd/src/hip/libfen_hip.so $(ls face-super-resolution_amd/csrc/build_var/libfen_hip_*.so 2>/dev/null)"
@@ -22,6 +22,7 @@ PY
     echo "   $(tail -1 gpurun_out/ab_t.log)"
   done
 done
+timeout -k 10 120 python tools/bench_ssim.py 2>&1 | grep -v amdgpu.ids | tail -3
 if [ "${DPOV:-0}" = "1" ]; then
   timeout -k 10 400 python tools/dp_overlap.py > gpurun_out/dp_overlap.json 2> gpurun_out/dp_overlap.log
   rc=$?; grep -v amdgpu.ids gpurun_out/dp_overlap.log | tail -8; cat gpurun_out/dp_overlap.json; exit $rc
