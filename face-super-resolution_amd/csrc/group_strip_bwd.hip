@@ -37,7 +37,24 @@ constexpr int O_RED = O_FILT + 9 * TAPB;      // [8 waves][64] f32 row partials 
 constexpr int O_CST = O_RED + 8 * 64 * 4;     // alpha [64] of the running RCAB
 constexpr int O_GATE = O_CST + 64 * 4;        // rs * s [64], g [64] of the running RCAB
 constexpr int O_SCR = O_GATE + 128 * 4;       // SE backward scratch [64], ticket words
+#ifdef FEN_GS_STAMPS
+// diagnostic build only (`make gsstamp`, tools/stamp_strip_bwd.py): s_memrealtime stamps of every
+// wave in LDS, copied to the workspace's tail at the end; no stamp executes in the product build
+constexpr int NSTAMP = 136;
+constexpr int O_STAMP = O_SCR + 80 * 4;
+constexpr int GSB_LDS = O_STAMP + 8 * NSTAMP * 2;
+#define GSTAMP(i)                                                                              \
+    do {                                                                                       \
+        unsigned long long _rt;                                                                \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_rt)::"memory");        \
+        if (lane == 0 && (i) < NSTAMP) stamp_lds[wave * NSTAMP + (i)] = (unsigned short)((unsigned)_rt - t_start); \
+    } while (0)
+#else
 constexpr int GSB_LDS = O_SCR + 80 * 4;
+#define GSTAMP(i) \
+    do {          \
+    } while (0)
+#endif
 static_assert(GSB_LDS <= 163840, "LDS budget");
 static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignment");
 
@@ -54,6 +71,9 @@ __host__ __device__ inline WsB wsb_layout(int B, int S) {
     const size_t rows = (size_t)B * S * 2 * 2 * ROWB;   // [img][strip][parity][side] rows
     L.bd = o; o += rows;
     L.bz = o; o += rows;
+#ifdef FEN_GS_STAMPS
+    o += (size_t)B * S * 8 * NSTAMP * 2;            // [block ticket][wave][NSTAMP] u16 (10 ns ticks)
+#endif
     L.total = o;
     return L;
 }
@@ -94,6 +114,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
     float* gate = (float*)(smem + O_GATE);
     float* scr = (float*)(smem + O_SCR);
     int* tick_lds = (int*)(scr + 64);
+#ifdef FEN_GS_STAMPS
+    unsigned short* stamp_lds = (unsigned short*)(smem + O_STAMP);
+#endif
 
     const int tid = threadIdx.x;
     int lane = tid & 63;
@@ -107,11 +130,20 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
     if (tid == 0) {
         tick_lds[0] = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tick_lds[1] = __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef FEN_GS_STAMPS
+        unsigned long long t0;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+        tick_lds[2] = (int)(unsigned)t0;
+#endif
     }
     for (int i = tid; i < IMG_BYTES / 16; i += 512) *(uint4*)(img + i * 16) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     const int ticket = __builtin_amdgcn_readfirstlane(tick_lds[0]);
     const unsigned epoch = (unsigned)__builtin_amdgcn_readfirstlane(tick_lds[1]);
+#ifdef FEN_GS_STAMPS
+    const unsigned t_start = (unsigned)__builtin_amdgcn_readfirstlane(tick_lds[2]);   // the block's clock origin
+#endif
+    GSTAMP(0);
     auto tag_of = [&](int k) -> unsigned { return (epoch << 8) | (unsigned)(k + 1); };
     int im = ticket / S, strip = ticket - im * S;
     int r0 = strip * SR;
@@ -244,6 +276,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
     for (int k = 0; k <= NB; ++k) {
         const int jr = NB - k;                              // k >= 1: this step's RCAB
         const int par = k & 1;
+        const int sb = 2 + 12 * k;                          // this step's stamp slots
+        GSTAMP(sb);
         {
             int ll = lane;
             asm volatile("" : "+v"(ll), "+s"(im), "+s"(strip), "+s"(S), "+s"(r0));
@@ -295,7 +329,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             }
             // ================= conv2^T =================
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            GSTAMP(sb + 1);
             conv_phase<T>(acc, img, filt, 1, wave, q, c16);
+            GSTAMP(sb + 2);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this conv's taps; the halo rows
             if (hwave) {                                    // its half of dt's halo row, same arithmetic
                 const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
@@ -316,11 +352,13 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
             __syncthreads();                                // B_X: dt's image complete; kh = 1 slots free
+            GSTAMP(sb + 3);
             issue_kh1(ci + 1);                              // conv1^T's kh = 1 taps
             uint2 zv[4][4];
             load_acc(A.z1[jr], zv);                         // PReLU's input, for the epilogue
             conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
             conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
+            GSTAMP(sb + 4);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             // ---- dz1 = conv2^T(dt) * PReLU'(z1) -> LDS (own row), boundary row out, HBM; the
             // row's dalpha partials sum conv2^T(dt) * z1 * [z1 <= 0] (blocks.py:146's PReLU).
@@ -358,7 +396,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                             make_float4(sv[0], sv[1], sv[2], sv[3]);
                 }
             }
+            GSTAMP(sb + 5);
             __syncthreads();                                // B_E: dt's reads done (all slots free); taps visible
+            GSTAMP(sb + 6);
             issue_kh02(ci + 1);
             write_row_lds(wave + 1, zd);
             if (bwave) store_row(wsr, rowoff(L.bz, strip, par, side), zd, 16);
@@ -369,7 +409,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
 #pragma unroll
                 for (int p = 0; p < 4; ++p) acc[m][p] = zero4();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            GSTAMP(sb + 7);
             conv_phase<T>(acc, img, filt, 1, wave, q, c16);     // own dz1 row only: no barrier
+            GSTAMP(sb + 8);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv1^T's other taps; the dz1 boundary stores
             if (bwave && lane == 0 && !(A.fault && ticket == 1 && k == 1 && side == 0))
                 __hip_atomic_store(flag_of(strip, side, 0), tag_of(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -387,6 +429,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
             conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
+            GSTAMP(sb + 9);
         }
         if (k > 0 && jr == 0) {
             // ---- the group input's gradient: d + conv1^T(dz1) + dy (the group's skip) (+ dres)
@@ -452,6 +495,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 1), tag_of(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GSTAMP(sb + 10);
         __syncthreads();                                    // B_Z: the row sums in red; conv reads done (all slots free)
         if (wave == 3) {
             // the strip's partial as {tag, value} granules (one 8-B sc1 store each), rows in order
@@ -550,13 +594,22 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GSTAMP(sb + 11);
         __syncthreads();                                    // B_G: the next RCAB's rs * s and g in LDS
     }
+    GSTAMP(NSTAMP - 1);
     // ---- the last block out advances the epoch and resets the ticket counters for the next launch
     if (!ok) __hip_atomic_fetch_or(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) strip_finish(ctl, B * S, A.status, FEN_STATUS_GS_BWD);
+#ifdef FEN_GS_STAMPS
+    __syncthreads();
+    {
+        unsigned short* dst = (unsigned short*)(A.work + L.bz + (size_t)B * S * 2 * 2 * ROWB) + (size_t)ticket * 8 * NSTAMP;
+        for (int i = tid; i < 8 * NSTAMP; i += 512) dst[i] = stamp_lds[i];
+    }
+#endif
 }
 
 template <typename T>

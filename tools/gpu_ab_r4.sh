@@ -23,6 +23,10 @@ PY
   done
 done
 timeout -k 10 120 python tools/bench_ssim.py 2>&1 | grep -v amdgpu.ids | tail -3
+if [ "${STAMPS:-0}" = "1" ] && [ -f face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so ]; then
+  FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so timeout -k 10 200 python tools/stamp_strip.py 2>&1 | grep -v amdgpu.ids
+  FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so timeout -k 10 200 python tools/stamp_strip_bwd.py 2>&1 | grep -v amdgpu.ids
+fi
 if [ "${DPOV:-0}" = "1" ]; then
   timeout -k 10 400 python tools/dp_overlap.py > gpurun_out/dp_overlap.json 2> gpurun_out/dp_overlap.log
   rc=$?; grep -v amdgpu.ids gpurun_out/dp_overlap.log | tail -8; cat gpurun_out/dp_overlap.json; exit $rc
