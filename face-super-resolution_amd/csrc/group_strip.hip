@@ -72,6 +72,17 @@ static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignmen
     } while (0)
 #endif
 
+// Training (SAVE): a wave's save stores (the backward's operands, 8 buffer stores per row) are
+// issued LAST before a wait that only needs the older hand-off traffic (tap DMA, boundary-row
+// stores and loads), and that wait leaves them in flight -- s_waitcnt vmcnt(8 per saved row)
+// instead of vmcnt(0): vector-memory ops retire in issue order.  A compiler barrier keeps the
+// saves behind the older ops.  GS_DRAIN_ALL restores the full drains (A/B).
+#ifdef GS_DRAIN_ALL
+#define GS_VMCNT_SAVES(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define GS_VMCNT_SAVES(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#endif
+
 // workspace: control words, counters, pool partials, boundary rows
 struct Ws {
     size_t cnt, flg, part, bx, bt, ba, total;
@@ -338,7 +349,6 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         }
         // x_j's boundary rows for the neighbours (their halo rows of x_{j+1})
         if (!gc && bwave) store_row(wsr, rowoff(L.bx, strip, par, side), xr, 16);
-        if (SAVE && j > 0) save_row(gc ? A.x_last : A.sv_x[j], xr);   // x_0 is the group input
         if (j > 0 && hwave) {
             // the neighbour's x_{j-1}, t_{j-1} rows (this wave's half), after its flag (its
             // storing wave drained them, then signalled): this wave polls and loads (row 1);
@@ -354,6 +364,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + k * 1024, 0, 16));
             }
         }
+        if (SAVE && j > 0) {                                // x_0 is the group input
+            asm volatile("" ::: "memory");                  // the saves after every op the wait below needs
+            save_row(gc ? A.x_last : A.sv_x[j], xr);
+        }
 
         // ================= conv1 (or the group conv): 3 phases =================
         f32x4 acc[4][4];                                    // conv1 (group conv), then conv2
@@ -368,7 +382,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         GSTAMP(sb + 1);
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);
         GSTAMP(sb + 2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this conv's taps; the halo rows
+        if (SAVE && j > 0) GS_VMCNT_SAVES(8);                 // this conv's taps; the halo rows (x_j's save in flight)
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (j > 0 && hwave) {                               // its half of x_j's halo row, same arithmetic
             const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
             const float4 gb = *(const float4*)(gate + (lane & 7) * 8 + 4);
@@ -457,8 +472,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's pieces of conv2's kh = 1 taps
         __syncthreads();                                    // B_E: x_j's reads done (all slots free); those taps visible
         issue_kh02(ci + 1);
+        uint2 zv[4][4];
         if (SAVE) {                                         // z1 = conv1 + b1 (PReLU's input)
-            uint2 zv[4][4];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const float4 bb = *(const float4*)(cst + 16 * m + 4 * q);
@@ -466,12 +481,15 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 for (int p = 0; p < 4; ++p)
                     zv[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
             }
-            save_row(A.sv_z1[j], zv);
         }
         if (!early) a1_epilogue();
         write_row_lds(wave + 1, av);
         if (bwave) store_row(wsr, rowoff(L.ba, strip, par, side), av, 16);
-        if (SAVE) save_row(A.sv_a1[j], av);
+        if (SAVE) {
+            asm volatile("" ::: "memory");
+            save_row(A.sv_z1[j], zv);
+            save_row(A.sv_a1[j], av);
+        }
         // ================= conv2 =================
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -481,7 +499,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         GSTAMP(sb + 4);
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);     // own a1 row only: no barrier
         GSTAMP(sb + 5);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv2's other taps; the a1 boundary stores
+        if (SAVE) GS_VMCNT_SAVES(16);                         // conv2's other taps; the a1 boundary stores
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // a1's boundary row is out: its storing wave signals for itself (one lane, after its drain)
         if (bwave && lane == 0 && !(A.fault && ticket == 1 && j == 0 && side == 0))
             __hip_atomic_store(flag_of(strip, side, 0), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -578,7 +597,6 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 tr[m][p] = pk4<T>(acc[m][p][0] + bb.x, acc[m][p][1] + bb.y, acc[m][p][2] + bb.z, acc[m][p][3] + bb.w);
         }
         if (bwave) store_row(wsr, rowoff(L.bt, strip, par, side), tr, 16);   // t_j's boundary row
-        if (SAVE) save_row(A.sv_t[j], tr);
         if (wave == 1) {
             // the gate of RCAB j (blocks.py:83-92): mean over the image from the S strip
             // partials, each an 8-B {tag, value} granule (the data is the flag: sc1 loads
@@ -659,7 +677,13 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             cv = src ? src[lane] : 0.f;
         }
         // x_j's and t_j's boundary rows out: drained, then the storing wave signals for itself
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (SAVE) {                                         // t_j's save: last, left in flight
+            asm volatile("" ::: "memory");
+            save_row(A.sv_t[j], tr);
+            GS_VMCNT_SAVES(8);
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 1), tag_of(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         GSTAMP(sb + 8);

@@ -56,6 +56,14 @@ constexpr int GSB_LDS = O_SCR + 80 * 4;
     } while (0)
 #endif
 static_assert(GSB_LDS <= 163840, "LDS budget");
+// a wave's dt / dz1 save stores (8 per row) are issued last before the wait that follows them
+// and left in flight by it (vmcnt(8) instead of vmcnt(0): vector-memory ops retire in issue
+// order); GSB_DRAIN_ALL restores the full drains (A/B)
+#ifdef GSB_DRAIN_ALL
+#define GSB_VMCNT_SAVES(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define GSB_VMCNT_SAVES(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#endif
 static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignment");
 
 // workspace: control words, flags, SE partials, boundary rows of d and dz1
@@ -301,22 +309,6 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             const int ci = 2 * k - 1;
             issue_kh02(ci);                                 // conv2^T's kh = 0, 2 taps (slots free since B_G)
             if (wave == 2) cst[lane] = cv;                  // alpha of RCAB jr, read after B_E
-            // ---- dt = d * rs * s + g (as stored, 16-bit): the LDS image's own row, HBM for the
-            // weight gradient
-            {
-                uint2 dv[4][4];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float4 ga = *(const float4*)(gate + 16 * m + 4 * q);
-                    const float4 gb = *(const float4*)(gate + 64 + 16 * m + 4 * q);
-#pragma unroll
-                    for (int p = 0; p < 4; ++p)
-                        dv[m][p] = pk4<T>(lo16<T>(dr[m][p].x) * ga.x + gb.x, hi16<T>(dr[m][p].x) * ga.y + gb.y,
-                                          lo16<T>(dr[m][p].y) * ga.z + gb.z, hi16<T>(dr[m][p].y) * ga.w + gb.w);
-                }
-                write_row_lds(wave + 1, dv);
-                save_row(A.dt[jr], dv);
-            }
             uint4 nd[HK];
             if (hwave) {
                 // the neighbour's d row (this wave's half), after its flag: lands during phase 1
@@ -327,12 +319,31 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                 for (int kk = 0; kk < HK; ++kk)
                     nd[kk] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, od + kk * 1024, 0, 16));
             }
+            // ---- dt = d * rs * s + g (as stored, 16-bit): the LDS image's own row, HBM for the
+            // weight gradient
+            uint2 dv[4][4];
+            {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float4 ga = *(const float4*)(gate + 16 * m + 4 * q);
+                    const float4 gb = *(const float4*)(gate + 64 + 16 * m + 4 * q);
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+                        dv[m][p] = pk4<T>(lo16<T>(dr[m][p].x) * ga.x + gb.x, hi16<T>(dr[m][p].x) * ga.y + gb.y,
+                                          lo16<T>(dr[m][p].y) * ga.z + gb.z, hi16<T>(dr[m][p].y) * ga.w + gb.w);
+                }
+                write_row_lds(wave + 1, dv);
+            }
+            // dt's row out for the weight gradient: issued after every op the wait below needs,
+            // and left in flight by it (vector-memory ops retire in issue order)
+            asm volatile("" ::: "memory");
+            save_row(A.dt[jr], dv);
             // ================= conv2^T =================
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             GSTAMP(sb + 1);
             conv_phase<T>(acc, img, filt, 1, wave, q, c16);
             GSTAMP(sb + 2);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this conv's taps; the halo rows
+            GSB_VMCNT_SAVES(8);                                 // this conv's taps; the halo rows (dt's save in flight)
             if (hwave) {                                    // its half of dt's halo row, same arithmetic
                 const float4 ga = *(const float4*)(gate + (lane & 7) * 8);
                 const float4 gb = *(const float4*)(gate + (lane & 7) * 8 + 4);
@@ -402,6 +413,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             issue_kh02(ci + 1);
             write_row_lds(wave + 1, zd);
             if (bwave) store_row(wsr, rowoff(L.bz, strip, par, side), zd, 16);
+            asm volatile("" ::: "memory");
             save_row(A.dz1[jr], zd);
             // ================= conv1^T =================
 #pragma unroll
@@ -412,7 +424,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             GSTAMP(sb + 7);
             conv_phase<T>(acc, img, filt, 1, wave, q, c16);     // own dz1 row only: no barrier
             GSTAMP(sb + 8);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // conv1^T's other taps; the dz1 boundary stores
+            GSB_VMCNT_SAVES(8);                                 // conv1^T's other taps; the dz1 boundary stores
             if (bwave && lane == 0 && !(A.fault && ticket == 1 && k == 1 && side == 0))
                 __hip_atomic_store(flag_of(strip, side, 0), tag_of(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();                                // B_Y: dz1's image complete; kh = 1 slots free
