@@ -325,8 +325,15 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         const int ci = gc ? 2 * NB : 2 * j;
         GSTAMP(sb);
         uint4 nx[4], nt[4];
+        // the halo waves poll the neighbour's flag before issuing their tap DMA: a poll waits on
+        // every older vector-memory op of its wave (vmcnt(0))
+#ifndef GS_OLD_ORDER
+        const bool dma_late = hwave;
+#else
+        const bool dma_late = false;
+#endif
         if (j > 0) {
-            issue_kh02(ci);                                 // this conv's kh = 0, 2 taps (slots free since B_G)
+            if (!dma_late) issue_kh02(ci);                  // this conv's kh = 0, 2 taps (slots free since B_G)
             if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;   // read after B_E / B_Z
             // ---- x_j = x_{j-1} + rs * s * t_{j-1} (t as stored: rounded), own row in registers
             float g[4][4];
@@ -364,6 +371,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + k * 1024, 0, 16));
             }
         }
+        if (dma_late && j > 0) issue_kh02(ci);
         if (SAVE && j > 0) {                                // x_0 is the group input
             asm volatile("" ::: "memory");                  // the saves after every op the wait below needs
             save_row(gc ? A.x_last : A.sv_x[j], xr);

@@ -307,7 +307,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
         } else {
             const int ci = 2 * k - 1;
+#ifdef GSB_OLD_START
             issue_kh02(ci);                                 // conv2^T's kh = 0, 2 taps (slots free since B_G)
+#endif
             if (wave == 2) cst[lane] = cv;                  // alpha of RCAB jr, read after B_E
             uint4 nd[HK];
             if (hwave) {
@@ -319,6 +321,11 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                 for (int kk = 0; kk < HK; ++kk)
                     nd[kk] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, od + kk * 1024, 0, 16));
             }
+#ifndef GSB_OLD_START
+            // after the poll (a poll waits on every older vector-memory op of its wave; the
+            // neighbour's flag was set before its B_Z, so before this block passed B_G)
+            issue_kh02(ci);                                 // conv2^T's kh = 0, 2 taps (slots free since B_G)
+#endif
             // ---- dt = d * rs * s + g (as stored, 16-bit): the LDS image's own row, HBM for the
             // weight gradient
             uint2 dv[4][4];
@@ -428,6 +435,23 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             if (bwave && lane == 0 && !(A.fault && ticket == 1 && k == 1 && side == 0))
                 __hip_atomic_store(flag_of(strip, side, 0), tag_of(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();                                // B_Y: dz1's image complete; kh = 1 slots free
+#ifdef GSB_NEW_HALO
+            // the boundary waves poll for the neighbour's dz1 row first (its flag follows its own
+            // phase 1, like this block's B_Y) and load it before the tap DMA and t: the poll then
+            // waits on no other load, and the row lands during phase 2
+            uint4 hv[8];
+            if (bwave) {
+                ok = ok && poll_eq(flag_of(nb_strip, 1 - side, 0), tag_of(k));
+                load_row(rowoff(L.bz, nb_strip, par, 1 - side), hv);
+            }
+            if (jr > 0) issue_kh1(ci + 2);                  // the next RCAB's conv2^T
+            load_acc(jr > 0 ? A.t[jr - 1] : A.dy, tv);
+            conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
+            if (bwave) {                                    // -> this wave's private halo row
+                halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+#else
             if (jr > 0) issue_kh1(ci + 2);                  // the next RCAB's conv2^T
             load_acc(jr > 0 ? A.t[jr - 1] : A.dy, tv);
             conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
@@ -440,6 +464,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                 halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
+#endif
             conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
             GSTAMP(sb + 9);
         }

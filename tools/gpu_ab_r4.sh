@@ -24,6 +24,7 @@ PY
 done
 timeout -k 10 120 python tools/bench_ssim.py 2>&1 | grep -v amdgpu.ids | tail -3
 timeout -k 10 120 python tools/op_times.py 2>&1 | grep -v amdgpu.ids | tail -30
+[ "${TRAINOPS:-0}" = "1" ] && { TRAIN=1 timeout -k 10 300 python tools/op_times.py 2>&1 | grep -v amdgpu.ids | tail -60; }
 if [ "${STAMPS:-0}" = "1" ] && [ -f face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so ]; then
   FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so timeout -k 10 200 python tools/stamp_strip.py 2>&1 | grep -v amdgpu.ids
   FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so timeout -k 10 200 python tools/stamp_strip_bwd.py 2>&1 | grep -v amdgpu.ids
