@@ -6,6 +6,8 @@
 Launches the RCAB conv1 (64->64 + bias + PReLU, bf16, B=32, 64x64) a few times and prints,
 per phase, the median over blocks of the time since the kernel's earliest block start
 (s_memrealtime, 100 MHz) and the median per-block duration in shader cycles (s_memtime).
+UP=1: the inference upsampler's stage 1 instead (64 -> 256 + bias + PReLU + PixelShuffle,
+fp16, 128x128 -> 256x256, packed mode 1).
 """
 import json
 import os
@@ -20,22 +22,26 @@ import torch  # noqa: E402
 from src.hip import lib as L, net  # noqa: E402
 from src.hip.program import Ctx, ptr  # noqa: E402
 
-B, H, W, C = int(os.environ.get("B", "32")), 64, 64, 64
+UP = os.environ.get("UP", "0") == "1"
+B, C = int(os.environ.get("B", "32")), 64
+H = W = 128 if UP else 64
+CO, MODE = (4 * C, 1) if UP else (C, 0)
+DT = torch.float16 if UP else torch.bfloat16
 torch.manual_seed(0)
-ctx = Ctx(torch.bfloat16, "cuda")
-x = torch.randn(B, H, W, C, device="cuda", dtype=torch.bfloat16)
-w = torch.randn(C, C, 3, 3, device="cuda") * 0.05
-wp = torch.empty(ctx.lib.fen_packed_elems(0, C, C), dtype=torch.bfloat16, device="cuda")
-ctx.emit("pack", ctx.lib.fen_pack_conv_w, ctx.code, 0, C, C, ptr(w), ptr(wp))
-bias = torch.zeros(C, device="cuda")
+ctx = Ctx(DT, "cuda")
+x = torch.randn(B, H, W, C, device="cuda", dtype=DT)
+w = torch.randn(CO, C, 3, 3, device="cuda") * 0.05
+wp = torch.empty(ctx.lib.fen_packed_elems(MODE, CO, C), dtype=DT, device="cuda")
+ctx.emit("pack", ctx.lib.fen_pack_conv_w, ctx.code, MODE, CO, C, ptr(w), ptr(wp))
+bias = torch.zeros(CO, device="cuda")
 alpha = torch.full((C,), 0.25, device="cuda")
-y = torch.empty_like(x)
+y = torch.empty(B, 2 * H, 2 * W, C, device="cuda", dtype=DT) if UP else torch.empty_like(x)
 nblk = 1024
 st = torch.zeros(nblk * 8 * 32, dtype=torch.int64, device="cuda")
-epi = int(os.environ.get("EPI", str(L.EPI_PRELU)))
+epi = int(os.environ.get("EPI", str(L.EPI_PRELU | (L.EPI_SHUFFLE if UP else 0))))
 for _ in range(int(os.environ.get("REPS", "30"))):
     st.zero_()
-    net.conv(ctx, x, wp, B, H, W, C, C, bias=bias, epi=epi, alpha=alpha, y=y, loss_part=st,
+    net.conv(ctx, x, wp, B, H, W, C, CO, bias=bias, epi=epi, alpha=alpha, y=y, loss_part=st,
              debug=int(os.environ.get("DEBUG", "0")))
 torch.cuda.synchronize()
 a = st.view(nblk, 8, 16, 2).cpu().numpy().astype(np.int64)
