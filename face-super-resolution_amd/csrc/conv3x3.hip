@@ -229,7 +229,12 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                 }
                 if (epi & FEN_EPI_PRELU_BWD) {
                     float pv[4];
-                    ld4<T>((const char*)d.pre_in + oi * sizeof(T), pv);
+                    const bool rec = d.post_in && all_pos4(al4);   // pre-activation from the PReLU output
+                    ld4<T>((const char*)(rec ? d.post_in : d.pre_in) + oi * sizeof(T), pv);
+                    if (rec) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) pv[r] = prelu_pre_from_post(pv[r], __builtin_amdgcn_rcpf(al4[r]));
+                    }
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         psum[m][r] += prelu_dalpha_f(v[r], pv[r]);
@@ -518,23 +523,40 @@ __device__ __forceinline__ void conv_tile_rows2(f32x4 (&acc)[MT][NT], const char
     };
     loadB(0, B0);
     loadA(0, A0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < 6; ++g) {
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
             const int st = g * 3 + kh;
+            int nl = 0;
             if (st + 1 < 18) {
                 if (st & 1) loadA(st + 1, A0); else loadA(st + 1, A1);
+                nl += MT;
             }
             if (kh == 0 && g + 1 < 6) {
                 if (g & 1) loadB(g + 1, B0); else loadB(g + 1, B1);
+                nl += NB;
             }
+#ifdef G_BURST
             __builtin_amdgcn_sched_barrier(0);
+#endif
             if (st & 1) {
                 if (g & 1) mma(A1, B1, kh); else mma(A1, B0, kh);
             } else {
                 if (g & 1) mma(A0, B1, kh); else mma(A0, B0, kh);
             }
+#ifndef G_BURST
+            // one wave per SIMD computes while the other group services: the next step's
+            // fragment reads go out one per MFMA instead of as a burst ahead of them, so the
+            // matrix pipe does not drain while the wave issues them
+            if (nl > 0) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+#pragma unroll
+            for (int i = 0; i < MT * NT; ++i) {
+                if (i < nl) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                if (i + (nl > 0 ? 1 : 0) < MT * NT) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -736,6 +758,14 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
         __builtin_amdgcn_s_barrier();
     }
     FEN_STAMP(1);
+    // pre_elide: all 64 slopes of this block's channels > 0 -> y_pre is not written (the
+    // backward recovers it from y); block-uniform, so the store counts stay wave-uniform
+    bool wpre = PRELU && d.y_pre;
+    if (wpre && d.pre_elide) {
+        bool allpos = true;
+        for (int i = 0; i < 64; ++i) allpos = allpos && cst[64 + i] > 0.f;
+        wpre = !allpos;
+    }
 
     const int pend = max(2 * nj0 - 1, 2 * nj1);              // last phase (an epilogue)
     f32x4 acc[MT][NT];
@@ -770,6 +800,9 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
             uint2 pv[PIN ? MT : 1][PIN ? NT : 1];
             int b = 0, h0 = 0, w0 = 0, t = 0;
             bool full = true;
+            bool rec_m[MT];                                      // PBWD: pre-activation from post_in
+#pragma unroll
+            for (int m = 0; m < MT; ++m) rec_m[m] = PBWD && d.post_in && all_pos4(cst + 64 + m * 16 + 4 * q);
             if (ret) {
                 t = tile_of(grp, jp);
                 b = t / tpi;
@@ -785,7 +818,10 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                     for (int m = 0; m < MT; ++m) {
 #pragma unroll
                         for (int k = 0; k < NRES; ++k) rv[k][m][n] = *(const uint2*)((const char*)d.res[k] + (oi + m * 16) * 2);
-                        if constexpr (PIN) pv[m][n] = *(const uint2*)((const char*)d.pre_in + (oi + m * 16) * 2);
+                        if constexpr (PIN) {
+                            const void* src = (PBWD && rec_m[m]) ? d.post_in : d.pre_in;
+                            pv[m][n] = *(const uint2*)((const char*)src + (oi + m * 16) * 2);
+                        }
                     }
                 }
             }
@@ -822,6 +858,10 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                             pf[1] = hi16<T>(pv[m][n].x);
                             pf[2] = lo16<T>(pv[m][n].y);
                             pf[3] = hi16<T>(pv[m][n].y);
+                            if (PBWD && rec_m[m]) {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) pf[r] = prelu_pre_from_post(pf[r], __builtin_amdgcn_rcpf(al4[r]));
+                            }
                         }
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -862,7 +902,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                         } else {
                             off = ((size_t)(b * H + h) * W + w) * Cout + cob;
                         }
-                        if (PRELU && d.y_pre) {
+                        if (wpre) {
                             st4<T>((char*)d.y_pre + off * 2, v);
                             ++nst;
                         }

@@ -127,6 +127,7 @@ struct GsArgs {
     void* x_last;
     int* status;                              // optional: a timed-out wait is reported here
     int fault;                                // test-only: image 0 strip 1 skips one a1 flag
+    int pre_elide;                            // training: no z1 save for an RCAB whose slopes are all > 0
 };
 
 template <typename T, bool SAVE>
@@ -167,6 +168,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         unsigned long long t0;
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
         tick_lds[2] = (int)(unsigned)t0;
+        tick_lds[3] = (int)(unsigned)__builtin_amdgcn_s_memtime();
 #endif
     }
     // zero the LDS image (halo rows of edge strips and the zero columns stay zero)
@@ -481,6 +483,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         __syncthreads();                                    // B_E: x_j's reads done (all slots free); those taps visible
         issue_kh02(ci + 1);
         uint2 zv[4][4];
+        // pre_elide: z1 is recoverable from a1 when all 64 slopes of RCAB j are > 0 (lane = channel)
+        const bool wz1 = SAVE && !(A.pre_elide && __ballot(cst[64 + lane] > 0.f) == ~0ull);
         if (SAVE) {                                         // z1 = conv1 + b1 (PReLU's input)
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -495,7 +499,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         if (bwave) store_row(wsr, rowoff(L.ba, strip, par, side), av, 16);
         if (SAVE) {
             asm volatile("" ::: "memory");
-            save_row(A.sv_z1[j], zv);
+            if (wz1) save_row(A.sv_z1[j], zv);
             save_row(A.sv_a1[j], av);
         }
         // ================= conv2 =================
@@ -507,7 +511,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         GSTAMP(sb + 4);
         conv_phase<T>(acc, img, filt, 1, wave, q, c16);     // own a1 row only: no barrier
         GSTAMP(sb + 5);
-        if (SAVE) GS_VMCNT_SAVES(16);                         // conv2's other taps; the a1 boundary stores
+        if (SAVE && wz1) GS_VMCNT_SAVES(16);                  // conv2's other taps; the a1 boundary stores
+        else if (SAVE) GS_VMCNT_SAVES(8);                     // (a1's save only)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // a1's boundary row is out: its storing wave signals for itself (one lane, after its drain)
         if (bwave && lane == 0 && !(A.fault && ticket == 1 && j == 0 && side == 0))
@@ -705,6 +710,11 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     if (tid == 0) strip_finish(ctl, B * S, A.status, FEN_STATUS_GS_FWD);
 #ifdef FEN_GS_STAMPS
     __syncthreads();
+    // the block's shader clock: s_memtime cycles / 16 over the block's life, in wave 1's end
+    // slot (the tools read the end stamp of wave 0 only)
+    if (tid == 0)
+        stamp_lds[NSTAMP + NSTAMP - 1] = (unsigned short)(((unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tick_lds[3]) >> 4);
+    __syncthreads();
     {
         unsigned short* dst = (unsigned short*)(A.work + L.ba + (size_t)B * S * 2 * 2 * ROWB) + (size_t)ticket * 8 * NSTAMP;
         for (int i = tid; i < 8 * NSTAMP; i += 512) dst[i] = stamp_lds[i];
@@ -756,7 +766,7 @@ extern "C" int fen_group_strip(const fen_group_strip_desc* d, void* stream) {
     a.res_scale = d->res_scale, a.inv_hw = 1.0f / (float)(d->H * d->W);
     a.x = d->x, a.y = d->y, a.work = (char*)d->work;
     a.save = d->save ? 1 : 0;
-    a.status = d->status, a.fault = d->fault;
+    a.status = d->status, a.fault = d->fault, a.pre_elide = d->pre_elide;
     if (a.save) {
         if (!d->x_last) return FEN_EINVAL;
         a.x_last = d->x_last;

@@ -110,6 +110,7 @@ struct GsbArgs {
     char* work;
     int* status;                              // optional: a timed-out wait is reported here
     int fault;                                // test-only: image 0 strip 1 skips one dz1 flag
+    const void* a1[FEN_GS_MAXNB];             // optional: z1 recovered from a1 where every slope > 0
 };
 
 template <typename T>
@@ -373,7 +374,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             GSTAMP(sb + 3);
             issue_kh1(ci + 1);                              // conv1^T's kh = 1 taps
             uint2 zv[4][4];
-            load_acc(A.z1[jr], zv);                         // PReLU's input, for the epilogue
+            // PReLU's input, for the epilogue: z1, or a1 when every slope of RCAB jr is > 0 (the
+            // forward's pre_elide may not have written z1 then; lane = channel)
+            const bool recz = A.a1[jr] != nullptr && __ballot(cst[lane] > 0.f) == ~0ull;
+            load_acc(recz ? A.a1[jr] : A.z1[jr], zv);
             conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
             conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
             GSTAMP(sb + 4);
@@ -393,11 +397,16 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                 for (int m = 0; m < 4; ++m) {
                     const float4 aa = *(const float4*)(cst + 16 * m + 4 * q);
                     const float alp[4] = {aa.x, aa.y, aa.z, aa.w};
+                    // recovery factor: z = a1 * (s + (1 - s) * ia), ia = 1 / alpha (1: z1 as read)
+                    const float ia[4] = {recz ? __builtin_amdgcn_rcpf(alp[0]) : 1.f, recz ? __builtin_amdgcn_rcpf(alp[1]) : 1.f,
+                                         recz ? __builtin_amdgcn_rcpf(alp[2]) : 1.f, recz ? __builtin_amdgcn_rcpf(alp[3]) : 1.f};
                     float ds[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int p = 0; p < 4; ++p) {
-                        const float z[4] = {lo16<T>(zv[m][p].x), hi16<T>(zv[m][p].x), lo16<T>(zv[m][p].y),
-                                            hi16<T>(zv[m][p].y)};
+                        const float z[4] = {prelu_pre_from_post(lo16<T>(zv[m][p].x), ia[0]),
+                                            prelu_pre_from_post(hi16<T>(zv[m][p].x), ia[1]),
+                                            prelu_pre_from_post(lo16<T>(zv[m][p].y), ia[2]),
+                                            prelu_pre_from_post(hi16<T>(zv[m][p].y), ia[3])};
                         float v[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
@@ -690,6 +699,7 @@ extern "C" int fen_group_strip_bwd(const fen_group_strip_bwd_desc* d, void* stre
         a.w[2 * k - 1] = d->w2t[j], a.w[2 * k] = d->w1t[j];
         a.alpha[j] = d->alpha[j], a.fc1[j] = d->fc1[j], a.fc2[j] = d->fc2[j];
         a.z1[j] = d->z1[j], a.t[j] = d->t[j], a.s[j] = d->s[j], a.mean[j] = d->mean[j], a.hid[j] = d->hid[j];
+        a.a1[j] = d->a1[j];
         a.dt[j] = d->dt[j], a.dz1[j] = d->dz1[j], a.dal[j] = d->dalpha_part[j];
         a.dw1p[j] = d->dw1p[j], a.dw2p[j] = d->dw2p[j];
     }

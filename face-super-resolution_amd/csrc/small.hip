@@ -505,17 +505,59 @@ __global__ __launch_bounds__(1024) void k_conv_first_finalize(int nb, int Ci, in
 
 // --------------- conv_last dgrad + PReLU backward + PixelShuffle inverse ---------------
 // dout NHWC16 [B,H,W,16], w [Co][C][3][3] -> da[px][c] -> dv = da*(pre>0?1:alpha[c])
-// -> du[b][h/2][w/2][4c + 2(h&1) + (w&1)];  block = 16x16 source px = 8x8 du px
-template <typename T>
-__global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, int C, int Co, const T* __restrict__ dout,
-                                  const float* __restrict__ w, const T* __restrict__ pre,
+// -> du[b][h/2][w/2][4c + 2(h&1) + (w&1)];  block = 16x16 source px = 8x8 du px.
+// Thread (k = tid % (C/2)) owns channels 2k, 2k+1 of du pixels tid / (C/2) + 256/(C/2) * j.
+// Memory-latency bound (the FMAs are 7 GFLOP at B=32, 256x256): for 16-bit operands and
+// C <= 64 (LPRE) the block's whole pre-activation tile (16x16 px x C, <= 32 KB) is loaded into
+// LDS together with the dout halo -- one round trip per block instead of one per du pixel.
+template <typename T, int C>
+__global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, int Co, const T* __restrict__ dout,
+                                  const float* __restrict__ w, const T* __restrict__ pre, const T* __restrict__ post,
                                   const float* __restrict__ alpha, T* __restrict__ du, float* __restrict__ part) {
+    constexpr int K2 = C / 2;
+#ifdef CLD_GLOBAL_PRE   // A/B: the pre-activations read from global per du pixel
+    constexpr bool LPRE = false;
+#else
+    constexpr bool LPRE = sizeof(T) == 2 && C <= 64;
+#endif
+    constexpr int PRE_U4 = LPRE ? 256 * C * 2 / 16 : 1;   // 16-B pieces of the tile
     __shared__ float4 sd[18 * 18];          // dout tile + halo, channels 0..2 (3 = pad)
     __shared__ float sdal[256 * 2];
+    __shared__ uint4 spre[PRE_U4];          // [16 rows][16 px][C] pre-activations (LPRE)
     const int tid = threadIdx.x;
     const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
     const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
     const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+    if constexpr (LPRE) {
+        constexpr int PPR = C * 2 / 16;     // 16-B pieces per pixel (8 channels: two groups of 4)
+        static_assert(256 % PPR == 0, "a thread's pieces share one channel chunk");
+        // each group of 4 channels from post (slopes all > 0: recovered below) or pre; the
+        // thread's chunk (8 channels) is the same for all its pieces
+        const int pcq = tid % PPR;
+        const bool r0 = post && all_pos4(alpha + pcq * 8), r1 = post && all_pos4(alpha + pcq * 8 + 4);
+        const char* src0 = (const char*)(r0 ? post : pre);
+        const char* src1 = (const char*)(r1 ? post : pre);
+        uint4 v[(PRE_U4 + 255) / 256];
+#pragma unroll
+        for (int j = 0; j < (PRE_U4 + 255) / 256; ++j) {
+            const int i = tid + j * 256;
+            const int px = i / PPR;
+            const int gh = h0 + (px >> 4), gw = w0 + (px & 15);
+            v[j] = make_uint4(0u, 0u, 0u, 0u);
+            if (i < PRE_U4 && gh < H && gw < W) {
+                const size_t o = (((size_t)(b * H + gh) * W + gw) * C) * 2 + pcq * 16;
+                if (r0 == r1) {
+                    v[j] = *(const uint4*)(src0 + o);
+                } else {
+                    const uint2 lo = *(const uint2*)(src0 + o), hi = *(const uint2*)(src1 + o + 8);
+                    v[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < (PRE_U4 + 255) / 256; ++j)
+            if (tid + j * 256 < PRE_U4) spre[tid + j * 256] = v[j];
+    }
     for (int i = tid; i < 18 * 18; i += 256) {
         const int r = i / 18, c = i % 18;
         const int gh = h0 + r - 1, gw = w0 + c - 1;
@@ -527,7 +569,6 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
         }
         sd[i] = v;
     }
-    const int K2 = C / 2;
     const int k = tid % K2;                 // channel pair (2k, 2k+1), fixed per thread
     float wr[2][3][9];
 #pragma unroll
@@ -538,6 +579,9 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
             for (int t = 0; t < 9; ++t)
                 wr[e][co][t] = co < Co ? w[((size_t)co * C + 2 * k + e) * 9 + t] : 0.f;
     const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
+    const bool rec = post && all_pos4(alpha + ((2 * k) & ~3));   // this pair's group of 4
+    // branch-free recovery: p = y * (s + (1 - s) * ia) is y itself when ia = 1 (read from pre)
+    const float ia0 = rec ? __builtin_amdgcn_rcpf(al0) : 1.f, ia1 = rec ? __builtin_amdgcn_rcpf(al1) : 1.f;
     __syncthreads();
     float dal0 = 0.f, dal1 = 0.f;
     const int Hh = H >> 1, Wh = W >> 1;
@@ -560,8 +604,19 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
                     da0 += g.x * wr[0][0][tp] + g.y * wr[0][1][tp] + g.z * wr[0][2][tp];
                     da1 += g.x * wr[1][0][tp] + g.y * wr[1][1][tp] + g.z * wr[1][2][tp];
                 }
-            const size_t pi = ((size_t)(b * H + h0 + sh) * W + w0 + sw) * C + 2 * k;
-            const float p0 = tof<T>(pre[pi]), p1 = tof<T>(pre[pi + 1]);
+            float p0, p1;
+            if constexpr (LPRE) {
+                const unsigned pw = ((const unsigned*)spre)[(sh * 16 + sw) * K2 + k];
+                p0 = lo16<T>(pw);
+                p1 = hi16<T>(pw);
+            } else {
+                const size_t pi = ((size_t)(b * H + h0 + sh) * W + w0 + sw) * C + 2 * k;
+                const T* src = rec ? post : pre;
+                p0 = tof<T>(src[pi]);
+                p1 = tof<T>(src[pi + 1]);
+            }
+            p0 = prelu_pre_from_post(p0, ia0);
+            p1 = prelu_pre_from_post(p1, ia1);
             dal0 += prelu_dalpha_f(da0, p0);
             dal1 += prelu_dalpha_f(da1, p1);
             out[t] = prelu_bwd_f(da0, p0, al0);
@@ -1483,21 +1538,32 @@ extern "C" size_t fen_conv_last_dgrad_part_rows(int B, int H, int W) {
 }
 
 extern "C" int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const void* dout, const float* w,
-                                   const void* pre, const float* alpha, void* du, float* part, void* stream) {
+                                   const void* pre, const void* post, const float* alpha, void* du, float* part,
+                                   void* stream) {
     if (!dout || !w || !pre || !alpha || !du || !part || Co > 3 || C < 32 || C > 256 || 256 % (C / 2) || (H | W) & 1)
         return FEN_EINVAL;
     const int nb = (int)fen_conv_last_dgrad_part_rows(B, H, W);
-    if (dtype == FEN_BF16)
-        hipLaunchKernelGGL(k_conv_last_dgrad<bf16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co, (const bf16*)dout,
-                           w, (const bf16*)pre, alpha, (bf16*)du, part);
-    else if (dtype == FEN_F16)
-        hipLaunchKernelGGL(k_conv_last_dgrad<f16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co, (const f16*)dout,
-                           w, (const f16*)pre, alpha, (f16*)du, part);
-    else if (dtype == FEN_F32)
-        hipLaunchKernelGGL(k_conv_last_dgrad<float>, dim3(nb), dim3(256), 0, STREAM, B, H, W, C, Co,
-                           (const float*)dout, w, (const float*)pre, alpha, (float*)du, part);
-    else
-        return FEN_EINVAL;
+    auto launch = [&](auto tag) -> int {
+        using T = decltype(tag);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, STREAM, B, H, W, Co, (const T*)dout, w, (const T*)pre,
+                               (const T*)post, alpha, (T*)du, part);
+        };
+        switch (C) {
+            case 32: go(k_conv_last_dgrad<T, 32>); break;
+            case 64: go(k_conv_last_dgrad<T, 64>); break;
+            case 128: go(k_conv_last_dgrad<T, 128>); break;
+            case 256: go(k_conv_last_dgrad<T, 256>); break;
+            default: return FEN_EINVAL;
+        }
+        return FEN_OK;
+    };
+    int rc;
+    if (dtype == FEN_BF16) rc = launch(bf16{});
+    else if (dtype == FEN_F16) rc = launch(f16{});
+    else if (dtype == FEN_F32) rc = launch(0.f);
+    else return FEN_EINVAL;
+    if (rc != FEN_OK) return rc;
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -111,20 +111,46 @@ __device__ __forceinline__ void conv_phase(f32x4 (&acc)[4][4], const char* img, 
         const int kw = s >> 1, chunk = (s & 1) * 4 + q;
         const char* ab = slot0 + kw * TAPB + c16 * 128 + ((chunk ^ ((c16 >> 1) & 7)) << 4);
         const char* bb = rowp + (c16 + kw) * 128 + ((chunk ^ ((c16 + kw) & 7)) << 4);
+#ifdef GS_BURST
 #pragma unroll
         for (int m = 0; m < 4; ++m) a[m] = *(const uint4*)(ab + m * 2048);
 #pragma unroll
         for (int p = 0; p < 4; ++p) b[p] = *(const uint4*)(bb + p * 2048);
+#else
+        // in the order the next step's MFMAs (m-major) consume them
+        b[0] = *(const uint4*)bb;
+        a[0] = *(const uint4*)ab;
+#pragma unroll
+        for (int p = 1; p < 4; ++p) b[p] = *(const uint4*)(bb + p * 2048);
+#pragma unroll
+        for (int m = 1; m < 4; ++m) a[m] = *(const uint4*)(ab + m * 2048);
+#endif
     };
     load(0, A[0], Bf[0]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
         if (s + 1 < 6) load(s + 1, A[(s + 1) & 1], Bf[(s + 1) & 1]);
+#ifdef GS_BURST
         __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int p = 0; p < 4; ++p) mma16<T>(acc[m][p], A[s & 1][m], Bf[s & 1][p]);
+#ifndef GS_BURST
+        // the next step's 8 fragment reads one per MFMA, not as a burst ahead of the 16
+        // MFMAs: a SIMD's two waves leave every barrier together, and two bursts at once
+        // drained the matrix pipe
+        if (s + 1 < 6) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        }
+#endif
         __builtin_amdgcn_sched_barrier(0);
     }
 }

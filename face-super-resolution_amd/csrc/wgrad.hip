@@ -379,24 +379,29 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
         const char* hx = cur;
         const char* ty = cur + HALO_SLOT;
         uint4 A0[MC], B0[9], A1[MC], B1[9];
+        auto loadA = [&](int s, uint4 (&A)[MC], int h, int m) {
+            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ty + offA[h][m] + s * ASTEP));
+            const uint2 u = __builtin_bit_cast(uint2, v);
+            if (h == 0) { A[m].x = u.x; A[m].y = u.y; } else { A[m].z = u.x; A[m].w = u.y; }
+        };
+        auto loadB = [&](int s, uint4 (&Bf)[9], int h, int tap) {
+            const int kh = tap / 3, kw = tap % 3;
+            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)(hx + offB[h][kw] + (2 * s + kh) * (HALO * 128)));
+            const uint2 u = __builtin_bit_cast(uint2, v);
+            if (h == 0) { Bf[tap].x = u.x; Bf[tap].y = u.y; } else { Bf[tap].z = u.x; Bf[tap].w = u.y; }
+        };
+        // the (MC + 9) x 2 fragment reads of step s, in the order the tap-major MFMAs consume them
         auto load = [&](int s, uint4 (&A)[MC], uint4 (&Bf)[9]) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int m = 0; m < MC; ++m) {
+                loadA(s, A, 0, m);
+                loadA(s, A, 1, m);
+            }
 #pragma unroll
-                for (int m = 0; m < MC; ++m) {
-                    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(ty + offA[h][m] + s * ASTEP));
-                    const uint2 u = __builtin_bit_cast(uint2, v);
-                    if (h == 0) { A[m].x = u.x; A[m].y = u.y; } else { A[m].z = u.x; A[m].w = u.y; }
-                }
-#pragma unroll
-                for (int tap = 0; tap < 9; ++tap) {
-                    const int kh = tap / 3, kw = tap % 3;
-                    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(hx + offB[h][kw] + (2 * s + kh) * (HALO * 128)));
-                    const uint2 u = __builtin_bit_cast(uint2, v);
-                    if (h == 0) { Bf[tap].x = u.x; Bf[tap].y = u.y; } else { Bf[tap].z = u.x; Bf[tap].w = u.y; }
-                }
+            for (int tap = 0; tap < 9; ++tap) {
+                loadB(s, Bf, 0, tap);
+                loadB(s, Bf, 1, tap);
             }
         };
         auto mma = [&](int s, const uint4 (&A)[MC], const uint4 (&Bf)[9]) {
@@ -412,16 +417,37 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
                 for (int m = 0; m < MC; ++m) mma16<bf16>(accb[m], A[m], ones);
             }
         };
+        // WG_BURST: the next step's reads as one burst ahead of the MFMAs (A/B); by default
+        // they go out between the MFMAs (two per MFMA first, then one), so the two waves of a
+        // SIMD, which leave the tile barrier together, do not drain the matrix pipe at once
+        auto spread = [&]() {
+#ifndef WG_BURST
+            constexpr int NR = 2 * (MC + 9), NM = 9 * MC, N2 = NR - NM;   // reads, MFMAs, double slots
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (i < N2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+#endif
+        };
         load(0, A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s = 0; s < 8; s += 2) {
             load(s + 1, A1, B1);
+#ifdef WG_BURST
             __builtin_amdgcn_sched_barrier(0);
+#endif
             mma(s, A0, B0);
+            spread();
             __builtin_amdgcn_sched_barrier(0);
             if (s + 2 < 8) load(s + 2, A0, B0);
+#ifdef WG_BURST
             __builtin_amdgcn_sched_barrier(0);
+#endif
             mma(s + 1, A1, B1);
+            if (s + 2 < 8) spread();
             __builtin_amdgcn_sched_barrier(0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile's pieces landed

@@ -33,6 +33,7 @@ class ConvDesc(Structure):
         ("part", c_void_p), ("lr", c_void_p), ("scale", c_int), ("clamp", c_int), ("hr", c_void_p),
         ("dout", c_void_p), ("l1_scale", c_float), ("loss_part", c_void_p), ("debug", c_int),
         ("s2d_in", c_int), ("s2d_out", c_int),
+        ("pre_elide", c_int), ("post_in", c_void_p),
     ]
 
 
@@ -82,6 +83,7 @@ class GroupStripDesc(Structure):
         ("save", c_int), ("sv_x", c_void_p * GS_MAXNB), ("sv_z1", c_void_p * GS_MAXNB),
         ("sv_a1", c_void_p * GS_MAXNB), ("sv_t", c_void_p * GS_MAXNB), ("sv_mean", c_void_p * GS_MAXNB),
         ("sv_hid", c_void_p * GS_MAXNB), ("x_last", c_void_p), ("status", c_void_p), ("fault", c_int),
+        ("pre_elide", c_int),
     ]
 
 
@@ -95,6 +97,7 @@ class GroupStripBwdDesc(Structure):
         ("hid", c_void_p * GS_MAXNB), ("dt", c_void_p * GS_MAXNB), ("dz1", c_void_p * GS_MAXNB),
         ("dalpha_part", c_void_p * GS_MAXNB), ("dw1p", c_void_p * GS_MAXNB), ("dw2p", c_void_p * GS_MAXNB),
         ("work", c_void_p), ("work_bytes", c_size_t), ("status", c_void_p), ("fault", c_int),
+        ("a1", c_void_p * GS_MAXNB),
     ]
 
 
@@ -140,7 +143,7 @@ _SIGS = {
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),
     "fen_conv_first_wgrad": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_int, c_void_p, c_void_p]),
     "fen_conv_last_dgrad_part_rows": (c_size_t, [c_int] * 3),
-    "fen_conv_last_dgrad": (c_int, [c_int] * 6 + [c_void_p] * 6 + [c_void_p]),
+    "fen_conv_last_dgrad": (c_int, [c_int] * 6 + [c_void_p] * 7 + [c_void_p]),
     "fen_se_fwd": (c_int, [c_int, c_int, c_int, c_int, c_float] + [c_void_p] * 6 + [c_void_p]),
     "fen_se_fused": (c_int, [c_int] * 6 + [c_float] + [c_void_p] * 7 + [c_float, c_void_p, c_void_p, c_void_p]),
     "fen_se_apply": (c_int, [c_int] * 4 + [c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),

@@ -74,6 +74,16 @@ RCAB_C128 = os.environ.get("FEN_RCAB_C128", "1") != "0"
 # the fen_se_bwd + fen_se_bwd_apply pair (FEN_SE_BWD=pair; shapes outside the fused
 # kernel's envelope always take the pair)
 SE_BWD_FUSED = os.environ.get("FEN_SE_BWD", "fused") != "pair"
+# inference: the upsampler and conv_last run over the batch in chunks of this many images, so a
+# chunk's x2 / x4 activations (16.8 + 67 MB per 8 images at 64 -> 256) are written and re-read
+# while they sit in the 256-MB Infinity Cache instead of making a round trip through HBM
+# (0 = the whole batch in one pass)
+TAIL_CHUNK = int(os.environ.get("FEN_TAIL_CHUNK", "0"))
+# training: the upsampler stages' pre-activations are not saved where the PReLU slopes are > 0
+# (their 4-channel groups); the backward recovers v = a > 0 ? a : a / alpha from the stage
+# output a (fen_conv_desc.pre_elide / post_in) -- 268 + 67 MB fewer writes and reads per step
+# at B=32; FEN_PRE_ELIDE=0 saves and reads v as before
+PRE_ELIDE = os.environ.get("FEN_PRE_ELIDE", "1") != "0"
 
 
 def tiles(H: int, W: int) -> int:
@@ -142,7 +152,7 @@ class Weights:
 # --------------------------------------------------------------------------------------
 def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, y=None, y_pre=None,
          res: Sequence = (), pre_in=None, part=None, lr=None, scale=0, clamp=0, hr=None, dout=None,
-         l1_scale=0.0, loss_part=None, debug=0, s2d_in=0, s2d_out=0) -> None:
+         l1_scale=0.0, loss_part=None, debug=0, s2d_in=0, s2d_out=0, pre_elide=0, post_in=None) -> None:
     d = L.ConvDesc()
     d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = ctx.code, B, H, W, Cin, Cout
     d.x, d.w, d.bias = ptr(x), ptr(wpk), ptr(bias)
@@ -155,6 +165,7 @@ def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, 
     d.l1_scale, d.loss_part = float(l1_scale), ptr(loss_part)
     d.debug = debug
     d.s2d_in, d.s2d_out = s2d_in, s2d_out
+    d.pre_elide, d.post_in = int(pre_elide), ptr(post_in)
     ctx.emit("conv3x3", ctx.lib.fen_conv3x3, byref(d))
 
 
@@ -456,9 +467,15 @@ class Forward:
             else:
                 blocks.append(dict(s=sg))
         x_last = None
+        z1_elided = False
         if self.save:
             x_last = ctx.alloc(x.shape)
             d.save, d.x_last = 1, ptr(x_last)
+            # z1 of an RCAB whose slopes are all > 0 is left unwritten when the backward will be
+            # the strip backward, which recovers it from a1 (PRE_ELIDE)
+            z1_elided = PRE_ELIDE and GROUP_STRIP_BWD and bool(
+                ctx.lib.fen_group_strip_bwd_supported(ctx.code, B, H, W, C, s.Cr, s.NB))
+            d.pre_elide = int(z1_elided)
         d.wg, d.bg = ptr(Wt.packed(pre + "conv", 0)), ptr(p[pre + "conv.bias"])
         nbytes = int(ctx.lib.fen_group_strip_work_bytes(B, H))
         work = ctx.persistent_zeros(f"group_strip/{B}x{H}", nbytes)
@@ -466,7 +483,7 @@ class Forward:
         d.status, d.fault = L.strip_status_ptr(ctx.device), GS_FAULT & 1
         ctx.emit("group_strip", ctx.lib.fen_group_strip, byref(d))
         ctx.keep(d)
-        return dict(blocks=blocks, x=x, x_last=x_last)
+        return dict(blocks=blocks, x=x, x_last=x_last, z1_elided=z1_elided)
 
     def _c128_ok(self, x) -> bool:
         B, H, W, C = x.shape
@@ -582,9 +599,9 @@ class Forward:
             return (RCAB_C128 and not self.save and
                     bool(ctx.lib.fen_rcab_c128_supported(ctx.code, B, hh_, ww_, C, max(s.Cr, 1))))
 
-        def c128_launch(name, mode, x_, w_, bias_, y_, alpha_=None, res_=None):
+        def c128_launch(name, mode, x_, w_, bias_, y_, alpha_=None, res_=None, b_=None):
             d = L.RcabC128Desc()
-            d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.mode = ctx.code, B, x_.shape[1], x_.shape[2], C, max(s.Cr, 1), mode
+            d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.mode = ctx.code, b_ or B, x_.shape[1], x_.shape[2], C, max(s.Cr, 1), mode
             d.res_scale = float(s.res_scale)
             d.x, d.w, d.bias, d.y = ptr(x_), ptr(w_), ptr(bias_), ptr(y_)
             d.alpha, d.res = ptr(alpha_), ptr(res_)
@@ -597,29 +614,35 @@ class Forward:
         else:
             conv(ctx, feat, Wt.packed("conv_after_body", 0), B, H, W, C, C, bias=p["conv_after_body.bias"], y=fb,
                  res=(feat0,))
-        h, hh, ww = fb, H, W
-        stages = []
-        for st in range(s.n_stages):
-            key = f"upsample.stages.{st}."
-            a = ctx.alloc((B, 2 * hh, 2 * ww, C)) if self.save else ctx.scratch(f"up_a{st & 1}", (B, 2 * hh, 2 * ww, C))
-            v = ctx.alloc((B, 2 * hh, 2 * ww, C)) if self.save else None
-            if c128(hh, ww):
-                c128_launch("c128_upsample", 4, h, Wt.packed(key + "conv", 1), p[key + "conv.bias"], a,
-                            alpha_=p[key + "prelu.weight"])
-            else:
-                conv(ctx, h, Wt.packed(key + "conv", 1), B, hh, ww, C, 4 * C, bias=p[key + "conv.bias"],
-                     epi=L.EPI_PRELU | L.EPI_SHUFFLE, alpha=p[key + "prelu.weight"], y=a, y_pre=v)
-            stages.append(dict(x=h, v=v, a=a, H=hh, W=ww))
-            h, hh, ww = a, 2 * hh, 2 * ww
         if out is None:
-            out = ctx.alloc((B, s.out_ch, hh, ww), torch.float32)
+            out = ctx.alloc((B, s.out_ch, H << s.n_stages, W << s.n_stages), torch.float32)
+        bc = B
+        if TAIL_CHUNK > 0 and not self.save and hr is None and B % TAIL_CHUNK == 0:
+            bc = TAIL_CHUNK
         dout = loss_part = None
-        if hr is not None:
-            dout = ctx.alloc((B, hh, ww, 16)) if self.save else ctx.scratch("dout", (B, hh, ww, 16))
-            loss_part = ctx.scratch("loss_part", (B * tiles(hh, ww), 1), torch.float32)
-        conv(ctx, h, Wt.packed("conv_last", 0), B, hh, ww, C, s.out_ch, bias=p["conv_last.bias"],
-             epi=L.EPI_LAST, y=out, lr=x_lr, scale=s.scale, clamp=0 if training else 1, hr=hr, dout=dout,
-             l1_scale=l1_scale, loss_part=loss_part)
+        for b0 in range(0, B, bc):
+            h, hh, ww = fb[b0:b0 + bc], H, W
+            stages = []
+            for st in range(s.n_stages):
+                key = f"upsample.stages.{st}."
+                shp = (bc, 2 * hh, 2 * ww, C)
+                a = ctx.alloc(shp) if self.save else ctx.scratch(f"up_a{st & 1}", shp)
+                v = ctx.alloc(shp) if self.save else None
+                if c128(hh, ww):
+                    c128_launch("c128_upsample", 4, h, Wt.packed(key + "conv", 1), p[key + "conv.bias"], a,
+                                alpha_=p[key + "prelu.weight"], b_=bc)
+                else:
+                    conv(ctx, h, Wt.packed(key + "conv", 1), bc, hh, ww, C, 4 * C, bias=p[key + "conv.bias"],
+                         epi=L.EPI_PRELU | L.EPI_SHUFFLE, alpha=p[key + "prelu.weight"], y=a, y_pre=v,
+                         pre_elide=PRE_ELIDE)
+                stages.append(dict(x=h, v=v, a=a, H=hh, W=ww))
+                h, hh, ww = a, 2 * hh, 2 * ww
+            if hr is not None:
+                dout = ctx.alloc((B, hh, ww, 16)) if self.save else ctx.scratch("dout", (B, hh, ww, 16))
+                loss_part = ctx.scratch("loss_part", (B * tiles(hh, ww), 1), torch.float32)
+            conv(ctx, h, Wt.packed("conv_last", 0), bc, hh, ww, C, s.out_ch, bias=p["conv_last.bias"],
+                 epi=L.EPI_LAST, y=out[b0:b0 + bc], lr=x_lr[b0:b0 + bc], scale=s.scale, clamp=0 if training else 1,
+                 hr=hr, dout=dout, l1_scale=l1_scale, loss_part=loss_part)
         saved = dict(feat=feat, fb=fb, stages=stages, a_last=h, dout=dout, loss_part=loss_part, Ho=hh, Wo=ww)
         return out, saved
 
@@ -747,9 +770,12 @@ class Backward:
     def _strip_bwd_ok(self, sv: dict, dy: torch.Tensor, extra_res: Sequence) -> bool:
         B, H, W, C = dy.shape
         blocks = sv.get("blocks") or []
-        return (GROUP_STRIP_BWD and self.s.NB > 0 and len(extra_res) <= 1 and self.ctx.code != L.F32
-                and len(blocks) == self.s.NB and all(b.get("z1") is not None for b in blocks)
-                and bool(self.ctx.lib.fen_group_strip_bwd_supported(self.ctx.code, B, H, W, C, self.s.Cr, self.s.NB)))
+        ok = (GROUP_STRIP_BWD and self.s.NB > 0 and len(extra_res) <= 1 and self.ctx.code != L.F32
+              and len(blocks) == self.s.NB and all(b.get("z1") is not None for b in blocks)
+              and bool(self.ctx.lib.fen_group_strip_bwd_supported(self.ctx.code, B, H, W, C, self.s.Cr, self.s.NB)))
+        if sv.get("z1_elided") and not ok:   # only the strip backward recovers an unwritten z1
+            raise L.FenError("group backward: the forward elided z1 but the strip backward does not apply")
+        return ok
 
     def _group_strip_bwd(self, sv: dict, dy: torch.Tensor, pre: str, extra_res: Sequence, dx_out) -> torch.Tensor:
         """The group's backward in one fen_group_strip_bwd launch (data gradients, SE backward,
@@ -774,6 +800,8 @@ class Backward:
             d.alpha[b] = ptr(p[q + "prelu.weight"])
             d.fc1[b], d.fc2[b] = ptr(p[ca + "0.weight"]), ptr(p[ca + "2.weight"])
             d.z1[b], d.t[b] = ptr(blk["z1"]), ptr(blk["t"])
+            if PRE_ELIDE:
+                d.a1[b] = ptr(blk["a1"])
             d.s[b], d.mean[b], d.hid[b] = ptr(blk["s"]), ptr(blk["mean"]), ptr(blk["hid"])
             o = dict(dt=ctx.scratch(f"gsb_dt{b}", dy.shape), dz1=ctx.scratch(f"gsb_dz1{b}", dy.shape),
                      dal=ctx.scratch(f"gsb_dal{b}", (B * H, C), torch.float32),
@@ -847,8 +875,8 @@ class Backward:
         dal = ctx.scratch(f"bw_dal_up{len(stages) - 1}", (rows, C), torch.float32)
         du = ctx.scratch(f"bw_du{(len(stages) - 1) & 1}", (B, last["H"], last["W"], 4 * C))
         ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, Ho, Wo, C, s.out_ch, ptr(sv["dout"]),
-                 ptr(p["conv_last.weight"]), ptr(last["v"]), ptr(p[f"upsample.stages.{len(stages) - 1}.prelu.weight"]),
-                 ptr(du), ptr(dal))
+                 ptr(p["conv_last.weight"]), ptr(last["v"]), ptr(last["a"]) if PRE_ELIDE else None,
+                 ptr(p[f"upsample.stages.{len(stages) - 1}.prelu.weight"]), ptr(du), ptr(dal))
         self.cs.add(dal, rows, C, G[f"upsample.stages.{len(stages) - 1}.prelu.weight"])
         for st in reversed(range(len(stages))):
             info = stages[st]
@@ -861,7 +889,8 @@ class Backward:
                 T = tiles(hh, ww)
                 dal = ctx.scratch(f"bw_dal_up{st - 1}", (B * T, C), torch.float32)
                 conv(ctx, du, Wt.packed(key + "conv", 2), B, hh, ww, 4 * C, C, epi=L.EPI_PRELU_BWD | L.EPI_UNSHUFFLE,
-                     alpha=p[f"upsample.stages.{st - 1}.prelu.weight"], pre_in=prev["v"], y=du_prev, part=dal)
+                     alpha=p[f"upsample.stages.{st - 1}.prelu.weight"], pre_in=prev["v"], y=du_prev, part=dal,
+                     post_in=prev["a"] if PRE_ELIDE else None)
                 self.cs.add(dal, B * T, C, G[f"upsample.stages.{st - 1}.prelu.weight"])
                 du = du_prev
             else:

@@ -83,6 +83,14 @@ typedef struct {
      * tile (its data gradient, mode-2 pack, Cout = 4C).  0 = off.  Streamed kernel only.       */
     int s2d_in;
     int s2d_out;
+    /* Training's saved pre-activation of a PReLU with positive slopes is redundant: for an
+     * aligned group of 4 channels (c & ~3 .. +3) whose slopes are all > 0, v = y > 0 ? y : y/alpha.
+     * pre_elide (FEN_EPI_PRELU with y_pre): the kernel MAY skip y_pre for such groups (it may
+     * also write it).  post_in (FEN_EPI_PRELU_BWD): the PReLU output y, same layout as pre_in, or
+     * NULL; for such groups the pre-activation is recovered from post_in and pre_in is not read,
+     * every other group reads pre_in.  (The upsampler stages, blocks.py:225-226.)              */
+    int pre_elide;
+    const void* post_in;
 } fen_conv_desc;
 
 int fen_conv3x3(const fen_conv_desc* d, void* stream);
@@ -134,11 +142,13 @@ int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const fl
 
 /* conv_last data gradient fused with the previous stage's PReLU backward and the
  * PixelShuffle inverse: dout NHWC16 [B,H,W,16] -> du NHWC [B,H/2,W/2,4C];
- * pre = that stage's pre-activation NHWC [B,H,W,C]; part[B*tiles][C] dalpha partials.    */
+ * pre = that stage's pre-activation NHWC [B,H,W,C]; part[B*tiles][C] dalpha partials.
+ * post = that stage's PReLU output (same layout) or NULL: as fen_conv_desc.post_in, groups of
+ * 4 channels with all slopes > 0 recover the pre-activation from it and do not read pre.   */
 size_t fen_conv_last_dgrad_part_rows(int B, int H, int W);
 int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const void* dout,
-                        const float* w, const void* pre, const float* alpha, void* du,
-                        float* part, void* stream);
+                        const float* w, const void* pre, const void* post, const float* alpha,
+                        void* du, float* part, void* stream);
 
 /* Channel attention (blocks.py:44-92) forward: pool partials -> s = sigmoid(W2 relu(W1 mean)) */
 int fen_se_fwd(int B, int C, int Cr, int nparts, float inv_hw, const float* part,
@@ -272,6 +282,9 @@ typedef struct {
     int fault;                         /* test-only fault injection: nonzero = the block with
                                           ticket 1 skips RCAB 0's a1 flag (its neighbour's wait
                                           times out after ~1 s); 0 in production              */
+    /* training: sv_z1[j] is not written when every slope alpha[j][c] is > 0 (z1 = a1 > 0 ? a1 :
+     * a1 / alpha then; fen_group_strip_bwd given a1 recovers it); 0 = always written          */
+    int pre_elide;
 } fen_group_strip_desc;
 #define FEN_STATUS_GS_FWD 1            /* a fen_group_strip wait timed out (output invalid)     */
 #define FEN_STATUS_GS_BWD 2            /* a fen_group_strip_bwd wait timed out                  */
@@ -360,6 +373,10 @@ typedef struct {
     size_t work_bytes;
     int* status;                       /* as fen_group_strip_desc.status (FEN_STATUS_GS_BWD)   */
     int fault;                         /* test-only: ticket 1 skips the first RCAB's dz1 flag  */
+    /* optional (NULL = off): the saved a1 = PReLU(z1); for an RCAB whose slopes are all > 0 the
+     * pre-activation is recovered from it (a1 > 0 ? a1 : a1 / alpha) and z1[j] is not read --
+     * the forward's pre_elide                                                                */
+    const void* a1[FEN_GS_MAXNB];
 } fen_group_strip_bwd_desc;
 int fen_group_strip_bwd_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
 size_t fen_group_strip_bwd_work_bytes(int B, int H);

@@ -169,10 +169,15 @@ def test_group_strip_training_saves_match_chain(B, H):
     x_j, z1, a1, t_j, s, mean, hid and the chain's output -- equal to the per-RCAB training
     launches' saved tensors within the chain tolerance (2e-3 rel per RCAB; the two kernels sum
     in different orders), the gates within 2e-3; the output as in test_group_strip_vs_deferred_chain."""
+    from src.hip import net
     dtype, n = torch.bfloat16, 4
     q = _params(n, seed=21)
     x = torch.randn(B, H, 64, 64, generator=torch.Generator().manual_seed(4)).to(DEV, dtype)
-    ys, svs, used = _run_save(q, n, x, dtype, True)
+    old_pe, net.PRE_ELIDE = net.PRE_ELIDE, False      # every saved tensor written (z1 included)
+    try:
+        ys, svs, used = _run_save(q, n, x, dtype, True)
+    finally:
+        net.PRE_ELIDE = old_pe
     yd, svd, used_d = _run_save(q, n, x, dtype, False)
     assert used and not used_d
     tol = 2e-3 * (n + 1)

@@ -221,3 +221,33 @@ def test_group_strip_bwd_graph_replay():
         for k in G:
             assert torch.equal(G[k], g_e[k]), k
         assert _work_error(ctx) == [(0, 0, 0)]
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_group_strip_pre_elide(mixed, monkeypatch):
+    """fen_group_strip_desc.pre_elide / fen_group_strip_bwd_desc.a1 (net.PRE_ELIDE): the training
+    forward leaves z1 unwritten for an RCAB whose slopes are all > 0 and the backward recovers
+    it from a1.  PReLU' depends on z1's sign only, so dx and every gradient but the slopes' are
+    bit-identical to the run that saves z1; the slopes' gradient (sum g * z1 over z1 <= 0)
+    differs by a1's rounding (bf16: 2^-9 relative per term).  mixed: RCAB 1 has one slope
+    <= 0 -- it saves and reads z1, so its slope gradient is bit-identical too."""
+    from src.hip import net
+    B, H, n = 4, 64, 3
+    q = _params(n, seed=31)
+    if mixed:
+        q["rg.blocks.1.prelu.weight"][3] = -0.1
+    _, _, _, x, dy, _ = _inputs(B, H, torch.bfloat16, seed=32)
+    out = {}
+    for el in (False, True):
+        monkeypatch.setattr(net, "PRE_ELIDE", el)
+        dx, G, ctx, used = _fwd_bwd(q, n, x, dy, torch.bfloat16, True)
+        assert used
+        assert all(e == 0 for (_, _, e) in _work_error(ctx))
+        out[el] = (dx.clone(), {k: v.clone() for k, v in G.items()})
+    assert torch.equal(out[True][0], out[False][0])
+    for k, g0 in out[False][1].items():
+        g1 = out[True][1][k]
+        if k.endswith("prelu.weight") and not (mixed and k.startswith("rg.blocks.1.")):
+            assert _rel(g1, g0) <= 1e-2, (k, _rel(g1, g0))
+        else:
+            assert torch.equal(g1, g0), k

@@ -132,10 +132,13 @@ def test_conv_dot_epilogue(dtype, B, H, W, nres):
 
 
 @pytest.mark.parametrize("dtype", DT_FWD)
-def test_upsample_conv_shuffle_prelu(dtype):
+@pytest.mark.parametrize("B,H,W", [(2, 16, 32), (2, 16, 64), (1, 24, 128)])
+def test_upsample_conv_shuffle_prelu(dtype, B, H, W):
+    """The upsampler stage conv (64 -> 256 + bias + PixelShuffle + PReLU, y_pre kept), partial
+    and full tile rows, several tiles per block."""
     from src.hip import lib as L, net
     torch.manual_seed(2)
-    B, H, W, C = 2, 16, 32, 64
+    C = 64
     x = torch.randn(B, C, H, W)
     w = torch.randn(4 * C, C, 3, 3) * 0.05
     b = torch.randn(4 * C) * 0.1
@@ -597,3 +600,125 @@ def test_s2d_stride2_conv(dtype, B, H, W, Cin, Cout):
     L.check(ctx.lib.fen_s2d2(ctx.code, B, H, W, Cin, ptr(xs), ptr(back), 1, s), "s2d_inv")
     torch.cuda.synchronize()
     assert torch.equal(back, xd)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,H,W,C", [(2, 64, 64, 64), (1, 36, 20, 64), (1, 40, 24, 32), (1, 32, 32, 128)])
+def test_conv_last_dgrad(dtype, B, H, W, C):
+    """fen_conv_last_dgrad (conv_last^T 3 -> C + the last upsampler stage's PReLU backward +
+    PixelShuffle inverse + dalpha partials) against torch autograd of conv(prelu(v)) in fp32;
+    16-bit at C <= 64 runs the LDS pre-activation tile, the rest the per-pixel reads; H = 36
+    leaves a partial tile row."""
+    from src.hip.program import ptr
+    torch.manual_seed(21)
+    Co = 3
+    v = torch.randn(B, C, H, W)
+    a = (torch.rand(C) * 0.5).requires_grad_(True)
+    w = torch.randn(Co, C, 3, 3) * 0.05
+    g = torch.randn(B, Co, H, W)
+    ctx = _ctx(dtype)
+    vq = nhwc(v, dtype)
+    vv = nchw(vq).requires_grad_(True)            # the rounded operand the kernel sees
+    F.conv2d(O.prelu(vv, a), w, None, padding=1).mul(g).sum().backward()
+    ref = vv.grad.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H // 2, W // 2)
+    dout = torch.zeros(B, H, W, 16)
+    dout[..., :Co] = g.permute(0, 2, 3, 1)
+    gq = dout.to(DEV, dtype)
+    du = ctx.alloc((B, H // 2, W // 2, 4 * C))
+    rows = ctx.lib.fen_conv_last_dgrad_part_rows(B, H, W)
+    part = ctx.alloc((rows, C), torch.float32)
+    wd, ad = w.to(DEV).contiguous(), a.detach().to(DEV)
+    ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, H, W, C, Co, ptr(gq), ptr(wd), ptr(vq),
+             None, ptr(ad), ptr(du), ptr(part))
+    torch.cuda.synchronize()
+    if dtype != torch.float32:                    # dout rounded to 16 bits too: compare against that
+        gg = gq[..., :Co].float().cpu().permute(0, 3, 1, 2)
+        vv.grad = None
+        a.grad = None
+        F.conv2d(O.prelu(vv, a), w, None, padding=1).mul(gg).sum().backward()
+        ref = vv.grad.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H // 2, W // 2)
+    assert (nchw(du) - ref).abs().max() <= _tol(dtype, ref)
+    da = part.sum(0).cpu()
+    rel = float((da - a.grad).norm() / a.grad.norm())
+    assert rel <= (1e-5 if dtype == torch.float32 else 1e-4), rel
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("amode", ["pos", "mixed"])
+@pytest.mark.parametrize("H,W", [(16, 16), (8, 64)])
+def test_pre_elide_upsampler(dtype, amode, H, W):
+    """fen_conv_desc.pre_elide / post_in and fen_conv_last_dgrad's post: the upsampler stage's
+    forward skips y_pre where every slope of its 64-channel block is > 0 (left NaN here), and the
+    backward kernels recover v = a > 0 ? a : a / alpha for 4-channel groups whose slopes are all
+    > 0 and read pre only for the others -- pre is NaN wherever it must not be read.  Results
+    against torch autograd of conv(prelu(v)) on the kernel's own rounded v."""
+    from src.hip import lib as L, net
+    from src.hip.program import ptr
+    torch.manual_seed(23)
+    B, C = 2, 64
+    alpha = torch.rand(C) * 0.4 + 0.05
+    if amode == "mixed":
+        alpha[5], alpha[9], alpha[40] = -0.2, 0.0, -0.05
+    mixed_grp = torch.zeros(C, dtype=torch.bool)
+    for c in range(0, C, 4):
+        mixed_grp[c:c + 4] = bool((alpha[c:c + 4] <= 0).any())
+    ctx = _ctx(dtype)
+    x = torch.randn(B, C, H, W)
+    w_up = torch.randn(4 * C, C, 3, 3) * 0.05
+    b_up = torch.randn(4 * C) * 0.1
+    wp = _pack(ctx, w_up, 1)
+    a = ctx.alloc((B, 2 * H, 2 * W, C))
+    v = torch.full((B, 2 * H, 2 * W, C), float("nan"), device=DEV, dtype=dtype)
+    net.conv(ctx, nhwc(x, dtype), wp, B, H, W, C, 4 * C, bias=b_up.to(DEV), epi=L.EPI_PRELU | L.EPI_SHUFFLE,
+             alpha=alpha.to(DEV), y=a, y_pre=v, pre_elide=1)
+    torch.cuda.synchronize()
+    if amode == "pos":
+        assert bool(torch.isnan(v).all())                  # not written
+        vref = torch.where(a.float() > 0, a.float(), a.float() / alpha.to(DEV))
+    else:
+        assert bool(torch.isfinite(v).all())               # the block has a slope <= 0: written
+        vref = v.float()
+    # backward 1: conv_last dgrad from (pre with NaN in the recoverable groups, post = a)
+    Co, Hs, Ws = 3, 2 * H, 2 * W
+    pre_bwd = v.clone()
+    pre_bwd[..., ~mixed_grp.to(DEV)] = float("nan")
+    wl = torch.randn(Co, C, 3, 3) * 0.05
+    g = torch.randn(B, Co, Hs, Ws)
+    dout = torch.zeros(B, Hs, Ws, 16)
+    dout[..., :Co] = g.permute(0, 2, 3, 1)
+    gq = dout.to(DEV, dtype)
+    du = ctx.alloc((B, H, W, 4 * C))
+    part = ctx.alloc((ctx.lib.fen_conv_last_dgrad_part_rows(B, Hs, Ws), C), torch.float32)
+    wld, ad = wl.to(DEV).contiguous(), alpha.to(DEV)
+    ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, Hs, Ws, C, Co, ptr(gq), ptr(wld),
+             ptr(pre_bwd), ptr(a), ptr(ad), ptr(du), ptr(part))
+    torch.cuda.synchronize()
+    vv = vref.cpu().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    al = alpha.clone().requires_grad_(True)
+    gg = gq[..., :Co].float().cpu().permute(0, 3, 1, 2)
+    F.conv2d(O.prelu(vv, al), wl, None, padding=1).mul(gg).sum().backward()
+    ref = vv.grad.reshape(B, C, H, 2, W, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H, W)
+    assert bool(torch.isfinite(du.float()).all())
+    assert (nchw(du) - ref).abs().max() <= _tol(dtype, ref)
+    rel = float((part.sum(0).cpu() - al.grad).norm() / al.grad.norm())
+    # "mixed": the reference's v is the kernel's rounded v, the kernel's recovered a / alpha
+    # differs from it by the output rounding (bf16: 2^-9 relative) in the recovered groups
+    assert rel <= (1e-3 if amode == "pos" else 1e-2), rel
+    # backward 2: the stage dgrad epilogue (PRELU_BWD | UNSHUFFLE) with pre_in / post_in
+    w2 = torch.randn(4 * C, C, 3, 3) * 0.05
+    dy = torch.randn(B, 4 * C, Hs, Ws)
+    wp2 = _pack(ctx, w2, 2)
+    du2 = ctx.alloc((B, H, W, 4 * C))
+    part2 = ctx.alloc((B * net.tiles(Hs, Ws), C), torch.float32)
+    net.conv(ctx, nhwc(dy, dtype), wp2, B, Hs, Ws, 4 * C, C, epi=L.EPI_PRELU_BWD | L.EPI_UNSHUFFLE, alpha=ad,
+             pre_in=pre_bwd, post_in=a, y=du2, part=part2)
+    torch.cuda.synchronize()
+    vv.grad = None
+    al.grad = None
+    dyq = nhwc(dy, dtype).float().cpu().permute(0, 3, 1, 2)
+    F.conv2d(O.prelu(vv, al), w2, None, padding=1).mul(dyq).sum().backward()
+    ref2 = vv.grad.reshape(B, C, H, 2, W, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H, W)
+    assert bool(torch.isfinite(du2.float()).all())
+    assert (nchw(du2) - ref2).abs().max() <= _tol(dtype, ref2)
+    rel2 = float((part2.sum(0).cpu() - al.grad).norm() / al.grad.norm())
+    assert rel2 <= 2e-2, rel2

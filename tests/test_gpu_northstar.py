@@ -83,3 +83,30 @@ def test_g9_engine_batch32(g9, precision):
     for i in range(16):
         assert torch.equal(out[2 * i:2 * i + 2], out[:2]), i
     _check(out[:2], g9, precision)
+
+
+@pytest.mark.parametrize("chunk", [8, 4])
+def test_g9_engine_tail_chunks(g9, chunk, monkeypatch):
+    """FEN_TAIL_CHUNK: the inference upsampler + conv_last over the batch in chunks (the
+    activations stay in the Infinity Cache).  Images are independent, so the chunked engine's
+    output is bit-identical to the one-pass engine's at B=32 (fp16), and still matches the
+    reference."""
+    from src.hip import net
+    from src.hip.engine import FENEngine
+    m = seeded_model(full_ctor("fp16"), g9).to(DEV).eval()
+    x = torch.from_numpy(g9["lr"]).repeat(16, 1, 1, 1).to(DEV)
+    outs = {}
+    for c in (0, chunk):
+        monkeypatch.setattr(net, "TAIL_CHUNK", c)
+        eng = FENEngine(m, batch=32, lr_hw=(64, 64), dtype=torch.float16, train=False)
+        ncv = sum(op[0] == "conv3x3" for op in eng.ctx.ops)
+        outs.setdefault("ncv", []).append(ncv)
+        eng.x.copy_(x)
+        eng.capture()
+        eng.replay()
+        torch.cuda.synchronize()
+        outs[c] = eng.out.cpu()
+        del eng
+    assert outs["ncv"][1] - outs["ncv"][0] == 3 * (32 // chunk - 1)   # 2 upsampler stages + conv_last per chunk
+    assert torch.equal(outs[chunk], outs[0])
+    _check(outs[chunk][:2], g9, "fp16")

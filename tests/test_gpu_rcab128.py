@@ -240,3 +240,24 @@ def test_rcab128_net_vs_oracle(prec):
     err = float((out - ref).abs().max())
     print(f"{prec}: max |out - oracle| {err:.2e}")
     assert err <= (6e-3 if prec == "fp16" else 2e-2), err
+
+
+def test_rcab128_net_tail_chunks(monkeypatch):
+    """The 128-channel engine with its upsampler + conv_last in chunks of 2 images (FEN_TAIL_CHUNK)
+    is bit-identical to the one-pass engine at B=4."""
+    from src.hip import net
+    from src.hip.engine import FENEngine
+    from src.models import FaceEnhanceNet
+    torch.manual_seed(3)
+    m = FaceEnhanceNet(num_channels=C, num_groups=1, blocks_per_group=2, reduction_ratio=4, scale_factor=4,
+                       precision="fp16")
+    x = torch.rand(4, 3, 64, 64, generator=torch.Generator().manual_seed(12)).to(DEV)
+    outs = {}
+    for c in (0, 2):
+        monkeypatch.setattr(net, "TAIL_CHUNK", c)
+        eng = FENEngine(m, batch=4, lr_hw=(64, 64), dtype=torch.float16, train=False, device=DEV)
+        names = [op[0] for op in eng.ctx.ops]
+        assert names.count("c128_upsample") == (2 if c == 0 else 4)
+        outs[c] = eng.forward(x).cpu()
+        del eng
+    assert torch.equal(outs[2], outs[0])

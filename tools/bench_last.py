@@ -51,7 +51,7 @@ print(json.dumps({"pool_dot_us": round(us, 2), "GBs": round(2 * ta.numel() * 2 /
 pre = torch.randn(B, 256, 256, 64, device='cuda', dtype=torch.bfloat16); al = torch.full((64,), 0.25, device='cuda')
 du = torch.empty(B, 128, 128, 256, device='cuda', dtype=torch.bfloat16); do.normal_()
 dal = torch.empty(ctx.lib.fen_conv_last_dgrad_part_rows(B, 256, 256), 64, device='cuda')
-us = timeit(lambda: ctx.emit('cld', ctx.lib.fen_conv_last_dgrad, ctx.code, B, 256, 256, 64, 3, ptr(do), ptr(wl), ptr(pre),
+us = timeit(lambda: ctx.emit('cld', ctx.lib.fen_conv_last_dgrad, ctx.code, B, 256, 256, 64, 3, ptr(do), ptr(wl), ptr(pre), None,
                              ptr(al), ptr(du), ptr(dal)))
 print(json.dumps({"conv_last_dgrad_us": round(us, 2), "GBs": round((pre.numel() * 2 + du.numel() * 2 + do.numel() * 2) / us / 1e3, 1),
                   "du_sum": float(du.float().abs().sum())}))

@@ -3,8 +3,8 @@
 # then (DPOV=1) the DP exchange overlap measurement
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_gpu_group_strip.py tests/test_gpu_group_strip_bwd.py tests/test_gpu_strip_status.py tests/test_gpu_ssim.py -m gpu -v -s -x --timeout 200 --timeout-method thread > gpurun_out/ab_tests.log 2>&1
-rc=$?; echo "strip tests rc=$rc"; grep -E "passed|failed|Error" gpurun_out/ab_tests.log | tail -4
+timeout -k 10 500 python -u -m pytest ${TESTS:-tests/test_gpu_group_strip.py tests/test_gpu_group_strip_bwd.py tests/test_gpu_strip_status.py tests/test_gpu_ssim.py} -m gpu -v -s -x --timeout 200 --timeout-method thread > gpurun_out/ab_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|Error" gpurun_out/ab_tests.log | tail -4
 [ $rc -eq 0 ] || { tail -30 gpurun_out/ab_tests.log; exit 1; }
 libs="face-super-resolution_amd/src/hip/libfen_hip.so $(ls face-super-resolution_amd/csrc/build_var/libfen_hip_*.so 2>/dev/null)"
 for rep in 1 2; do
@@ -28,6 +28,9 @@ timeout -k 10 120 python tools/op_times.py 2>&1 | grep -v amdgpu.ids | tail -30
 if [ "${STAMPS:-0}" = "1" ] && [ -f face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so ]; then
   FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so timeout -k 10 200 python tools/stamp_strip.py 2>&1 | grep -v amdgpu.ids
   FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_gsstamp.so timeout -k 10 200 python tools/stamp_strip_bwd.py 2>&1 | grep -v amdgpu.ids
+fi
+if [ "${UPSTAMP:-0}" = "1" ]; then
+  FEN_HIP_LIB=face-super-resolution_amd/csrc/build_stamp/libfen_hip_stamp.so UP=1 REPS=12000 timeout -k 10 200 python tools/stamp_conv.py 2>&1 | grep -v amdgpu.ids
 fi
 if [ "${DPOV:-0}" = "1" ]; then
   timeout -k 10 400 python tools/dp_overlap.py > gpurun_out/dp_overlap.json 2> gpurun_out/dp_overlap.log

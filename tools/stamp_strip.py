@@ -34,7 +34,7 @@ def main():
     eng = FENEngine(m, batch=B, lr_hw=(64, 64), dtype=torch.float16, train=False, device="cuda")
     _, x = bench_batch(B, 0)
     eng.x.copy_(x)
-    for _ in range(5):
+    for _ in range(int(os.environ.get("REPS", "1500"))):   # >= 2 s back to back: the clock under load
         eng.forward()
     torch.cuda.synchronize()
     buf = eng.ctx._shared["pz:group_strip/32x64"]
@@ -45,6 +45,8 @@ def main():
     med = np.median
     print(f"launch: first conv ready {med(st[:, :, 1]):.2f} us; end {med(st[:, 0, NSTAMP - 1]):.2f} us "
           f"(max {st[:, 0, NSTAMP - 1].max():.2f})")
+    ghz = st[:, 1, NSTAMP - 1] * 100 * 16 / np.maximum(st[:, 0, NSTAMP - 1] * 1000, 1)
+    print(f"in-kernel shader clock (s_memtime / s_memrealtime over each block's life): median {med(ghz):.3f} GHz")
     rows = []
     for j in range(1, 10):
         b = 2 + 9 * j
