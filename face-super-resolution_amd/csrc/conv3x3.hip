@@ -203,6 +203,9 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
 #pragma unroll
         for (int r = 0; r < 4; ++r) psum[m][r] = 0.f;
 
+    bool rec4[MT];                                        // PRELU_BWD from post_in (see fen.h)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) rec4[m] = (epi & FEN_EPI_PRELU_BWD) && d.post_in && all_pos4(ec.alpha[m]);
     // pass 1: elementwise epilogue in registers (acc <- pre-activation value)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -228,13 +231,10 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                     }
                 }
                 if (epi & FEN_EPI_PRELU_BWD) {
+                    // post_in (every slope of the group > 0): the PReLU output has the
+                    // pre-activation's sign; the slope partials are rescaled by 1 / alpha below
                     float pv[4];
-                    const bool rec = d.post_in && all_pos4(al4);   // pre-activation from the PReLU output
-                    ld4<T>((const char*)(rec ? d.post_in : d.pre_in) + oi * sizeof(T), pv);
-                    if (rec) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) pv[r] = prelu_pre_from_post(pv[r], __builtin_amdgcn_rcpf(al4[r]));
-                    }
+                    ld4<T>((const char*)(rec4[m] ? d.post_in : d.pre_in) + oi * sizeof(T), pv);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         psum[m][r] += prelu_dalpha_f(v[r], pv[r]);
@@ -264,7 +264,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
         for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float s = group16_sum(psum[m][r]);
+                const float s = group16_sum(psum[m][r]) * (rec4[m] ? __builtin_amdgcn_rcpf(ec.alpha[m][r]) : 1.f);
                 if (c16 == 0) red[wr * COT + wc * CW + m * 16 + q * 4 + r] = s;
             }
         epi_barrier<RAW>();
@@ -858,10 +858,6 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                             pf[1] = hi16<T>(pv[m][n].x);
                             pf[2] = lo16<T>(pv[m][n].y);
                             pf[3] = hi16<T>(pv[m][n].y);
-                            if (PBWD && rec_m[m]) {
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) pf[r] = prelu_pre_from_post(pf[r], __builtin_amdgcn_rcpf(al4[r]));
-                            }
                         }
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -916,7 +912,9 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                     for (int m = 0; m < MT; ++m)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            const float sv = group16_sum(psum[m][r]);
+                            // PBWD from post_in: the slope partials were taken over the PReLU output
+                            const float sv = group16_sum(psum[m][r]) *
+                                             ((PBWD && rec_m[m]) ? __builtin_amdgcn_rcpf(cst[64 + m * 16 + 4 * q + r]) : 1.f);
                             if (c16 == 0) rg[m * 16 + 4 * q + r] = sv;
                         }
                     pending_part = t;

@@ -180,12 +180,6 @@ __device__ __forceinline__ float prelu_bwd_f(float dy, float pre, float a) {
 }
 // contribution to dL/da: dy * pre where pre <= 0
 __device__ __forceinline__ float prelu_dalpha_f(float dy, float pre) { return dy * pre * (1.f - pos_step(pre)); }
-// the pre-activation recovered from the PReLU output y, given ia = 1 / slope (slope > 0):
-// y > 0 ? y : y * ia (fen_conv_desc.post_in; ia = 1 leaves y unchanged)
-__device__ __forceinline__ float prelu_pre_from_post(float y, float ia) {
-    const float s = pos_step(y);
-    return y * (s + (1.f - s) * ia);
-}
 __device__ __forceinline__ bool all_pos4(const float* a) { return a[0] > 0.f && a[1] > 0.f && a[2] > 0.f && a[3] > 0.f; }
 
 // The wave index, provably wave-uniform to the compiler (threadIdx.x >> 6 alone is divergent

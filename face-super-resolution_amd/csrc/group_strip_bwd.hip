@@ -397,16 +397,13 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                 for (int m = 0; m < 4; ++m) {
                     const float4 aa = *(const float4*)(cst + 16 * m + 4 * q);
                     const float alp[4] = {aa.x, aa.y, aa.z, aa.w};
-                    // recovery factor: z = a1 * (s + (1 - s) * ia), ia = 1 / alpha (1: z1 as read)
-                    const float ia[4] = {recz ? __builtin_amdgcn_rcpf(alp[0]) : 1.f, recz ? __builtin_amdgcn_rcpf(alp[1]) : 1.f,
-                                         recz ? __builtin_amdgcn_rcpf(alp[2]) : 1.f, recz ? __builtin_amdgcn_rcpf(alp[3]) : 1.f};
                     float ds[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int p = 0; p < 4; ++p) {
-                        const float z[4] = {prelu_pre_from_post(lo16<T>(zv[m][p].x), ia[0]),
-                                            prelu_pre_from_post(hi16<T>(zv[m][p].x), ia[1]),
-                                            prelu_pre_from_post(lo16<T>(zv[m][p].y), ia[2]),
-                                            prelu_pre_from_post(hi16<T>(zv[m][p].y), ia[3])};
+                        // recz: a1 has z1's sign (PReLU' is exact); the slope partial sums
+                        // g * a1 over a1 <= 0, i.e. alpha times the z1 sum: scaled by 1 / alpha below
+                        const float z[4] = {lo16<T>(zv[m][p].x), hi16<T>(zv[m][p].x), lo16<T>(zv[m][p].y),
+                                            hi16<T>(zv[m][p].y)};
                         float v[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
@@ -417,7 +414,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                     }
                     float sv[4];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) sv[i] = group16_sum(ds[i]);
+                    for (int i = 0; i < 4; ++i) sv[i] = group16_sum(ds[i]) * (recz ? __builtin_amdgcn_rcpf(alp[i]) : 1.f);
                     if (c16 == 0)
                         *(float4*)(dal + (size_t)(im * H + r0 + wave) * 64 + 16 * m + 4 * q) =
                             make_float4(sv[0], sv[1], sv[2], sv[3]);

@@ -511,7 +511,8 @@ __global__ __launch_bounds__(1024) void k_conv_first_finalize(int nb, int Ci, in
 // C <= 64 (LPRE) the block's whole pre-activation tile (16x16 px x C, <= 32 KB) is loaded into
 // LDS together with the dout halo -- one round trip per block instead of one per du pixel.
 template <typename T, int C>
-__global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, int Co, const T* __restrict__ dout,
+__global__ __launch_bounds__(256) void k_conv_last_dgrad(
+                                  int B, int H, int W, int Co, const T* __restrict__ dout,
                                   const float* __restrict__ w, const T* __restrict__ pre, const T* __restrict__ post,
                                   const float* __restrict__ alpha, T* __restrict__ du, float* __restrict__ part) {
     constexpr int K2 = C / 2;
@@ -534,9 +535,9 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
         // each group of 4 channels from post (slopes all > 0: recovered below) or pre; the
         // thread's chunk (8 channels) is the same for all its pieces
         const int pcq = tid % PPR;
-        const bool r0 = post && all_pos4(alpha + pcq * 8), r1 = post && all_pos4(alpha + pcq * 8 + 4);
-        const char* src0 = (const char*)(r0 ? post : pre);
-        const char* src1 = (const char*)(r1 ? post : pre);
+        // the tile is read from post when given (no wait on the slopes first); a half whose group
+        // of 4 has a slope <= 0 is read again from pre afterwards (the rare case)
+        const char* src = (const char*)(post ? post : pre);
         uint4 v[(PRE_U4 + 255) / 256];
 #pragma unroll
         for (int j = 0; j < (PRE_U4 + 255) / 256; ++j) {
@@ -544,13 +545,28 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
             const int px = i / PPR;
             const int gh = h0 + (px >> 4), gw = w0 + (px & 15);
             v[j] = make_uint4(0u, 0u, 0u, 0u);
-            if (i < PRE_U4 && gh < H && gw < W) {
-                const size_t o = (((size_t)(b * H + gh) * W + gw) * C) * 2 + pcq * 16;
-                if (r0 == r1) {
-                    v[j] = *(const uint4*)(src0 + o);
-                } else {
-                    const uint2 lo = *(const uint2*)(src0 + o), hi = *(const uint2*)(src1 + o + 8);
-                    v[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            if (i < PRE_U4 && gh < H && gw < W)
+                v[j] = *(const uint4*)(src + (((size_t)(b * H + gh) * W + gw) * C) * 2 + pcq * 16);
+        }
+        if (post) {
+            const bool r0 = all_pos4(alpha + pcq * 8), r1 = all_pos4(alpha + pcq * 8 + 4);
+            if (!(r0 && r1)) {
+#pragma unroll
+                for (int j = 0; j < (PRE_U4 + 255) / 256; ++j) {
+                    const int i = tid + j * 256;
+                    const int px = i / PPR;
+                    const int gh = h0 + (px >> 4), gw = w0 + (px & 15);
+                    if (i < PRE_U4 && gh < H && gw < W) {
+                        const char* o = (const char*)pre + (((size_t)(b * H + gh) * W + gw) * C) * 2 + pcq * 16;
+                        if (!r0) {
+                            const uint2 lo = *(const uint2*)o;
+                            v[j].x = lo.x, v[j].y = lo.y;
+                        }
+                        if (!r1) {
+                            const uint2 hi = *(const uint2*)(o + 8);
+                            v[j].z = hi.x, v[j].w = hi.y;
+                        }
+                    }
                 }
             }
         }
@@ -579,9 +595,10 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
             for (int t = 0; t < 9; ++t)
                 wr[e][co][t] = co < Co ? w[((size_t)co * C + 2 * k + e) * 9 + t] : 0.f;
     const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
-    const bool rec = post && all_pos4(alpha + ((2 * k) & ~3));   // this pair's group of 4
-    // branch-free recovery: p = y * (s + (1 - s) * ia) is y itself when ia = 1 (read from pre)
-    const float ia0 = rec ? __builtin_amdgcn_rcpf(al0) : 1.f, ia1 = rec ? __builtin_amdgcn_rcpf(al1) : 1.f;
+    // post (this pair's group of 4 has every slope > 0): p below is the PReLU output a, which has
+    // the pre-activation's sign (all PReLU' needs); where a <= 0 the pre-activation is a / alpha,
+    // so the slope gradient's sum of da * p * [p <= 0] is taken over a and scaled once at the end
+    const bool rec = post && all_pos4(alpha + ((2 * k) & ~3));
     __syncthreads();
     float dal0 = 0.f, dal1 = 0.f;
     const int Hh = H >> 1, Wh = W >> 1;
@@ -615,8 +632,6 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
                 p0 = tof<T>(src[pi]);
                 p1 = tof<T>(src[pi + 1]);
             }
-            p0 = prelu_pre_from_post(p0, ia0);
-            p1 = prelu_pre_from_post(p1, ia1);
             dal0 += prelu_dalpha_f(da0, p0);
             dal1 += prelu_dalpha_f(da1, p1);
             out[t] = prelu_bwd_f(da0, p0, al0);
@@ -629,6 +644,10 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(int B, int H, int W, in
             *(uint4*)o = pack16<float>(out);
             *(uint4*)(o + 16) = pack16<float>(out + 4);
         }
+    }
+    if (rec) {
+        dal0 *= __builtin_amdgcn_rcpf(al0);
+        dal1 *= __builtin_amdgcn_rcpf(al1);
     }
     sdal[tid * 2] = dal0;
     sdal[tid * 2 + 1] = dal1;

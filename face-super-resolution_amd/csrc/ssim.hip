@@ -72,6 +72,24 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     for (int k = 0; k < CB; ++k)
 #pragma unroll
         for (int o = 0; o < CW2; ++o) dacc[k][o] = 0.f;
+    // the E2 x E2 inputs of a channel: every load of the thread issued before the first LDS write
+    // (one memory round trip per channel instead of one per 256 elements); with CB > 1 the next
+    // channel's are issued as soon as this one's are in LDS, under its passes
+    constexpr int NLD = (E2 * E2 + 255) / 256;
+    float lp[NLD], lt[NLD];
+    auto load_in = [&](int chn) {
+        const size_t pl = (size_t)(b * C + chn) * H * W;
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int i = tid + k * 256;
+            const int r = i / E2, c = i % E2, gy = gy0 + r, gx = gx0 + c;
+            const bool in = i < E2 * E2 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+            const size_t e = in ? pl + (size_t)gy * W + gx : 0;
+            lp[k] = in ? pred[e] : 0.f;
+            lt[k] = in ? target[e] : 0.f;
+        }
+    };
+    load_in(CB > 1 ? 0 : (int)blockIdx.z % C);
 #pragma unroll
     for (int cc = 0; cc < CB; ++cc) {
     if (CB > 1 && cc >= C) break;
@@ -80,13 +98,17 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     const float* pp = pred + (size_t)plane * H * W;
     const float* tp = target + (size_t)plane * H * W;
     if (CB > 1 && cc > 0) __syncthreads();                // the previous channel's reads of sb / hp / red done
-    for (int i = tid; i < E2 * E2; i += 256) {
-        const int r = i / E2, c = i % E2, gy = gy0 + r, gx = gx0 + c;
-        const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-        sp[r * PS + c] = in ? pp[(size_t)gy * W + gx] : 0.f;
-        st[r * PS + c] = in ? tp[(size_t)gy * W + gx] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+        const int i = tid + k * 256;
+        if (i < E2 * E2) {
+            const int r = i / E2, c = i % E2;
+            sp[r * PS + c] = lp[k];
+            st[r * PS + c] = lt[k];
+        }
     }
     __syncthreads();
+    if (CB > 1 && cc + 1 < CB && cc + 1 < C) load_in(cc + 1);
     for (int i = tid; i < E2 * NCH; i += 256) {
         const int r = i / NCH, c0 = (i % NCH) * CW;
         float o[5][CW];
@@ -181,12 +203,19 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
                 }
             }
             if (gx >= W) continue;
+            float pr[CW2], tr[CW2];                               // L2-hot: this block staged them
+#pragma unroll
+            for (int o = 0; o < CW2; ++o) {
+                const int gy = min(h0 + r0 + o, H - 1);
+                pr[o] = pp[(size_t)gy * W + gx];
+                tr[o] = tp[(size_t)gy * W + gx];
+            }
 #pragma unroll
             for (int o = 0; o < CW2; ++o) {
                 const int gy = h0 + r0 + o;
                 if (gy >= H) break;
                 const size_t e = (size_t)gy * W + gx;
-                const float p = pp[e], t = tp[e];                // L2-hot: this block staged them
+                const float p = pr[o], t = tr[o];
                 const float d = grad_scale * (m[0][o] + 2.f * p * m[1][o] + t * m[2][o]);
                 if constexpr (CB > 1) {
                     dacc[cc][o] = d;
