@@ -313,8 +313,10 @@ def time_gan_step(steps, B=16):
     return {"metric": "training images/sec (stage-3 GAN iteration: D update + G update, L1 0.01 + perceptual 1 + "
                       "adversarial 0.005) at batch 16/GPU", "value": round(B * steps / el, 2),
             "ms_per_step": round(1000.0 * el / steps, 3), "steps": steps, "loss": loss,
-            "path": "Trainer iteration replayed from a captured hipGraph (capture_gan_step; module autograd "
-                    "over the HIP kernels), VGG19 and D random-init",
+            "path": ("Trainer iteration replayed from a captured hipGraph (capture_gan_step; module autograd "
+                     "over the HIP kernels), VGG19 and D random-init" if tr._capture_gan() else
+                     "Trainer iteration, eager (N > 1: the module path's hook-issued RCCL all-reduces are not "
+                     "captured unless FEN_GAN_CAPTURE_DP=1), VGG19 and D random-init"),
             "eager": {"value": round(B * steps / el_e, 2), "ms_per_step": round(1000.0 * el_e / steps, 3)}}
 
 

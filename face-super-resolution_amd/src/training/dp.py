@@ -41,6 +41,10 @@ def init_rccl(device: torch.device, **kw) -> None:
                            "step needs it off (ProcessGroupNCCL re-records cached events inside the "
                            "capture). Unset it or set it to 0.")
     os.environ[EVENT_CACHE_VAR] = "0"
+    # the flight recorder keeps every collective's events for its dumps; nothing here reads
+    # them, and an entry recorded inside a capture is one more event a host-side query can
+    # trip on (a user's explicit setting is kept)
+    os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "0")
     dist.init_process_group("nccl", device_id=device, **kw)
 
 

@@ -315,15 +315,20 @@ class Trainer:
         return loss.detach()
 
     def _capture_gan(self) -> bool:
-        """World size 1, or N > 1 over RCCL with the event cache off (`dp.init_rccl`): the
-        exchanges are stream-ordered (RCCL on side streams forked and joined inside the captured
-        iteration).  gloo (host-staged) or a user's own `init_process_group('nccl')` with the
-        event cache on run the iteration eagerly."""
+        """World size 1: captured.  With an exchange (N > 1, or the tests' forced one-rank
+        group) the iteration runs eagerly unless FEN_GAN_CAPTURE_DP=1 (and then only over RCCL
+        with the event cache off, `dp.init_rccl`): the module path's all-reduces are issued from
+        autograd's post-accumulate hooks, and a capture of them aborted the process in
+        ProcessGroupNCCL's watchdog (hipErrorCapturedEvent) once in the round-4 GPU runs after
+        a clean series -- an abort takes the whole run with it, so the capture is opt-in there.
+        The engine's DP step (collectives from the program's marks) stays captured."""
+        import os
         from .dp import _rccl_capture_ok
         if not (bool(self.config.capture_gan_step) and torch.cuda.is_available() and self._accum() == 1):
             return False
         if self.world > 1 or getattr(self, "_dp_force", False):
-            return dist.is_available() and dist.is_initialized() and _rccl_capture_ok()
+            return (os.environ.get("FEN_GAN_CAPTURE_DP") == "1" and dist.is_available() and dist.is_initialized()
+                    and _rccl_capture_ok())
         return True
 
     def _make_d_capturable(self) -> None:

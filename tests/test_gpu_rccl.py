@@ -127,18 +127,23 @@ def test_engine_captured_step_over_rccl():
         dist.destroy_process_group()
 
 
-def test_gan_captured_iteration_over_rccl(tmp_path):
+def test_gan_iteration_over_rccl(tmp_path):
     """The stage-3 GAN iteration with the module path's bucketed exchanges (dp.ParamGradExchange:
     the generator's tail / group / head buckets and the discriminator's two, each all-reduced
     from a post-accumulate hook as the backward completes it, stream-ordered), forced on a
-    one-rank RCCL group and replayed from a captured hipGraph: bit-identical to the eager,
-    exchange-free iteration (losses, generator arena, discriminator parameters and buffers)."""
+    one-rank RCCL group: bit-identical to the exchange-free iteration (losses, generator arena,
+    discriminator parameters and buffers).  With an exchange the iteration runs eagerly unless
+    FEN_GAN_CAPTURE_DP=1 (Trainer._capture_gan: a capture of hook-issued RCCL collectives
+    aborted in ProcessGroupNCCL's watchdog once); with it set, the replayed graph is checked too."""
+    import os
     from test_gpu_gan_capture import _state, _trainer
     eager = _trainer(False, tmp_path / "e")
     _init_one_rank()
     try:
         cap = _trainer(True, tmp_path / "c")
         cap._dp_force = True
+        captured = os.environ.get("FEN_GAN_CAPTURE_DP") == "1"
+        assert cap._capture_gan() == captured
         gen = torch.Generator().manual_seed(5)
         for i in range(5):
             hr = torch.rand(2, 3, 128, 128, generator=gen).to(DEV)
@@ -147,7 +152,8 @@ def test_gan_captured_iteration_over_rccl(tmp_path):
             assert le == lc, (i, le, lc)
             for a, b in zip(_state(eager), _state(cap)):
                 assert torch.equal(a, b), i
-        assert cap._gan_graph is not None and cap._g_ex is not None and cap._d_ex is not None
+        assert (cap._gan_graph is not None) == captured
+        assert cap._g_ex is not None and cap._d_ex is not None
         assert len(cap._g_ex.ranges) == 2 + 1 and len(cap._d_ex.ranges) == 2   # tail, rg0, head
     finally:
         dist.destroy_process_group()
