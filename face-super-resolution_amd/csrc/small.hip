@@ -660,161 +660,6 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(
     }
 }
 
-// The same op on MFMA (16-bit, C = 32 / 64): per block the 256 source pixels' conv_last^T is the
-// GEMM [256 px x 32 k] x [32 k x C], k = 3 * tap + co (27 real, 5 zero), one 16x16x32 k-step.
-// Wave w takes the block's du pixels 16w .. 16w+15 as 4 m-tiles whose 16 rows are (du pixel,
-// sub-position t), so a lane's 4 accumulator rows are the 4 values of du[pixel][4c .. 4c+3]:
-// PReLU backward on them and ONE 8-B store.  A fragments are gathered from the dout halo in
-// LDS, B fragments (the weights, bf16 / fp16) built once per block; the pre-activation tile in
-// LDS as in k_conv_last_dgrad.  Replaces 1728 VALU FMAs per du pixel with 4 MFMAs per 16 rows:
-// the launch is then bound by its 67 + 268 MB of reads and 268 MB of writes (B=32, 256x256).
-template <typename T, int C>
-__global__ __launch_bounds__(256) void k_conv_last_dgrad_m(int B, int H, int W, int Co, const T* __restrict__ dout,
-                                                           const float* __restrict__ w, const T* __restrict__ pre,
-                                                           const T* __restrict__ post, const float* __restrict__ alpha,
-                                                           T* __restrict__ du, float* __restrict__ part) {
-    static_assert(sizeof(T) == 2 && (C == 32 || C == 64), "16-bit, C = 32 or 64");
-    constexpr int NT = C / 16;                       // 16-channel n-tiles
-    constexpr int PRE_U4 = 256 * C * 2 / 16;
-    constexpr int PPR = C * 2 / 16;
-    __shared__ float sd[18 * 18 * 4];                // dout tile + halo, channels 0..2 (3 = pad)
-    __shared__ uint4 spre[PRE_U4];                   // [16 rows][16 px][C]
-    __shared__ float sdal[4][C];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q = lane >> 4, c16 = lane & 15;
-    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
-    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
-    const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
-    const int Hh = H >> 1, Wh = W >> 1;
-    // ---- the pre-activation tile (post when given; halves with a slope <= 0 re-read from pre)
-    {
-        const int pcq = tid % PPR;
-        const char* src = (const char*)(post ? post : pre);
-        uint4 v[PRE_U4 / 256];
-#pragma unroll
-        for (int j = 0; j < PRE_U4 / 256; ++j) {
-            const int px = (tid + j * 256) / PPR;
-            const int gh = h0 + (px >> 4), gw = w0 + (px & 15);
-            v[j] = make_uint4(0u, 0u, 0u, 0u);
-            if (gh < H && gw < W) v[j] = *(const uint4*)(src + (((size_t)(b * H + gh) * W + gw) * C) * 2 + pcq * 16);
-        }
-        if (post) {
-            const bool r0 = all_pos4(alpha + pcq * 8), r1 = all_pos4(alpha + pcq * 8 + 4);
-            if (!(r0 && r1)) {
-#pragma unroll
-                for (int j = 0; j < PRE_U4 / 256; ++j) {
-                    const int px = (tid + j * 256) / PPR;
-                    const int gh = h0 + (px >> 4), gw = w0 + (px & 15);
-                    if (gh < H && gw < W) {
-                        const char* o = (const char*)pre + (((size_t)(b * H + gh) * W + gw) * C) * 2 + pcq * 16;
-                        if (!r0) {
-                            const uint2 lo = *(const uint2*)o;
-                            v[j].x = lo.x, v[j].y = lo.y;
-                        }
-                        if (!r1) {
-                            const uint2 hi = *(const uint2*)(o + 8);
-                            v[j].z = hi.x, v[j].w = hi.y;
-                        }
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < PRE_U4 / 256; ++j) spre[tid + j * 256] = v[j];
-    }
-    // ---- the dout halo (fp32 in LDS)
-    for (int i = tid; i < 18 * 18; i += 256) {
-        const int r = i / 18, c = i % 18;
-        const int gh = h0 + r - 1, gw = w0 + c - 1;
-        float t4[4] = {0.f, 0.f, 0.f, 0.f};
-        if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
-            ld4<T>((const char*)dout + ((size_t)(b * H + gh) * W + gw) * 16 * sizeof(T), t4);
-        *(float4*)(sd + i * 4) = make_float4(t4[0], Co > 1 ? t4[1] : 0.f, Co > 2 ? t4[2] : 0.f, 0.f);
-    }
-    // ---- B fragments: lane (q, c16) of n-tile n holds w[co][n*16 + c16][tap] for k = 8q .. 8q+7
-    uint4 bw[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-        float f[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int k = 8 * q + e, tap = k / 3, co = k - 3 * tap;
-            f[e] = (k < 27 && co < Co) ? w[((size_t)co * C + n * 16 + c16) * 9 + tap] : 0.f;
-        }
-        bw[n] = pack16<T>(f);
-    }
-    // slopes of this lane's channels; a 4-channel group with every slope > 0 read post (its
-    // slope partial rescaled by 1 / alpha at the end)
-    float al[NT];
-    bool rec[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-        const int c = n * 16 + c16;
-        al[n] = alpha[c];
-        rec[n] = post && all_pos4(alpha + (c & ~3));
-    }
-    __syncthreads();
-    // ---- per m-tile: its A fragment (row c16 = (du pixel dp = 16 wave + 4m + c16 / 4, t = c16 % 4)),
-    // NT MFMAs, then the epilogue of its accumulators: lane (q, c16) holds rows 4q + r = (du
-    // pixel 16 wave + 4m + q, t = r), channel n*16 + c16 -- PReLU backward at the pre-activation,
-    // the slope partials, one 8-B store
-    float dal[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) dal[n] = 0.f;
-    const unsigned short* sp16 = (const unsigned short*)spre;
-#pragma unroll 1
-    for (int m = 0; m < 4; ++m) {
-        uint4 af;
-        {
-            const int dp = 16 * wave + 4 * m + (c16 >> 2), t = c16 & 3;
-            const int sh = 2 * (dp >> 3) + (t >> 1), sw = 2 * (dp & 7) + (t & 1);   // local source pixel
-            float f[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int k = 8 * q + e, tap = k / 3, co = k - 3 * tap;
-                const int kh = tap / 3, kw = tap - 3 * kh;
-                f[e] = k < 27 ? sd[((sh - kh + 2) * 18 + (sw - kw + 2)) * 4 + co] : 0.f;
-            }
-            af = pack16<T>(f);
-        }
-        f32x4 acc[NT];
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-            acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-            mma16<T>(acc[n], af, bw[n]);
-        }
-        const int dp = 16 * wave + 4 * m + q;
-        const int hh = dp >> 3, ww = dp & 7;
-        const int gh2 = (h0 >> 1) + hh, gw2 = (w0 >> 1) + ww;
-        const bool valid = gh2 < Hh && gw2 < Wh;
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-            const int c = n * 16 + c16;
-            float o[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int sh = 2 * hh + (r >> 1), sw = 2 * ww + (r & 1);
-                const float p = lo16<T>((unsigned)sp16[(sh * 16 + sw) * C + c]);
-                const float da = acc[n][r];
-                dal[n] += valid ? prelu_dalpha_f(da, p) : 0.f;
-                o[r] = prelu_bwd_f(da, p, al[n]);
-            }
-            if (valid) st4<T>((char*)du + (((size_t)(b * Hh + gh2) * Wh + gw2) * (4 * C) + 4 * c) * sizeof(T), o);
-        }
-    }
-    // the 4 lanes of a channel (q = 0..3), then the 4 waves, in a fixed order
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-        float v = dal[n];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        if (rec[n]) v *= __builtin_amdgcn_rcpf(al[n]);
-        if (q == 0) sdal[wave][n * 16 + c16] = v;
-    }
-    __syncthreads();
-    if (tid < C) part[(size_t)blockIdx.x * C + tid] = (sdal[0][tid] + sdal[1][tid]) + (sdal[2][tid] + sdal[3][tid]);
-}
-
 // ------------------------------- channel attention -------------------------------
 // blocks.py:83-92: mean -> fc0 (C->Cr, no bias) -> ReLU -> fc2 (Cr->C) -> sigmoid, for image
 // b, by one 256-thread block, into sg[C] (LDS).  Written for latency: every global load of a
@@ -1711,16 +1556,6 @@ extern "C" size_t fen_conv_last_dgrad_part_rows(int B, int H, int W) {
     return (size_t)B * ((H + 15) / 16) * ((W + 15) / 16);
 }
 
-// FEN_CLD_VALU=1: the VALU form for 16-bit too (A/B)
-static bool cld_valu() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("FEN_CLD_VALU");
-        v = (e && e[0] == '1') ? 1 : 0;
-    }
-    return v == 1;
-}
-
 extern "C" int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const void* dout, const float* w,
                                    const void* pre, const void* post, const float* alpha, void* du, float* part,
                                    void* stream) {
@@ -1733,10 +1568,6 @@ extern "C" int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co
             hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, STREAM, B, H, W, Co, (const T*)dout, w, (const T*)pre,
                                (const T*)post, alpha, (T*)du, part);
         };
-        if constexpr (sizeof(T) == 2) {     // 16-bit at C = 32 / 64: the MFMA form
-            if (C == 32 && !cld_valu()) { go(k_conv_last_dgrad_m<T, 32>); return FEN_OK; }
-            if (C == 64 && !cld_valu()) { go(k_conv_last_dgrad_m<T, 64>); return FEN_OK; }
-        }
         switch (C) {
             case 32: go(k_conv_last_dgrad<T, 32>); break;
             case 64: go(k_conv_last_dgrad<T, 64>); break;

@@ -631,14 +631,11 @@ def test_conv_last_dgrad(dtype, B, H, W, C):
     ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, H, W, C, Co, ptr(gq), ptr(wd), ptr(vq),
              None, ptr(ad), ptr(du), ptr(part))
     torch.cuda.synchronize()
-    if dtype != torch.float32:
-        # dout rounded to 16 bits too, and at C <= 64 the MFMA form's 16-bit weights: compare
-        # against those operands
+    if dtype != torch.float32:                    # dout rounded to 16 bits too: compare against that
         gg = gq[..., :Co].float().cpu().permute(0, 3, 1, 2)
-        wq = w.to(dtype).float() if C <= 64 else w
         vv.grad = None
         a.grad = None
-        F.conv2d(O.prelu(vv, a), wq, None, padding=1).mul(gg).sum().backward()
+        F.conv2d(O.prelu(vv, a), w, None, padding=1).mul(gg).sum().backward()
         ref = vv.grad.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H // 2, W // 2)
     assert (nchw(du) - ref).abs().max() <= _tol(dtype, ref)
     da = part.sum(0).cpu()
@@ -699,8 +696,7 @@ def test_pre_elide_upsampler(dtype, amode, H, W):
     vv = vref.cpu().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
     al = alpha.clone().requires_grad_(True)
     gg = gq[..., :Co].float().cpu().permute(0, 3, 1, 2)
-    # the 16-bit conv_last dgrad runs on MFMA with 16-bit weights
-    F.conv2d(O.prelu(vv, al), wl.to(dtype).float(), None, padding=1).mul(gg).sum().backward()
+    F.conv2d(O.prelu(vv, al), wl, None, padding=1).mul(gg).sum().backward()
     ref = vv.grad.reshape(B, C, H, 2, W, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H, W)
     assert bool(torch.isfinite(du.float()).all())
     assert (nchw(du) - ref).abs().max() <= _tol(dtype, ref)
