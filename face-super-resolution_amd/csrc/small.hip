@@ -1194,8 +1194,17 @@ struct ColJobK {
     float scale;
     int accumulate;
     int blk0;   // first block of this job
+    int nsplit; // row slices (tall narrow jobs): blocks per 64-column block
+    int slot0;  // its first slot in the split scratch
 };
 constexpr int COLSUM_MAXJ = 40;
+// Tall narrow jobs (the strip backward's slope rows, 2048 x 64 per RCAB) are split into up to 8
+// row slices, one block each; the slices' partial rows go through this scratch and the last
+// block of a column block sums them in slice order (deterministic).  One colsum launch at a
+// time uses it (they run on the launching stream, in program order).
+constexpr int COLSUM_SLOTS = 2 * COLSUM_MAXJ;
+__device__ float g_cs_part[COLSUM_SLOTS][8][64];
+__device__ unsigned g_cs_cnt[COLSUM_SLOTS];
 struct ColJobs {
     int n;
     ColJobK j[COLSUM_MAXJ];
@@ -1226,16 +1235,19 @@ __global__ __launch_bounds__(1024) void k_colsum_multi(const ColJobs jobs) {
         }
         return;
     }
-    const int c = ((int)blockIdx.x - jb.blk0) * 64 + lane;
+    const int local = (int)blockIdx.x - jb.blk0, ns = jb.nsplit;
+    const int cb = local / ns, sp = local - cb * ns;
+    const int c = cb * 64 + lane;
+    // this block's rows: [r_lo, r_hi) of slice sp
+    const int r_lo = (int)((long long)rows * sp / ns), r_hi = (int)((long long)rows * (sp + 1) / ns);
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     if (c < cols) {
-        const float* p = jb.part + c;
+        const float* p = jb.part + (size_t)r_lo * cols + c;
+        const int rows_ = r_hi - r_lo;
         int r = w;
-        // 32 rows in flight per lane: the tall jobs (the strip backward's dalpha rows, 2048 x 64,
-        // conv_last's 8192 x 64 at B=32) are one block wide, so their time is rows / 512
-        // dependent memory round trips (8 in flight measured 19 us per launch at 2048 rows)
+        // 32 rows in flight per lane (a tall narrow job's slice is one or two round trips)
         float a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f;
-        for (; r + 496 < rows; r += 512) {
+        for (; r + 496 < rows_; r += 512) {
             float v[32];
 #pragma unroll
             for (int k = 0; k < 32; ++k) v[k] = p[(size_t)(r + 16 * k) * cols];
@@ -1245,7 +1257,7 @@ __global__ __launch_bounds__(1024) void k_colsum_multi(const ColJobs jobs) {
                 a4 += v[k + 4]; a5 += v[k + 5]; a6 += v[k + 6]; a7 += v[k + 7];
             }
         }
-        for (; r + 112 < rows; r += 128) {
+        for (; r + 112 < rows_; r += 128) {
             a0 += p[(size_t)r * cols];
             a1 += p[(size_t)(r + 16) * cols];
             a2 += p[(size_t)(r + 32) * cols];
@@ -1256,22 +1268,46 @@ __global__ __launch_bounds__(1024) void k_colsum_multi(const ColJobs jobs) {
             a7 += p[(size_t)(r + 112) * cols];
         }
         a0 += a4; a1 += a5; a2 += a6; a3 += a7;
-        for (; r + 48 < rows; r += 64) {
+        for (; r + 48 < rows_; r += 64) {
             a0 += p[(size_t)r * cols];
             a1 += p[(size_t)(r + 16) * cols];
             a2 += p[(size_t)(r + 32) * cols];
             a3 += p[(size_t)(r + 48) * cols];
         }
-        for (; r < rows; r += 16) a0 += p[(size_t)r * cols];
+        for (; r < rows_; r += 16) a0 += p[(size_t)r * cols];
     }
     red[w][lane] = (a0 + a1) + (a2 + a3);
     __syncthreads();
-    if (w == 0 && c < cols) {
+    if (ns == 1) {
+        if (w == 0 && c < cols) {
+            float t = 0.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) t += red[k][lane];
+            t *= jb.scale;
+            jb.out[c] = jb.accumulate ? jb.out[c] + t : t;
+        }
+        return;
+    }
+    // split job: the slice's partial row out (agent-scope stores, drained), then one arrival;
+    // the column block's last arrival sums the slices in order (agent-scope loads)
+    __shared__ int last;
+    const int slot = jb.slot0 + cb;
+    if (w == 0) {
         float t = 0.f;
 #pragma unroll
         for (int k = 0; k < 16; ++k) t += red[k][lane];
+        __hip_atomic_store(&g_cs_part[slot][sp][lane], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            last = __hip_atomic_fetch_add(&g_cs_cnt[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ns - 1);
+    }
+    __syncthreads();
+    if (last && w == 0) {
+        float t = 0.f;
+        for (int k = 0; k < ns; ++k) t += __hip_atomic_load(&g_cs_part[slot][k][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t *= jb.scale;
-        jb.out[c] = jb.accumulate ? jb.out[c] + t : t;
+        if (c < cols) jb.out[c] = jb.accumulate ? jb.out[c] + t : t;
+        if (lane == 0) __hip_atomic_store(&g_cs_cnt[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1745,12 +1781,19 @@ extern "C" int fen_colsum_multi(int njobs, const fen_colsum_job* jobs, void* str
     if (njobs <= 0 || njobs > COLSUM_MAXJ || !jobs) return FEN_EINVAL;
     ColJobs k;
     k.n = njobs;
-    int blk = 0;
+    int blk = 0, slot = 0;
     for (int i = 0; i < njobs; ++i) {
         const fen_colsum_job& j = jobs[i];
         if (!j.part || !j.out || j.rows <= 0 || j.cols <= 0) return FEN_EINVAL;
-        k.j[i] = ColJobK{j.part, j.out, j.rows, j.cols, j.scale, j.accumulate, blk};
-        blk += j.cols == 1 ? 1 : (j.cols + 63) / 64;
+        const int ncb = (j.cols + 63) / 64;
+        // tall narrow jobs (conv_last's 8192 x 64 slope rows at B=32): up to 8 row slices of
+        // >= 512 rows.  At 2048 rows (the strip backward's, 10 per launch) a split measured
+        // 12.3 vs 11.2 us per launch: the split's combine costs more than the round trips saved
+        int ns = 1;
+        if (j.cols > 1 && ncb <= 2 && j.rows >= 4096 && slot + ncb <= COLSUM_SLOTS) ns = j.rows / 512 < 8 ? j.rows / 512 : 8;
+        k.j[i] = ColJobK{j.part, j.out, j.rows, j.cols, j.scale, j.accumulate, blk, ns, slot};
+        if (ns > 1) slot += ncb;
+        blk += j.cols == 1 ? 1 : ncb * ns;
     }
     hipLaunchKernelGGL(k_colsum_multi, dim3(blk), dim3(1024), 0, STREAM, k);
     FEN_CHECK_LAUNCH();

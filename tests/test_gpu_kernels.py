@@ -722,3 +722,39 @@ def test_pre_elide_upsampler(dtype, amode, H, W):
     assert (nchw(du2) - ref2).abs().max() <= _tol(dtype, ref2)
     rel2 = float((part2.sum(0).cpu() - al.grad).norm() / al.grad.norm())
     assert rel2 <= 2e-2, rel2
+
+
+def test_colsum_multi_split_jobs():
+    """fen_colsum_multi over the shapes the backward queues (the strip backward's slope rows
+    2048 x 64, conv_last's 8192 x 64, the SE rows 32 x 1024, a ragged 1000 x 96, the loss column),
+    tall narrow jobs split into row slices with an ordered last-block combine: column sums
+    (scaled, one accumulated) against float64 torch, and bit-identical on a repeat."""
+    import ctypes
+    from src.hip import lib as L
+    torch.manual_seed(31)
+    shapes = [(2048, 64), (8192, 64), (32, 1024), (1000, 96), (4096, 1), (700, 16)]
+    parts = [torch.randn(r, c, device=DEV) for r, c in shapes]
+    outs = [torch.randn(c, device=DEV) for _, c in shapes]
+    init = [o.clone() for o in outs]
+    lib = L.load()
+
+    def run():
+        arr = (L.ColsumJob * len(shapes))()
+        for i, ((r, c), p, o) in enumerate(zip(shapes, parts, outs)):
+            arr[i].part, arr[i].out, arr[i].rows, arr[i].cols = p.data_ptr(), o.data_ptr(), r, c
+            arr[i].scale, arr[i].accumulate = 0.5, int(i == 2)
+        L.check(lib.fen_colsum_multi(len(shapes), ctypes.cast(arr, ctypes.c_void_p),
+                                     torch.cuda.current_stream().cuda_stream), "colsum_multi")
+        torch.cuda.synchronize()
+
+    run()
+    for i, (p, o) in enumerate(zip(parts, outs)):
+        ref = p.double().sum(0) * 0.5 + (init[i].double() if i == 2 else 0.0)
+        assert float((o.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max())), i
+    first = [o.clone() for o in outs]
+    for i in range(len(outs)):
+        if i == 2:
+            outs[i].copy_(init[i])
+    run()
+    for a, b in zip(first, outs):
+        assert torch.equal(a, b)
