@@ -21,11 +21,12 @@ Also reported (field "train"): the stage-1 generator training step (bicubic /4 L
 synthesis, forward, L1, backward, RCCL gradient all-reduce over xGMI for N>1, clip,
 AdamW) at batch 32 per GPU -- the DP path of the north star.
 
-roofline: the dominant kernel is k_group_strip (group_strip.hip): one ResidualGroup -- 10 fused
-  RCABs (conv1 -> PReLU -> conv2 -> SE gate -> scaled residual) + the group conv + skip, 64 ch,
-  64x64, B=32 -- as one persistent launch; algorithmic FLOPs per launch = 21 convs x 2 *
-  32*64*64 px * 64 co * 576 (= 9 taps * 64 ci) = 203 GFLOP (9.66 per conv, 19.33 per RCAB),
-  timed live here with HIP events on the launch stream; peak = 2500 TFLOP/s fp16 / bf16 dense.
+roofline: the dominant kernel is k_group_strip (group_strip.hip) in its chained form
+  (fen_group_strip_chain): the body's 6 ResidualGroups -- each 10 fused RCABs (conv1 -> PReLU ->
+  conv2 -> SE gate -> scaled residual) + the group conv + skip, 64 ch, 64x64, B=32 -- as one
+  persistent launch; algorithmic FLOPs per launch = 6 x 21 convs x 2 * 32*64*64 px * 64 co *
+  576 (= 9 taps * 64 ci) = 1217.6 GFLOP (9.66 per conv, 19.33 per RCAB), timed live here
+  with HIP events on the launch stream; peak = 2500 TFLOP/s fp16 / bf16 dense.
 pcie_inclusive: the same forward with the batch handed over as NCHW fp32 pinned host buffers
 (H2D of the LR batch, graph replay, D2H of the SR batch, serial on one stream) -- reported
 beside `value`, never as it.
@@ -109,10 +110,19 @@ def timed(fn, steps, warmup, world):
 
 
 def dominant_op(engine):
-    """The launch the roofline is quoted on: a whole ResidualGroup (fen_group_strip: NB fused
-    RCABs -- conv1 + PReLU + conv2 + SE gate + scaled residual each -- and the group conv, one
-    persistent launch; algorithmic FLOPs = (2 NB + 1) 64->64 convs), else an RCAB of the per-RCAB
-    chain (fen_rcab_deferred), else the RCAB conv1 (64->64, 64x64, B=32) of the per-op path."""
+    """The launch the roofline is quoted on: the body's G ResidualGroups (fen_group_strip_chain,
+    one persistent launch; algorithmic FLOPs = G (2 NB + 1) 64->64 convs), else a whole
+    ResidualGroup (fen_group_strip: NB fused RCABs -- conv1 + PReLU + conv2 + SE gate + scaled
+    residual each -- and the group conv; (2 NB + 1) convs), else an RCAB of the per-RCAB chain
+    (fen_rcab_deferred), else the RCAB conv1 (64->64, 64x64, B=32) of the per-op path."""
+    for op in engine.ctx.ops:
+        if op[0] == "group_strip_chain":
+            ds, ng = op[2]
+            d = ds[0]
+            conv = 2.0 * d.B * d.H * d.W * 64 * 576
+            return op, "k_group_strip chain (the body: %d ResidualGroups in one launch, each %d x [conv1+PReLU+conv2+" \
+                       "SE gate+residual] + group conv + skip, 64ch %dx%d, B=%d)" % (ng, d.nb, d.H, d.W, d.B), \
+                ng * (2 * d.nb + 1) * conv
     for op in engine.ctx.ops:
         if op[0] == "group_strip":
             d = op[2][0]._obj
@@ -347,13 +357,14 @@ def load_traffic(label):
     (profiles/rNN_pmc_*.json, tools/prof_summary.py pmc; the latest round's first), or None
     when none matches it."""
     import glob
+    best = None                                   # the longest matching key; latest round first
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_*.json")), reverse=True):
         with open(p) as f:
             js = json.load(f)
         key = js.get("kernel_key")
-        if key and label.startswith(key):
-            return js.get("hbm_bytes_per_launch")
-    return None
+        if key and label.startswith(key) and (best is None or len(key) > len(best[0])):
+            best = (key, js.get("hbm_bytes_per_launch"))
+    return best[1] if best else None
 
 
 def main():

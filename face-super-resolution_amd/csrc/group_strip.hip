@@ -36,6 +36,11 @@
 // (rcab_deferred.hip) rounds them (t rounded before the gate product, as if stored).
 #include "strip_common.h"
 
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
 namespace {
 
 using namespace gs;
@@ -85,25 +90,41 @@ static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignmen
 
 // workspace: control words, counters, pool partials, boundary rows
 struct Ws {
-    size_t cnt, flg, part, bx, bt, ba, total;
+    size_t cnt, flg, part, bx, bt, ba, bo, stamp, total;
 };
 __host__ __device__ inline Ws ws_layout(int B, int S) {
     Ws L;
     size_t o = 256;                          // [0] ticket [1] done [2] error [3] launch epoch
     L.cnt = o;
-    L.flg = o;  o += (size_t)B * S * 4 * 128;  // per (strip, side, kind) a flag on its own line
+    L.flg = o;  o += (size_t)B * S * 6 * 128;  // per (strip, side, kind) a flag on its own line
     L.part = o; o += (size_t)B * 2 * S * 64 * 8;   // [img][parity][strip][64] {tag, value} granules
     o = (o + 255) & ~(size_t)255;
     const size_t rows = (size_t)B * S * 2 * 2 * ROWB;   // [img][strip][parity][side] rows
     L.bx = o; o += rows;
     L.bt = o; o += rows;
     L.ba = o; o += rows;
+    L.bo = o; o += rows / 2;                 // chained groups: a group output's boundary rows [img][strip][side]
+    L.stamp = o;
 #ifdef FEN_GS_STAMPS
     o += (size_t)B * S * 8 * NSTAMP * 2;            // [block ticket][wave][NSTAMP] u16 (10 ns ticks)
 #endif
     L.total = o;
     return L;
 }
+
+// chained groups (fen_group_strip_chain): per group its input / output and parameters, in
+// device memory after the workspace (a launch's arguments would exceed 4 KB)
+struct GsTab {
+    const void* x;
+    void* y;
+    const void* w[2 * FEN_GS_MAXNB + 1];
+    const float* bias[2 * FEN_GS_MAXNB + 1];
+    const float* alpha[FEN_GS_MAXNB];
+    const float* fc1[FEN_GS_MAXNB];
+    const float* fc2[FEN_GS_MAXNB];
+    float* s_out[FEN_GS_MAXNB];
+};
+inline size_t gs_tab_offset(int B, int S) { return (ws_layout(B, S).total + 255) & ~(size_t)255; }
 
 struct GsArgs {
     int B, H, S, NB, Cr;
@@ -128,10 +149,13 @@ struct GsArgs {
     int* status;                              // optional: a timed-out wait is reported here
     int fault;                                // test-only: image 0 strip 1 skips one a1 flag
     int pre_elide;                            // training: no z1 save for an RCAB whose slopes are all > 0
+    const GsTab* tab;                         // MULTI: ng groups in a row, parameters from here
+    int ng;
 };
 
-template <typename T, bool SAVE>
+template <typename T, bool SAVE, bool MULTI>
 __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
+    static_assert(!(SAVE && MULTI), "chained groups: inference only");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* img = smem + O_IMG;
     char* filt = smem + O_FILT;
@@ -158,6 +182,24 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     int S = A.S;
     const Ws L = ws_layout(B, S);
     int* ctl = (int*)A.work;
+    // the running group's input / output and parameters: the launch's arguments, or (MULTI,
+    // groups g = 0 .. ng-1 in a row, group g's output = group g+1's input) the table's row g
+    int g = 0;
+    const int NG = MULTI ? A.ng : 1;
+    // (table entries are wave-uniform: readfirstlane'd, whatever load the compiler picks)
+    auto uni = [](const void* p_) -> void* {
+        const unsigned long long v = (unsigned long long)p_;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+        return (void*)(((unsigned long long)hi << 32) | lo);
+    };
+    // the table through the constant address space: scalar loads (it is never written in a launch)
+    typedef const __attribute__((address_space(4))) GsTab CTab;
+    CTab* ctab = (CTab*)A.tab;
+    auto Gx = [&]() -> const void* { return MULTI ? uni(ctab[g].x) : A.x; };
+    auto Gy = [&]() -> void* { return MULTI ? uni(ctab[g].y) : A.y; };
+    auto Gw = [&](int ci) -> const void* { return MULTI ? uni(ctab[g].w[ci]) : A.w[ci]; };
+    auto Gb = [&](int ci) -> const float* { return MULTI ? (const float*)uni(ctab[g].bias[ci]) : A.bias[ci]; };
+    auto Ga = [&](int j_) -> const float* { return MULTI ? (const float*)uni(ctab[g].alpha[j_]) : A.alpha[j_]; };
 
     // ---- the strip: a ticket in start order (an image's strips are running blocks); the
     // launch's epoch (tags of this launch's hand-offs: never equal to an earlier launch's)
@@ -176,7 +218,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     __syncthreads();
     const int ticket = __builtin_amdgcn_readfirstlane(tick_lds[0]);
     const unsigned epoch = (unsigned)__builtin_amdgcn_readfirstlane(tick_lds[1]);
-    auto tag_of = [&](int j) -> unsigned { return (epoch << 8) | (unsigned)(j + 1); };
+    int kbase = 0, rbase = 0;                               // the group's first step / RCAB (MULTI)
+    // a step's tag: unique per (launch, group, step) (MULTI: ng * (nb + 1) < 255 steps)
+    auto tag_of = [&](int j) -> unsigned { return (epoch << 8) | (unsigned)(kbase + j + 1); };
 #ifdef FEN_GS_STAMPS
     const unsigned t_start = (unsigned)__builtin_amdgcn_readfirstlane(tick_lds[2]);   // the block's clock origin
 #endif
@@ -197,15 +241,17 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     const size_t act_bytes = (size_t)B * H * SW * 128;
     const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc((void*)A.work, 0, (int)L.total, 0x00020000);
     unsigned* flg = (unsigned*)(A.work + L.flg);
-    // one flag word per (strip, side, kind), own 128-B line: kind 0 = a1 row, 1 = x / t rows
-    auto flag_of = [&](int s_, int sd, int kind) -> unsigned* { return flg + (((im * S + s_) * 2 + sd) * 2 + kind) * 32; };
+    // one flag word per (strip, side, kind), own 128-B line: kind 0 = a1 row, 1 = x / t rows,
+    // 2 = a chained group's output row
+    auto flag_of = [&](int s_, int sd, int kind) -> unsigned* { return flg + (((im * S + s_) * 2 + sd) * 3 + kind) * 32; };
     auto rowoff = [&](size_t base, int s_, int par, int sd) -> int {
         return (int)(base + ((size_t)((im * S + s_) * 2 + par) * 2 + sd) * ROWB);
     };
+    auto booff = [&](int s_, int sd) -> int { return (int)(L.bo + ((size_t)(im * S + s_) * 2 + sd) * ROWB); };
 
     // ---- filter taps by LDS-DMA: tap k of conv `ci` into slot k (this wave's 1-KB piece)
-    auto issue_taps = [&](int ci, int k0, int n) {     // taps k0 .. k0 + n - 1
-        const i32x4 wr = make_rsrc(A.w[ci], 9u * 64u * 128u);
+    auto issue_taps = [&](const void* wp, int k0, int n) {     // taps k0 .. k0 + n - 1
+        const i32x4 wr = make_rsrc(wp, 9u * 64u * 128u);
         int ll = lane;
         asm volatile("" : "+v"(ll));
         const int s = wave * 64 + ll, r = s >> 3, pc = s & 7;
@@ -213,10 +259,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         for (int k = k0; k < k0 + n; ++k)
             dma16(wr, __builtin_amdgcn_readfirstlane(lds_addr(filt + k * TAPB + wave * 1024)), v0 + k * TAPB);
     };
-    auto issue_kh1 = [&](int ci) { issue_taps(ci, 3, 3); };
-    auto issue_kh02 = [&](int ci) {
-        issue_taps(ci, 0, 3);
-        issue_taps(ci, 6, 3);
+    auto issue_kh1 = [&](const void* wp) { issue_taps(wp, 3, 3); };
+    auto issue_kh02 = [&](const void* wp) {
+        issue_taps(wp, 0, 3);
+        issue_taps(wp, 6, 3);
     };
 
     // ---- per-lane helpers on the accumulator layout: lane (q, c16) holds channels
@@ -274,13 +320,13 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     };
 
     // ================= start-up: conv1_0's taps, x_0, constants =================
-    issue_taps(0, 0, 9);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, (int)act_bytes, 0x00020000);
+    issue_taps(Gw(0), 0, 9);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)Gx(), 0, (int)act_bytes, 0x00020000);
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int p = 0; p < 4; ++p)
-            xr[m][p] = *(const uint2*)((const char*)A.x + px_off(r0 + wave, p) + (16 * m + 4 * q) * 2);
+            xr[m][p] = *(const uint2*)((const char*)Gx() + px_off(r0 + wave, p) + (16 * m + 4 * q) * 2);
     if (bwave) {
         uint4 hv[8];
         const int row = wave == 0 ? r0 - 1 : r0 + SR;
@@ -294,9 +340,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         halo_to_lds(wave == 0 ? 0 : SR + 1, hv);
     }
     float cv = 0.f;
-    if (wave == 2) cv = A.bias[0][lane];
-    if (wave == 3) cv = A.alpha[0][lane];
-    if (wave == 4) cv = A.bias[1][lane];
+    if (wave == 2) cv = Gb(0)[lane];
+    if (wave == 3) cv = Ga(0)[lane];
+    if (wave == 4) cv = Gb(1)[lane];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;
     write_row_lds(wave + 1, xr);
@@ -314,9 +360,13 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     uint2 tr[4][4];                                         // t_j as stored (16-bit), for the next combine
     const int khP2 = wave == 0 ? 2 : 0, khP3 = 2 - khP2;   // wave 0's upper halo row is read last
     bool ok = true;
-    for (int j = 0; j <= NB; ++j) {
+    for (;;) {                                              // groups (one unless MULTI)
+    kbase = g * (NB + 1), rbase = g * NB;
+    for (int j = 0;; ++j) {                                // one exit: the group conv's break
         const bool gc = j == NB;
-        const int par = j & 1;
+        // boundary rows and pool partials double-buffered by RCAB count (not step: a group conv
+        // publishes neither, and each buffer's reuse is ordered by the hand-offs of the RCAB between)
+        const int par = (rbase + j) & 1;
         const int sb = 2 + 9 * j;                           // this step's stamp slots
         {
             // opaque per step: what is computed from these is recomputed here, not hoisted
@@ -334,15 +384,17 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
 #else
         const bool dma_late = false;
 #endif
-        if (j > 0) {
-            if (!dma_late) issue_kh02(ci);                  // this conv's kh = 0, 2 taps (slots free since B_G)
+        if (j > 0 || g > 0) {
+            if (!dma_late) issue_kh02(Gw(ci));              // this conv's kh = 0, 2 taps (slots free since B_G)
             if (wave >= 2 && wave <= 4) cst[(wave - 2) * 64 + lane] = cv;   // read after B_E / B_Z
+        }
+        if (j > 0) {
             // ---- x_j = x_{j-1} + rs * s * t_{j-1} (t as stored: rounded), own row in registers
-            float g[4][4];
+            float gt[4][4];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const float4 gv = *(const float4*)(gate + 16 * m + 4 * q);
-                g[m][0] = gv.x, g[m][1] = gv.y, g[m][2] = gv.z, g[m][3] = gv.w;
+                gt[m][0] = gv.x, gt[m][1] = gv.y, gt[m][2] = gv.z, gt[m][3] = gv.w;
             }
 #pragma unroll
             for (int m = 0; m < 4; ++m)
@@ -351,18 +403,18 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                     __builtin_amdgcn_sched_barrier(0);
                     const float x0 = lo16<T>(xr[m][p].x), x1 = hi16<T>(xr[m][p].x);
                     const float x2 = lo16<T>(xr[m][p].y), x3 = hi16<T>(xr[m][p].y);
-                    xr[m][p] = pk4<T>(lo16<T>(tr[m][p].x) * g[m][0] + x0, hi16<T>(tr[m][p].x) * g[m][1] + x1,
-                                      lo16<T>(tr[m][p].y) * g[m][2] + x2, hi16<T>(tr[m][p].y) * g[m][3] + x3);
+                    xr[m][p] = pk4<T>(lo16<T>(tr[m][p].x) * gt[m][0] + x0, hi16<T>(tr[m][p].x) * gt[m][1] + x1,
+                                      lo16<T>(tr[m][p].y) * gt[m][2] + x2, hi16<T>(tr[m][p].y) * gt[m][3] + x3);
                 }
-            write_row_lds(wave + 1, xr);
         }
+        if (j > 0 || g > 0) write_row_lds(wave + 1, xr);    // (a chained group's x_0: the previous output)
         // x_j's boundary rows for the neighbours (their halo rows of x_{j+1})
         if (!gc && bwave) store_row(wsr, rowoff(L.bx, strip, par, side), xr, 16);
         if (j > 0 && hwave) {
             // the neighbour's x_{j-1}, t_{j-1} rows (this wave's half), after its flag (its
             // storing wave drained them, then signalled): this wave polls and loads (row 1);
             // the loads land during phase 1
-            const int pp = (j - 1) & 1;
+            const int pp = (rbase + j - 1) & 1;
             const int ns = hs == 0 ? strip - 1 : strip + 1;
             ok = ok && poll_eq(flag_of(ns, 1 - hs, 1), tag_of(j - 1));
             const int ox = rowoff(L.bx, ns, pp, 1 - hs) + (lane + 64 * hk0) * 16;
@@ -373,7 +425,17 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 nt[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ot + k * 1024, 0, 16));
             }
         }
-        if (dma_late && j > 0) issue_kh02(ci);
+        if (MULTI && j == 0 && g > 0 && hwave) {
+            // a chained group's x_0 halo: this wave's half of the neighbour's previous group
+            // output row, after its flag (kind 2)
+            const int ns = hs == 0 ? strip - 1 : strip + 1;
+            ok = ok && poll_eq(flag_of(ns, 1 - hs, 2), tag_of(-1));
+            const int ox = booff(ns, 1 - hs) + (lane + 64 * hk0) * 16;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                nx[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wsr, ox + k * 1024, 0, 16));
+        }
+        if (dma_late && (j > 0 || g > 0)) issue_kh02(Gw(ci));
         if (SAVE && j > 0) {                                // x_0 is the group input
             asm volatile("" ::: "memory");                  // the saves after every op the wait below needs
             save_row(gc ? A.x_last : A.sv_x[j], xr);
@@ -409,9 +471,15 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 *(uint4*)(hb + k * 1024) = pack16<T>(yv);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else if (MULTI && j == 0 && g > 0 && hwave) {
+            char* hb = img + (hs == 0 ? 0 : SR + 1) * IROW + hcol((lane >> 3) + 1, lane & 7) + hk0 * 1024;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *(uint4*)(hb + k * 1024) = nx[k];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         __syncthreads();                                    // B_X: every image row written; kh = 1 slots free
-        if (!gc) issue_kh1(ci + 1);
+        if (!gc) issue_kh1(Gw(ci + 1));
+        else if (MULTI && g + 1 < NG) issue_kh1(uni(ctab[g + 1].w[0]));   // the next group's conv1_0
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
         GSTAMP(sb + 3);
@@ -419,11 +487,23 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             // ---- out = conv + bias + the group input (blocks.py:188-189): its own rows read
             // again here (once per launch; kept out of the conv's register peak)
             uint2 x0r[4][4];
+            if (MULTI) {
+                // sc1 loads: a chained group's input is the previous group's output, rows this
+                // wave stored in this launch
+                const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)Gx(), 0, (int)act_bytes, 0x00020000);
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
+                for (int m = 0; m < 4; ++m)
 #pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    x0r[m][p] = *(const uint2*)((const char*)A.x + px_off(r0 + wave, p) + (16 * m + 4 * q) * 2);
+                    for (int p = 0; p < 4; ++p)
+                        x0r[m][p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                                  grs, (int)(px_off(r0 + wave, p) + (16 * m + 4 * q) * 2), 0, 16));
+            } else {
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+                        x0r[m][p] = *(const uint2*)((const char*)A.x + px_off(r0 + wave, p) + (16 * m + 4 * q) * 2);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             uint2 ov[4][4];
 #pragma unroll
@@ -440,8 +520,33 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                     ov[m][p] = pk4<T>(v[0], v[1], v[2], v[3]);
                 }
             }
-            const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(A.y, 0, (int)act_bytes, 0x00020000);
+            const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(Gy(), 0, (int)act_bytes, 0x00020000);
             store_row(yrs, (int)((size_t)(im * H + r0 + wave) * SW * 128), ov, 0);
+            if (MULTI) {
+                // the next group: x_0 = this output (registers), its boundary rows to the
+                // neighbours (kind 2), its first RCAB's constants.  x and t are reassigned on
+                // every path out of the step (t is dead until the next conv2: a constant ends the
+                // last t's live range at this step's combine instead of holding it through the
+                // group conv)
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        xr[m][p] = ov[m][p];
+                        tr[m][p] = make_uint2(0u, 0u);
+                    }
+                if (g + 1 < NG) {
+                    if (bwave) store_row(wsr, booff(strip, side), xr, 16);
+                    if (wave >= 2 && wave <= 4) {
+                        CTab& nt_ = ctab[g + 1];
+                        cv = ((const float*)uni(wave == 2 ? nt_.bias[0] : wave == 3 ? nt_.alpha[0] : nt_.bias[1]))[lane];
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (bwave && lane == 0)
+                        __hip_atomic_store(flag_of(strip, side, 2), tag_of(NB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __syncthreads();                        // the group conv's image reads done; the next conv1's kh = 1 taps visible
+                }
+            }
             break;
         }
         // ---- conv1 epilogue: a1 = PReLU(conv1 + b1) -> LDS (own row), boundary rows out; the
@@ -481,7 +586,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         if (early) a1_epilogue();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's pieces of conv2's kh = 1 taps
         __syncthreads();                                    // B_E: x_j's reads done (all slots free); those taps visible
-        issue_kh02(ci + 1);
+        issue_kh02(Gw(ci + 1));
         uint2 zv[4][4];
         // pre_elide: z1 is recoverable from a1 when all 64 slopes of RCAB j are > 0 (lane = channel)
         const bool wz1 = SAVE && !(A.pre_elide && __ballot(cst[64 + lane] > 0.f) == ~0ull);
@@ -586,7 +691,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         pool_slice(wave);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();                                    // B_Z: the partial's eight channel slices in red; kh = 1 slots free
-        issue_kh1(j + 1 < NB ? ci + 2 : 2 * NB);
+        issue_kh1(Gw(j + 1 < NB ? ci + 2 : 2 * NB));
         if (wave == 3) publish_partial();
         GSTAMP(sb + 6);
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
@@ -619,9 +724,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             // (the weight pointers made opaque here: buffer loads are speculatable, and
             // hoisted out of this wave's branch they held 32 VGPRs in every wave)
             const int Cr = A.Cr, jj = lane & 15, qq = lane >> 4;
-            const float* f1p = A.fc1[j];
-            const float* f2p = A.fc2[j];
-            const float* b2p = A.bias[2 * j + 1];
+            const float* f1p = MULTI ? (const float*)uni(ctab[g].fc1[j]) : A.fc1[j];
+            const float* f2p = MULTI ? (const float*)uni(ctab[g].fc2[j]) : A.fc2[j];
+            const float* b2p = Gb(2 * j + 1);
             asm volatile("" : "+s"(f1p), "+s"(f2p), "+s"(b2p));
             const __amdgpu_buffer_rsrc_t f1r = __builtin_amdgcn_make_buffer_rsrc((void*)f1p, 0, Cr * 64 * 4, 0x00020000);
             const __amdgpu_buffer_rsrc_t f2r = __builtin_amdgcn_make_buffer_rsrc((void*)f2p, 0, Cr * 64 * 4, 0x00020000);
@@ -677,7 +782,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             for (int k = 0; k < 16; ++k) z += w2v[k] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hid), k));
             const float sg = 1.f / (1.f + expf(-z));
             gate[lane] = sg * A.res_scale;
-            if (strip == 0 && A.s_out[j]) A.s_out[j][im * 64 + lane] = sg;
+            float* so = MULTI ? (float*)uni(ctab[g].s_out[j]) : A.s_out[j];
+            if (strip == 0 && so) so[im * 64 + lane] = sg;
             if (strip == 0 && SAVE) {
                 A.sv_mean[j][im * 64 + lane] = mean;
                 if (lane < Cr) A.sv_hid[j][im * Cr + lane] = hid;
@@ -685,8 +791,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         }
         if (wave >= 2 && wave <= 4) {                       // the next conv's epilogue constants
             const bool ng = j + 1 == NB;
-            const float* src = ng ? (wave == 4 ? A.bias[2 * NB] : nullptr)
-                                  : (wave == 2 ? A.bias[2 * j + 2] : wave == 3 ? A.alpha[j + 1] : A.bias[2 * j + 3]);
+            const float* src = ng ? (wave == 4 ? Gb(2 * NB) : nullptr)
+                                  : (wave == 2 ? Gb(2 * j + 2) : wave == 3 ? Ga(j + 1) : Gb(2 * j + 3));
             cv = src ? src[lane] : 0.f;
         }
         // x_j's and t_j's boundary rows out: drained, then the storing wave signals for itself
@@ -702,6 +808,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         GSTAMP(sb + 8);
         __syncthreads();                                    // B_G: the gate in LDS; conv2's reads done (all slots free)
     }
+    if (!MULTI || ++g >= NG) break;
+    }
     GSTAMP(NSTAMP - 1);
     // ---- the last block out advances the epoch and resets the ticket counters for the next launch
     if (!ok) __hip_atomic_fetch_or(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -716,7 +824,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         stamp_lds[NSTAMP + NSTAMP - 1] = (unsigned short)(((unsigned)__builtin_amdgcn_s_memtime() - (unsigned)tick_lds[3]) >> 4);
     __syncthreads();
     {
-        unsigned short* dst = (unsigned short*)(A.work + L.ba + (size_t)B * S * 2 * 2 * ROWB) + (size_t)ticket * 8 * NSTAMP;
+        unsigned short* dst = (unsigned short*)(A.work + L.stamp) + (size_t)ticket * 8 * NSTAMP;
         for (int i = tid; i < 8 * NSTAMP; i += 512) dst[i] = stamp_lds[i];
     }
 #endif
@@ -733,15 +841,48 @@ int gs_num_cus() {
     return g_gs_cus;
 }
 
-template <typename T, bool SAVE>
+template <typename T, bool SAVE, bool MULTI = false>
 void launch_gs(const GsArgs& a, int grid, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_group_strip<T, SAVE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_group_strip<T, SAVE, MULTI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   GS_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL((k_group_strip<T, SAVE>), dim3(grid), dim3(512), GS_LDS, s, a);
+    hipLaunchKernelGGL((k_group_strip<T, SAVE, MULTI>), dim3(grid), dim3(512), GS_LDS, s, a);
+}
+
+// the chained groups' tables a prepare call wrote, by workspace: a launch whose descriptors
+// differ from the table in its workspace is refused (the table would be stale)
+std::mutex g_chain_mu;
+std::map<const void*, std::vector<GsTab>> g_chain_tabs;
+
+int chain_tab(const fen_group_strip_desc* d, int ng, std::vector<GsTab>& tab) {
+    if (!d || ng <= 0) return FEN_EINVAL;
+    const fen_group_strip_desc& d0 = d[0];
+    if (!fen_group_strip_supported(d0.dtype, d0.B, d0.H, d0.W, d0.C, d0.Cr, d0.nb)) return FEN_EUNSUPPORTED;
+    if (ng * (d0.nb + 1) > 254) return FEN_EUNSUPPORTED;                      // step tags
+    tab.assign(ng, GsTab{});
+    for (int g = 0; g < ng; ++g) {
+        const fen_group_strip_desc& e = d[g];
+        if (e.dtype != d0.dtype || e.B != d0.B || e.H != d0.H || e.W != d0.W || e.C != d0.C || e.Cr != d0.Cr ||
+            e.nb != d0.nb || e.res_scale != d0.res_scale || e.save || e.work != d0.work)
+            return FEN_EINVAL;
+        if (!e.x || !e.y || !e.wg || !e.bg || e.x == e.y) return FEN_EINVAL;
+        if (g > 0 && e.x != d[g - 1].y) return FEN_EINVAL;                   // a chain: output -> next input
+        GsTab& t = tab[g];
+        t.x = e.x, t.y = e.y;
+        for (int j = 0; j < e.nb; ++j) {
+            if (!e.w1[j] || !e.b1[j] || !e.alpha[j] || !e.w2[j] || !e.b2[j] || !e.fc1[j] || !e.fc2[j])
+                return FEN_EINVAL;
+            t.w[2 * j] = e.w1[j], t.bias[2 * j] = e.b1[j];
+            t.w[2 * j + 1] = e.w2[j], t.bias[2 * j + 1] = e.b2[j];
+            t.alpha[j] = e.alpha[j], t.fc1[j] = e.fc1[j], t.fc2[j] = e.fc2[j], t.s_out[j] = e.s_out[j];
+        }
+        t.w[2 * e.nb] = e.wg, t.bias[2 * e.nb] = e.bg;
+    }
+    if (!d0.work || d0.work_bytes < gs_tab_offset(d0.B, d0.H / SR) + (size_t)ng * sizeof(GsTab)) return FEN_EINVAL;
+    return FEN_OK;
 }
 
 }  // namespace
@@ -797,6 +938,53 @@ extern "C" int fen_group_strip(const fen_group_strip_desc* d, void* stream) {
         if (a.save) launch_gs<bf16, true>(a, grid, s);
         else launch_gs<bf16, false>(a, grid, s);
     }
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" size_t fen_group_strip_chain_work_bytes(int B, int H, int ng) {
+    if (B <= 0 || H <= 0 || H % SR || ng <= 0) return 0;
+    return gs_tab_offset(B, H / SR) + (size_t)ng * sizeof(GsTab);
+}
+
+extern "C" int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng) {
+    std::vector<GsTab> tab;
+    const int rc = chain_tab(d, ng, tab);
+    if (rc != FEN_OK) return rc;
+    char* dst = (char*)d[0].work + gs_tab_offset(d[0].B, d[0].H / SR);
+    const hipError_t e = hipMemcpy(dst, tab.data(), tab.size() * sizeof(GsTab), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        fen_detail::last_hip_error = (int)e;
+        return FEN_EHIP;
+    }
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    g_chain_tabs[d[0].work] = tab;
+    return FEN_OK;
+}
+
+extern "C" int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, void* stream) {
+    std::vector<GsTab> tab;
+    const int rc = chain_tab(d, ng, tab);
+    if (rc != FEN_OK) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_chain_mu);
+        const auto it = g_chain_tabs.find(d[0].work);
+        if (it == g_chain_tabs.end() || it->second.size() != tab.size() ||
+            memcmp(it->second.data(), tab.data(), tab.size() * sizeof(GsTab)) != 0)
+            return FEN_EINVAL;                                  // not prepared with these descriptors
+    }
+    const fen_group_strip_desc& d0 = d[0];
+    GsArgs a{};
+    a.B = d0.B, a.H = d0.H, a.S = d0.H / SR, a.NB = d0.nb, a.Cr = d0.Cr;
+    a.res_scale = d0.res_scale, a.inv_hw = 1.0f / (float)(d0.H * d0.W);
+    a.work = (char*)d0.work;
+    a.status = d0.status, a.fault = d0.fault;
+    a.tab = (const GsTab*)((const char*)d0.work + gs_tab_offset(d0.B, d0.H / SR));
+    a.ng = ng;
+    const int grid = d0.B * (d0.H / SR);
+    hipStream_t s = (hipStream_t)stream;
+    if (d0.dtype == FEN_F16) launch_gs<f16, false, true>(a, grid, s);
+    else launch_gs<bf16, false, true>(a, grid, s);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -143,12 +143,13 @@ class FENEngine:
         s, ctx = self.spec, self.ctx
         fw = Forward(s, ctx, self.Wt, save=self.train)
         feat0 = fw.head(self.x)
-        h = feat0
-        self.saved = []
-        for g in range(s.G):
-            out = None if self.train else ctx.scratch(f"grp_pp{g & 1}", feat0.shape)
-            h, sv = fw.group(h, g, out=out)
-            self.saved.append(sv)
+        if self.train:
+            h, self.saved = feat0, []
+            for g in range(s.G):
+                h, sv = fw.group(h, g)
+                self.saved.append(sv)
+        else:
+            h, self.saved = fw.body(feat0, [ctx.scratch(f"grp_pp{g & 1}", feat0.shape) for g in range(s.G)])
         hr = self.hr if self.train else None
         _, self.saved_tail = fw.tail(h, feat0, self.x, training, out=self.out, hr=hr,
                                      l1_scale=self.l1_scale if self.train else 0.0)

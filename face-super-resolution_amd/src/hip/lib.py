@@ -132,6 +132,9 @@ _SIGS = {
     "fen_group_strip_supported": (c_int, [c_int] * 7),
     "fen_group_strip_work_bytes": (c_size_t, [c_int, c_int]),
     "fen_group_strip": (c_int, [POINTER(GroupStripDesc), c_void_p]),
+    "fen_group_strip_chain_work_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "fen_group_strip_chain_prepare": (c_int, [POINTER(GroupStripDesc), c_int]),
+    "fen_group_strip_chain": (c_int, [POINTER(GroupStripDesc), c_int, c_void_p]),
     "fen_group_strip_bwd_supported": (c_int, [c_int] * 7),
     "fen_group_strip_bwd_work_bytes": (c_size_t, [c_int, c_int]),
     "fen_group_strip_bwd": (c_int, [POINTER(GroupStripBwdDesc), c_void_p]),

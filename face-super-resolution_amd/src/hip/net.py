@@ -65,6 +65,9 @@ GROUP_STRIP = os.environ.get("FEN_GROUP_STRIP", "1") != "0"
 # ... and the training forward too (the kernel then writes the backward's saved tensors);
 # FEN_GROUP_STRIP_TRAIN=0 keeps training on the per-RCAB launches
 GROUP_STRIP_TRAIN = os.environ.get("FEN_GROUP_STRIP_TRAIN", "1") != "0"
+# inference: the body's G groups as ONE fen_group_strip_chain launch (strips stay on their CUs
+# across groups); FEN_GROUP_CHAIN=0 keeps a fen_group_strip launch per group
+GROUP_CHAIN = os.environ.get("FEN_GROUP_CHAIN", "1") != "0"
 # inference at 128 channels (BASELINE configs[4]): a ResidualGroup as 2 * nb + 1 fen_rcab_c128
 # launches (rcab128.hip: each RCAB's gate deferred into the next conv's input, its pool sums in
 # conv2's epilogue) where the envelope holds (16-bit, H % 4 == 0, W % 64 == 0, Cr <= 32);
@@ -437,9 +440,57 @@ class Forward:
         """The whole group in one fen_group_strip launch: y = conv(chain(x)) + b + x; in training
         (self.save) the launch also writes every RCAB's x_j, z1, a1, t_j, s, mean, hid and the
         chain's output (the backward's operands, the per-RCAB launches' saved set)."""
+        ctx = self.ctx
+        B, H = x.shape[0], x.shape[1]
+        d = L.GroupStripDesc()
+        sv = self._group_strip_desc(d, x, pre, names, y)
+        nbytes = int(ctx.lib.fen_group_strip_work_bytes(B, H))
+        work = ctx.persistent_zeros(f"group_strip/{B}x{H}", nbytes)
+        d.work, d.work_bytes = ptr(work), nbytes
+        d.status, d.fault = L.strip_status_ptr(ctx.device), GS_FAULT & 1
+        ctx.emit("group_strip", ctx.lib.fen_group_strip, byref(d))
+        ctx.keep(d)
+        return sv
+
+    def _chain_ok(self, x) -> bool:
+        return GROUP_CHAIN and not self.save and self.s.G > 1 and self._strip_ok(x) and not self._c128_ok(x)
+
+    def body(self, x: torch.Tensor, outs: Sequence[torch.Tensor]):
+        """The body's ResidualGroups (custom.py:168-169, blocks.py:185-189 each) -> (h, saved per
+        group); outs[g] is group g's output (consecutive outputs distinct, outs[0] not x).  In
+        inference on the strip kernels: ONE fen_group_strip_chain launch (GROUP_CHAIN), each
+        strip resident on its CU through all G groups; otherwise a launch (or chain) per group."""
+        s, ctx = self.s, self.ctx
+        if not self._chain_ok(x):
+            saved, h = [], x
+            for g in range(s.G):
+                h, sv = self.group(h, g, out=outs[g])
+                saved.append(sv)
+            return h, saved
+        B, H = x.shape[0], x.shape[1]
+        G = s.G
+        ds = (L.GroupStripDesc * G)()
+        saved, h = [], x
+        for g in range(G):
+            names = [f"group{g}_rcab{b}" for b in range(s.NB)]
+            saved.append(self._group_strip_desc(ds[g], h, f"residual_groups.{g}.", names, outs[g]))
+            h = outs[g]
+        nbytes = int(ctx.lib.fen_group_strip_chain_work_bytes(B, H, G))
+        # the chain's own workspace (its parameter table is this program's)
+        work = torch.zeros(nbytes, dtype=torch.uint8, device=ctx.device)
+        ctx.keep(work)
+        for g in range(G):
+            ds[g].work, ds[g].work_bytes = ptr(work), nbytes
+            ds[g].status, ds[g].fault = L.strip_status_ptr(ctx.device), GS_FAULT & 1
+        L.check(ctx.lib.fen_group_strip_chain_prepare(ds, G), "group_strip_chain_prepare")
+        ctx.emit("group_strip_chain", ctx.lib.fen_group_strip_chain, ds, G)
+        ctx.keep(ds)
+        return h, saved
+
+    def _group_strip_desc(self, d, x: torch.Tensor, pre: str, names: Sequence[str], y: torch.Tensor) -> dict:
+        """Fill a fen_group_strip descriptor (all but the workspace) -> the group's saved set."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = x.shape
-        d = L.GroupStripDesc()
         d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.nb = ctx.code, B, H, W, C, s.Cr, s.NB
         d.res_scale = float(s.res_scale)
         d.x, d.y = ptr(x), ptr(y)
@@ -477,12 +528,6 @@ class Forward:
                 ctx.lib.fen_group_strip_bwd_supported(ctx.code, B, H, W, C, s.Cr, s.NB))
             d.pre_elide = int(z1_elided)
         d.wg, d.bg = ptr(Wt.packed(pre + "conv", 0)), ptr(p[pre + "conv.bias"])
-        nbytes = int(ctx.lib.fen_group_strip_work_bytes(B, H))
-        work = ctx.persistent_zeros(f"group_strip/{B}x{H}", nbytes)
-        d.work, d.work_bytes = ptr(work), nbytes
-        d.status, d.fault = L.strip_status_ptr(ctx.device), GS_FAULT & 1
-        ctx.emit("group_strip", ctx.lib.fen_group_strip, byref(d))
-        ctx.keep(d)
         return dict(blocks=blocks, x=x, x_last=x_last, z1_elided=z1_elided)
 
     def _c128_ok(self, x) -> bool:

@@ -291,6 +291,18 @@ typedef struct {
 int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
 size_t fen_group_strip_work_bytes(int B, int H);
 int fen_group_strip(const fen_group_strip_desc* d, void* stream);
+/* ng consecutive ResidualGroups (reference custom.py:168-169, the body's group loop) as ONE
+ * launch, inference: d[0..ng-1] are the groups' descriptors as for fen_group_strip (save = 0),
+ * d[g].y == d[g+1].x, all sharing d[0].work (fen_group_strip_chain_work_bytes(B, H, ng) bytes:
+ * the workspace plus the groups' parameter table), d[0].status / fault used.  A strip stays on
+ * its CU across the groups: group g's output rows become group g+1's x_0 in registers, the
+ * neighbours' boundary rows by hand-off; each group's output is still written to d[g].y (the
+ * next group's skip input).  fen_group_strip_chain_prepare writes the table (a synchronous
+ * copy: once, outside a graph capture, before the first launch); a launch whose descriptors
+ * differ from the prepared table returns FEN_EINVAL.  ng * (nb + 1) <= 254.                  */
+size_t fen_group_strip_chain_work_bytes(int B, int H, int ng);
+int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng);
+int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, void* stream);
 
 /* 128-channel RCAB convs (BASELINE configs[4]: num_channels = 128, Cr = 32; RCAB blocks.py:
  * 135-153, ChannelAttention blocks.py:83-92, ResidualGroup blocks.py:185-189), one launch per

@@ -1,0 +1,176 @@
+"""GPU parity of fen_group_strip_chain -- the body's G ResidualGroups (reference
+custom.py:168-169; each group blocks.py:185-189 with RCABs blocks.py:135-153) as ONE launch in
+which every strip stays on its CU across the groups -- against a fen_group_strip launch per
+group (itself oracle-checked in test_gpu_group_strip.py) and against the CPU oracle.
+
+The chain does the per-group launches' arithmetic exactly (a group's output rounded to the
+16-bit format, then kept in registers as the next group's x_0; the neighbours' rows of it by
+hand-off; the skip input re-read from the output buffer), so the outputs and every gate are
+compared BIT-EXACT with the per-group launches; the oracle bound is the per-group test's
+(5e-3 bf16 / 1e-3 fp16 rel-L2 per RCAB + 1) summed over the groups.  Shapes: the bench's
+(B=32, 64x64, 6 groups x 10 RCABs), one strip per image (H=8), 16 strips (H=128), more strips
+than CUs (B=40), one image, 2 / 3 groups.  Graph replays are bit-identical with the counters
+back at zero; a skipped hand-off flag surfaces as FenError."""
+import pytest
+import torch
+
+from oracle import fen_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DT = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def _params(G, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    C, Cr = 64, 16
+    q = {}
+    for gi in range(G):
+        pre = f"residual_groups.{gi}."
+        for j in range(n):
+            b = f"{pre}blocks.{j}."
+            q[b + "conv1.weight"] = torch.randn(C, C, 3, 3, generator=g) * 0.06
+            q[b + "conv1.bias"] = torch.randn(C, generator=g) * 0.1
+            q[b + "prelu.weight"] = torch.rand(C, generator=g) * 0.5
+            q[b + "conv2.weight"] = torch.randn(C, C, 3, 3, generator=g) * 0.06
+            q[b + "conv2.bias"] = torch.randn(C, generator=g) * 0.1
+            q[b + "channel_attention.fc.0.weight"] = torch.randn(Cr, C, generator=g) * 0.3
+            q[b + "channel_attention.fc.2.weight"] = torch.randn(C, Cr, generator=g) * 0.3
+        q[pre + "conv.weight"] = torch.randn(C, C, 3, 3, generator=g) * 0.05
+        q[pre + "conv.bias"] = torch.randn(C, generator=g) * 0.1
+    return q
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm())
+
+
+def _run(q, G, n, x, dtype, chain=True, record=False, fault=0):
+    from src.hip import net
+    from src.hip.net import Forward, NetSpec, Weights
+    from src.hip.program import Ctx
+    old = net.GROUP_CHAIN, net.GS_FAULT
+    net.GROUP_CHAIN, net.GS_FAULT = chain, fault
+    try:
+        ctx = Ctx(dtype, DEV, record=record)
+        Wt = Weights({k: v.to(DEV) for k, v in q.items()}, dtype, DEV)
+        ctx.keep(Wt)
+        attn = {}
+        fw = Forward(NetSpec(C=64, G=G, NB=n, Cr=16), ctx, Wt, save=False, attn=attn)
+        used = fw._chain_ok(x)
+        outs = [torch.empty_like(x), torch.empty_like(x)]
+        ctx.keep(outs)
+        h, _ = fw.body(x, [outs[g & 1] for g in range(G)])
+        if not record:
+            torch.cuda.synchronize()
+    finally:
+        net.GROUP_CHAIN, net.GS_FAULT = old
+    return h, attn, ctx, used
+
+
+@pytest.mark.parametrize("prec", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,H,G,n", [(32, 64, 6, 10), (2, 64, 3, 2), (3, 8, 2, 2), (2, 128, 2, 1), (40, 64, 2, 2),
+                                     (1, 64, 3, 1)])
+def test_group_chain_bit_exact_vs_per_group(prec, B, H, G, n):
+    from src.hip import lib as L
+    dtype = DT[prec]
+    q = _params(G, n, seed=40 + G + n)
+    x = torch.randn(B, H, 64, 64, generator=torch.Generator().manual_seed(11)).to(DEV, dtype)
+    yc, attn_c, ctx, used = _run(q, G, n, x, dtype, chain=True)
+    assert used, "outside fen_group_strip_chain's envelope"
+    L.check_strip_status()
+    yg, attn_g, _, _ = _run(q, G, n, x, dtype, chain=False)
+    assert torch.equal(yc, yg)
+    assert sorted(attn_c) == sorted(attn_g) and len(attn_c) == G * n
+    for k in attn_c:
+        assert torch.equal(attn_c[k], attn_g[k]), k
+    # again on the same workspace: deterministic, counters reset by the first launch
+    yc2, _, _, _ = _run(q, G, n, x, dtype, chain=True)
+    assert torch.equal(yc2, yc)
+
+
+@pytest.mark.parametrize("prec", ["fp16", "bf16"])
+def test_group_chain_vs_oracle(prec):
+    dtype = DT[prec]
+    B, H, G, n = 2, 16, 3, 2
+    q = _params(G, n, seed=9)
+    x = torch.randn(B, 64, H, 64, generator=torch.Generator().manual_seed(5)).to(dtype).float()
+    qr = {k: (v.to(dtype).float() if v.dim() == 4 else v) for k, v in q.items()}
+    ref = x
+    for g in range(G):
+        ref = O.residual_group(ref, qr, f"residual_groups.{g}.", n, 0.2)
+        ref = ref.to(dtype).float()                       # the group output as stored
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV, dtype)
+    y, _, _, used = _run(q, G, n, xd, dtype)
+    assert used
+    r = _rel(y.float().cpu().permute(0, 3, 1, 2), ref)
+    tol = (5e-3 if prec == "bf16" else 1e-3) * (n + 1) * G
+    print(f"{prec}: rel {r:.2e}")
+    assert r <= tol, r
+
+
+def test_group_chain_graph_replay():
+    """Recorded (one op) and replayed from a hipGraph five times: bit-identical to the eager
+    launch, no wait timed out."""
+    from src.hip import lib as L
+    dtype, G, n = torch.float16, 6, 10
+    q = _params(G, n, seed=12)
+    x = torch.randn(32, 64, 64, 64, generator=torch.Generator().manual_seed(3)).to(DEV, dtype)
+    y_e, _, _, _ = _run(q, G, n, x, dtype)
+    y, _, ctx, _ = _run(q, G, n, x, dtype, record=True)
+    assert [op[0] for op in ctx.ops] == ["group_strip_chain"]
+    ctx.run()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_e)
+    gph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gph):
+        ctx.run()
+    for _ in range(5):
+        y.zero_()
+        gph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, y_e)
+        L.check_strip_status()
+
+
+def test_group_chain_failed_wait_raises():
+    """Fault injection (test-only flag): the block with ticket 1 skips its first a1 flag; the
+    neighbour's bounded wait expires and the launch reports it -- FenError, not an output."""
+    from src.hip import lib as L
+    dtype, G, n = torch.bfloat16, 2, 1
+    q = _params(G, n, seed=3)
+    x = torch.randn(2, 64, 64, 64, generator=torch.Generator().manual_seed(1)).to(DEV, dtype)
+    _run(q, G, n, x, dtype, fault=1)
+    with pytest.raises(L.FenError):
+        L.check_strip_status()
+    L.check_strip_status()                                # cleared
+    y, _, _, _ = _run(q, G, n, x, dtype)                  # the workspace is usable again
+    yg, _, _, _ = _run(q, G, n, x, dtype, chain=False)
+    assert torch.equal(y, yg)
+
+
+def test_group_chain_refuses_unprepared():
+    """A launch whose descriptors differ from the prepared table is refused (FEN_EINVAL)."""
+    from src.hip import lib as L
+    dtype, G, n = torch.float16, 2, 1
+    q = _params(G, n, seed=4)
+    x = torch.randn(1, 64, 64, 64, generator=torch.Generator().manual_seed(2)).to(DEV, dtype)
+    _, _, ctx, _ = _run(q, G, n, x, dtype, record=True)
+    name, fn, (ds, ng) = ctx.ops[0]
+    assert name == "group_strip_chain"
+    s = torch.cuda.current_stream().cuda_stream
+    old = ds[1].fc1[0]
+    ds[1].fc1[0] = ds[1].fc2[0]                           # valid descriptors, not the prepared table
+    try:
+        assert fn(ds, ng, s) != 0
+    finally:
+        ds[1].fc1[0] = old
+    old = ds[1].x
+    ds[1].x = ds[1].y                                     # not a chain (x aliases y)
+    try:
+        assert fn(ds, ng, s) != 0
+    finally:
+        ds[1].x = old
+    assert fn(ds, ng, s) == 0
+    torch.cuda.synchronize()
