@@ -11,6 +11,8 @@
 // filtered combination on the tile.  No intermediate map touches HBM.  fp32 throughout.
 #include "fen_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int SR = 5;       // window radius (window 11)
@@ -22,27 +24,40 @@ struct SsimWin {
 inline int nblk(size_t n, int t = 256) { return (int)((n + t - 1) / t); }
 
 // Horizontal pass over NCH column chunks of CW outputs: thread keeps the CW + 10 inputs of
-// its chunk in registers and reads each LDS element once.
+// its chunk in registers and reads each LDS element once.  Packed fp32 (v_pk_fma_f32): the
+// (p, t) and (p^2, t^2) sums two at a time, p t alone -- 3 FMA instructions per tap, not 5.
+__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 template <int CW>
 __device__ __forceinline__ void hrow(const SsimWin& win, const float* p, const float* t, float (&o)[5][CW]) {
-    float pv[CW + 2 * SR], tv[CW + 2 * SR];
+    f32x2 pt[CW + 2 * SR], sq[CW + 2 * SR];
+    float cr[CW + 2 * SR];
 #pragma unroll
-    for (int i = 0; i < CW + 2 * SR; ++i) { pv[i] = p[i]; tv[i] = t[i]; }
+    for (int i = 0; i < CW + 2 * SR; ++i) {
+        pt[i] = f32x2{p[i], t[i]};
+        sq[i] = pt[i] * pt[i];
+        cr[i] = pt[i].x * pt[i].y;
+    }
 #pragma unroll
     for (int c = 0; c < CW; ++c) {
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+        f32x2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
+        float s4 = 0.f;
 #pragma unroll
         for (int j = 0; j < 2 * SR + 1; ++j) {
-            const float pp = pv[c + j], tt = tv[c + j], g = win.g[j];
-            s0 += g * pp; s1 += g * tt; s2 += g * pp * pp; s3 += g * tt * tt; s4 += g * pp * tt;
+            const f32x2 g2 = {win.g[j], win.g[j]};
+            s01 = pfma(g2, pt[c + j], s01);
+            s23 = pfma(g2, sq[c + j], s23);
+            s4 = fmaf(win.g[j], cr[c + j], s4);
         }
-        o[0][c] = s0; o[1][c] = s1; o[2][c] = s2; o[3][c] = s3; o[4][c] = s4;
+        o[0][c] = s01.x; o[1][c] = s01.y; o[2][c] = s23.x; o[3][c] = s23.y; o[4][c] = s4;
     }
 }
 
-// CB > 1 (grad_mode 2, C <= CB): one block takes every channel of its tile in turn and adds the
-// gradients to the NHWC16 buffer once, 4 channels per 8-B (16-bit) / 16-B (fp32) read-modify-
-// write per pixel, instead of C blocks each rewriting one 2-byte channel of every pixel row.
+// CB > 1 (grad_mode 2, C <= CB): one block takes every channel of its tile in turn, keeps each
+// channel's gradient tile in LDS and adds them to the NHWC16 buffer once at the end, 4 channels
+// per 8-B (16-bit) / 16-B (fp32) read-modify-write per pixel, every thread 4 pixels, the reads
+// issued before the last channel's passes; instead of C blocks each rewriting one 2-byte
+// channel of every pixel row.
 template <bool GRAD, typename T, int CB>
 __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const float* __restrict__ pred,
                                               const float* __restrict__ target, const SsimWin win, float C1,
@@ -53,13 +68,17 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     constexpr int O1 = GRAD ? SR : 0;             // tile offset inside E1
     constexpr int CW = GRAD ? 7 : 8;              // register block of the map passes (E1 = 6 or 4 of them)
     constexpr int NCH = E1 / CW;
-    constexpr int CW2 = 8, NCH2 = ST / CW2;       // register block of the gradient passes
+    constexpr int CW2 = 8, NCH2 = ST / CW2;       // horizontal gradient pass: 8-column chunks
+    constexpr int RV = 4, NRV = ST / RV;          // vertical gradient pass: 4-row chunks (ST * NRV = 256 items)
     constexpr int PS = E2 + 1;
+    constexpr bool LDSG = GRAD && CB > 1;         // the gradient tiles kept in LDS
     // sb: p, t on E2 x E2; after the first pass, a / b / c on E1 x E1 (3 E1 (E1+1) <= 2 E2 PS)
     __shared__ float sb[2 * E2 * PS];
     __shared__ float hp[5][E2][E1 + 1];           // horizontal sums (reused for a, b, c)
-    __shared__ float red[256];
+    __shared__ float dg[LDSG ? CB : 1][LDSG ? ST : 1][LDSG ? ST + 1 : 1];   // per channel d(sum S)/dp
+    __shared__ float red[4];
     static_assert(3 * E1 * (E1 + 1) <= 2 * E2 * PS, "a/b/c alias");
+    static_assert(ST * NRV == 256, "one vertical gradient item per thread");
     float* sp = sb;
     float* st = sb + E2 * PS;
     float (*abc)[E1][E1 + 1] = (float (*)[E1][E1 + 1])sb;
@@ -67,11 +86,6 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     const int h0 = blockIdx.y * ST, w0 = blockIdx.x * ST;
     const int gy0 = h0 - O1 - SR, gx0 = w0 - O1 - SR;     // image coords of E2's (0, 0)
     const int b = CB > 1 ? (int)blockIdx.z : (int)blockIdx.z / C;
-    float dacc[CB][CW2];                                  // CB > 1: this thread's gradients, per channel
-#pragma unroll
-    for (int k = 0; k < CB; ++k)
-#pragma unroll
-        for (int o = 0; o < CW2; ++o) dacc[k][o] = 0.f;
     // the E2 x E2 inputs of a channel: every load of the thread issued before the first LDS write
     // (one memory round trip per channel instead of one per 256 elements); with CB > 1 the next
     // channel's are issued as soon as this one's are in LDS, under its passes
@@ -88,6 +102,14 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
             lp[k] = in ? pred[e] : 0.f;
             lt[k] = in ? target[e] : 0.f;
         }
+    };
+    // the final read-modify-write's pixels: thread tid takes pixels tid + 256 k of the tile (row-
+    // major: a wave's 64 lanes are two tile rows, 32 consecutive pixels each)
+    typedef typename std::conditional<sizeof(T) == 2, uint2, float4>::type GV;
+    GV gv[4];
+    auto grad_ptr = [&](int k) -> GV* {
+        const int pix = tid + 256 * k, gy = h0 + pix / ST, gx = w0 + pix % ST;
+        return (gy < H && gx < W) ? (GV*)((T*)grad + (((size_t)b * H + gy) * W + gx) * 16) : nullptr;
     };
     load_in(CB > 1 ? 0 : (int)blockIdx.z % C);
 #pragma unroll
@@ -109,6 +131,14 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     }
     __syncthreads();
     if (CB > 1 && cc + 1 < CB && cc + 1 < C) load_in(cc + 1);
+    if (LDSG && (cc + 1 == CB || cc + 1 == C)) {
+        // the last channel: the gradient buffer's pixels in flight under its passes
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const GV* q = grad_ptr(k);
+            if (q) gv[k] = *q;
+        }
+    }
     for (int i = tid; i < E2 * NCH; i += 256) {
         const int r = i / NCH, c0 = (i % NCH) * CW;
         float o[5][CW];
@@ -119,34 +149,36 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
             for (int c = 0; c < CW; ++c) hp[k][r][c0 + c] = o[k][c];
     }
     __syncthreads();
-    // vertical pass: thread = (column, CW-row chunk), the chunk's CW + 10 rows read once
+    // vertical pass: thread = (column, CW-row chunk), the chunk's CW + 10 rows read once; the
+    // (mp, mt) and (E[p^2], E[t^2]) sums packed
     float acc = 0.f;
     for (int i = tid; i < E1 * NCH; i += 256) {
         const int c = i % E1, r0 = (i / E1) * CW;
-        float m[5][CW];
+        f32x2 m01[CW], m23[CW];
+        float m4[CW];
 #pragma unroll
-        for (int k = 0; k < 5; ++k)
-#pragma unroll
-            for (int o = 0; o < CW; ++o) m[k][o] = 0.f;
+        for (int o = 0; o < CW; ++o) m01[o] = m23[o] = f32x2{0.f, 0.f}, m4[o] = 0.f;
 #pragma unroll
         for (int rr = 0; rr < CW + 2 * SR; ++rr) {
-            float v[5];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) v[k] = hp[k][r0 + rr][c];
+            const f32x2 v01 = {hp[0][r0 + rr][c], hp[1][r0 + rr][c]};
+            const f32x2 v23 = {hp[2][r0 + rr][c], hp[3][r0 + rr][c]};
+            const float v4 = hp[4][r0 + rr][c];
 #pragma unroll
             for (int o = 0; o < CW; ++o) {
                 const int j = rr - o;
                 if (j >= 0 && j <= 2 * SR) {
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) m[k][o] += win.g[j] * v[k];
+                    const f32x2 g2 = {win.g[j], win.g[j]};
+                    m01[o] = pfma(g2, v01, m01[o]);
+                    m23[o] = pfma(g2, v23, m23[o]);
+                    m4[o] = fmaf(win.g[j], v4, m4[o]);
                 }
             }
         }
 #pragma unroll
         for (int o = 0; o < CW; ++o) {
             const int r = r0 + o;
-            const float mp = m[0][o], mt = m[1][o];
-            const float spp = m[2][o] - mp * mp, stt = m[3][o] - mt * mt, spt = m[4][o] - mp * mt;
+            const float mp = m01[o].x, mt = m01[o].y;
+            const float spp = m23[o].x - mp * mp, stt = m23[o].y - mt * mt, spt = m4[o] - mp * mt;
             const float A1 = 2.f * mp * mt + C1, A2 = 2.f * spt + C2;
             const float B1 = mp * mp + mt * mt + C1, B2 = spp + stt + C2;
             const float S = (A1 * A2) / (B1 * B2);
@@ -164,108 +196,100 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     }
     if constexpr (GRAD) {
         __syncthreads();
-        for (int i = tid; i < E1 * NCH2; i += 256) {          // horizontal pass of a, b, c
+        for (int i = tid; i < E1 * NCH2; i += 256) {          // horizontal pass of a, b (packed) and c
             const int r = i / NCH2, c0 = (i % NCH2) * CW2;
+            f32x2 vab[CW2 + 2 * SR];
+            float vc[CW2 + 2 * SR];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                float v[CW2 + 2 * SR];
+            for (int q = 0; q < CW2 + 2 * SR; ++q) vab[q] = f32x2{abc[0][r][c0 + q], abc[1][r][c0 + q]}, vc[q] = abc[2][r][c0 + q];
 #pragma unroll
-                for (int q = 0; q < CW2 + 2 * SR; ++q) v[q] = abc[k][r][c0 + q];
+            for (int c = 0; c < CW2; ++c) {
+                f32x2 sab = {0.f, 0.f};
+                float sc = 0.f;
 #pragma unroll
-                for (int c = 0; c < CW2; ++c) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 2 * SR + 1; ++j) s += win.g[j] * v[c + j];
-                    hp[k][r][c0 + c] = s;
+                for (int j = 0; j < 2 * SR + 1; ++j) {
+                    sab = pfma(f32x2{win.g[j], win.g[j]}, vab[c + j], sab);
+                    sc = fmaf(win.g[j], vc[c + j], sc);
                 }
+                hp[0][r][c0 + c] = sab.x;
+                hp[1][r][c0 + c] = sab.y;
+                hp[2][r][c0 + c] = sc;
             }
         }
         __syncthreads();
-        for (int i = tid; i < ST * NCH2; i += 256) {          // vertical pass + the gradient
-            const int c = i % ST, r0 = (i / ST) * CW2, gx = w0 + c;
-            float m[3][CW2];
+        {                                                     // vertical pass + the gradient: one item per thread
+            const int c = tid % ST, r0 = (tid / ST) * RV, gx = w0 + c;
+            float pr[RV], tr[RV];                             // L2-hot: this block staged them
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
+            for (int o = 0; o < RV; ++o) {
+                const int gy = min(h0 + r0 + o, H - 1);
+                const bool in = gx < W;
+                pr[o] = in ? pp[(size_t)gy * W + gx] : 0.f;
+                tr[o] = in ? tp[(size_t)gy * W + gx] : 0.f;
+            }
+            f32x2 mab[RV];
+            float mc[RV];
 #pragma unroll
-                for (int o = 0; o < CW2; ++o) m[k][o] = 0.f;
+            for (int o = 0; o < RV; ++o) mab[o] = f32x2{0.f, 0.f}, mc[o] = 0.f;
 #pragma unroll
-            for (int rr = 0; rr < CW2 + 2 * SR; ++rr) {
-                float v[3];
+            for (int rr = 0; rr < RV + 2 * SR; ++rr) {
+                const f32x2 vab = {hp[0][r0 + rr][c], hp[1][r0 + rr][c]};
+                const float vc = hp[2][r0 + rr][c];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) v[k] = hp[k][r0 + rr][c];
-#pragma unroll
-                for (int o = 0; o < CW2; ++o) {
+                for (int o = 0; o < RV; ++o) {
                     const int j = rr - o;
                     if (j >= 0 && j <= 2 * SR) {
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) m[k][o] += win.g[j] * v[k];
+                        mab[o] = pfma(f32x2{win.g[j], win.g[j]}, vab, mab[o]);
+                        mc[o] = fmaf(win.g[j], vc, mc[o]);
                     }
                 }
             }
-            if (gx >= W) continue;
-            float pr[CW2], tr[CW2];                               // L2-hot: this block staged them
 #pragma unroll
-            for (int o = 0; o < CW2; ++o) {
-                const int gy = min(h0 + r0 + o, H - 1);
-                pr[o] = pp[(size_t)gy * W + gx];
-                tr[o] = tp[(size_t)gy * W + gx];
-            }
-#pragma unroll
-            for (int o = 0; o < CW2; ++o) {
+            for (int o = 0; o < RV; ++o) {
+                const float d = grad_scale * (mab[o].x + 2.f * pr[o] * mab[o].y + tr[o] * mc[o]);
                 const int gy = h0 + r0 + o;
-                if (gy >= H) break;
-                const size_t e = (size_t)gy * W + gx;
-                const float p = pr[o], t = tr[o];
-                const float d = grad_scale * (m[0][o] + 2.f * p * m[1][o] + t * m[2][o]);
-                if constexpr (CB > 1) {
-                    dacc[cc][o] = d;
-                } else if (grad_mode == 1) {
-                    ((float*)grad)[(size_t)plane * H * W + e] = d;
-                } else {
-                    T* q = (T*)grad + (((size_t)b * H + gy) * W + gx) * 16 + ch;
-                    *q = fromf<T>(tof<T>(*q) + d);
+                if constexpr (LDSG) {
+                    dg[cc][r0 + o][c] = d;
+                } else if (gx < W && gy < H) {
+                    const size_t e = (size_t)gy * W + gx;
+                    if (grad_mode == 1) {
+                        ((float*)grad)[(size_t)plane * H * W + e] = d;
+                    } else {
+                        T* q = (T*)grad + (((size_t)b * H + gy) * W + gx) * 16 + ch;
+                        *q = fromf<T>(tof<T>(*q) + d);
+                    }
                 }
             }
         }
     }
-    red[tid] = acc;
+    // the tile's SSIM sum: wave sums (fixed tree), then the 4 waves in order
+    acc = wave_sum(acc);
+    if ((tid & 63) == 0) red[tid >> 6] = acc;
     __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if (tid < s) red[tid] += red[tid + s];
-        __syncthreads();
-    }
     if (tid == 0) {
         const int ntile = gridDim.x * gridDim.y;
-        part[((size_t)ch * ntile + blockIdx.y * gridDim.x + blockIdx.x) * B + b] = red[0];
+        part[((size_t)ch * ntile + blockIdx.y * gridDim.x + blockIdx.x) * B + b] = ((red[0] + red[1]) + red[2]) + red[3];
     }
     }   // channels
-    if constexpr (GRAD && CB > 1) {
+    if constexpr (LDSG) {
+#ifdef SSIM_NO_RMW
+        // A/B only: the gradient's read-modify-write skipped (kept live by an improbable store)
+        if (dg[0][tid & 31][tid >> 5] == 1234.5f) ((float*)grad)[tid] = tof<T>(((const T*)&gv[0])[0]);
+        return;
+#endif
+        __syncthreads();                                      // every channel's dg tile written
         // channels 0..3 of each pixel in one read-modify-write (channels >= C written back as read)
-        for (int i = tid; i < ST * NCH2; i += 256) {
-            const int c = i % ST, r0 = (i / ST) * CW2, gx = w0 + c;
-            if (gx >= W) continue;
 #pragma unroll
-            for (int o = 0; o < CW2; ++o) {
-                const int gy = h0 + r0 + o;
-                if (gy >= H) break;
-                T* q = (T*)grad + (((size_t)b * H + gy) * W + gx) * 16;
-                if constexpr (sizeof(T) == 2) {
-                    uint2 u = *(const uint2*)q;
-                    const T* v = (const T*)&u;
-                    T w4[4] = {v[0], v[1], v[2], v[3]};
+        for (int k = 0; k < 4; ++k) {
+            GV* q = grad_ptr(k);
+            if (!q) continue;
+            const int pix = tid + 256 * k, r = pix / ST, c = pix % ST;
+            GV u = gv[k];
+            T* v = (T*)&u;
 #pragma unroll
-                    for (int k = 0; k < CB && k < 4; ++k)
-                        if (k < C) w4[k] = fromf<T>(tof<T>(w4[k]) + dacc[k][o]);
-                    *(uint2*)q = *(const uint2*)w4;
-                } else {
-                    float4 u = *(const float4*)q;
-                    float* v = (float*)&u;
-#pragma unroll
-                    for (int k = 0; k < CB && k < 4; ++k)
-                        if (k < C) v[k] += dacc[k][o];
-                    *(float4*)q = u;
-                }
-            }
+            for (int kk = 0; kk < CB && kk < 4; ++kk)
+                if (kk < C) v[kk] = fromf<T>(tof<T>(v[kk]) + dg[kk][r][c]);
+            *q = u;
         }
     }
 }
