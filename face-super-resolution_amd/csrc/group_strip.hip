@@ -123,6 +123,14 @@ struct GsTab {
     const float* fc1[FEN_GS_MAXNB];
     const float* fc2[FEN_GS_MAXNB];
     float* s_out[FEN_GS_MAXNB];
+    // training (SAVE): the group's saved set, as GsArgs
+    void* sv_x[FEN_GS_MAXNB];
+    void* sv_z1[FEN_GS_MAXNB];
+    void* sv_a1[FEN_GS_MAXNB];
+    void* sv_t[FEN_GS_MAXNB];
+    float* sv_mean[FEN_GS_MAXNB];
+    float* sv_hid[FEN_GS_MAXNB];
+    void* x_last;
 };
 inline size_t gs_tab_offset(int B, int S) { return (ws_layout(B, S).total + 255) & ~(size_t)255; }
 
@@ -155,7 +163,6 @@ struct GsArgs {
 
 template <typename T, bool SAVE, bool MULTI>
 __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
-    static_assert(!(SAVE && MULTI), "chained groups: inference only");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* img = smem + O_IMG;
     char* filt = smem + O_FILT;
@@ -438,7 +445,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         if (dma_late && (j > 0 || g > 0)) issue_kh02(Gw(ci));
         if (SAVE && j > 0) {                                // x_0 is the group input
             asm volatile("" ::: "memory");                  // the saves after every op the wait below needs
-            save_row(gc ? A.x_last : A.sv_x[j], xr);
+            save_row(MULTI ? uni(gc ? ctab[g].x_last : ctab[g].sv_x[j]) : gc ? A.x_last : A.sv_x[j], xr);
         }
 
         // ================= conv1 (or the group conv): 3 phases =================
@@ -604,8 +611,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         if (bwave) store_row(wsr, rowoff(L.ba, strip, par, side), av, 16);
         if (SAVE) {
             asm volatile("" ::: "memory");
-            if (wz1) save_row(A.sv_z1[j], zv);
-            save_row(A.sv_a1[j], av);
+            if (wz1) save_row(MULTI ? uni(ctab[g].sv_z1[j]) : A.sv_z1[j], zv);
+            save_row(MULTI ? uni(ctab[g].sv_a1[j]) : A.sv_a1[j], av);
         }
         // ================= conv2 =================
 #pragma unroll
@@ -785,8 +792,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             float* so = MULTI ? (float*)uni(ctab[g].s_out[j]) : A.s_out[j];
             if (strip == 0 && so) so[im * 64 + lane] = sg;
             if (strip == 0 && SAVE) {
-                A.sv_mean[j][im * 64 + lane] = mean;
-                if (lane < Cr) A.sv_hid[j][im * Cr + lane] = hid;
+                float* smn = MULTI ? (float*)uni(ctab[g].sv_mean[j]) : A.sv_mean[j];
+                float* shd = MULTI ? (float*)uni(ctab[g].sv_hid[j]) : A.sv_hid[j];
+                smn[im * 64 + lane] = mean;
+                if (lane < Cr) shd[im * Cr + lane] = hid;
             }
         }
         if (wave >= 2 && wave <= 4) {                       // the next conv's epilogue constants
@@ -798,7 +807,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         // x_j's and t_j's boundary rows out: drained, then the storing wave signals for itself
         if (SAVE) {                                         // t_j's save: last, left in flight
             asm volatile("" ::: "memory");
-            save_row(A.sv_t[j], tr);
+            save_row(MULTI ? uni(ctab[g].sv_t[j]) : A.sv_t[j], tr);
             GS_VMCNT_SAVES(8);
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -866,7 +875,8 @@ int chain_tab(const fen_group_strip_desc* d, int ng, std::vector<GsTab>& tab) {
     for (int g = 0; g < ng; ++g) {
         const fen_group_strip_desc& e = d[g];
         if (e.dtype != d0.dtype || e.B != d0.B || e.H != d0.H || e.W != d0.W || e.C != d0.C || e.Cr != d0.Cr ||
-            e.nb != d0.nb || e.res_scale != d0.res_scale || e.save || e.work != d0.work)
+            e.nb != d0.nb || e.res_scale != d0.res_scale || (e.save != 0) != (d0.save != 0) || e.work != d0.work ||
+            e.pre_elide != d0.pre_elide)
             return FEN_EINVAL;
         if (!e.x || !e.y || !e.wg || !e.bg || e.x == e.y) return FEN_EINVAL;
         if (g > 0 && e.x != d[g - 1].y) return FEN_EINVAL;                   // a chain: output -> next input
@@ -880,6 +890,17 @@ int chain_tab(const fen_group_strip_desc* d, int ng, std::vector<GsTab>& tab) {
             t.alpha[j] = e.alpha[j], t.fc1[j] = e.fc1[j], t.fc2[j] = e.fc2[j], t.s_out[j] = e.s_out[j];
         }
         t.w[2 * e.nb] = e.wg, t.bias[2 * e.nb] = e.bg;
+        if (e.save) {                                    // as fen_group_strip's checks
+            if (!e.x_last) return FEN_EINVAL;
+            t.x_last = e.x_last;
+            for (int j = 0; j < e.nb; ++j) {
+                if ((j > 0 && !e.sv_x[j]) || !e.sv_z1[j] || !e.sv_a1[j] || !e.sv_t[j] || !e.sv_mean[j] ||
+                    !e.sv_hid[j] || !e.s_out[j])
+                    return FEN_EINVAL;
+                t.sv_x[j] = e.sv_x[j], t.sv_z1[j] = e.sv_z1[j], t.sv_a1[j] = e.sv_a1[j], t.sv_t[j] = e.sv_t[j];
+                t.sv_mean[j] = e.sv_mean[j], t.sv_hid[j] = e.sv_hid[j];
+            }
+        }
     }
     if (!d0.work || d0.work_bytes < gs_tab_offset(d0.B, d0.H / SR) + (size_t)ng * sizeof(GsTab)) return FEN_EINVAL;
     return FEN_OK;
@@ -981,10 +1002,17 @@ extern "C" int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, void
     a.status = d0.status, a.fault = d0.fault;
     a.tab = (const GsTab*)((const char*)d0.work + gs_tab_offset(d0.B, d0.H / SR));
     a.ng = ng;
+    a.save = d0.save ? 1 : 0;
+    a.pre_elide = d0.pre_elide;
     const int grid = d0.B * (d0.H / SR);
     hipStream_t s = (hipStream_t)stream;
-    if (d0.dtype == FEN_F16) launch_gs<f16, false, true>(a, grid, s);
-    else launch_gs<bf16, false, true>(a, grid, s);
+    if (d0.dtype == FEN_F16) {
+        if (a.save) launch_gs<f16, true, true>(a, grid, s);
+        else launch_gs<f16, false, true>(a, grid, s);
+    } else {
+        if (a.save) launch_gs<bf16, true, true>(a, grid, s);
+        else launch_gs<bf16, false, true>(a, grid, s);
+    }
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

@@ -143,11 +143,8 @@ class FENEngine:
         s, ctx = self.spec, self.ctx
         fw = Forward(s, ctx, self.Wt, save=self.train)
         feat0 = fw.head(self.x)
-        if self.train:
-            h, self.saved = feat0, []
-            for g in range(s.G):
-                h, sv = fw.group(h, g)
-                self.saved.append(sv)
+        if self.train:   # every group output kept: the next group's saved input
+            h, self.saved = fw.body(feat0, [ctx.alloc(feat0.shape) for _ in range(s.G)])
         else:
             h, self.saved = fw.body(feat0, [ctx.scratch(f"grp_pp{g & 1}", feat0.shape) for g in range(s.G)])
         hr = self.hr if self.train else None

@@ -68,6 +68,9 @@ GROUP_STRIP_TRAIN = os.environ.get("FEN_GROUP_STRIP_TRAIN", "1") != "0"
 # inference: the body's G groups as ONE fen_group_strip_chain launch (strips stay on their CUs
 # across groups); FEN_GROUP_CHAIN=0 keeps a fen_group_strip launch per group
 GROUP_CHAIN = os.environ.get("FEN_GROUP_CHAIN", "1") != "0"
+# ... and the training forward too (the launch writes every group's saved set);
+# FEN_GROUP_CHAIN_TRAIN=0 keeps a training launch per group
+GROUP_CHAIN_TRAIN = os.environ.get("FEN_GROUP_CHAIN_TRAIN", "1") != "0"
 # inference at 128 channels (BASELINE configs[4]): a ResidualGroup as 2 * nb + 1 fen_rcab_c128
 # launches (rcab128.hip: each RCAB's gate deferred into the next conv's input, its pool sums in
 # conv2's epilogue) where the envelope holds (16-bit, H % 4 == 0, W % 64 == 0, Cr <= 32);
@@ -453,13 +456,16 @@ class Forward:
         return sv
 
     def _chain_ok(self, x) -> bool:
-        return GROUP_CHAIN and not self.save and self.s.G > 1 and self._strip_ok(x) and not self._c128_ok(x)
+        return (GROUP_CHAIN and (not self.save or GROUP_CHAIN_TRAIN) and self.s.G > 1 and self._strip_ok(x) and
+                not self._c128_ok(x))
 
     def body(self, x: torch.Tensor, outs: Sequence[torch.Tensor]):
         """The body's ResidualGroups (custom.py:168-169, blocks.py:185-189 each) -> (h, saved per
-        group); outs[g] is group g's output (consecutive outputs distinct, outs[0] not x).  In
-        inference on the strip kernels: ONE fen_group_strip_chain launch (GROUP_CHAIN), each
-        strip resident on its CU through all G groups; otherwise a launch (or chain) per group."""
+        group); outs[g] is group g's output (consecutive outputs distinct, outs[0] not x; in
+        training all distinct: each is the next group's saved input).  On the strip kernels: ONE
+        fen_group_strip_chain launch (GROUP_CHAIN; training: GROUP_CHAIN_TRAIN, the launch also
+        writes every group's saved set), each strip resident on its CU through all G groups;
+        otherwise a launch (or chain) per group."""
         s, ctx = self.s, self.ctx
         if not self._chain_ok(x):
             saved, h = [], x

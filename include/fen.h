@@ -292,7 +292,8 @@ int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int
 size_t fen_group_strip_work_bytes(int B, int H);
 int fen_group_strip(const fen_group_strip_desc* d, void* stream);
 /* ng consecutive ResidualGroups (reference custom.py:168-169, the body's group loop) as ONE
- * launch, inference: d[0..ng-1] are the groups' descriptors as for fen_group_strip (save = 0),
+ * launch: d[0..ng-1] are the groups' descriptors as for fen_group_strip (all with the same
+ * save and pre_elide: training writes every group's saved set as fen_group_strip does),
  * d[g].y == d[g+1].x, all sharing d[0].work (fen_group_strip_chain_work_bytes(B, H, ng) bytes:
  * the workspace plus the groups' parameter table), d[0].status / fault used.  A strip stays on
  * its CU across the groups: group g's output rows become group g+1's x_0 in registers, the

@@ -174,3 +174,53 @@ def test_group_chain_refuses_unprepared():
         ds[1].x = old
     assert fn(ds, ng, s) == 0
     torch.cuda.synchronize()
+
+
+def _run_save(q, G, n, x, dtype, chain):
+    from src.hip import net
+    from src.hip.net import Forward, NetSpec, Weights
+    from src.hip.program import Ctx
+    old = net.GROUP_CHAIN
+    net.GROUP_CHAIN = chain
+    try:
+        ctx = Ctx(dtype, DEV)
+        Wt = Weights({k: v.to(DEV) for k, v in q.items()}, dtype, DEV)
+        ctx.keep(Wt)
+        fw = Forward(NetSpec(C=64, G=G, NB=n, Cr=16), ctx, Wt, save=True)
+        used = fw._chain_ok(x)
+        outs = [torch.empty_like(x) for _ in range(G)]
+        ctx.keep(outs)
+        h, saved = fw.body(x, outs)
+        torch.cuda.synchronize()
+    finally:
+        net.GROUP_CHAIN = old
+    return h, saved, used
+
+
+@pytest.mark.parametrize("B,H,G,n,elide", [(32, 64, 6, 10, True), (2, 64, 3, 2, False), (3, 16, 2, 3, True)])
+def test_group_chain_training_saves_bit_exact(B, H, G, n, elide):
+    """Training form (bf16): the chained launch writes every group's saved set -- each RCAB's
+    x_j, z1 (unless elided), a1, t_j, s, mean, hid and the chain's output -- bit-identical to a
+    training launch per group, and the same outputs."""
+    from src.hip import lib as L, net
+    dtype = torch.bfloat16
+    q = _params(G, n, seed=60 + n)
+    x = torch.randn(B, H, 64, 64, generator=torch.Generator().manual_seed(8)).to(DEV, dtype)
+    old_pe, net.PRE_ELIDE = net.PRE_ELIDE, elide
+    try:
+        yc, svc, used = _run_save(q, G, n, x, dtype, True)
+        yg, svg, used_g = _run_save(q, G, n, x, dtype, False)
+    finally:
+        net.PRE_ELIDE = old_pe
+    L.check_strip_status()
+    assert used and not used_g
+    assert torch.equal(yc, yg)
+    assert len(svc) == len(svg) == G
+    for g in range(G):
+        a, b = svc[g], svg[g]
+        assert a["z1_elided"] == b["z1_elided"]
+        assert torch.equal(a["x"], b["x"]) and torch.equal(a["x_last"], b["x_last"]), g
+        for j, (u, v) in enumerate(zip(a["blocks"], b["blocks"])):
+            keys = ("x", "a1", "t", "mean", "hid", "s") + (() if a["z1_elided"] else ("z1",))
+            for k in keys:
+                assert torch.equal(u[k], v[k]), (g, j, k)
