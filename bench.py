@@ -24,9 +24,9 @@ AdamW) at batch 32 per GPU -- the DP path of the north star.
 roofline: the dominant kernel is k_group_strip (group_strip.hip) in its chained form
   (fen_group_strip_chain): the body's 6 ResidualGroups -- each 10 fused RCABs (conv1 -> PReLU ->
   conv2 -> SE gate -> scaled residual) + the group conv + skip, 64 ch, 64x64, B=32 -- as one
-  persistent launch; algorithmic FLOPs per launch = 6 x 21 convs x 2 * 32*64*64 px * 64 co *
-  576 (= 9 taps * 64 ci) = 1217.6 GFLOP (9.66 per conv, 19.33 per RCAB), timed live here
-  with HIP events on the launch stream; peak = 2500 TFLOP/s fp16 / bf16 dense.
+  persistent launch, conv_after_body its last step; algorithmic FLOPs per launch = (6 x 21 + 1)
+  convs x 2 * 32*64*64 px * 64 co * 576 (= 9 taps * 64 ci) = 1227.3 GFLOP (9.66 per conv),
+  timed live here with HIP events on the launch stream; peak = 2500 TFLOP/s fp16 / bf16 dense.
 pcie_inclusive: the same forward with the batch handed over as NCHW fp32 pinned host buffers
 (H2D of the LR batch, graph replay, D2H of the SR batch, serial on one stream) -- reported
 beside `value`, never as it.
@@ -117,12 +117,13 @@ def dominant_op(engine):
     (fen_rcab_deferred), else the RCAB conv1 (64->64, 64x64, B=32) of the per-op path."""
     for op in engine.ctx.ops:
         if op[0] == "group_strip_chain":
-            ds, ng = op[2]
+            ds, ng, tail = op[2]
             d = ds[0]
             conv = 2.0 * d.B * d.H * d.W * 64 * 576
             return op, "k_group_strip chain (the body: %d ResidualGroups in one launch, each %d x [conv1+PReLU+conv2+" \
-                       "SE gate+residual] + group conv + skip, 64ch %dx%d, B=%d)" % (ng, d.nb, d.H, d.W, d.B), \
-                ng * (2 * d.nb + 1) * conv
+                       "SE gate+residual] + group conv + skip%s, 64ch %dx%d, B=%d)" % (
+                           ng, d.nb, "; + conv_after_body" if tail is not None else "", d.H, d.W, d.B), \
+                (ng * (2 * d.nb + 1) + (1 if tail is not None else 0)) * conv
     for op in engine.ctx.ops:
         if op[0] == "group_strip":
             d = op[2][0]._obj

@@ -117,6 +117,7 @@ __host__ __device__ inline Ws ws_layout(int B, int S) {
 struct GsTab {
     const void* x;
     void* y;
+    const void* skip;                        // the residual added after the group conv (x; the tail: feat0)
     const void* w[2 * FEN_GS_MAXNB + 1];
     const float* bias[2 * FEN_GS_MAXNB + 1];
     const float* alpha[FEN_GS_MAXNB];
@@ -159,6 +160,7 @@ struct GsArgs {
     int pre_elide;                            // training: no z1 save for an RCAB whose slopes are all > 0
     const GsTab* tab;                         // MULTI: ng groups in a row, parameters from here
     int ng;
+    int tail;                                 // MULTI: + conv_after_body as a group of no RCABs (table row ng)
 };
 
 template <typename T, bool SAVE, bool MULTI>
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     // the running group's input / output and parameters: the launch's arguments, or (MULTI,
     // groups g = 0 .. ng-1 in a row, group g's output = group g+1's input) the table's row g
     int g = 0;
-    const int NG = MULTI ? A.ng : 1;
+    const int NG = MULTI ? A.ng + A.tail : 1;
     // (table entries are wave-uniform: readfirstlane'd, whatever load the compiler picks)
     auto uni = [](const void* p_) -> void* {
         const unsigned long long v = (unsigned long long)p_;
@@ -369,8 +371,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     bool ok = true;
     for (;;) {                                              // groups (one unless MULTI)
     kbase = g * (NB + 1), rbase = g * NB;
+    const bool gtail = MULTI && g >= A.ng;                  // conv_after_body: a "group" of no RCABs
     for (int j = 0;; ++j) {                                // one exit: the group conv's break
-        const bool gc = j == NB;
+        const bool gc = j == (gtail ? 0 : NB);
         // boundary rows and pool partials double-buffered by RCAB count (not step: a group conv
         // publishes neither, and each buffer's reuse is ordered by the hand-offs of the RCAB between)
         const int par = (rbase + j) & 1;
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             asm volatile("" : "+v"(ll), "+s"(im), "+s"(strip), "+s"(S), "+s"(r0));
             lane = ll, q = ll >> 4, c16 = ll & 15;
         }
-        const int ci = gc ? 2 * NB : 2 * j;
+        const int ci = gc ? (gtail ? 0 : 2 * NB) : 2 * j;
         GSTAMP(sb);
         uint4 nx[4], nt[4];
         // the halo waves poll the neighbour's flag before issuing their tap DMA: a poll waits on
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             if (MULTI) {
                 // sc1 loads: a chained group's input is the previous group's output, rows this
                 // wave stored in this launch
-                const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)Gx(), 0, (int)act_bytes, 0x00020000);
+                const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(uni(ctab[g].skip), 0, (int)act_bytes, 0x00020000);
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -546,7 +549,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                     if (bwave) store_row(wsr, booff(strip, side), xr, 16);
                     if (wave >= 2 && wave <= 4) {
                         CTab& nt_ = ctab[g + 1];
-                        cv = ((const float*)uni(wave == 2 ? nt_.bias[0] : wave == 3 ? nt_.alpha[0] : nt_.bias[1]))[lane];
+                        if (g + 1 < A.ng)                   // its first RCAB's b1, alpha, b2
+                            cv = ((const float*)uni(wave == 2 ? nt_.bias[0] : wave == 3 ? nt_.alpha[0] : nt_.bias[1]))[lane];
+                        else                                // the tail conv's bias (the group conv's slot)
+                            cv = wave == 4 ? ((const float*)uni(nt_.bias[0]))[lane] : 0.f;
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (bwave && lane == 0)
@@ -866,12 +872,13 @@ void launch_gs(const GsArgs& a, int grid, hipStream_t s) {
 std::mutex g_chain_mu;
 std::map<const void*, std::vector<GsTab>> g_chain_tabs;
 
-int chain_tab(const fen_group_strip_desc* d, int ng, std::vector<GsTab>& tab) {
+int chain_tab(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail, std::vector<GsTab>& tab) {
     if (!d || ng <= 0) return FEN_EINVAL;
     const fen_group_strip_desc& d0 = d[0];
     if (!fen_group_strip_supported(d0.dtype, d0.B, d0.H, d0.W, d0.C, d0.Cr, d0.nb)) return FEN_EUNSUPPORTED;
-    if (ng * (d0.nb + 1) > 254) return FEN_EUNSUPPORTED;                      // step tags
-    tab.assign(ng, GsTab{});
+    const int rows = ng + (tail ? 1 : 0);
+    if (rows * (d0.nb + 1) > 254) return FEN_EUNSUPPORTED;                    // step tags
+    tab.assign(rows, GsTab{});
     for (int g = 0; g < ng; ++g) {
         const fen_group_strip_desc& e = d[g];
         if (e.dtype != d0.dtype || e.B != d0.B || e.H != d0.H || e.W != d0.W || e.C != d0.C || e.Cr != d0.Cr ||
@@ -881,7 +888,7 @@ int chain_tab(const fen_group_strip_desc* d, int ng, std::vector<GsTab>& tab) {
         if (!e.x || !e.y || !e.wg || !e.bg || e.x == e.y) return FEN_EINVAL;
         if (g > 0 && e.x != d[g - 1].y) return FEN_EINVAL;                   // a chain: output -> next input
         GsTab& t = tab[g];
-        t.x = e.x, t.y = e.y;
+        t.x = e.x, t.y = e.y, t.skip = e.x;
         for (int j = 0; j < e.nb; ++j) {
             if (!e.w1[j] || !e.b1[j] || !e.alpha[j] || !e.w2[j] || !e.b2[j] || !e.fc1[j] || !e.fc2[j])
                 return FEN_EINVAL;
@@ -902,7 +909,16 @@ int chain_tab(const fen_group_strip_desc* d, int ng, std::vector<GsTab>& tab) {
             }
         }
     }
-    if (!d0.work || d0.work_bytes < gs_tab_offset(d0.B, d0.H / SR) + (size_t)ng * sizeof(GsTab)) return FEN_EINVAL;
+    if (tail) {
+        // conv_after_body (custom.py:172-175): y = conv(body output) + bias + skip
+        if (!tail->w || !tail->bias || !tail->skip || !tail->y || tail->y == d[ng - 1].y || tail->y == tail->skip)
+            return FEN_EINVAL;
+        GsTab& t = tab[ng];
+        t.x = d[ng - 1].y, t.y = tail->y, t.skip = tail->skip;
+        t.w[0] = tail->w, t.bias[0] = tail->bias;
+        if (d0.save) t.x_last = d[ng - 1].y;                     // (unused: no save in a group of no RCABs)
+    }
+    if (!d0.work || d0.work_bytes < gs_tab_offset(d0.B, d0.H / SR) + (size_t)rows * sizeof(GsTab)) return FEN_EINVAL;
     return FEN_OK;
 }
 
@@ -965,12 +981,12 @@ extern "C" int fen_group_strip(const fen_group_strip_desc* d, void* stream) {
 
 extern "C" size_t fen_group_strip_chain_work_bytes(int B, int H, int ng) {
     if (B <= 0 || H <= 0 || H % SR || ng <= 0) return 0;
-    return gs_tab_offset(B, H / SR) + (size_t)ng * sizeof(GsTab);
+    return gs_tab_offset(B, H / SR) + (size_t)(ng + 1) * sizeof(GsTab);     // + the tail's row
 }
 
-extern "C" int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng) {
+extern "C" int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail) {
     std::vector<GsTab> tab;
-    const int rc = chain_tab(d, ng, tab);
+    const int rc = chain_tab(d, ng, tail, tab);
     if (rc != FEN_OK) return rc;
     char* dst = (char*)d[0].work + gs_tab_offset(d[0].B, d[0].H / SR);
     const hipError_t e = hipMemcpy(dst, tab.data(), tab.size() * sizeof(GsTab), hipMemcpyHostToDevice);
@@ -983,9 +999,10 @@ extern "C" int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int 
     return FEN_OK;
 }
 
-extern "C" int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, void* stream) {
+extern "C" int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail,
+                                     void* stream) {
     std::vector<GsTab> tab;
-    const int rc = chain_tab(d, ng, tab);
+    const int rc = chain_tab(d, ng, tail, tab);
     if (rc != FEN_OK) return rc;
     {
         std::lock_guard<std::mutex> lk(g_chain_mu);
@@ -1002,6 +1019,7 @@ extern "C" int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, void
     a.status = d0.status, a.fault = d0.fault;
     a.tab = (const GsTab*)((const char*)d0.work + gs_tab_offset(d0.B, d0.H / SR));
     a.ng = ng;
+    a.tail = tail ? 1 : 0;
     a.save = d0.save ? 1 : 0;
     a.pre_elide = d0.pre_elide;
     const int grid = d0.B * (d0.H / SR);

@@ -143,13 +143,14 @@ class FENEngine:
         s, ctx = self.spec, self.ctx
         fw = Forward(s, ctx, self.Wt, save=self.train)
         feat0 = fw.head(self.x)
+        fb = fw.fb_buffer(feat0.shape)   # conv_after_body's output: the chained launch may compute it
         if self.train:   # every group output kept: the next group's saved input
-            h, self.saved = fw.body(feat0, [ctx.alloc(feat0.shape) for _ in range(s.G)])
+            h, self.saved = fw.body(feat0, [ctx.alloc(feat0.shape) for _ in range(s.G)], fb=fb)
         else:
-            h, self.saved = fw.body(feat0, [ctx.scratch(f"grp_pp{g & 1}", feat0.shape) for g in range(s.G)])
+            h, self.saved = fw.body(feat0, [ctx.scratch(f"grp_pp{g & 1}", feat0.shape) for g in range(s.G)], fb=fb)
         hr = self.hr if self.train else None
         _, self.saved_tail = fw.tail(h, feat0, self.x, training, out=self.out, hr=hr,
-                                     l1_scale=self.l1_scale if self.train else 0.0)
+                                     l1_scale=self.l1_scale if self.train else 0.0, fb=fb if fw.fb_done else None)
         if self.train:
             lp = self.saved_tail["loss_part"]
             colsum(ctx, lp, lp.shape[0], 1, self.loss, scale=1.0 / (self.B * s.out_ch * self.H * self.W))

@@ -87,6 +87,10 @@ class GroupStripDesc(Structure):
     ]
 
 
+class GroupStripChainTail(Structure):    # fen_group_strip_chain_tail: conv_after_body in the chain
+    _fields_ = [("w", c_void_p), ("bias", c_void_p), ("skip", c_void_p), ("y", c_void_p)]
+
+
 class GroupStripBwdDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("Cr", c_int), ("nb", c_int),
@@ -133,8 +137,8 @@ _SIGS = {
     "fen_group_strip_work_bytes": (c_size_t, [c_int, c_int]),
     "fen_group_strip": (c_int, [POINTER(GroupStripDesc), c_void_p]),
     "fen_group_strip_chain_work_bytes": (c_size_t, [c_int, c_int, c_int]),
-    "fen_group_strip_chain_prepare": (c_int, [POINTER(GroupStripDesc), c_int]),
-    "fen_group_strip_chain": (c_int, [POINTER(GroupStripDesc), c_int, c_void_p]),
+    "fen_group_strip_chain_prepare": (c_int, [POINTER(GroupStripDesc), c_int, POINTER(GroupStripChainTail)]),
+    "fen_group_strip_chain": (c_int, [POINTER(GroupStripDesc), c_int, POINTER(GroupStripChainTail), c_void_p]),
     "fen_group_strip_bwd_supported": (c_int, [c_int] * 7),
     "fen_group_strip_bwd_work_bytes": (c_size_t, [c_int, c_int]),
     "fen_group_strip_bwd": (c_int, [POINTER(GroupStripBwdDesc), c_void_p]),

@@ -71,6 +71,9 @@ GROUP_CHAIN = os.environ.get("FEN_GROUP_CHAIN", "1") != "0"
 # ... and the training forward too (the launch writes every group's saved set);
 # FEN_GROUP_CHAIN_TRAIN=0 keeps a training launch per group
 GROUP_CHAIN_TRAIN = os.environ.get("FEN_GROUP_CHAIN_TRAIN", "1") != "0"
+# ... with conv_after_body as the chain's last step (a group of no RCABs); FEN_CHAIN_AFTER_BODY=0
+# keeps it a conv launch of its own
+CHAIN_AFTER_BODY = os.environ.get("FEN_CHAIN_AFTER_BODY", "1") != "0"
 # inference at 128 channels (BASELINE configs[4]): a ResidualGroup as 2 * nb + 1 fen_rcab_c128
 # launches (rcab128.hip: each RCAB's gate deferred into the next conv's input, its pool sums in
 # conv2's epilogue) where the envelope holds (16-bit, H % 4 == 0, W % 64 == 0, Cr <= 32);
@@ -455,18 +458,25 @@ class Forward:
         ctx.keep(d)
         return sv
 
+    def fb_buffer(self, shape) -> torch.Tensor:
+        """conv_after_body's output buffer (kept for backward in training)."""
+        return self.ctx.alloc(shape) if self.save else self.ctx.scratch("tail_fb", shape)
+
     def _chain_ok(self, x) -> bool:
         return (GROUP_CHAIN and (not self.save or GROUP_CHAIN_TRAIN) and self.s.G > 1 and self._strip_ok(x) and
                 not self._c128_ok(x))
 
-    def body(self, x: torch.Tensor, outs: Sequence[torch.Tensor]):
+    def body(self, x: torch.Tensor, outs: Sequence[torch.Tensor], fb: Optional[torch.Tensor] = None):
         """The body's ResidualGroups (custom.py:168-169, blocks.py:185-189 each) -> (h, saved per
         group); outs[g] is group g's output (consecutive outputs distinct, outs[0] not x; in
         training all distinct: each is the next group's saved input).  On the strip kernels: ONE
         fen_group_strip_chain launch (GROUP_CHAIN; training: GROUP_CHAIN_TRAIN, the launch also
         writes every group's saved set), each strip resident on its CU through all G groups;
-        otherwise a launch (or chain) per group."""
+        otherwise a launch (or chain) per group.  With `fb` given and the chain taken, the same
+        launch also computes conv_after_body (custom.py:172-175: fb = conv(h) + b + x) into fb and
+        self.fb_done is set (tail() then skips that conv)."""
         s, ctx = self.s, self.ctx
+        self.fb_done = False
         if not self._chain_ok(x):
             saved, h = [], x
             for g in range(s.G):
@@ -488,9 +498,17 @@ class Forward:
         for g in range(G):
             ds[g].work, ds[g].work_bytes = ptr(work), nbytes
             ds[g].status, ds[g].fault = L.strip_status_ptr(ctx.device), GS_FAULT & 1
-        L.check(ctx.lib.fen_group_strip_chain_prepare(ds, G), "group_strip_chain_prepare")
-        ctx.emit("group_strip_chain", ctx.lib.fen_group_strip_chain, ds, G)
+        tail = None
+        if fb is not None and CHAIN_AFTER_BODY:
+            tail = L.GroupStripChainTail()
+            tail.w, tail.bias = ptr(self.Wt.packed("conv_after_body", 0)), ptr(self.Wt.p["conv_after_body.bias"])
+            tail.skip, tail.y = ptr(x), ptr(fb)
+            ctx.keep(tail)
+        tp = byref(tail) if tail is not None else None
+        L.check(ctx.lib.fen_group_strip_chain_prepare(ds, G, tp), "group_strip_chain_prepare")
+        ctx.emit("group_strip_chain", ctx.lib.fen_group_strip_chain, ds, G, tp)
         ctx.keep(ds)
+        self.fb_done = tail is not None
         return h, saved
 
     def _group_strip_desc(self, d, x: torch.Tensor, pre: str, names: Sequence[str], y: torch.Tensor) -> dict:
@@ -640,11 +658,15 @@ class Forward:
         return y, dict(blocks=blocks, x=x, x_last=h)
 
     def tail(self, feat: torch.Tensor, feat0: torch.Tensor, x_lr: torch.Tensor, training: bool,
-             out: Optional[torch.Tensor] = None, hr: Optional[torch.Tensor] = None, l1_scale: float = 0.0):
-        """conv_after_body + skip, upsampler, conv_last + bicubic skip (+ clamp / + L1 grad)."""
+             out: Optional[torch.Tensor] = None, hr: Optional[torch.Tensor] = None, l1_scale: float = 0.0,
+             fb: Optional[torch.Tensor] = None):
+        """conv_after_body + skip, upsampler, conv_last + bicubic skip (+ clamp / + L1 grad).
+        fb given: conv_after_body's output, already computed (the chained body launch)."""
         s, ctx, Wt, p = self.s, self.ctx, self.Wt, self.Wt.p
         B, H, W, C = feat.shape
-        fb = ctx.alloc(feat.shape) if self.save else ctx.scratch("tail_fb", feat.shape)
+        fb_given = fb is not None
+        if fb is None:
+            fb = self.fb_buffer(feat.shape)
 
         def c128(hh_, ww_) -> bool:   # the 128-channel kernels (inference)
             return (RCAB_C128 and not self.save and
@@ -659,7 +681,9 @@ class Forward:
             ctx.emit(name, ctx.lib.fen_rcab_c128, byref(d))
             ctx.keep(d)
 
-        if c128(H, W):
+        if fb_given:
+            pass
+        elif c128(H, W):
             c128_launch("c128_after_body", 3, feat, Wt.packed("conv_after_body", 0), p["conv_after_body.bias"], fb,
                         res_=feat0)
         else:

@@ -300,10 +300,18 @@ int fen_group_strip(const fen_group_strip_desc* d, void* stream);
  * neighbours' boundary rows by hand-off; each group's output is still written to d[g].y (the
  * next group's skip input).  fen_group_strip_chain_prepare writes the table (a synchronous
  * copy: once, outside a graph capture, before the first launch); a launch whose descriptors
- * differ from the prepared table returns FEN_EINVAL.  ng * (nb + 1) <= 254.                  */
-size_t fen_group_strip_chain_work_bytes(int B, int H, int ng);
-int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng);
-int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, void* stream);
+ * differ from the prepared table (or tail) returns FEN_EINVAL.  (ng + 1) * (nb + 1) <= 254.  */
+/* optional: the body's conv_after_body (custom.py:172-175: conv(body output) + bias + feat0) as
+ * a last "group" of no RCABs in the same launch; its input is d[ng-1].y                        */
+typedef struct {
+    const void* w;             /* conv_after_body packed mode 0 [9][64][64]                    */
+    const float* bias;         /* [64]                                                         */
+    const void* skip;          /* the residual added: the body's input (feat0)                 */
+    void* y;                   /* out NHWC [B,H,64,64] (not d[ng-1].y, not skip)               */
+} fen_group_strip_chain_tail;
+size_t fen_group_strip_chain_work_bytes(int B, int H, int ng);   /* room for ng groups + a tail */
+int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail);
+int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail, void* stream);
 
 /* 128-channel RCAB convs (BASELINE configs[4]: num_channels = 128, Cr = 32; RCAB blocks.py:
  * 135-153, ChannelAttention blocks.py:83-92, ResidualGroup blocks.py:185-189), one launch per

@@ -157,22 +157,22 @@ def test_group_chain_refuses_unprepared():
     q = _params(G, n, seed=4)
     x = torch.randn(1, 64, 64, 64, generator=torch.Generator().manual_seed(2)).to(DEV, dtype)
     _, _, ctx, _ = _run(q, G, n, x, dtype, record=True)
-    name, fn, (ds, ng) = ctx.ops[0]
+    name, fn, (ds, ng, tp) = ctx.ops[0]
     assert name == "group_strip_chain"
     s = torch.cuda.current_stream().cuda_stream
     old = ds[1].fc1[0]
     ds[1].fc1[0] = ds[1].fc2[0]                           # valid descriptors, not the prepared table
     try:
-        assert fn(ds, ng, s) != 0
+        assert fn(ds, ng, tp, s) != 0
     finally:
         ds[1].fc1[0] = old
     old = ds[1].x
     ds[1].x = ds[1].y                                     # not a chain (x aliases y)
     try:
-        assert fn(ds, ng, s) != 0
+        assert fn(ds, ng, tp, s) != 0
     finally:
         ds[1].x = old
-    assert fn(ds, ng, s) == 0
+    assert fn(ds, ng, tp, s) == 0
     torch.cuda.synchronize()
 
 
@@ -224,3 +224,48 @@ def test_group_chain_training_saves_bit_exact(B, H, G, n, elide):
             keys = ("x", "a1", "t", "mean", "hid", "s") + (() if a["z1_elided"] else ("z1",))
             for k in keys:
                 assert torch.equal(u[k], v[k]), (g, j, k)
+
+
+@pytest.mark.parametrize("prec", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,H,G,n", [(32, 64, 6, 10), (3, 16, 2, 1)])
+def test_group_chain_after_body(prec, B, H, G, n):
+    """conv_after_body (custom.py:172-175) as the chain's last step (a group of no RCABs):
+    fb = conv(body output) + bias + feat0 against the per-op conv launch on the chain's own body
+    output (same rounding points; the two kernels sum the 576 products in different orders:
+    rel-L2 <= 1e-3 fp16 / 5e-3 bf16), the body output itself bit-exact."""
+    from src.hip import lib as L, net
+    from src.hip.net import Forward, NetSpec, Weights, conv
+    from src.hip.program import Ctx
+    dtype = DT[prec]
+    q = _params(G, n, seed=77)
+    g = torch.Generator().manual_seed(78)
+    q["conv_after_body.weight"] = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    q["conv_after_body.bias"] = torch.randn(64, generator=g) * 0.1
+    x = torch.randn(B, H, 64, 64, generator=torch.Generator().manual_seed(6)).to(DEV, dtype)
+    ctx = Ctx(dtype, DEV)
+    Wt = Weights({k: v.to(DEV) for k, v in q.items()}, dtype, DEV)
+    ctx.keep(Wt)
+    fw = Forward(NetSpec(C=64, G=G, NB=n, Cr=16), ctx, Wt, save=False)
+    outs = [torch.empty_like(x), torch.empty_like(x)]
+    fb = torch.empty_like(x)
+    h, _ = fw.body(x, [outs[i & 1] for i in range(G)], fb=fb)
+    assert fw.fb_done and fw._chain_ok(x)
+    torch.cuda.synchronize()
+    L.check_strip_status()
+    ref = torch.empty_like(x)
+    conv(ctx, h, Wt.packed("conv_after_body", 0), B, H, 64, 64, 64, bias=Wt.p["conv_after_body.bias"], y=ref,
+         res=(x,))
+    torch.cuda.synchronize()
+    r = _rel(fb.float(), ref.float())
+    print(f"{prec} B={B}: conv_after_body rel {r:.2e}")
+    assert r <= (5e-3 if prec == "bf16" else 1e-3), r
+    old = net.CHAIN_AFTER_BODY
+    net.CHAIN_AFTER_BODY = False
+    try:
+        fw2 = Forward(NetSpec(C=64, G=G, NB=n, Cr=16), ctx, Wt, save=False)
+        h2, _ = fw2.body(x, [torch.empty_like(x) for _ in range(G)], fb=torch.empty_like(x))
+        assert not fw2.fb_done
+        torch.cuda.synchronize()
+    finally:
+        net.CHAIN_AFTER_BODY = old
+    assert torch.equal(h, h2)

@@ -17,7 +17,7 @@ echo "write rc=$?"
 ALG=$(grep algorithmic_bytes_per_launch gpurun_out/profc/fetch.log | awk '{print $2}')
 python tools/prof_summary.py pmc "$(find gpurun_out/profc/fetch -name '*counter_collection.csv' | head -1)" \
     "$(find gpurun_out/profc/write -name '*counter_collection.csv' | head -1)" gpurun_out/profc/pmc_k_group_strip_chain.json \
-    "k_group_strip chain" "$ALG" "k_group_strip chain (the body: 6 ResidualGroups x (10 RCABs + group conv), one launch), fp16, B=32, 64x64x64" "k_group_strip!bwd"
+    "k_group_strip chain" "$ALG" "k_group_strip chain (the body: 6 ResidualGroups x (10 RCABs + group conv) + conv_after_body, one launch), fp16, B=32, 64x64x64" "k_group_strip!bwd"
 cat gpurun_out/profc/pmc_k_group_strip_chain.json
 i=0
 while read -r set; do

@@ -29,9 +29,9 @@ for gi, j in [(gi, j) for gi in range(NG) for j in range(NB)]:
     q[b + "conv2.bias"] = torch.randn(C, generator=g) * 0.1
     q[b + "channel_attention.fc.0.weight"] = torch.randn(CR, C, generator=g) * 0.3
     q[b + "channel_attention.fc.2.weight"] = torch.randn(C, CR, generator=g) * 0.3
-for pre in ([f"residual_groups.{gi}." for gi in range(NG)] if CHAIN else ["rg."]):
-    q[pre + "conv.weight"] = torch.randn(C, C, 3, 3, generator=g) * 0.05
-    q[pre + "conv.bias"] = torch.randn(C, generator=g) * 0.1
+for pre in ([f"residual_groups.{gi}.conv." for gi in range(NG)] + ["conv_after_body."] if CHAIN else ["rg.conv."]):
+    q[pre + "weight"] = torch.randn(C, C, 3, 3, generator=g) * 0.05
+    q[pre + "bias"] = torch.randn(C, generator=g) * 0.1
 pd = {k: v.cuda() for k, v in q.items()}
 ctx = Ctx(dt, "cuda", record=True)
 Wt = Weights(pd, dt, "cuda")
@@ -40,8 +40,9 @@ fw = Forward(NetSpec(C=C, G=NG, NB=NB, Cr=CR), ctx, Wt, save=False)
 if CHAIN:
     assert fw._chain_ok(x)
     outs = [torch.empty_like(x), torch.empty_like(x)]
-    y, _ = fw.body(x, [outs[gi & 1] for gi in range(NG)])
-    assert [op[0] for op in ctx.ops] == ["group_strip_chain"]
+    fb = torch.empty_like(x)                  # conv_after_body as the chain's last step
+    y, _ = fw.body(x, [outs[gi & 1] for gi in range(NG)], fb=fb)
+    assert [op[0] for op in ctx.ops] == ["group_strip_chain"] and fw.fb_done
 else:
     assert fw._strip_ok(x)
     y, _ = fw.group(x, 0, pre="rg.")
@@ -50,4 +51,6 @@ for _ in range(REPS):
 torch.cuda.synchronize()
 # the input read and the (last) output written once, every group's filters, SE weights and biases
 alg = 2 * x.numel() * 2 + NG * ((2 * NB + 1) * 9 * C * C * 2 + NB * 2 * CR * C * 4 + (3 * NB + 1) * C * 4)
+if CHAIN:   # + conv_after_body: its filter and bias, its output written (the body output is then internal)
+    alg += 9 * C * C * 2 + C * 4
 print("algorithmic_bytes_per_launch", alg)
