@@ -490,24 +490,26 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
         __syncthreads();                                    // B_X: every image row written; kh = 1 slots free
         if (!gc) issue_kh1(Gw(ci + 1));
         else if (MULTI && g + 1 < NG) issue_kh1(uni(ctab[g + 1].w[0]));   // the next group's conv1_0
+        uint2 x0r[4][4];                                    // the group conv's skip input, own row
+        if (MULTI && gc) {
+            // issued here, in flight under phases 2-3 (the chained kernel has the registers);
+            // sc1 loads: a chained group's input is the previous group's output, rows this wave
+            // stored in this launch
+            const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(uni(ctab[g].skip), 0, (int)act_bytes, 0x00020000);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    x0r[m][p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                              grs, (int)(px_off(r0 + wave, p) + (16 * m + 4 * q) * 2), 0, 16));
+        }
         conv_phase<T>(acc, img, filt, khP2, wave, q, c16);
         conv_phase<T>(acc, img, filt, khP3, wave, q, c16);
         GSTAMP(sb + 3);
         if (gc) {
             // ---- out = conv + bias + the group input (blocks.py:188-189): its own rows read
             // again here (once per launch; kept out of the conv's register peak)
-            uint2 x0r[4][4];
-            if (MULTI) {
-                // sc1 loads: a chained group's input is the previous group's output, rows this
-                // wave stored in this launch
-                const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(uni(ctab[g].skip), 0, (int)act_bytes, 0x00020000);
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-#pragma unroll
-                    for (int p = 0; p < 4; ++p)
-                        x0r[m][p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
-                                                                  grs, (int)(px_off(r0 + wave, p) + (16 * m + 4 * q) * 2), 0, 16));
-            } else {
+            if (!MULTI) {
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -531,6 +533,17 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 }
             }
             const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(Gy(), 0, (int)act_bytes, 0x00020000);
+            const bool handoff = MULTI && g + 1 < NG;
+            if (handoff && wave >= 2 && wave <= 4) {
+                // the next group's first constants: its first RCAB's b1, alpha, b2, or the tail
+                // conv's bias (the group conv's slot); issued before the stores (see below)
+                CTab& nt_ = ctab[g + 1];
+                if (g + 1 < A.ng) cv = ((const float*)uni(wave == 2 ? nt_.bias[0] : wave == 3 ? nt_.alpha[0] : nt_.bias[1]))[lane];
+                else cv = wave == 4 ? ((const float*)uni(nt_.bias[0]))[lane] : 0.f;
+            }
+            // the boundary rows for the neighbours before the output row: the flag waits for
+            // those (and every older op) only, the output's 8 stores stay in flight
+            if (handoff && bwave) store_row(wsr, booff(strip, side), ov, 16);
             store_row(yrs, (int)((size_t)(im * H + r0 + wave) * SW * 128), ov, 0);
             if (MULTI) {
                 // the next group: x_0 = this output (registers), its boundary rows to the
@@ -545,16 +558,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                         xr[m][p] = ov[m][p];
                         tr[m][p] = make_uint2(0u, 0u);
                     }
-                if (g + 1 < NG) {
-                    if (bwave) store_row(wsr, booff(strip, side), xr, 16);
-                    if (wave >= 2 && wave <= 4) {
-                        CTab& nt_ = ctab[g + 1];
-                        if (g + 1 < A.ng)                   // its first RCAB's b1, alpha, b2
-                            cv = ((const float*)uni(wave == 2 ? nt_.bias[0] : wave == 3 ? nt_.alpha[0] : nt_.bias[1]))[lane];
-                        else                                // the tail conv's bias (the group conv's slot)
-                            cv = wave == 4 ? ((const float*)uni(nt_.bias[0]))[lane] : 0.f;
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (handoff) {
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
                     if (bwave && lane == 0)
                         __hip_atomic_store(flag_of(strip, side, 2), tag_of(NB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __syncthreads();                        // the group conv's image reads done; the next conv1's kh = 1 taps visible
