@@ -181,15 +181,17 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
             const float spp = m23[o].x - mp * mp, stt = m23[o].y - mt * mt, spt = m4[o] - mp * mt;
             const float A1 = 2.f * mp * mt + C1, A2 = 2.f * spt + C2;
             const float B1 = mp * mp + mt * mt + C1, B2 = spp + stt + C2;
-            const float S = (A1 * A2) / (B1 * B2);
+            // v_rcp_f32 (1 ulp) for the five quotients: B1, B2 >= C1, C2 > 0 (no zero / denormal
+            // divisor); IEEE division sequences here were a quarter of the kernel's VALU issue
+            const float r1 = __builtin_amdgcn_rcpf(B1), r2 = __builtin_amdgcn_rcpf(B2), iB = r1 * r2;
+            const float S = (A1 * A2) * iB;
             const int gy = h0 - O1 + r, gx = w0 - O1 + c;
             const bool in = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
             const bool own = r >= O1 && r < O1 + ST && c >= O1 && c < O1 + ST;
             if (in && own) acc += S;
             if constexpr (GRAD) {
-                const float iB = 1.f / (B1 * B2);
-                abc[0][r][c] = in ? 2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (1.f / B1 - 1.f / B2) : 0.f;
-                abc[1][r][c] = in ? -S / B2 : 0.f;
+                abc[0][r][c] = in ? 2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (r1 - r2) : 0.f;
+                abc[1][r][c] = in ? -S * r2 : 0.f;
                 abc[2][r][c] = in ? 2.f * A1 * iB : 0.f;
             }
         }
