@@ -28,7 +28,8 @@ roofline: the dominant kernel is k_group_strip (group_strip.hip) in its chained 
   convs x 2 * 32*64*64 px * 64 co * 576 (= 9 taps * 64 ci) = 1227.3 GFLOP (9.66 per conv),
   timed live here with HIP events on the launch stream; peak = 2500 TFLOP/s fp16 / bf16 dense.
 pcie_inclusive: the same forward with the batch handed over as NCHW fp32 pinned host buffers
-(H2D of the LR batch, graph replay, D2H of the SR batch, serial on one stream) -- reported
+(H2D of the LR batch, graph replay, D2H of the SR batch, serial on one stream), and
+("pipelined") with consecutive batches' copies on a copy stream under the replays -- reported
 beside `value`, never as it.
 cpu_baseline: the CPU oracle (oracle/fen_oracle.py, fp32 PyTorch-CPU restatement of the
 reference forward) on this node's host cores, rank 0, N=1 only: eval at B=2 and B=32 and one
@@ -192,6 +193,60 @@ def time_pcie_inclusive(eng, x, steps, warmup, world):
     return {"value": round(B * world * steps / t, 2), "unit": "images/sec", "ms_per_step": round(1000.0 * t / steps, 4),
             "bytes_h2d": hx.numel() * 4, "bytes_d2h": hout.numel() * 4,
             "note": "NCHW fp32 pinned host in/out, copies serial with the graph replay"}
+
+
+def time_pcie_pipelined(eng, x, steps, warmup, world):
+    """images/s when the boundary hands over host buffers and consecutive batches are pipelined:
+    the H2D of batch i+1 and the D2H of batch i-1 run on a copy stream while batch i's graph
+    replays (pinned host buffers and device staging buffers, two of each; the staging copies into
+    / out of the engine's own buffers are D2D on the compute stream)."""
+    main = torch.cuda.current_stream()
+    cs = torch.cuda.Stream()
+    hx = [x.cpu().pin_memory() for _ in range(2)]
+    hout = [torch.empty(eng.out.shape, dtype=eng.out.dtype).pin_memory() for _ in range(2)]
+    din = [torch.empty_like(eng.x) for _ in range(2)]
+    dout = [torch.empty_like(eng.out) for _ in range(2)]
+    ev = {k: [torch.cuda.Event() for _ in range(2)] for k in ("in", "used", "out", "d2h")}
+
+    def run(n):
+        with torch.cuda.stream(cs):
+            din[0].copy_(hx[0], non_blocking=True)
+            ev["in"][0].record(cs)
+        for i in range(n):
+            b = i & 1
+            with torch.cuda.stream(cs):                   # the next batch's H2D, its staging buffer free
+                cs.wait_event(ev["used"][1 - b])
+                din[1 - b].copy_(hx[1 - b], non_blocking=True)
+                ev["in"][1 - b].record(cs)
+            main.wait_event(ev["in"][b])
+            eng.x.copy_(din[b])
+            ev["used"][b].record(main)
+            main.wait_event(ev["d2h"][b])                 # this staging output free (batch i-2's D2H done)
+            eng.replay()
+            dout[b].copy_(eng.out)
+            ev["out"][b].record(main)
+            with torch.cuda.stream(cs):                   # this batch's D2H under the next replay
+                cs.wait_event(ev["out"][b])
+                hout[b].copy_(dout[b], non_blocking=True)
+                ev["d2h"][b].record(cs)
+        cs.synchronize()
+
+    run(warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt)
+    B = x.shape[0]
+    return {"value": round(B * world * steps / dt, 2), "unit": "images/sec", "ms_per_step": round(1000.0 * dt / steps, 4),
+            "note": "NCHW fp32 pinned host in/out; H2D of batch i+1 and D2H of batch i-1 on a copy stream under "
+                    "batch i's replay"}
 
 
 def conv_flop(cin, cout, h, w, k=3):
@@ -448,6 +503,7 @@ def main():
                      "per_rcab_us_equiv": round(kern_ms * 1e3 * RCAB_CONV_FLOP * 2 / kern_flop, 3)},
     }
     out["pcie_inclusive"] = time_pcie_inclusive(eng, x, args.steps, args.warmup, world)
+    out["pcie_inclusive"]["pipelined"] = time_pcie_pipelined(eng, x, args.steps, args.warmup, world)
     del eng
     torch.cuda.empty_cache()
     # the same workload in the other 16-bit format (BASELINE configs[1] names bf16)
