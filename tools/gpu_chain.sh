@@ -4,7 +4,7 @@ mkdir -p gpurun_out/chain
 timeout -k 10 300 python -u -m pytest tests/test_gpu_group_chain.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/chain/t1.log 2>&1
 rc=$?; echo "chain tests rc=$rc"; tail -25 gpurun_out/chain/t1.log | grep -E "PASS|FAIL|Error|error|passed|failed" | head -30
 [ $rc -eq 0 ] || exit 1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_northstar.py tests/test_gpu_group_strip.py tests/test_gpu_train64.py tests/test_gpu_net.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/chain/t2.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_northstar.py tests/test_gpu_group_strip.py tests/test_gpu_train64.py tests/test_gpu_net.py tests/test_gpu_module.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/chain/t2.log 2>&1
 rc=$?; echo "northstar rc=$rc"; tail -3 gpurun_out/chain/t2.log
 [ $rc -eq 0 ] || exit 1
 for rep in 1 2; do
