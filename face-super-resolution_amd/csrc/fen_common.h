@@ -173,13 +173,10 @@ template <> __device__ __forceinline__ void mma16<float>(f32x4& acc, const uint4
 // 48-element epilogue became ~1000 instructions and ~2 us).
 __device__ __forceinline__ float prelu_f(float v, float a) { return fmaxf(v, 0.f) + a * fminf(v, 0.f); }
 __device__ __forceinline__ float pos_step(float v) { return v > 0.f ? 1.f : 0.f; }
-// dy * dPReLU(pre)/dpre = dy * (pre > 0 ? 1 : a)
-__device__ __forceinline__ float prelu_bwd_f(float dy, float pre, float a) {
-    const float s = pos_step(pre);
-    return dy * (s + (1.f - s) * a);
-}
-// contribution to dL/da: dy * pre where pre <= 0
-__device__ __forceinline__ float prelu_dalpha_f(float dy, float pre) { return dy * pre * (1.f - pos_step(pre)); }
+// dy * dPReLU(pre)/dpre = dy * (pre > 0 ? 1 : a): one compare, one select, one multiply
+__device__ __forceinline__ float prelu_bwd_f(float dy, float pre, float a) { return dy * (pre > 0.f ? 1.f : a); }
+// contribution to dL/da: dy * pre where pre <= 0 (the compare above reused, one select)
+__device__ __forceinline__ float prelu_dalpha_f(float dy, float pre) { return dy * (pre > 0.f ? 0.f : pre); }
 __device__ __forceinline__ bool all_pos4(const float* a) { return a[0] > 0.f && a[1] > 0.f && a[2] > 0.f && a[3] > 0.f; }
 
 // The wave index, provably wave-uniform to the compiler (threadIdx.x >> 6 alone is divergent
