@@ -111,3 +111,42 @@ def test_conv_dot_epilogue_validation_without_gpu():
     assert lib.fen_conv3x3(d, None) == -2
     d.epi = L.EPI_DOT | L.EPI_UNSHUFFLE
     assert lib.fen_conv3x3(d, None) == -2
+
+
+def test_group_strip_chain_validation_without_gpu():
+    """fen_group_strip_chain's host checks run before any copy or launch: a broken chain, too many
+    step tags and a launch without a matching prepared table are refused on CPU."""
+    from src.hip import lib as L
+    lib = L.load()
+    B, H, nb, G = 2, 64, 2, 3
+    nbytes = lib.fen_group_strip_chain_work_bytes(B, H, G)
+    assert nbytes > lib.fen_group_strip_work_bytes(B, H)
+    assert lib.fen_group_strip_chain_work_bytes(B, 12, G) == 0          # H not a multiple of 8
+    ds = (L.GroupStripDesc * G)()
+    for g in range(G):
+        d = ds[g]
+        d.dtype, d.B, d.H, d.W, d.C, d.Cr, d.nb, d.res_scale = 1, B, H, 64, 64, 16, nb, 0.2
+        d.x, d.y = 0x10000 * (g + 1), 0x10000 * (g + 2)                  # group g's output = g+1's input
+        for j in range(nb):
+            d.w1[j] = d.b1[j] = d.alpha[j] = d.w2[j] = d.b2[j] = d.fc1[j] = d.fc2[j] = 0x1000
+        d.wg = d.bg = 0x1000
+        d.work, d.work_bytes = 0x100000, nbytes
+    # a launch with no prepared table for this workspace
+    assert lib.fen_group_strip_chain(ds, G, None, None) == -1
+    # not a chain: group 1's input is not group 0's output
+    ds[1].x = 0x90000
+    assert lib.fen_group_strip_chain(ds, G, None, None) == -1
+    assert lib.fen_group_strip_chain_prepare(ds, G, None) == -1
+    ds[1].x = ds[0].y
+    # the conv_after_body step may not write the body's output or its skip
+    t = L.GroupStripChainTail()
+    t.w = t.bias = 0x1000
+    t.skip, t.y = ds[0].x, ds[G - 1].y
+    assert lib.fen_group_strip_chain_prepare(ds, G, t) == -1
+    # more steps than the 8-bit step tags hold: (nb + 1) * groups > 254
+    big = (L.GroupStripDesc * 13)()
+    for g in range(13):
+        big[g] = ds[0]
+        big[g].nb = 19
+        big[g].x, big[g].y = 0x10000 * (g + 1), 0x10000 * (g + 2)
+    assert lib.fen_group_strip_chain_prepare(big, 13, None) == -2
