@@ -269,3 +269,24 @@ def test_group_chain_after_body(prec, B, H, G, n):
     finally:
         net.CHAIN_AFTER_BODY = old
     assert torch.equal(h, h2)
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_engine_program_uses_the_chain(train):
+    """The bench's engine (B=32, 6x10, 64x64; inference fp16, training bf16) records the body as
+    ONE group_strip_chain launch with conv_after_body inside it: no per-group strip launches and
+    no separate conv_after_body conv (its 64->64 conv at 64x64 with the feat0 residual)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import build_model
+    from src.hip.engine import FENEngine
+    prec = "bf16" if train else "fp16"
+    eng = FENEngine(build_model(prec), batch=32, lr_hw=(64, 64), dtype=DT[prec], train=train, device=DEV)
+    ops = [op[0] for op in eng.ctx.ops]
+    assert ops.count("group_strip_chain") == 1 and "group_strip" not in ops, ops[:6]
+    name, fn, (ds, ng, tail) = next(op for op in eng.ctx.ops if op[0] == "group_strip_chain")
+    assert ng == 6 and tail is not None and ds[0].save == int(train)
+    if not train:   # (training's program also holds the backward's 64->64 dgrads)
+        convs = [op[2][0]._obj for op in eng.ctx.ops if op[0] == "conv3x3" and op[1] is not None]
+        assert not any(d.Cin == 64 and d.Cout == 64 and d.H == 64 and d.W == 64 for d in convs)
