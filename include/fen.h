@@ -300,7 +300,9 @@ int fen_group_strip(const fen_group_strip_desc* d, void* stream);
  * neighbours' boundary rows by hand-off; each group's output is still written to d[g].y (the
  * next group's skip input).  fen_group_strip_chain_prepare writes the table (a synchronous
  * copy: once, outside a graph capture, before the first launch); a launch whose descriptors
- * differ from the prepared table (or tail) returns FEN_EINVAL.  (ng + 1) * (nb + 1) <= 254.  */
+ * differ from the prepared table (or tail) returns FEN_EINVAL.  The table lives in `work`:
+ * prepare again whenever `work` is (re)allocated, even at the same address (the refusal
+ * compares descriptors, it cannot see a fresh buffer).  (ng + 1) * (nb + 1) <= 254.          */
 /* optional: the body's conv_after_body (custom.py:172-175: conv(body output) + bias + feat0) as
  * a last "group" of no RCABs in the same launch; its input is d[ng-1].y                        */
 typedef struct {
