@@ -133,7 +133,19 @@ struct GsTab {
     float* sv_hid[FEN_GS_MAXNB];
     void* x_last;
 };
-inline size_t gs_tab_offset(int B, int S) { return (ws_layout(B, S).total + 255) & ~(size_t)255; }
+inline size_t gs_tab_offset(int B, int S) { return ((ws_layout(B, S).total + 255) & ~(size_t)255) + 256; }   // rows (header before)
+// the table's header (256 B, then the rows): written by prepare, checked by every block of a
+// launch before it reads a row -- a workspace that was never prepared (zeros), or prepared for
+// other descriptors, fails the check and the launch reports FEN_STATUS_GS_TABLE instead of
+// dereferencing a stale or null row
+struct GsTabHdr {
+    unsigned long long magic;
+    unsigned long long hash;                 // FNV-1a of the rows as written
+    int rows;
+    int pad[59];
+};
+static_assert(sizeof(GsTabHdr) == 256, "header size");
+constexpr unsigned long long GS_TAB_MAGIC = 0x4645'4e43'4841'494eull;   // "FENCHAIN"
 
 struct GsArgs {
     int B, H, S, NB, Cr;
@@ -159,6 +171,7 @@ struct GsArgs {
     int fault;                                // test-only: image 0 strip 1 skips one a1 flag
     int pre_elide;                            // training: no z1 save for an RCAB whose slopes are all > 0
     const GsTab* tab;                         // MULTI: ng groups in a row, parameters from here
+    unsigned long long tab_hash;              // MULTI: what the header must hold (this launch's rows)
     int ng;
     int tail;                                 // MULTI: + conv_after_body as a group of no RCABs (table row ng)
 };
@@ -225,6 +238,19 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
     // zero the LDS image (halo rows of edge strips and the zero columns stay zero)
     for (int i = tid; i < IMG_BYTES / 16; i += 512) *(uint4*)(img + i * 16) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
+    if (MULTI) {
+        // the table's header against this launch's descriptors (block-uniform: every block reads
+        // the same header, so either all blocks run or all leave here, nothing waits on a leaver)
+        const GsTabHdr* hdr = (const GsTabHdr*)((const char*)A.tab - sizeof(GsTabHdr));
+        const bool bad = hdr->magic != GS_TAB_MAGIC || hdr->hash != A.tab_hash || hdr->rows != A.ng + A.tail;
+        if (bad) {
+            if (tid == 0) {
+                __hip_atomic_fetch_or(ctl + 2, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                strip_finish(ctl, B * S, A.status, FEN_STATUS_GS_FWD);
+            }
+            return;
+        }
+    }
     const int ticket = __builtin_amdgcn_readfirstlane(tick_lds[0]);
     const unsigned epoch = (unsigned)__builtin_amdgcn_readfirstlane(tick_lds[1]);
     int kbase = 0, rbase = 0;                               // the group's first step / RCAB (MULTI)
@@ -872,10 +898,23 @@ void launch_gs(const GsArgs& a, int grid, hipStream_t s) {
     hipLaunchKernelGGL((k_group_strip<T, SAVE, MULTI>), dim3(grid), dim3(512), GS_LDS, s, a);
 }
 
-// the chained groups' tables a prepare call wrote, by workspace: a launch whose descriptors
-// differ from the table in its workspace is refused (the table would be stale)
-std::mutex g_chain_mu;
-std::map<const void*, std::vector<GsTab>> g_chain_tabs;
+// FNV-1a over the table rows: the launch recomputes it from its own descriptors and the kernel
+// compares it with the header prepare wrote
+unsigned long long tab_hash(const std::vector<GsTab>& tab) {
+    unsigned long long h = 0xcbf29ce484222325ull;
+    const unsigned char* p = (const unsigned char*)tab.data();
+    for (size_t i = 0, n = tab.size() * sizeof(GsTab); i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+    return h;
+}
+
+// the table goes to the device as kernel arguments (no host buffer outlives the call, no host
+// sync, capturable): 3.5-KB chunks, one tiny launch each
+struct TabChunk {
+    unsigned int w[896];
+};
+__global__ __launch_bounds__(256) void k_tab_write(unsigned int* __restrict__ dst, const TabChunk c, int nw) {
+    for (int i = threadIdx.x; i < nw; i += 256) dst[i] = c.w[i];
+}
 
 int chain_tab(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail, std::vector<GsTab>& tab) {
     if (!d || ng <= 0) return FEN_EINVAL;
@@ -989,18 +1028,25 @@ extern "C" size_t fen_group_strip_chain_work_bytes(int B, int H, int ng) {
     return gs_tab_offset(B, H / SR) + (size_t)(ng + 1) * sizeof(GsTab);     // + the tail's row
 }
 
-extern "C" int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail) {
+extern "C" int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail,
+                                             void* stream) {
     std::vector<GsTab> tab;
     const int rc = chain_tab(d, ng, tail, tab);
     if (rc != FEN_OK) return rc;
-    char* dst = (char*)d[0].work + gs_tab_offset(d[0].B, d[0].H / SR);
-    const hipError_t e = hipMemcpy(dst, tab.data(), tab.size() * sizeof(GsTab), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        fen_detail::last_hip_error = (int)e;
-        return FEN_EHIP;
+    std::vector<unsigned int> words((sizeof(GsTabHdr) + tab.size() * sizeof(GsTab)) / 4, 0u);
+    GsTabHdr hdr{};
+    hdr.magic = GS_TAB_MAGIC, hdr.hash = tab_hash(tab), hdr.rows = (int)tab.size();
+    memcpy(words.data(), &hdr, sizeof(hdr));
+    memcpy((char*)words.data() + sizeof(hdr), tab.data(), tab.size() * sizeof(GsTab));
+    unsigned int* dst = (unsigned int*)((char*)d[0].work + gs_tab_offset(d[0].B, d[0].H / SR) - sizeof(GsTabHdr));
+    hipStream_t s = (hipStream_t)stream;
+    for (size_t o = 0; o < words.size(); o += 896) {
+        TabChunk c;
+        const int nw = (int)std::min<size_t>(896, words.size() - o);
+        memcpy(c.w, words.data() + o, nw * 4);
+        hipLaunchKernelGGL(k_tab_write, dim3(1), dim3(256), 0, s, dst + o, c, nw);
     }
-    std::lock_guard<std::mutex> lk(g_chain_mu);
-    g_chain_tabs[d[0].work] = tab;
+    FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
 
@@ -1009,13 +1055,6 @@ extern "C" int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, cons
     std::vector<GsTab> tab;
     const int rc = chain_tab(d, ng, tail, tab);
     if (rc != FEN_OK) return rc;
-    {
-        std::lock_guard<std::mutex> lk(g_chain_mu);
-        const auto it = g_chain_tabs.find(d[0].work);
-        if (it == g_chain_tabs.end() || it->second.size() != tab.size() ||
-            memcmp(it->second.data(), tab.data(), tab.size() * sizeof(GsTab)) != 0)
-            return FEN_EINVAL;                                  // not prepared with these descriptors
-    }
     const fen_group_strip_desc& d0 = d[0];
     GsArgs a{};
     a.B = d0.B, a.H = d0.H, a.S = d0.H / SR, a.NB = d0.nb, a.Cr = d0.Cr;
@@ -1023,6 +1062,7 @@ extern "C" int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, cons
     a.work = (char*)d0.work;
     a.status = d0.status, a.fault = d0.fault;
     a.tab = (const GsTab*)((const char*)d0.work + gs_tab_offset(d0.B, d0.H / SR));
+    a.tab_hash = tab_hash(tab);
     a.ng = ng;
     a.tail = tail ? 1 : 0;
     a.save = d0.save ? 1 : 0;

@@ -1977,12 +1977,17 @@ extern "C" int fen_status_word(void** host, void** dev) {
     return FEN_OK;
 }
 
+extern "C" int fen_status_take(void* host) {
+    return host ? __atomic_exchange_n((int*)host, 0, __ATOMIC_ACQ_REL) : 0;
+}
+
 extern "C" const char* fen_status_string(int code) {
     switch (code) {
         case FEN_OK: return "FEN_OK";
         case FEN_EINVAL: return "FEN_EINVAL: invalid pointer, shape or alignment";
         case FEN_EUNSUPPORTED: return "FEN_EUNSUPPORTED: configuration not implemented by the gfx950 kernels";
         case FEN_EHIP: return "FEN_EHIP: HIP kernel launch failed";
+        case FEN_ERCCL: return "FEN_ERCCL: RCCL call failed";
         default: return "FEN_?: unknown status";
     }
 }

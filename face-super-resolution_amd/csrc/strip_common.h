@@ -74,8 +74,9 @@ __device__ __forceinline__ void strip_finish(int* ctl, int nblk, int* status, in
     if (__hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
         if (status) {
             const int e = __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (e) {
-                __hip_atomic_store(status, status_bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (e) {   // bit 0: a timed-out wait (status_bit); bit 1: a chain table mismatch
+                __hip_atomic_store(status, ((e & 1) ? status_bit : 0) | ((e & 2) ? FEN_STATUS_GS_TABLE : 0),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(ctl + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }

@@ -17,7 +17,13 @@ random crop -> horizontal flip -> rot90 -> colour jitter; val / test: the full i
 
 Keywords the path cannot honour raise (return_filename=True, an .h5 data root); `hue` is
 accepted and, as in the reference (transforms.py:228-257 never reads it), has no effect.
-Under torch.distributed every rank reads its own shard of the files.
+
+Under torch.distributed every rank reads its own shard of the images -- files or synthetic
+indices alike -- with DistributedSampler's counts (`rank_shard`): train drops the remainder so
+every rank has n // world images (and, with drop_last batching, the same number of steps: a
+rank with one more step would pair its gradient all-reduce with another rank's end-of-epoch
+reduction), other modes pad by wrapping round to ceil(n / world).  Per-sample augmentation
+draws are seeded by (seed, rank) so the ranks' draws are independent.
 """
 from __future__ import annotations
 
@@ -78,12 +84,18 @@ class NpyHRDataset(Dataset):
         if not self.files:
             raise FileNotFoundError(f"no .npy images under {root}")
         self.size, self.flip, self.rot, self.train = hr_patch_size, horizontal_flip, random_rotate90, train
-        self.rng = np.random.default_rng(seed)
+        self.seed, self.epoch = seed, 0
 
     def __len__(self):
         return len(self.files)
 
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
+
     def __getitem__(self, i):
+        # one generator per (seed, epoch, sample): DataLoader workers each hold a copy of the
+        # dataset, so a shared generator would repeat the same draws in every worker and epoch
+        self.rng = np.random.default_rng((self.seed, self.epoch, int(i)))
         a = np.load(self.files[i], allow_pickle=False)
         t = torch.from_numpy(np.ascontiguousarray(a)).permute(2, 0, 1).float()
         if a.dtype == np.uint8:
@@ -98,17 +110,43 @@ class NpyHRDataset(Dataset):
 
 
 class SyntheticU8Images:
-    """n seeded HxWx3 uint8 images (the CLI's --synthetic N on the GPU data path)."""
+    """n seeded HxWx3 uint8 images (the CLI's --synthetic N on the GPU data path); `index`
+    (optional) maps this view's positions to image ids (a rank's shard)."""
 
-    def __init__(self, n: int, size: int, seed: int = 0):
+    def __init__(self, n: int, size: int, seed: int = 0, index=None):
         self.n, self.size, self.seed = n, size, seed
+        self.index = list(index) if index is not None else None
 
     def __len__(self):
-        return self.n
+        return len(self.index) if self.index is not None else self.n
 
     def __getitem__(self, i):
+        i = self.index[int(i)] if self.index is not None else int(i)
         r = np.random.default_rng(self.seed * 1_000_003 + int(i))
         return r.integers(0, 256, (self.size, self.size, 3), dtype=np.uint8)
+
+
+def rank_shard(n: int, train: bool, rank: Optional[int] = None, world: Optional[int] = None):
+    """This rank's item indices out of n, DistributedSampler-style (no shuffle: the loaders
+    shuffle within the shard): indices rank, rank + world, ...; train keeps n // world of them
+    (equal step counts on every rank), other modes ceil(n / world), wrapping round.  Without
+    torch.distributed: all of range(n)."""
+    if rank is None or world is None:
+        if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            return list(range(n))
+        rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
+    if world <= 1:
+        return list(range(n))
+    m = n // world if train else -(-n // world)
+    if m == 0:
+        raise ValueError(f"{n} images cannot give each of {world} ranks one")
+    return [(rank + world * j) % n for j in range(m)]
+
+
+def _rank() -> int:
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_rank()
+    return 0
 
 
 class _NpyImages:
@@ -135,10 +173,7 @@ def _files(data_root: str, mode: str):
     files = sorted(os.path.join(root, f) for f in os.listdir(root) if f.endswith(".npy"))
     if not files:
         raise FileNotFoundError(f"no .npy images under {root}")
-    if torch.distributed.is_available() and torch.distributed.is_initialized():
-        r, w = torch.distributed.get_rank(), torch.distributed.get_world_size()
-        files = files[r::w]
-    return files
+    return [files[i] for i in rank_shard(len(files), mode == "train")]
 
 
 def get_dataloader(data_root: Optional[str], mode: str = "train", batch_size: int = 16, num_workers: int = 4,
@@ -163,8 +198,9 @@ def get_dataloader(data_root: Optional[str], mode: str = "train", batch_size: in
     train = mode == "train"
     dev = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
     jitter = color_jitter_prob if train else 0.0
+    rseed = seed + 1_000_033 * _rank()          # independent augmentation draws per rank
     if synthetic:
-        u8 = SyntheticU8Images(synthetic, hr_patch_size, seed + (0 if train else 1))
+        u8 = SyntheticU8Images(synthetic, hr_patch_size, seed + (0 if train else 1), rank_shard(synthetic, train))
     else:
         files = _files(data_root, mode)
         u8 = _NpyImages(files) if np.load(files[0], mmap_mode="r", allow_pickle=False).dtype == np.uint8 else None
@@ -172,15 +208,18 @@ def get_dataloader(data_root: Optional[str], mode: str = "train", batch_size: in
         from .device_loader import DeviceHRLoader
         P = hr_patch_size if train else int(u8[0].shape[0])
         return DeviceHRLoader(u8, batch_size, P, horizontal_flip, random_rotate90, jitter, brightness, contrast,
-                              saturation, seed=seed, shuffle=train, drop_last=train, device=dev, train=train)
+                              saturation, seed=rseed, shuffle=train, drop_last=train, device=dev, train=train)
     if jitter > 0:
         raise ValueError(f"color_jitter_prob={color_jitter_prob}: colour jitter (transforms.py:228-257, a uint8 HSV "
                          "round trip) runs on the GPU data path only -- uint8 images on a GPU device; set "
                          "augmentation.color_jitter.probability: 0 for this source")
     if synthetic:
         ds = SyntheticHRDataset(synthetic, hr_patch_size, seed + (0 if train else 1))
+        idx = rank_shard(synthetic, train)
+        if len(idx) != synthetic:
+            ds = torch.utils.data.Subset(ds, idx)
     else:
-        ds = NpyHRDataset(None, hr_patch_size, horizontal_flip if train else 0.0, seed,
+        ds = NpyHRDataset(None, hr_patch_size, horizontal_flip if train else 0.0, rseed,
                           random_rotate90 if train else 0.0, train=train, files=files)
     return DataLoader(ds, batch_size=batch_size, shuffle=train, num_workers=num_workers, pin_memory=dev.type == "cuda",
                       drop_last=train)
@@ -195,8 +234,10 @@ def get_device_loader(data_root: str, mode: str = "train", batch_size: int = 16,
     from .device_loader import DeviceHRLoader
     train = mode == "train"
     return DeviceHRLoader(_NpyImages(_files(data_root, mode)), batch_size, hr_patch_size, horizontal_flip,
-                          random_rotate90, color_jitter_prob, brightness, contrast, saturation, seed=seed,
+                          random_rotate90, color_jitter_prob, brightness, contrast, saturation,
+                          seed=seed + 1_000_033 * _rank(),
                           shuffle=train, drop_last=train, device=device, train=train)
 
 
-__all__ = ["SyntheticHRDataset", "SyntheticU8Images", "NpyHRDataset", "get_dataloader", "get_device_loader"]
+__all__ = ["SyntheticHRDataset", "SyntheticU8Images", "NpyHRDataset", "get_dataloader", "get_device_loader",
+           "rank_shard"]

@@ -143,7 +143,7 @@ class FENEngine:
         s, ctx = self.spec, self.ctx
         fw = Forward(s, ctx, self.Wt, save=self.train)
         feat0 = fw.head(self.x)
-        fb = fw.fb_buffer(feat0.shape)   # conv_after_body's output: the chained launch may compute it
+        fb = fw.fb_for_chain(feat0)      # conv_after_body's output, if the chained launch computes it
         if self.train:   # every group output kept: the next group's saved input
             h, self.saved = fw.body(feat0, [ctx.alloc(feat0.shape) for _ in range(s.G)], fb=fb)
         else:

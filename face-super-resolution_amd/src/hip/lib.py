@@ -137,7 +137,8 @@ _SIGS = {
     "fen_group_strip_work_bytes": (c_size_t, [c_int, c_int]),
     "fen_group_strip": (c_int, [POINTER(GroupStripDesc), c_void_p]),
     "fen_group_strip_chain_work_bytes": (c_size_t, [c_int, c_int, c_int]),
-    "fen_group_strip_chain_prepare": (c_int, [POINTER(GroupStripDesc), c_int, POINTER(GroupStripChainTail)]),
+    "fen_group_strip_chain_prepare": (c_int, [POINTER(GroupStripDesc), c_int, POINTER(GroupStripChainTail),
+                                              c_void_p]),
     "fen_group_strip_chain": (c_int, [POINTER(GroupStripDesc), c_int, POINTER(GroupStripChainTail), c_void_p]),
     "fen_group_strip_bwd_supported": (c_int, [c_int] * 7),
     "fen_group_strip_bwd_work_bytes": (c_size_t, [c_int, c_int]),
@@ -193,6 +194,14 @@ _SIGS = {
     "fen_s2d_filter": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_status_word": (c_int, [POINTER(c_void_p), POINTER(c_void_p)]),
+    "fen_status_take": (c_int, [c_void_p]),
+    "fen_rccl_unique_id": (c_int, [c_void_p]),
+    "fen_rccl_init": (c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int]),
+    "fen_rccl_allreduce_bucket": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "fen_rccl_check": (c_int, [c_void_p]),
+    "fen_rccl_destroy": (c_int, [c_void_p]),
+    "fen_last_rccl_error": (ctypes.c_char_p, []),
+    "fen_rccl_library": (ctypes.c_char_p, []),
     "fen_status_string": (ctypes.c_char_p, [c_int]),
     "fen_last_hip_error": (ctypes.c_char_p, []),
     "fen_build_info": (ctypes.c_char_p, []),
@@ -230,10 +239,12 @@ def check(code: int, what: str = "") -> None:
         msg = load().fen_status_string(code).decode()
         if code == -3:
             msg += f" [{load().fen_last_hip_error().decode()}]"
+        elif code == -4:
+            msg += f" [{load().fen_last_rccl_error().decode()}]"
         raise FenError(f"{what}: {msg} (status {code})")
 
 
-STATUS_GS_FWD, STATUS_GS_BWD = 1, 2   # FEN_STATUS_GS_*
+STATUS_GS_FWD, STATUS_GS_BWD, STATUS_GS_TABLE = 1, 2, 4   # FEN_STATUS_GS_*
 
 _status = {}
 
@@ -253,7 +264,7 @@ def strip_status_ptr(device) -> int:
         with torch.cuda.device(key):
             check(load().fen_status_word(ctypes.byref(hp), ctypes.byref(dp)), "status_word")
         # the host reads it through ctypes: no torch op (and no sync) per check
-        ent = _status[key] = (int(dp.value), ctypes.c_int32.from_address(hp.value))
+        ent = _status[key] = (int(dp.value), int(hp.value))
     return ent[0]
 
 
@@ -261,10 +272,13 @@ def check_strip_status() -> None:
     """Raise FenError if a strip launch enqueued earlier reported a timed-out wait (its outputs,
     and everything computed from them, are invalid), and clear the word.  A launch still in
     flight is seen by a later check."""
-    for key, (_, word) in _status.items():
-        v = word.value
+    for key, (_, host) in _status.items():
+        v = load().fen_status_take(host)     # read + clear in one atomic exchange
         if v:
-            word.value = 0
+            if v & STATUS_GS_TABLE:
+                raise FenError(f"fen_group_strip_chain on cuda:{key}: the launch found no parameter table prepared "
+                               "for its descriptors in its workspace (fen_group_strip_chain_prepare after every "
+                               "(re)allocation); it computed nothing")
             kinds = [n for b, n in ((STATUS_GS_FWD, "fen_group_strip"), (STATUS_GS_BWD, "fen_group_strip_bwd"))
                      if v & b]
             raise FenError(f"{' / '.join(kinds) or 'strip kernel'} on cuda:{key}: a hand-off wait between "

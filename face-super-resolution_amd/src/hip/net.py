@@ -462,6 +462,11 @@ class Forward:
         """conv_after_body's output buffer (kept for backward in training)."""
         return self.ctx.alloc(shape) if self.save else self.ctx.scratch("tail_fb", shape)
 
+    def fb_for_chain(self, x: torch.Tensor) -> Optional[torch.Tensor]:
+        """conv_after_body's output buffer for body(fb=...) when the chained launch will compute
+        it; None otherwise (tail() then allocates its own: nothing is held unused)."""
+        return self.fb_buffer(x.shape) if (CHAIN_AFTER_BODY and self._chain_ok(x)) else None
+
     def _chain_ok(self, x) -> bool:
         return (GROUP_CHAIN and (not self.save or GROUP_CHAIN_TRAIN) and self.s.G > 1 and self._strip_ok(x) and
                 not self._c128_ok(x))
@@ -505,7 +510,8 @@ class Forward:
             tail.skip, tail.y = ptr(x), ptr(fb)
             ctx.keep(tail)
         tp = byref(tail) if tail is not None else None
-        L.check(ctx.lib.fen_group_strip_chain_prepare(ds, G, tp), "group_strip_chain_prepare")
+        L.check(ctx.lib.fen_group_strip_chain_prepare(ds, G, tp, torch.cuda.current_stream(ctx.device).cuda_stream),
+                "group_strip_chain_prepare")
         ctx.emit("group_strip_chain", ctx.lib.fen_group_strip_chain, ds, G, tp)
         ctx.keep(ds)
         self.fb_done = tail is not None

@@ -15,6 +15,15 @@ its own stream over xGMI; gloo on CPU in the tests) and joins them before the up
 Callers pre-scale the loss gradient by 1/world, so SUM = the gradient of the global-batch
 mean loss, exactly the DDP semantics; clip and AdamW run after the join on every rank on
 identical data (`trainer.py:490-503` ordering).
+
+On the GPU the collectives are RCCL called directly through the C-ABI (`RcclComm`:
+`fen_rccl_allreduce_bucket`, include/fen.h): one ncclAllReduce per bucket on a side stream,
+no c10d Work object, no HIP events, no watchdog -- torch.distributed only carries the
+communicator's unique id.  That is what makes a capture of collectives issued from autograd's
+device thread (the module path's post-accumulate hooks) safe: ProcessGroupNCCL hands a work
+issued outside the capturing thread's view to its watchdog, whose event queries then fail
+with hipErrorCapturedEvent and abort the process (round 4).  `FEN_DP_COMM=torch`
+keeps the torch.distributed collectives (gloo always uses them).
 """
 from __future__ import annotations
 
@@ -63,7 +72,81 @@ def exchange_capturable(group=None) -> bool:
 
 def _rccl_capture_ok(group=None) -> bool:
     import os
+    if use_direct_rccl(group):
+        return True
     return dist.get_backend(group) == "nccl" and os.environ.get(EVENT_CACHE_VAR) == "0"
+
+
+def use_direct_rccl(group=None) -> bool:
+    """The exchange's collectives go through `RcclComm` (the C-ABI) unless FEN_DP_COMM=torch:
+    on CUDA with a process group whose backend is nccl (RCCL), or none (one rank)."""
+    import os
+    if os.environ.get("FEN_DP_COMM", "rccl") == "torch":
+        return False
+    if not (dist.is_available() and dist.is_initialized()):
+        return True
+    return dist.get_backend(group) == "nccl"
+
+
+class RcclComm:
+    """One RCCL communicator over `group`'s ranks (one process per GPU), created through the
+    C-ABI (`fen_rccl_init`): rank 0 makes the unique id, torch.distributed broadcasts it
+    (the rendezvous is the only thing torch.distributed does here).  `allreduce(t, stream)`
+    enqueues an in-place fp32 SUM of `t` on `stream` -- graph-capturable from any thread.
+    Without an initialised process group it is a one-rank communicator (the tests)."""
+
+    _cache = {}
+
+    def __init__(self, device: torch.device, group=None):
+        import ctypes
+        from ..hip.lib import check, load
+        lib = load()
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if dist_on else 1
+        self.rank = dist.get_rank(group) if dist_on else 0
+        self.device = torch.device(device)
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            check(lib.fen_rccl_unique_id(uid.data_ptr()), "fen_rccl_unique_id")
+        if self.world > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            t = uid.to(self.device)
+            dist.broadcast(t, src=src, group=group)
+            uid = t.cpu()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.fen_rccl_init(ctypes.byref(h), uid.data_ptr(), self.world, self.rank, self.device.index),
+                  "fen_rccl_init")
+        self.handle = h.value
+        self.library = lib.fen_rccl_library().decode()
+
+    @classmethod
+    def get(cls, device: torch.device, group=None) -> "RcclComm":
+        """One communicator per (device, group) for the process (the engines, the module-path
+        exchanges and the trainer share it)."""
+        key = (str(torch.device(device)), id(group))
+        c = cls._cache.get(key)
+        if c is None:
+            c = cls._cache[key] = cls(device, group)
+        return c
+
+    def allreduce(self, t: torch.Tensor, stream: torch.cuda.Stream) -> None:
+        from ..hip.lib import check, load
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != self.device:
+            raise ValueError("RcclComm.allreduce: a contiguous fp32 tensor on the communicator's device")
+        check(load().fen_rccl_allreduce_bucket(self.handle, t.data_ptr(), t.numel(), stream.cuda_stream),
+              "fen_rccl_allreduce_bucket")
+
+    def check(self) -> None:
+        from ..hip.lib import check, load
+        check(load().fen_rccl_check(self.handle), "rccl")
+
+    @classmethod
+    def destroy_all(cls) -> None:
+        from ..hip.lib import load
+        for c in cls._cache.values():
+            load().fen_rccl_destroy(c.handle)
+        cls._cache = {}
 
 
 def _group_of(name: str) -> str:
@@ -118,27 +201,37 @@ class BucketExchange:
         self.views = {tag: flat[lo:hi] for tag, lo, hi in plan}
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.active = self.world > 1 or force
-        # gloo stages CUDA tensors through the host (not stream-ordered): only RCCL captures,
-        # and only with ProcessGroupNCCL's event cache off (init_rccl)
+        # direct RCCL (RcclComm) on the GPU; gloo stages CUDA tensors through the host (not
+        # stream-ordered) and is never captured; torch's RCCL only with the event cache off
+        self.comm = (RcclComm.get(flat.device, group) if (self.active and flat.is_cuda and use_direct_rccl(group))
+                     else None)
         self.capturable = bool(flat.is_cuda) and (not self.active or _rccl_capture_ok(group))
         self.stream = torch.cuda.Stream(device=flat.device) if (self.active and flat.is_cuda) else None
         self.works: List = []
         self._forked = False
+        self.base = None              # the stream launches fork from (default: the current one)
+        self.captured_launches: List[bool] = []   # per launch: was the fork inside a capture
 
     def launch(self, tag: str) -> None:
         if not self.active:
             return
         if self.stream is not None:
-            self.stream.wait_stream(torch.cuda.current_stream(self.flat.device))
+            base = self.base if self.base is not None else torch.cuda.current_stream(self.flat.device)
+            self.stream.wait_stream(base)
             with torch.cuda.stream(self.stream):
-                dist.all_reduce(self.views[tag], group=self.group)
+                self.captured_launches.append(torch.cuda.is_current_stream_capturing())
+                if self.comm is not None:
+                    self.comm.allreduce(self.views[tag], self.stream)
+                else:
+                    dist.all_reduce(self.views[tag], group=self.group)
             self._forked = True
         else:
             self.works.append(dist.all_reduce(self.views[tag], group=self.group, async_op=True))
 
     def wait(self) -> None:
         if self._forked:
-            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
+            base = self.base if self.base is not None else torch.cuda.current_stream(self.flat.device)
+            base.wait_stream(self.stream)
             self._forked = False
         for w in self.works:
             w.wait()
@@ -185,17 +278,25 @@ class ParamGradExchange:
                         lambda _p, bi=bi: self._arrived(bi)))
 
     def _arrived(self, bi: int) -> None:
+        """Runs on autograd's device thread.  The copy and the fork are pinned to the stream
+        that was current on the thread that armed the exchange (the backward's forward stream:
+        under a capture, the capturing stream), not to whatever the hook thread has current."""
         if not self.armed:
             return
         self._left[bi] -= 1
         if self._left[bi] == 0:
             a, b = self.ranges[bi]
-            torch._foreach_copy_(self.fviews[a:b], [p.grad for p in self.params[a:b]])
+            base = self.ex.base
+            ctx = torch.cuda.stream(base) if base is not None else _null()
+            with ctx:
+                torch._foreach_copy_(self.fviews[a:b], [p.grad for p in self.params[a:b]])
             self.ex.launch(f"b{bi}")
 
     def arm(self) -> None:
         self.armed = True
         self._left = [b - a for a, b in self.ranges]
+        if self.flat.is_cuda:
+            self.ex.base = torch.cuda.current_stream(self.flat.device)
 
     def wait(self) -> None:
         """Join; every bucket must have been launched by this backward."""
@@ -204,6 +305,7 @@ class ParamGradExchange:
         if any(self._left):
             raise RuntimeError(f"gradient buckets not complete after backward: {self._left}")
         self.ex.wait()
+        self.ex.base = None
         if self.copy_back:
             torch._foreach_copy_([p.grad for p in self.params], self.fviews)
         self.armed = False
@@ -212,6 +314,14 @@ class ParamGradExchange:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+class _null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 def even_buckets(n: int, k: int) -> List[Tuple[int, int]]:

@@ -7,7 +7,7 @@ load_checkpoint, and overfit_test.  What changes (trainer row):
     (trainer.py:416-421), forward, L1, backward, clip_grad_norm_, AdamW (458-503) -- is the
     fused HIP program of src.hip.engine.FENEngine (one hipGraph-able replay);
   * data parallel: one process per GPU (torchrun), each rank steps on its shard of the
-    batch stream (DistributedSampler or `shard=rank::world`), gradients are summed by RCCL
+    batch stream (src.data.rank_shard: equal-count shards per rank), gradients are summed by RCCL
     all-reduce buckets issued from inside the backward and overlapped with it; clip and
     AdamW run after the reduce so every rank stays identical; rank 0 logs/checkpoints;
   * one generator AdamW state (exp_avg / exp_avg_sq / step over the flat parameter arena)
@@ -315,18 +315,19 @@ class Trainer:
         return loss.detach()
 
     def _capture_gan(self) -> bool:
-        """World size 1: captured.  With an exchange (N > 1, or the tests' forced one-rank
-        group) the iteration runs eagerly unless FEN_GAN_CAPTURE_DP=1 (and then only over RCCL
-        with the event cache off, `dp.init_rccl`): the module path's all-reduces are issued from
-        autograd's post-accumulate hooks, and a capture of them aborted the process in
-        ProcessGroupNCCL's watchdog (hipErrorCapturedEvent) once in the round-4 GPU runs after
-        a clean series -- an abort takes the whole run with it, so the capture is opt-in there.
-        The engine's DP step (collectives from the program's marks) stays captured."""
+        """Captured at any world size: with an exchange (N > 1, or the tests' forced one-rank
+        group) the module path's bucket all-reduces are direct RCCL calls (dp.RcclComm, the
+        C-ABI's fen_rccl_allreduce_bucket) that record into the graph from autograd's hook thread
+        like any kernel -- no ProcessGroupNCCL work, event or watchdog is involved (the round-4
+        watchdog abort).  FEN_DP_COMM=torch (torch's collectives) captures only
+        with FEN_GAN_CAPTURE_DP=1; gloo never captures."""
         import os
-        from .dp import _rccl_capture_ok
+        from .dp import _rccl_capture_ok, use_direct_rccl
         if not (bool(self.config.capture_gan_step) and torch.cuda.is_available() and self._accum() == 1):
             return False
         if self.world > 1 or getattr(self, "_dp_force", False):
+            if use_direct_rccl():
+                return True
             return (os.environ.get("FEN_GAN_CAPTURE_DP") == "1" and dist.is_available() and dist.is_initialized()
                     and _rccl_capture_ok())
         return True
@@ -413,6 +414,9 @@ class Trainer:
         self.model.train()
         total, n = 0.0, 0
         k = self._accum()
+        ds = getattr(self.train_loader, "dataset", None)
+        if hasattr(ds, "set_epoch"):
+            ds.set_epoch(self.current_epoch)     # fresh per-sample augmentation draws each epoch
         for bi, batch in enumerate(self.train_loader):
             hr = self._shard(batch["hr"]).to(self.device, non_blocking=True)
             update = (bi + 1) % k == 0

@@ -27,7 +27,8 @@ typedef enum {
     FEN_OK = 0,
     FEN_EINVAL = -1,        /* bad pointer / shape / alignment                  */
     FEN_EUNSUPPORTED = -2,  /* valid request outside what the kernels implement */
-    FEN_EHIP = -3           /* a HIP launch error                               */
+    FEN_EHIP = -3,          /* a HIP launch error                               */
+    FEN_ERCCL = -4          /* an RCCL call failed (fen_last_rccl_error names it) */
 } fen_status;
 
 typedef enum { FEN_F32 = 0, FEN_BF16 = 1, FEN_F16 = 2 } fen_dtype;
@@ -288,6 +289,8 @@ typedef struct {
 } fen_group_strip_desc;
 #define FEN_STATUS_GS_FWD 1            /* a fen_group_strip wait timed out (output invalid)     */
 #define FEN_STATUS_GS_BWD 2            /* a fen_group_strip_bwd wait timed out                  */
+#define FEN_STATUS_GS_TABLE 4          /* a fen_group_strip_chain launch found no prepared table for
+                                          its descriptors in `work`: it computed nothing           */
 int fen_group_strip_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
 size_t fen_group_strip_work_bytes(int B, int H);
 int fen_group_strip(const fen_group_strip_desc* d, void* stream);
@@ -298,11 +301,15 @@ int fen_group_strip(const fen_group_strip_desc* d, void* stream);
  * the workspace plus the groups' parameter table), d[0].status / fault used.  A strip stays on
  * its CU across the groups: group g's output rows become group g+1's x_0 in registers, the
  * neighbours' boundary rows by hand-off; each group's output is still written to d[g].y (the
- * next group's skip input).  fen_group_strip_chain_prepare writes the table (a synchronous
- * copy: once, outside a graph capture, before the first launch); a launch whose descriptors
- * differ from the prepared table (or tail) returns FEN_EINVAL.  The table lives in `work`:
- * prepare again whenever `work` is (re)allocated, even at the same address (the refusal
- * compares descriptors, it cannot see a fresh buffer).  (ng + 1) * (nb + 1) <= 254.          */
+ * next group's skip input).  fen_group_strip_chain_prepare writes the parameter table into
+ * `work` (fen_group_strip_chain_work_bytes(B, H, ng) bytes: the workspace, a 256-B header, the
+ * rows), asynchronously on `stream` (kernel-argument copies: no host sync, no host buffer kept,
+ * capturable); prepare once per (descriptors, work) before the launches that use them, again
+ * after `work` is (re)allocated.  The launch hashes its own descriptors; every block compares
+ * that with the header before it reads a row, and on a mismatch (never prepared, prepared for
+ * other descriptors, a fresh buffer) the launch computes nothing and reports
+ * FEN_STATUS_GS_TABLE through d[0].status (else the workspace's error word, byte 8, bit 1).
+ * (ng + 1) * (nb + 1) <= 254.                                                                 */
 /* optional: the body's conv_after_body (custom.py:172-175: conv(body output) + bias + feat0) as
  * a last "group" of no RCABs in the same launch; its input is d[ng-1].y                        */
 typedef struct {
@@ -312,7 +319,8 @@ typedef struct {
     void* y;                   /* out NHWC [B,H,64,64] (not d[ng-1].y, not skip)               */
 } fen_group_strip_chain_tail;
 size_t fen_group_strip_chain_work_bytes(int B, int H, int ng);   /* room for ng groups + a tail */
-int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail);
+int fen_group_strip_chain_prepare(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail,
+                                  void* stream);
 int fen_group_strip_chain(const fen_group_strip_desc* d, int ng, const fen_group_strip_chain_tail* tail, void* stream);
 
 /* 128-channel RCAB convs (BASELINE configs[4]: num_channels = 128, Cr = 32; RCAB blocks.py:
@@ -579,6 +587,27 @@ int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const void* dy, vo
  * the current device and kept for the process; *host is what the host reads (no sync needed),
  * *dev what the kernels store to.  The only allocation the library makes.  0 or FEN_EHIP.  */
 int fen_status_word(void** host, void** dev);
+/* Read and clear a status word in one atomic exchange (a launch storing between a separate
+ * read and clear would otherwise be lost); `host` is fen_status_word's *host.  Returns the
+ * bits that were set (0: none).                                                            */
+int fen_status_take(void* host);
+
+/* Data-parallel gradient exchange (replaces DDP's bucketed all-reduce,
+ * reference trainer.py:126-134 / scripts/train.py:325-330).  One communicator per process
+ * (one process per GPU); each call of fen_rccl_allreduce_bucket is ONE in-place fp32 SUM
+ * ncclAllReduce of a contiguous bucket of the flat gradient arena, enqueued on `stream` --
+ * no host sync, no events, no watchdog, so it records into a hipGraph capture from any host
+ * thread.  RCCL is resolved at run time (the instance already in the process, else
+ * librccl.so.1).  The unique id (128 bytes) is made on one rank and distributed by the
+ * caller (torch.distributed broadcast).  fen_rccl_init blocks until all nranks have joined
+ * (ncclCommInitRank on `device`).  Errors: FEN_ERCCL + fen_last_rccl_error().              */
+int fen_rccl_unique_id(void* id);
+int fen_rccl_init(void** comm, const void* id, int nranks, int rank, int device);
+int fen_rccl_allreduce_bucket(void* comm, float* buf, size_t count, void* stream);
+int fen_rccl_check(void* comm);          /* ncclCommGetAsyncError: FEN_OK or FEN_ERCCL      */
+int fen_rccl_destroy(void* comm);
+const char* fen_last_rccl_error(void);
+const char* fen_rccl_library(void);      /* which librccl was resolved ("none" if absent)   */
 
 const char* fen_status_string(int code);
 /* hipGetErrorString() of the HIP error behind this thread's last FEN_EHIP, or "none". */

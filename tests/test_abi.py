@@ -115,7 +115,8 @@ def test_conv_dot_epilogue_validation_without_gpu():
 
 def test_group_strip_chain_validation_without_gpu():
     """fen_group_strip_chain's host checks run before any copy or launch: a broken chain, too many
-    step tags and a launch without a matching prepared table are refused on CPU."""
+    step tags and a tail aliasing the body's buffers are refused on CPU (a launch without a
+    matching prepared table is refused on the GPU, by the kernel: test_gpu_group_chain.py)."""
     from src.hip import lib as L
     lib = L.load()
     B, H, nb, G = 2, 64, 2, 3
@@ -131,22 +132,40 @@ def test_group_strip_chain_validation_without_gpu():
             d.w1[j] = d.b1[j] = d.alpha[j] = d.w2[j] = d.b2[j] = d.fc1[j] = d.fc2[j] = 0x1000
         d.wg = d.bg = 0x1000
         d.work, d.work_bytes = 0x100000, nbytes
-    # a launch with no prepared table for this workspace
-    assert lib.fen_group_strip_chain(ds, G, None, None) == -1
     # not a chain: group 1's input is not group 0's output
     ds[1].x = 0x90000
     assert lib.fen_group_strip_chain(ds, G, None, None) == -1
-    assert lib.fen_group_strip_chain_prepare(ds, G, None) == -1
+    assert lib.fen_group_strip_chain_prepare(ds, G, None, None) == -1
     ds[1].x = ds[0].y
     # the conv_after_body step may not write the body's output or its skip
     t = L.GroupStripChainTail()
     t.w = t.bias = 0x1000
     t.skip, t.y = ds[0].x, ds[G - 1].y
-    assert lib.fen_group_strip_chain_prepare(ds, G, t) == -1
+    assert lib.fen_group_strip_chain_prepare(ds, G, t, None) == -1
     # more steps than the 8-bit step tags hold: (nb + 1) * groups > 254
     big = (L.GroupStripDesc * 13)()
     for g in range(13):
         big[g] = ds[0]
         big[g].nb = 19
         big[g].x, big[g].y = 0x10000 * (g + 1), 0x10000 * (g + 2)
-    assert lib.fen_group_strip_chain_prepare(big, 13, None) == -2
+    assert lib.fen_group_strip_chain_prepare(big, 13, None, None) == -2
+
+
+def test_rccl_and_status_entry_points_without_gpu():
+    """fen_rccl_* validate their arguments before touching RCCL; fen_status_take reads and
+    clears a word in one atomic exchange (here on plain host memory)."""
+    import ctypes
+    from src.hip import lib as L
+    lib = L.load()
+    assert lib.fen_status_string(-4).startswith(b"FEN_ERCCL")
+    assert lib.fen_rccl_allreduce_bucket(None, None, 16, None) == -1
+    assert lib.fen_rccl_init(None, None, 1, 0, 0) == -1
+    h = ctypes.c_void_p()
+    uid = (ctypes.c_uint8 * 128)()
+    assert lib.fen_rccl_init(ctypes.byref(h), uid, 2, 2, 0) == -1       # rank outside nranks
+    assert lib.fen_rccl_check(None) == -1
+    assert lib.fen_rccl_destroy(None) == 0
+    w = ctypes.c_int32(3)
+    assert lib.fen_status_take(ctypes.addressof(w)) == 3 and w.value == 0
+    assert lib.fen_status_take(ctypes.addressof(w)) == 0
+    assert lib.fen_status_take(None) == 0

@@ -164,22 +164,33 @@ def test_gan_leg_d256_matches_cpu_replay(golden, g10):
     d_loss = (bce(dfwd(hr64), one) + bce(dfwd(sr_d), zero)) / 2
     d_loss.backward()
     ref_dgrad = {k: p.grad.detach().clone() for k, p in Dc.named_parameters()}
-    # yardstick for the D gradient: torch's own fp32 CPU run of the same D step (fp32 oracle
-    # generator's fake image, fp32 discriminator) against this float64 replay.  The real and fake
-    # branches cancel heavily in the first conv's weight gradient (test_gpu_gan_step.py), so
-    # fp32 rounding alone moves it (and the first conv's bias gradient) by several 1e-3 at input
-    # 256 -- in a summation-order-dependent direction; the HIP path may be no further from
-    # float64 than torch's fp32 is, x3 (measured 2.3-2.7x on those two tensors), and everywhere
-    # within test_gpu_gan_step's 5e-3
-    D2 = VGGStyleDiscriminator(input_size=256)
-    D2.load_state_dict(D0)
-    D2.train()
+    # yardstick for the D gradient: torch's own fp32 CPU discriminator against this float64
+    # replay, on fake images equal to the last bit or so (the HIP generator's, the fp32 oracle's,
+    # the float64 one rounded, the HIP one with 1-ulp noise).  Below features.7 the BN'd layers'
+    # gradients are small against the per-pixel terms they sum (ill-conditioned in either branch
+    # alone, real-vs-fake cancellation is nil: tools/dbg_d256.py, profiles/r05_d256_conditioning.txt),
+    # so fp32 rounding alone moves them by 2e-3 .. 1.3e-2, and which draw an input gets is luck:
+    # torch's fp32 on the rounded float64 fake is at 1.1e-2 where the HIP discriminator is at 5e-3.
+    # The HIP discriminator is held to 5e-3, or where torch's fp32 spread is wider, to that spread
+    m = FaceEnhanceNet(num_channels=64, num_groups=1, blocks_per_group=2, reduction_ratio=4, scale_factor=4,
+                       res_scale=0.2, precision="fp32")
+    m.load_state_dict(sd)
+    from src.training.trainer import bicubic_down4
     with torch.no_grad():
+        sr_d_hip = m.to(DEV).train()(bicubic_down4(hr.to(DEV))).cpu()   # what tr._gan_step's D sees
         sr_d32 = O.forward(sd, O.lr_from_hr(hr), shape, training=True)
+    ulp = torch.where(torch.rand(sr_d_hip.shape, generator=torch.Generator().manual_seed(1)) < 0.5, -1.0, 1.0)
+    fakes = [sr_d_hip, sr_d.float(), sr_d32, sr_d_hip * (1 + ulp * 2.0 ** -23)]
     one32, zero32 = torch.ones(2, 1), torch.zeros(2, 1)
-    ((bce(D2.classifier(D2.features(hr)), one32) + bce(D2.classifier(D2.features(sr_d32)), zero32)) / 2).backward()
-    sens = {k: float((p.grad.double() - ref_dgrad[k]).norm() / max(ref_dgrad[k].norm(), 1e-30))
-            for k, p in D2.named_parameters()}
+    sens = {}
+    for fk in fakes:
+        D2 = VGGStyleDiscriminator(input_size=256)
+        D2.load_state_dict(D0)
+        D2.train()
+        ((bce(D2.classifier(D2.features(hr)), one32) + bce(D2.classifier(D2.features(fk)), zero32)) / 2).backward()
+        for k, p in D2.named_parameters():
+            e = float((p.grad.double() - ref_dgrad[k]).norm() / max(ref_dgrad[k].norm(), 1e-30))
+            sens[k] = max(sens.get(k, 0.0), e)
     optd.step()
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in sd64.items()}
     sr = O.forward(leaves, lr, shape, training=True)
@@ -192,8 +203,6 @@ def test_gan_leg_d256_matches_cpu_replay(golden, g10):
     O.adamw_step(newp, {k: t * c for k, t in raw.items()}, {k: torch.zeros_like(t) for k, t in newp.items()},
                  {k: torch.zeros_like(t) for k, t in newp.items()}, 1, lr_g, wd=0.0)
     # --- HIP trainer (fp32) ---
-    m = FaceEnhanceNet(num_channels=64, num_groups=1, blocks_per_group=2, reduction_ratio=4, scale_factor=4,
-                       res_scale=0.2, precision="fp32")
     m.load_state_dict(sd)
     Dg = VGGStyleDiscriminator(input_size=256, precision="fp32")
     Dg.load_state_dict(D0)
@@ -219,8 +228,8 @@ def test_gan_leg_d256_matches_cpu_replay(golden, g10):
         ref = ref_dgrad[k].double()
         e = float((snap[k].cpu().double() - ref).norm() / max(ref.norm(), 1e-30))
         worst = max(worst, e)
-        print(f"  D {k}: rel {e:.2e} (torch fp32 {sens[k]:.2e})")
-        assert e <= max(5e-3, 3 * sens[k]), (k, e, sens[k])
+        print(f"  D {k}: rel {e:.2e} (torch fp32 spread {sens[k]:.2e})")
+        assert e <= max(5e-3, sens[k]), (k, e, sens[k])
     print(f"D gradients: worst rel {worst:.2e}; torch fp32 CPU vs float64 worst {max(sens.values()):.2e}")
     for k, v in Dg.state_dict().items():
         ref = Dc.state_dict()[k]

@@ -151,29 +151,70 @@ def test_group_chain_failed_wait_raises():
 
 
 def test_group_chain_refuses_unprepared():
-    """A launch whose descriptors differ from the prepared table is refused (FEN_EINVAL)."""
+    """The parameter table is checked by the kernel (ADVICE/VERDICT r4): a launch whose
+    descriptors differ from the prepared table, or whose workspace was reallocated (a fresh
+    zeroed buffer, and a stale copy of another table) and not prepared again, computes nothing
+    and raises FenError at the next status check -- never a launch on a stale or null row.  A
+    broken chain is refused on the host (FEN_EINVAL).  After prepare on the caller's stream
+    (asynchronous) the launch matches the original output bit for bit."""
     from src.hip import lib as L
     dtype, G, n = torch.float16, 2, 1
     q = _params(G, n, seed=4)
     x = torch.randn(1, 64, 64, 64, generator=torch.Generator().manual_seed(2)).to(DEV, dtype)
-    _, _, ctx, _ = _run(q, G, n, x, dtype, record=True)
+    y_ref, _, _, _ = _run(q, G, n, x, dtype)
+    L.check_strip_status()
+    y, _, ctx, _ = _run(q, G, n, x, dtype, record=True)
     name, fn, (ds, ng, tp) = ctx.ops[0]
     assert name == "group_strip_chain"
+    lib = L.load()
     s = torch.cuda.current_stream().cuda_stream
+    # valid descriptors, not the prepared table's: refused by the kernel, nothing written
     old = ds[1].fc1[0]
-    ds[1].fc1[0] = ds[1].fc2[0]                           # valid descriptors, not the prepared table
+    ds[1].fc1[0] = ds[1].fc2[0]
     try:
-        assert fn(ds, ng, tp, s) != 0
+        y.fill_(7.0)
+        assert fn(ds, ng, tp, s) == 0
+        torch.cuda.synchronize()
+        with pytest.raises(L.FenError, match="no parameter table"):
+            L.check_strip_status()
+        assert bool((y == 7.0).all())
     finally:
         ds[1].fc1[0] = old
+    # not a chain (x aliases y): refused on the host
     old = ds[1].x
-    ds[1].x = ds[1].y                                     # not a chain (x aliases y)
+    ds[1].x = ds[1].y
     try:
-        assert fn(ds, ng, tp, s) != 0
+        assert fn(ds, ng, tp, s) == -1
     finally:
         ds[1].x = old
+    # a reallocated workspace (zeros), launched without prepare
+    nbytes = int(ds[0].work_bytes)
+    work2 = torch.zeros(nbytes, dtype=torch.uint8, device=DEV)
+    old_work = ds[0].work
+    for g in range(ng):
+        ds[g].work = work2.data_ptr()
     assert fn(ds, ng, tp, s) == 0
     torch.cuda.synchronize()
+    with pytest.raises(L.FenError, match="no parameter table"):
+        L.check_strip_status()
+    # a stale table of other descriptors in it (prepared, then the descriptors change)
+    old = ds[0].b1[0]
+    ds[0].b1[0] = ds[0].b2[0]
+    assert lib.fen_group_strip_chain_prepare(ds, ng, tp, s) == 0
+    ds[0].b1[0] = old
+    assert fn(ds, ng, tp, s) == 0
+    torch.cuda.synchronize()
+    with pytest.raises(L.FenError, match="no parameter table"):
+        L.check_strip_status()
+    # prepared for these descriptors (async, on the stream): runs, bit-exact
+    assert lib.fen_group_strip_chain_prepare(ds, ng, tp, s) == 0
+    y.zero_()
+    assert fn(ds, ng, tp, s) == 0
+    torch.cuda.synchronize()
+    L.check_strip_status()
+    assert torch.equal(y, y_ref)
+    for g in range(ng):
+        ds[g].work = old_work
 
 
 def _run_save(q, G, n, x, dtype, chain):

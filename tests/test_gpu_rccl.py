@@ -130,30 +130,86 @@ def test_engine_captured_step_over_rccl():
 def test_gan_iteration_over_rccl(tmp_path):
     """The stage-3 GAN iteration with the module path's bucketed exchanges (dp.ParamGradExchange:
     the generator's tail / group / head buckets and the discriminator's two, each all-reduced
-    from a post-accumulate hook as the backward completes it, stream-ordered), forced on a
-    one-rank RCCL group: bit-identical to the exchange-free iteration (losses, generator arena,
-    discriminator parameters and buffers).  With an exchange the iteration runs eagerly unless
-    FEN_GAN_CAPTURE_DP=1 (Trainer._capture_gan: a capture of hook-issued RCCL collectives
-    aborted in ProcessGroupNCCL's watchdog once); with it set, the replayed graph is checked too."""
-    import os
+    from a post-accumulate hook on autograd's device thread as the backward completes it,
+    stream-ordered), forced on a one-rank RCCL group, CAPTURED (the default at any world size
+    since the exchange calls RCCL directly, dp.RcclComm): bit-identical to the exchange-free
+    iteration (losses, generator arena, discriminator parameters and buffers) over 2 eager
+    warm-ups, the capture and 9 replays; every bucket launch of the capturing iteration forked
+    from a capturing stream (so the graph holds the all-reduces, not an eager side effect)."""
     from test_gpu_gan_capture import _state, _trainer
     eager = _trainer(False, tmp_path / "e")
     _init_one_rank()
     try:
         cap = _trainer(True, tmp_path / "c")
         cap._dp_force = True
-        captured = os.environ.get("FEN_GAN_CAPTURE_DP") == "1"
-        assert cap._capture_gan() == captured
+        assert cap._capture_gan()
         gen = torch.Generator().manual_seed(5)
-        for i in range(5):
+        for i in range(12):
             hr = torch.rand(2, 3, 128, 128, generator=gen).to(DEV)
             le = float(eager._gan_iteration(hr))
             lc = float(cap._gan_iteration(hr))
             assert le == lc, (i, le, lc)
             for a, b in zip(_state(eager), _state(cap)):
                 assert torch.equal(a, b), i
-        assert (cap._gan_graph is not None) == captured
+        assert cap._gan_graph is not None
         assert cap._g_ex is not None and cap._d_ex is not None
         assert len(cap._g_ex.ranges) == 2 + 1 and len(cap._d_ex.ranges) == 2   # tail, rg0, head
+        assert cap._g_ex.ex.comm is not None and cap._d_ex.ex.comm is not None     # direct RCCL
+        g, d = cap._g_ex.ex.captured_launches, cap._d_ex.ex.captured_launches
+        # 2 eager iterations + the captured one went through Python; replays do not
+        assert g == [False] * 6 + [True] * 3, g
+        nd = cap.config.d_updates_per_g * 2
+        assert d == [False] * (2 * nd) + [True] * nd, d
+        cap._g_ex.ex.comm.check()
     finally:
         dist.destroy_process_group()
+
+
+def test_rccl_comm_direct_capture():
+    """dp.RcclComm without a process group (a one-rank communicator through the C-ABI's
+    fen_rccl_*): an in-place SUM is the identity, it records into a hipGraph from a side
+    thread (as autograd's hook thread issues it) and replays; the library it resolved is
+    torch's own RCCL instance (one RCCL per process)."""
+    import threading
+    from src.training.dp import RcclComm
+    assert not dist.is_initialized()
+    comm = RcclComm(torch.device("cuda", torch.cuda.current_device()))
+    assert comm.world == 1 and comm.rank == 0
+    assert "torch/lib/librccl" in comm.library, comm.library    # torch imported first: its instance
+    x = torch.randn(1 << 20, device=DEV)
+    ref = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    comm.allreduce(x, s)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    errs = []
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        x.mul_(2.0)
+        base = torch.cuda.current_stream()
+
+        def hook():
+            try:
+                side.wait_stream(base)
+                comm.allreduce(x, side)
+            except Exception as e:  # pragma: no cover - reported below
+                errs.append(e)
+        t = threading.Thread(target=hook)
+        t.start()
+        t.join()
+        base.wait_stream(side)
+        x.add_(1.0)
+    assert not errs, errs
+    x.copy_(ref)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    exp = ref.clone()
+    for _ in range(3):
+        exp = exp * 2.0 + 1.0
+    assert torch.allclose(x, exp, rtol=0, atol=0)
+    comm.check()
+    RcclComm.destroy_all()

@@ -167,17 +167,19 @@ def test_data_sources(tmp_path):
 def test_train_transform_matches_reference_order(tmp_path):
     """NpyHRDataset's train transform = PairedTransform.__call__ (transforms.py:188-216): a random
     crop when the image is larger than the patch, then flip (p), then rot90 (p, k in 1..3), the
-    draws in that order from one generator -- restated here with numpy on the HWC array."""
+    draws in that order from one generator (here one per (seed, epoch, sample), so DataLoader
+    workers do not repeat each other's draws) -- restated here with numpy on the HWC array."""
     from src.data import NpyHRDataset
     r = np.random.default_rng(0)
     imgs = [r.integers(0, 256, (48, 40, 3), dtype=np.uint8) for _ in range(4)]
     for i, a in enumerate(imgs):
         np.save(tmp_path / f"im{i}.npy", a)
     ds = NpyHRDataset(str(tmp_path), hr_patch_size=32, horizontal_flip=0.5, random_rotate90=0.7, seed=5)
-    ref_rng = np.random.default_rng(5)
     seen_flip = seen_rot = False
     for rep in range(6):
+        ds.set_epoch(rep)
         for i, a in enumerate(imgs):
+            ref_rng = np.random.default_rng((5, rep, i))
             top = int(ref_rng.integers(0, 48 - 32 + 1))
             left = int(ref_rng.integers(0, 40 - 32 + 1))
             h = a[top:top + 32, left:left + 32]
@@ -311,3 +313,47 @@ def test_trainer_accumulation_schedule():
         assert eng.calls == [(i + 1) % k == 0 for i in range(nb)], (k, eng.calls)
         assert tr.global_step == nb // k
         assert abs(out["loss"] - sum(48.0 * i for i in range(nb)) / nb) < 1e-9
+
+
+def test_rank_shards_disjoint_and_equal():
+    """src.data.rank_shard: a fake 2- and 3-rank world's train shards are disjoint
+    with equal lengths (equal step counts with drop_last batching), and together cover all but
+    the remainder; validation shards pad to ceil(n / world); the synthetic u8 source takes a
+    shard, so ranks see different images."""
+    import numpy as np
+    from src.data import SyntheticU8Images, rank_shard
+    for n, w in ((10, 2), (11, 2), (11, 3), (64, 8)):
+        sh = [rank_shard(n, True, r, w) for r in range(w)]
+        assert len({len(s) for s in sh}) == 1 and len(sh[0]) == n // w
+        flat = [i for s in sh for i in s]
+        assert len(set(flat)) == len(flat)
+        assert set(flat) <= set(range(n)) and len(flat) == n - n % w
+        va = [rank_shard(n, False, r, w) for r in range(w)]
+        assert {len(s) for s in va} == {-(-n // w)}
+        assert set(i for s in va for i in s) == set(range(n))
+    assert rank_shard(5, True, 0, 1) == list(range(5))
+    a = SyntheticU8Images(8, 16, 0, rank_shard(8, True, 0, 2))
+    b = SyntheticU8Images(8, 16, 0, rank_shard(8, True, 1, 2))
+    full = SyntheticU8Images(8, 16, 0)
+    assert len(a) == len(b) == 4
+    assert np.array_equal(a[1], full[2]) and np.array_equal(b[1], full[3])
+    assert not np.array_equal(a[0], b[0])
+
+
+def test_npy_dataset_draws_per_sample_and_epoch(tmp_path):
+    """NpyHRDataset draws each sample's crop / flip / rot90 from (seed, epoch, index): the same
+    in any DataLoader worker, different across epochs (a generator copied into each
+    worker repeated its draws)."""
+    import numpy as np
+    from src.data import NpyHRDataset
+    rng = np.random.default_rng(0)
+    for i in range(3):
+        np.save(tmp_path / f"{i}.npy", rng.integers(0, 256, (40, 40, 3), dtype=np.uint8))
+    ds = NpyHRDataset(str(tmp_path), hr_patch_size=16, horizontal_flip=0.5, random_rotate90=0.5, seed=1)
+    a0 = [ds[i]["hr"] for i in range(3)]
+    assert all(torch.equal(x, y) for x, y in zip(a0, [ds[i]["hr"] for i in range(3)]))
+    eps = []
+    for e in range(1, 6):
+        ds.set_epoch(e)
+        eps.append([ds[i]["hr"] for i in range(3)])
+    assert any(not torch.equal(x, y) for ep in eps for x, y in zip(a0, ep))
