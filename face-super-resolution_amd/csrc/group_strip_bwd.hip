@@ -314,9 +314,10 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             if (wave == 2) cst[lane] = cv;                  // alpha of RCAB jr, read after B_E
             uint4 nd[HK];
             if (hwave) {
-                // the neighbour's d row (this wave's half), after its flag: lands during phase 1
+                // the neighbour's d row (this wave's part): lands during phase 1.  No flag poll: its
+                // storing wave drained the row before its B_Z, after which its block published the SE
+                // partial that wave 1's sweep saw before this block's B_G (the hand-off's signal)
                 const int ns = hs == 0 ? strip - 1 : strip + 1;
-                ok = ok && poll_eq(flag_of(ns, 1 - hs, 1), tag_of(k - 1));
                 const int od = rowoff(L.bd, ns, (k - 1) & 1, 1 - hs) + (lane + 64 * hk0) * 16;
 #pragma unroll
                 for (int kk = 0; kk < HK; ++kk)
@@ -535,8 +536,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
         }
         const int jn = NB - 1 - k;                          // the next step's RCAB
         if (wave == 2) cv = A.alpha[jn][lane];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (bwave && lane == 0) __hip_atomic_store(flag_of(strip, side, 1), tag_of(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the d row drained before B_Z (see the step start)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         GSTAMP(sb + 10);
         __syncthreads();                                    // B_Z: the row sums in red; conv reads done (all slots free)
