@@ -391,9 +391,9 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             __syncthreads();                                // A/B variant: the epilogue after every wave's conv
 #endif
             uint2 zd[4][4];
+            float* dal = A.dal[jr];
+            asm volatile("" : "+s"(dal));
             {
-                float* dal = A.dal[jr];
-                asm volatile("" : "+s"(dal));
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     const float4 aa = *(const float4*)(cst + 16 * m + 4 * q);
@@ -416,15 +416,21 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
                     float sv[4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) sv[i] = group16_sum(ds[i]) * (recz ? __builtin_amdgcn_rcpf(alp[i]) : 1.f);
-                    if (c16 == 0)
-                        *(float4*)(dal + (size_t)(im * H + r0 + wave) * 64 + 16 * m + 4 * q) =
-                            make_float4(sv[0], sv[1], sv[2], sv[3]);
+                    // the row's partial -> red[wave] (free since the previous step's publish); the
+                    // strip's sum over its 8 rows goes out after B_E (8x fewer rows to column-sum)
+                    if (c16 == 0) *(float4*)(red + wave * 64 + 16 * m + 4 * q) = make_float4(sv[0], sv[1], sv[2], sv[3]);
                 }
             }
             GSTAMP(sb + 5);
             __syncthreads();                                // B_E: dt's reads done (all slots free); taps visible
             GSTAMP(sb + 6);
             issue_kh02(ci + 1);
+            if (wave == 2) {                                // the strip's dalpha partial, rows in order (before B_Y)
+                float a = 0.f;
+#pragma unroll
+                for (int w = 0; w < SR; ++w) a += red[w * 64 + lane];
+                dal[(size_t)(im * S + strip) * 64 + lane] = a;
+            }
             write_row_lds(wave + 1, zd);
             if (bwave) store_row(wsr, rowoff(L.bz, strip, par, side), zd, 16);
             asm volatile("" ::: "memory");
@@ -668,6 +674,8 @@ void launch_gsb(const GsbArgs& a, int grid, hipStream_t s) {
 }  // namespace
 
 extern "C" size_t fen_group_strip_bwd_work_bytes(int B, int H) { return wsb_layout(B, H / SR).total; }
+
+extern "C" int fen_group_strip_bwd_dal_rows(int B, int H) { return B * (H / SR); }
 
 extern "C" int fen_group_strip_bwd_supported(int dtype, int B, int H, int W, int C, int Cr, int nb) {
     if (!fen_group_strip_supported(dtype, B, H, W, C, Cr, nb)) return 0;

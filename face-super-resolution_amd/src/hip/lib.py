@@ -142,6 +142,7 @@ _SIGS = {
     "fen_group_strip_chain": (c_int, [POINTER(GroupStripDesc), c_int, POINTER(GroupStripChainTail), c_void_p]),
     "fen_group_strip_bwd_supported": (c_int, [c_int] * 7),
     "fen_group_strip_bwd_work_bytes": (c_size_t, [c_int, c_int]),
+    "fen_group_strip_bwd_dal_rows": (c_int, [c_int, c_int]),
     "fen_group_strip_bwd": (c_int, [POINTER(GroupStripBwdDesc), c_void_p]),
     "fen_rcab_c128_supported": (c_int, [c_int] * 6),
     "fen_rcab_c128_tiles": (c_int, [c_int] * 2),

@@ -873,6 +873,7 @@ class Backward:
             d.dres = ptr(extra_res[0])
         d.wgt = ptr(Wt.packed(pre + "conv", 2))
         outs = []
+        drows = int(ctx.lib.fen_group_strip_bwd_dal_rows(B, H))    # one dalpha partial row per strip
         for b in range(s.NB):
             q = f"{pre}blocks.{b}."
             ca = q + "channel_attention.fc."
@@ -885,7 +886,7 @@ class Backward:
                 d.a1[b] = ptr(blk["a1"])
             d.s[b], d.mean[b], d.hid[b] = ptr(blk["s"]), ptr(blk["mean"]), ptr(blk["hid"])
             o = dict(dt=ctx.scratch(f"gsb_dt{b}", dy.shape), dz1=ctx.scratch(f"gsb_dz1{b}", dy.shape),
-                     dal=ctx.scratch(f"gsb_dal{b}", (B * H, C), torch.float32),
+                     dal=ctx.scratch(f"gsb_dal{b}", (drows, C), torch.float32),
                      dw1p=ctx.scratch(f"gsb_dw1p{b}", (B, s.Cr * C), torch.float32),
                      dw2p=ctx.scratch(f"gsb_dw2p{b}", (B, s.Cr * C), torch.float32))
             d.dt[b], d.dz1[b], d.dalpha_part[b] = ptr(o["dt"]), ptr(o["dz1"]), ptr(o["dal"])
@@ -909,7 +910,7 @@ class Backward:
             blk, o = sv["blocks"][b], outs[b]
             wb.add(blk["a1"], o["dt"], B, H, W, C, C, G[q + "conv2.weight"], G[q + "conv2.bias"])
             wb.add(blk["x"], o["dz1"], B, H, W, C, C, G[q + "conv1.weight"], G[q + "conv1.bias"])
-            self.cs.add(o["dal"], B * H, C, G[q + "prelu.weight"])
+            self.cs.add(o["dal"], drows, C, G[q + "prelu.weight"])
             self.cs.add(o["dw1p"], B, s.Cr * C, G[ca + "0.weight"])
             self.cs.add(o["dw2p"], B, s.Cr * C, G[ca + "2.weight"])
         wb.flush()

@@ -372,8 +372,8 @@ int fen_rcab_c128(const fen_rcab_c128_desc* d, void* stream);
  *   d += conv1_j^T(dz1_j);  dx = d + dy (+ dres).
  * Writes dt_j and dz1_j (the conv2 / conv1 weight gradients' dy operands: run
  * fen_wgrad3x3_multi on (a1_j, dt_j), (x_j, dz1_j) and (x_last, dy) afterwards),
- * dalpha_part_j [B*H][64] (sum over each image row of conv2^T(dt) * z1 * [z1 <= 0]: column sums
- * give prelu.weight's gradient), dw1p_j [B][Cr][64] and dw2p_j [B][64][Cr] (per-image SE weight
+ * dalpha_part_j [fen_group_strip_bwd_dal_rows(B, H)][64] (sum over each strip of 8 image rows of
+ * conv2^T(dt) * z1 * [z1 <= 0], rows in order: column sums give prelu.weight's gradient), dw1p_j [B][Cr][64] and dw2p_j [B][64][Cr] (per-image SE weight
  * gradients: column sums over B).  Same strips, envelope and hand-off scheme as
  * fen_group_strip (its own `work`, fen_group_strip_bwd_work_bytes, ZEROED once).  w*t / wgt are
  * the mode-2 (transposed) packs.  dx may not alias dy or dres.                                */
@@ -397,7 +397,7 @@ typedef struct {
     const float* hid[FEN_GS_MAXNB];    /* saved ReLU(FC1(mean)) [B][Cr]                        */
     void* dt[FEN_GS_MAXNB];            /* out: dL/dt NHWC                                      */
     void* dz1[FEN_GS_MAXNB];           /* out: dL/dz1 NHWC                                     */
-    float* dalpha_part[FEN_GS_MAXNB];  /* out: [B*H][64]                                       */
+    float* dalpha_part[FEN_GS_MAXNB];  /* out: [B*H/8][64], one row per strip                   */
     float* dw1p[FEN_GS_MAXNB];         /* out: [B][Cr][64]                                     */
     float* dw2p[FEN_GS_MAXNB];         /* out: [B][64][Cr]                                     */
     void* work;
@@ -411,6 +411,7 @@ typedef struct {
 } fen_group_strip_bwd_desc;
 int fen_group_strip_bwd_supported(int dtype, int B, int H, int W, int C, int Cr, int nb);
 size_t fen_group_strip_bwd_work_bytes(int B, int H);
+int fen_group_strip_bwd_dal_rows(int B, int H);      /* rows of each dalpha_part_j: B * H / 8 */
 int fen_group_strip_bwd(const fen_group_strip_bwd_desc* d, void* stream);
 
 /* The RCAB backward's two data gradients in one launch (autograd of blocks.py:145-147):
