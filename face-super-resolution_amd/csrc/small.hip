@@ -507,6 +507,8 @@ __global__ __launch_bounds__(1024) void k_conv_first_finalize(int nb, int Ci, in
 // dout NHWC16 [B,H,W,16], w [Co][C][3][3] -> da[px][c] -> dv = da*(pre>0?1:alpha[c])
 // -> du[b][h/2][w/2][4c + 2(h&1) + (w&1)];  block = 16x16 source px = 8x8 du px.
 // Thread (k = tid % (C/2)) owns channels 2k, 2k+1 of du pixels tid / (C/2) + 256/(C/2) * j.
+// The blocks stride over the tiles (grid = fen_conv_last_dgrad_part_rows, one slope-partial
+// row each).
 // Memory-latency bound (the FMAs are 7 GFLOP at B=32, 256x256): for 16-bit operands and
 // C <= 64 (LPRE) the block's whole pre-activation tile (16x16 px x C, <= 32 KB) is loaded into
 // LDS together with the dout halo -- one round trip per block instead of one per du pixel.
@@ -526,8 +528,27 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(
     __shared__ float sdal[256 * 2];
     __shared__ uint4 spre[PRE_U4];          // [16 rows][16 px][C] pre-activations (LPRE)
     const int tid = threadIdx.x;
-    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
-    const int b = blockIdx.x / tpi, tile = blockIdx.x - b * tpi;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4), ntiles = B * tpi;
+    const int k = tid % K2;                 // channel pair (2k, 2k+1), fixed per thread
+    float wr[2][3][9];
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int co = 0; co < 3; ++co)
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                wr[e][co][t] = co < Co ? w[((size_t)co * C + 2 * k + e) * 9 + t] : 0.f;
+    const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
+    // post (this pair's group of 4 has every slope > 0): p below is the PReLU output a, which has
+    // the pre-activation's sign (all PReLU' needs); where a <= 0 the pre-activation is a / alpha,
+    // so the slope gradient's sum of da * p * [p <= 0] is taken over a and scaled once at the end
+    const bool rec = post && all_pos4(alpha + ((2 * k) & ~3));
+    float dal0 = 0.f, dal1 = 0.f;
+    const int Hh = H >> 1, Wh = W >> 1;
+    // grid-stride over the tiles: one slope-partial row per block (fen_conv_last_dgrad_part_rows)
+    for (int bt = blockIdx.x; bt < ntiles; bt += gridDim.x) {
+    __syncthreads();                        // the previous tile's LDS reads done
+    const int b = bt / tpi, tile = bt - b * tpi;
     const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
     if constexpr (LPRE) {
         constexpr int PPR = C * 2 / 16;     // 16-B pieces per pixel (8 channels: two groups of 4)
@@ -585,23 +606,7 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(
         }
         sd[i] = v;
     }
-    const int k = tid % K2;                 // channel pair (2k, 2k+1), fixed per thread
-    float wr[2][3][9];
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int co = 0; co < 3; ++co)
-#pragma unroll
-            for (int t = 0; t < 9; ++t)
-                wr[e][co][t] = co < Co ? w[((size_t)co * C + 2 * k + e) * 9 + t] : 0.f;
-    const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
-    // post (this pair's group of 4 has every slope > 0): p below is the PReLU output a, which has
-    // the pre-activation's sign (all PReLU' needs); where a <= 0 the pre-activation is a / alpha,
-    // so the slope gradient's sum of da * p * [p <= 0] is taken over a and scaled once at the end
-    const bool rec = post && all_pos4(alpha + ((2 * k) & ~3));
     __syncthreads();
-    float dal0 = 0.f, dal1 = 0.f;
-    const int Hh = H >> 1, Wh = W >> 1;
     for (int i = tid; i < 64 * K2; i += 256) {
         const int dp = i / K2;
         const int hh = dp >> 3, ww = dp & 7;
@@ -645,6 +650,7 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(
             *(uint4*)(o + 16) = pack16<float>(out + 4);
         }
     }
+    }
     if (rec) {
         dal0 *= __builtin_amdgcn_rcpf(al0);
         dal1 *= __builtin_amdgcn_rcpf(al1);
@@ -657,6 +663,379 @@ __global__ __launch_bounds__(256) void k_conv_last_dgrad(
         float s = 0.f;
         for (int r = kk; r < 256; r += K2) s += sdal[r * 2 + e];
         part[(size_t)blockIdx.x * C + tid] = s;
+    }
+}
+
+// The same for 16-bit operands and C = 64 (the network's last upsampler stage), persistent and
+// pipelined: CLD_GRID blocks (two per CU) walk the tiles in order; while a block computes tile i
+// from LDS its threads already hold tile i + 1's pre-activation chunks and dout halo in
+// registers (one memory round trip per tile overlapped with the previous tile's FMAs instead of
+// one exposed per block); the channel pair's two outputs as packed fp32 FMAs; the slope partials
+// accumulate over the block's tiles (one partial row per block).  Same arithmetic per output as
+// k_conv_last_dgrad (the same tap order), so the two agree to the summation order of dalpha.
+constexpr int CLD_GRID = 512;
+template <typename T>
+__global__ __launch_bounds__(256, 2) void k_cld_p(int B, int H, int W, int Co, const T* __restrict__ dout,
+                                                  const float* __restrict__ w, const T* __restrict__ pre,
+                                                  const T* __restrict__ post, const float* __restrict__ alpha,
+                                                  T* __restrict__ du, float* __restrict__ part) {
+    constexpr int C = 64, K2 = 32, NV = 8;          // 8 x 16-B pieces of the 16x16x64 tile per thread
+    __shared__ float4 sd[18 * 18];
+    __shared__ uint4 spre[256 * 8];
+    __shared__ float sdal[512];
+    const int tid = threadIdx.x;
+    const int twn = W >> 4, tpi = twn * (H >> 4), ntiles = B * tpi;
+    const int pcq = tid & 7;                        // the thread's 8-channel chunk of every pixel it loads
+    // each half (4 channels) of the chunk from post where the group's slopes are all > 0 (the
+    // PReLU output has the pre-activation's sign), else from pre
+    const bool plo = post && all_pos4(alpha + pcq * 8), phi = post && all_pos4(alpha + pcq * 8 + 4);
+    const char* slo = (const char*)(plo ? post : pre);
+    const char* shi = (const char*)(phi ? post : pre);
+    uint4 pv[NV];
+    uint2 dv[2];
+    auto load = [&](int t) {
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int px = (tid >> 3) + 32 * j;
+            const size_t o = (((size_t)(b * H + h0 + (px >> 4)) * W + w0 + (px & 15)) * C) * 2 + pcq * 16;
+            if (slo == shi) {
+                pv[j] = *(const uint4*)(slo + o);
+            } else {
+                const uint2 lo = *(const uint2*)(slo + o), hi = *(const uint2*)(shi + o + 8);
+                pv[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = tid + 256 * j, r = i / 18, c = i % 18;
+            const int gh = h0 + r - 1, gw = w0 + c - 1;
+            const bool in = i < 18 * 18 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            dv[j] = in ? *(const uint2*)((const char*)dout + ((size_t)(b * H + gh) * W + gw) * 16 * sizeof(T))
+                       : make_uint2(0u, 0u);
+        }
+    };
+    const int k = tid % K2;                         // channel pair (2k, 2k+1), fixed per thread
+    f32x2 wr[3][9];
+#pragma unroll
+    for (int co = 0; co < 3; ++co)
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp)
+            wr[co][tp] = co < Co ? f32x2{w[((size_t)co * C + 2 * k) * 9 + tp], w[((size_t)co * C + 2 * k + 1) * 9 + tp]}
+                                 : f32x2{0.f, 0.f};
+    const float al0 = alpha[2 * k], al1 = alpha[2 * k + 1];
+    const bool rec = post && all_pos4(alpha + ((2 * k) & ~3));
+    const int Hh = H >> 1, Wh = W >> 1;
+    float dal0 = 0.f, dal1 = 0.f;
+    int t = blockIdx.x;
+    if (t < ntiles) load(t);
+    for (; t < ntiles; t += gridDim.x) {
+        __syncthreads();                            // the previous tile's LDS reads done
+#pragma unroll
+        for (int j = 0; j < NV; ++j) spre[tid + 256 * j] = pv[j];   // piece (px, pcq) at px * 8 + pcq
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = tid + 256 * j;
+            if (i < 18 * 18) {
+                float t4[4];
+                ld4<T>(&dv[j], t4);
+                sd[i] = make_float4(t4[0], Co > 1 ? t4[1] : 0.f, Co > 2 ? t4[2] : 0.f, 0.f);
+            }
+        }
+        __syncthreads();
+        if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);   // the next tile, in flight under the FMAs
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+#pragma unroll 2
+        for (int m = 0; m < 8; ++m) {
+            const int dp = (tid >> 5) + 8 * m;      // du pixel of the tile (8 x 8)
+            const int hh = dp >> 3, ww = dp & 7;
+            float out[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int sh = 2 * hh + (q >> 1), sw = 2 * ww + (q & 1);   // local source pixel
+                f32x2 da = {0.f, 0.f};
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        const float4 g = sd[(sh - kh + 2) * 18 + (sw - kw + 2)];
+                        const int tp = kh * 3 + kw;
+                        da = __builtin_elementwise_fma(f32x2{g.x, g.x}, wr[0][tp], da);
+                        da = __builtin_elementwise_fma(f32x2{g.y, g.y}, wr[1][tp], da);
+                        da = __builtin_elementwise_fma(f32x2{g.z, g.z}, wr[2][tp], da);
+                    }
+                const unsigned pw = ((const unsigned*)spre)[(sh * 16 + sw) * K2 + k];
+                const float p0 = lo16<T>(pw), p1 = hi16<T>(pw);
+                dal0 += prelu_dalpha_f(da.x, p0);
+                dal1 += prelu_dalpha_f(da.y, p1);
+                out[q] = prelu_bwd_f(da.x, p0, al0);
+                out[4 + q] = prelu_bwd_f(da.y, p1, al1);
+            }
+            *(uint4*)((char*)du + (((size_t)(b * Hh + (h0 >> 1) + hh) * Wh + (w0 >> 1) + ww) * (4 * C) + 8 * k) * sizeof(T)) =
+                pack16<T>(out);
+        }
+    }
+    if (rec) {
+        dal0 *= __builtin_amdgcn_rcpf(al0);
+        dal1 *= __builtin_amdgcn_rcpf(al1);
+    }
+    sdal[tid * 2] = dal0;
+    sdal[tid * 2 + 1] = dal1;
+    __syncthreads();
+    if (tid < C) {
+        const int kk = tid >> 1, e = tid & 1;
+        float sum = 0.f;
+        for (int r = kk; r < 256; r += K2) sum += sdal[r * 2 + e];
+        part[(size_t)blockIdx.x * C + tid] = sum;
+    }
+}
+
+// conv_last's whole backward in one pass (16-bit, C = 64, post given, whole 16x16 tiles):
+//   du = unshuffle(PReLU'(conv_last^T dout)), the slope partials, and conv_last's weight and
+//   bias gradients -- instead of k_conv_last_dgrad plus a separate weight-gradient pass that
+//   reads the 268 MB stage output a second time (custom.py:177-184 backward).
+// Both products are GEMMs over one im2col matrix of the dout halo, X[r][k] (r = the tile's 256
+// source pixels, k = co * 9 + tap, 27 used of 32):
+//   da[r][c]  = sum_k X[r][k] W[k][c]        (M = r, N = c, K = k; W split hi + lo in 16 bits,
+//                                              two MFMAs: the fp32 weights to ~16 mantissa bits)
+//   dW[k][c] += sum_r X[r][k] a[r][c]        (M = k, N = c, K = r; accumulated over the tiles)
+// on 16x16x32 MFMAs.  Row order r = 4 * dp + q (dp = du pixel of the 8x8 du tile, q = 2 (h & 1) +
+// (w & 1)): a lane's 4 accumulator rows are the 4 source pixels of one du pixel, i.e. the 4
+// consecutive du channels 4c..4c+3 -- one 8-B store, 16 lanes 128 contiguous bytes.  LDS holds
+// X (r-major, the dgrad's A), X^T and the activation tile P^T (c-major: the weight gradient's
+// operands and the epilogue's 4 pixels of one channel in one 8-B read).  Persistent: CLD_GRID
+// blocks walk the tiles, the next tile's activation pieces and dout halo in registers under the
+// current tile's MFMAs; one partial row per block for the slopes, the weights and the bias.
+// P holds post (a) for groups of 4 channels whose slopes are all > 0 (the pre-activation's sign,
+// recovered as in k_conv_last_dgrad) and pre (v) for the others; the weight gradient needs a,
+// rebuilt there as rnd16(PReLU(v)) (the forward rounded PReLU(acc) once: one rounding apart).
+constexpr int CLB_XS = 40, CLB_TS = 264;   // 16-bit row strides of X, and of X^T / P^T (16-B aligned)
+constexpr int CLB_LDS = 18 * 18 * 8 + 256 * CLB_XS * 2 + 32 * CLB_TS * 2 + 64 * CLB_TS * 2;
+template <typename T>
+__global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, const T* __restrict__ dout,
+                                                   const float* __restrict__ w, const T* __restrict__ pre,
+                                                   const T* __restrict__ post, const float* __restrict__ alpha,
+                                                   T* __restrict__ du, float* __restrict__ dal_part,
+                                                   float* __restrict__ dw_part, float* __restrict__ db_part) {
+    constexpr int C = 64, XS = CLB_XS, TS = CLB_TS;
+    __shared__ __attribute__((aligned(16))) char smem[CLB_LDS];
+    uint2* hd = (uint2*)smem;                                        // dout halo, channels 0..3
+    unsigned short* X = (unsigned short*)(smem + 18 * 18 * 8);       // [256 r][XS]
+    unsigned short* XT = X + 256 * XS;                               // [32 k][TS]
+    unsigned short* PT = XT + 32 * TS;                               // [64 c][TS]
+    const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lq = lane >> 4;
+    const int wave = wave_id();
+    const int twn = W >> 4, tpi = twn * (H >> 4), ntiles = B * tpi;
+    // ---- loads: 4 pixel pairs (2P, 2P + 1) x one 8-channel chunk per thread, + 2 halo pixels
+    const int pcq = tid & 7, pp = tid >> 3;
+    const bool plo = all_pos4(alpha + pcq * 8), phi = all_pos4(alpha + pcq * 8 + 4);
+    const char* slo = (const char*)(plo ? post : pre);
+    const char* shi = (const char*)(phi ? post : pre);
+    uint4 pv[4][2];
+    uint2 dv[2];
+    auto load = [&](int t) {
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int px = 2 * (pp + 32 * j) + e;
+                const size_t o = (((size_t)(b * H + h0 + (px >> 4)) * W + w0 + (px & 15)) * C) * 2 + pcq * 16;
+                if (slo == shi) {
+                    pv[j][e] = *(const uint4*)(slo + o);
+                } else {
+                    const uint2 lo = *(const uint2*)(slo + o), hi = *(const uint2*)(shi + o + 8);
+                    pv[j][e] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                }
+            }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = tid + 256 * j, r = i / 18, c = i % 18;
+            const int gh = h0 + r - 1, gw = w0 + c - 1;
+            const bool in = i < 18 * 18 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            dv[j] = in ? *(const uint2*)((const char*)dout + ((size_t)(b * H + gh) * W + gw) * 16 * sizeof(T))
+                       : make_uint2(0u, 0u);
+        }
+    };
+    // ---- constants: the dgrad's B fragments (W[k][c], k = 8 lq + e, c = 16 n + l16) hi + lo
+    uint4 whi[4], wlo[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        float h8[8], l8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 8 * lq + e, co = k / 9, tap = k - 9 * co;
+            const float v = k < 9 * Co ? w[((size_t)co * C + 16 * n + l16) * 9 + tap] : 0.f;
+            h8[e] = rnd16<T>(v);
+            l8[e] = v - h8[e];
+        }
+        whi[n] = pack16<T>(h8);
+        wlo[n] = pack16<T>(l8);
+    }
+    float al[4], ial[4];
+    bool rec[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int c = 16 * n + l16;
+        al[n] = alpha[c];
+        ial[n] = __builtin_amdgcn_rcpf(al[n]);
+        rec[n] = all_pos4(alpha + (c & ~3));
+    }
+    float dal[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acw[2][4];                       // dW[k = 16 km + 4 lq + i][c = 16 n + l16], this wave's rows r
+#pragma unroll
+    for (int km = 0; km < 2; ++km)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acw[km][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum[3] = {0.f, 0.f, 0.f};
+    // ---- the im2col builder's role: pixel pair (2 p2, 2 p2 + 1) in r order, k half kh2
+    const int p2 = tid & 127, kh2 = tid >> 7;
+    const int Hh = H >> 1, Wh = W >> 1;
+    int t = blockIdx.x;
+    if (t < ntiles) load(t);
+    for (; t < ntiles; t += gridDim.x) {
+        __syncthreads();                                   // (A) the previous tile's LDS reads done
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (tid + 256 * j < 18 * 18) hd[tid + 256 * j] = dv[j];
+        {
+            // P^T[c][r]: the pair (2P, 2P + 1) is (r, r + 1), r = 4 dp + 2 ((P >> 3) & 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int P = pp + 32 * j;
+                const int r = 4 * ((P >> 4) * 8 + (P & 7)) + 2 * ((P >> 3) & 1);
+                const unsigned a0[4] = {pv[j][0].x, pv[j][0].y, pv[j][0].z, pv[j][0].w};
+                const unsigned a1[4] = {pv[j][1].x, pv[j][1].y, pv[j][1].z, pv[j][1].w};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const unsigned wd = __builtin_amdgcn_perm(a1[i >> 1], a0[i >> 1], (i & 1) ? 0x07060302u : 0x05040100u);
+                    *(unsigned*)(PT + (8 * pcq + i) * TS + r) = wd;
+                }
+            }
+        }
+        __syncthreads();                                   // (B) halo and P^T written
+        if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);   // the next tile, under this one's work
+        {
+            // X rows r0, r0 + 1 (k half kh2) and the matching X^T words; bias partials
+            const int r0 = 2 * p2;
+            unsigned short xv[2][16];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int r = r0 + e, dp = r >> 2, q = r & 3;
+                const int sh = 2 * (dp >> 3) + (q >> 1), sw = 2 * (dp & 7) + (q & 1);
+                uint2 g[9];
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) g[tap] = hd[(sh - tap / 3 + 2) * 18 + (sw - tap % 3 + 2)];
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) {
+                    const int k = 16 * kh2 + kk, co = k / 9, tap = k - 9 * co;
+                    unsigned short v = 0;
+                    if (co < 3 && co < Co) {
+                        const uint2 gg = g[tap < 9 ? tap : 0];
+                        const unsigned wd = co < 2 ? gg.x : gg.y;
+                        v = (unsigned short)((co == 1) ? (wd >> 16) : (wd & 0xffffu));
+                    }
+                    xv[e][kk] = v;
+                }
+                // bias: the centre tap (k = 9 co + 4) of the pixel's own dout
+#pragma unroll
+                for (int co = 0; co < 3; ++co)
+                    if ((9 * co + 4) / 16 == kh2) bsum[co] += tof<T>(__builtin_bit_cast(T, xv[e][(9 * co + 4) % 16]));
+                uint4 u0, u1;
+                u0.x = xv[e][0] | ((unsigned)xv[e][1] << 16);   u0.y = xv[e][2] | ((unsigned)xv[e][3] << 16);
+                u0.z = xv[e][4] | ((unsigned)xv[e][5] << 16);   u0.w = xv[e][6] | ((unsigned)xv[e][7] << 16);
+                u1.x = xv[e][8] | ((unsigned)xv[e][9] << 16);   u1.y = xv[e][10] | ((unsigned)xv[e][11] << 16);
+                u1.z = xv[e][12] | ((unsigned)xv[e][13] << 16); u1.w = xv[e][14] | ((unsigned)xv[e][15] << 16);
+                *(uint4*)(X + r * XS + 16 * kh2) = u0;
+                *(uint4*)(X + r * XS + 16 * kh2 + 8) = u1;
+            }
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk)
+                *(unsigned*)(XT + (16 * kh2 + kk) * TS + r0) = xv[0][kk] | ((unsigned)xv[1][kk] << 16);
+        }
+        __syncthreads();                                   // (C) X, X^T written
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        // weight gradient: this wave's 64 rows r, 2 K steps of 32
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int rb = 64 * wave + 32 * ks + 8 * lq;
+            uint4 A[2];
+#pragma unroll
+            for (int km = 0; km < 2; ++km) A[km] = *(const uint4*)(XT + (16 * km + l16) * TS + rb);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                uint4 Bv = *(const uint4*)(PT + (16 * n + l16) * TS + rb);
+                if (!rec[n]) {                             // P holds v: a = PReLU(v) in 16 bits
+                    float f[8];
+                    unpack16<T>(Bv, f);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) f[e] = prelu_f(f[e], al[n]);
+                    Bv = pack16<T>(f);
+                }
+#pragma unroll
+                for (int km = 0; km < 2; ++km) mma16<T>(acw[km][n], A[km], Bv);
+            }
+        }
+        // data gradient + PReLU' + unshuffle: 4 row blocks of 16 (4 du pixels each)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const uint4 A = *(const uint4*)(X + (64 * wave + 16 * mb + l16) * XS + 8 * lq);
+            const int dp = 16 * wave + 4 * mb + lq;        // du pixel of the tile
+            T* o = du + (((size_t)(b * Hh + (h0 >> 1) + (dp >> 3)) * Wh + (w0 >> 1) + (dp & 7)) * (4 * C));
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                mma16<T>(acc, A, whi[n]);
+                mma16<T>(acc, A, wlo[n]);
+                const int c = 16 * n + l16;
+                const uint2 pw = *(const uint2*)(PT + c * TS + 4 * dp);
+                const float pq[4] = {lo16<T>(pw.x), hi16<T>(pw.x), lo16<T>(pw.y), hi16<T>(pw.y)};
+                float ov[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    dal[n] += prelu_dalpha_f(acc[j], pq[j]);
+                    ov[j] = prelu_bwd_f(acc[j], pq[j], al[n]);
+                }
+                st4<T>(o + 4 * c, ov);
+            }
+        }
+    }
+    // ---- block partials: slopes (lanes of one l16 and the 4 waves), dW (the 4 waves), bias
+    __syncthreads();
+    float* red = (float*)(smem + 18 * 18 * 8);             // X / X^T / P^T are dead now
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        float v = rec[n] ? dal[n] * ial[n] : dal[n];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lq == 0) red[wave * 64 + 16 * n + l16] = v;
+    }
+    float* rw = red + 256;                                 // [4 waves][32 k][64 c]
+#pragma unroll
+    for (int km = 0; km < 2; ++km)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rw[(wave * 32 + 16 * km + 4 * lq + i) * 64 + 16 * n + l16] = acw[km][n][i];
+    float* rb3 = rw + 4 * 32 * 64;                         // [256 threads][3]
+#pragma unroll
+    for (int co = 0; co < 3; ++co) rb3[tid * 3 + co] = bsum[co];
+    __syncthreads();
+    if (tid < C) dal_part[(size_t)blockIdx.x * C + tid] = ((red[tid] + red[64 + tid]) + red[128 + tid]) + red[192 + tid];
+    const int nk = 9 * Co;
+    for (int i = tid; i < nk * C; i += 256) {
+        const int k = i / C, c = i - k * C, co = k / 9, tap = k - 9 * co;
+        const float v = ((rw[k * 64 + c] + rw[(32 + k) * 64 + c]) + rw[(64 + k) * 64 + c]) + rw[(96 + k) * 64 + c];
+        dw_part[(size_t)blockIdx.x * (Co * C * 9) + ((size_t)co * C + c) * 9 + tap] = v;
+    }
+    if (tid < Co) {
+        float v = 0.f;
+        for (int i = 0; i < 256; ++i) v += rb3[i * 3 + tid];
+        db_part[(size_t)blockIdx.x * Co + tid] = v;
     }
 }
 
@@ -1589,7 +1968,29 @@ extern "C" int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int 
 }
 
 extern "C" size_t fen_conv_last_dgrad_part_rows(int B, int H, int W) {
-    return (size_t)B * ((H + 15) / 16) * ((W + 15) / 16);
+    const size_t ntiles = (size_t)B * ((H + 15) / 16) * ((W + 15) / 16);
+    return ntiles < (size_t)CLD_GRID ? ntiles : (size_t)CLD_GRID;     // one partial row per block
+}
+
+extern "C" int fen_conv_last_bwd_supported(int dtype, int B, int H, int W, int C, int Co) {
+    return (dtype == FEN_BF16 || dtype == FEN_F16) && B > 0 && C == 64 && Co >= 1 && Co <= 3 && H > 0 && W > 0 &&
+           H % 16 == 0 && W % 16 == 0;
+}
+
+extern "C" int fen_conv_last_bwd(int dtype, int B, int H, int W, int C, int Co, const void* dout, const float* w,
+                                 const void* pre, const void* post, const float* alpha, void* du, float* dal_part,
+                                 float* dw_part, float* db_part, void* stream) {
+    if (!dout || !w || !pre || !post || !alpha || !du || !dal_part || !dw_part || !db_part) return FEN_EINVAL;
+    if (!fen_conv_last_bwd_supported(dtype, B, H, W, C, Co)) return FEN_EUNSUPPORTED;
+    const int nb = (int)fen_conv_last_dgrad_part_rows(B, H, W);
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_cl_bwd<bf16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, Co, (const bf16*)dout, w,
+                           (const bf16*)pre, (const bf16*)post, alpha, (bf16*)du, dal_part, dw_part, db_part);
+    else
+        hipLaunchKernelGGL(k_cl_bwd<f16>, dim3(nb), dim3(256), 0, STREAM, B, H, W, Co, (const f16*)dout, w,
+                           (const f16*)pre, (const f16*)post, alpha, (f16*)du, dal_part, dw_part, db_part);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
 }
 
 extern "C" int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const void* dout, const float* w,
@@ -1600,6 +2001,13 @@ extern "C" int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co
     const int nb = (int)fen_conv_last_dgrad_part_rows(B, H, W);
     auto launch = [&](auto tag) -> int {
         using T = decltype(tag);
+        if constexpr (sizeof(T) == 2) {
+            if (C == 64 && H % 16 == 0 && W % 16 == 0) {
+                hipLaunchKernelGGL((k_cld_p<T>), dim3(nb), dim3(256), 0, STREAM, B, H, W, Co, (const T*)dout, w,
+                                   (const T*)pre, (const T*)post, alpha, (T*)du, part);
+                return FEN_OK;
+            }
+        }
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, STREAM, B, H, W, Co, (const T*)dout, w, (const T*)pre,
                                (const T*)post, alpha, (T*)du, part);

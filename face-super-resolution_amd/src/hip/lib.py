@@ -152,6 +152,8 @@ _SIGS = {
     "fen_conv_first_work_floats": (c_size_t, [c_int] * 5),
     "fen_conv_first_wgrad": (c_int, [c_int] * 6 + [c_void_p] * 4 + [c_int, c_void_p, c_void_p]),
     "fen_conv_last_dgrad_part_rows": (c_size_t, [c_int] * 3),
+    "fen_conv_last_bwd_supported": (c_int, [c_int] * 6),
+    "fen_conv_last_bwd": (c_int, [c_int] * 6 + [c_void_p] * 9 + [c_void_p]),
     "fen_conv_last_dgrad": (c_int, [c_int] * 6 + [c_void_p] * 7 + [c_void_p]),
     "fen_se_fwd": (c_int, [c_int, c_int, c_int, c_int, c_float] + [c_void_p] * 6 + [c_void_p]),
     "fen_se_fused": (c_int, [c_int] * 6 + [c_float] + [c_void_p] * 7 + [c_float, c_void_p, c_void_p, c_void_p]),

@@ -238,6 +238,10 @@ WGRAD_STRIP_BATCH = max(1, min(32, int(os.environ.get("FEN_WGRAD_STRIP_BATCH", "
 # conv1^T) as ONE strip-resident fen_group_strip_bwd launch where its envelope holds (16-bit,
 # 64 ch, W = 64, H % 8 == 0); FEN_GROUP_STRIP_BWD=0 selects the per-RCAB launches
 GROUP_STRIP_BWD = os.environ.get("FEN_GROUP_STRIP_BWD", "1") != "0"
+# conv_last's data, slope, weight and bias gradients as ONE fen_conv_last_bwd pass over the last
+# stage's output (16-bit, 64 ch, whole 16x16 tiles, PRE_ELIDE); FEN_CL_BWD=0: the separate
+# weight-gradient pass + fen_conv_last_dgrad
+CL_BWD_FUSED = os.environ.get("FEN_CL_BWD", "1") != "0"
 # test-only fault injection for the strip kernels' bounded waits (fen_group_strip_desc.fault):
 # bit 0 = the forward launches, bit 1 = the backward launches skip one hand-off flag in one
 # strip, so its neighbour's wait times out and the launch reports through the status word
@@ -949,16 +953,29 @@ class Backward:
         C = s.C
         B, Ho, Wo = sv["dout"].shape[0], sv["Ho"], sv["Wo"]
         stages = sv["stages"]
-        # conv_last: weight grad (dy = zero-padded 16-channel dout), data grad fused with the
-        # last stage's PReLU backward and PixelShuffle inverse
-        self._wg("conv_last", sv["a_last"], sv["dout"], B, Ho, Wo, C, 16, cout_valid=s.out_ch)
         last = stages[-1]
         rows = ctx.lib.fen_conv_last_dgrad_part_rows(B, Ho, Wo)
         dal = ctx.scratch(f"bw_dal_up{len(stages) - 1}", (rows, C), torch.float32)
         du = ctx.scratch(f"bw_du{(len(stages) - 1) & 1}", (B, last["H"], last["W"], 4 * C))
-        ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, Ho, Wo, C, s.out_ch, ptr(sv["dout"]),
-                 ptr(p["conv_last.weight"]), ptr(last["v"]), ptr(last["a"]) if PRE_ELIDE else None,
-                 ptr(p[f"upsample.stages.{len(stages) - 1}.prelu.weight"]), ptr(du), ptr(dal))
+        alpha_last = p[f"upsample.stages.{len(stages) - 1}.prelu.weight"]
+        if CL_BWD_FUSED and PRE_ELIDE and ctx.lib.fen_conv_last_bwd_supported(ctx.code, B, Ho, Wo, C, s.out_ch):
+            # conv_last's data gradient (+ the last stage's PReLU backward and PixelShuffle
+            # inverse) and its weight / bias gradients in one pass over the stage output
+            co = s.out_ch
+            dwp = ctx.scratch("bw_cl_dw", (rows, co * C * 9), torch.float32)
+            dbp = ctx.scratch("bw_cl_db", (rows, co), torch.float32)
+            ctx.emit("conv_last_bwd", ctx.lib.fen_conv_last_bwd, ctx.code, B, Ho, Wo, C, co, ptr(sv["dout"]),
+                     ptr(p["conv_last.weight"]), ptr(last["v"]), ptr(last["a"]), ptr(alpha_last), ptr(du), ptr(dal),
+                     ptr(dwp), ptr(dbp))
+            self.cs.add(dwp, rows, co * C * 9, G["conv_last.weight"])
+            self.cs.add(dbp, rows, co, G["conv_last.bias"])
+        else:
+            # conv_last: weight grad (dy = zero-padded 16-channel dout), data grad fused with the
+            # last stage's PReLU backward and PixelShuffle inverse
+            self._wg("conv_last", sv["a_last"], sv["dout"], B, Ho, Wo, C, 16, cout_valid=s.out_ch)
+            ctx.emit("conv_last_dgrad", ctx.lib.fen_conv_last_dgrad, ctx.code, B, Ho, Wo, C, s.out_ch,
+                     ptr(sv["dout"]), ptr(p["conv_last.weight"]), ptr(last["v"]),
+                     ptr(last["a"]) if PRE_ELIDE else None, ptr(alpha_last), ptr(du), ptr(dal))
         self.cs.add(dal, rows, C, G[f"upsample.stages.{len(stages) - 1}.prelu.weight"])
         for st in reversed(range(len(stages))):
             info = stages[st]

@@ -143,13 +143,25 @@ int fen_conv_first_wgrad(int dtype, int B, int Ci, int H, int W, int C, const fl
 
 /* conv_last data gradient fused with the previous stage's PReLU backward and the
  * PixelShuffle inverse: dout NHWC16 [B,H,W,16] -> du NHWC [B,H/2,W/2,4C];
- * pre = that stage's pre-activation NHWC [B,H,W,C]; part[B*tiles][C] dalpha partials.
+ * pre = that stage's pre-activation NHWC [B,H,W,C]; part[rows][C] dalpha partials.
  * post = that stage's PReLU output (same layout) or NULL: as fen_conv_desc.post_in, groups of
- * 4 channels with all slopes > 0 recover the pre-activation from it and do not read pre.   */
+ * 4 channels with all slopes > 0 recover the pre-activation from it and do not read pre.
+ * part has fen_conv_last_dgrad_part_rows rows (one per block of the persistent grid; the
+ * slope gradient is their column sum).                                                     */
 size_t fen_conv_last_dgrad_part_rows(int B, int H, int W);
 int fen_conv_last_dgrad(int dtype, int B, int H, int W, int C, int Co, const void* dout,
                         const float* w, const void* pre, const void* post, const float* alpha,
                         void* du, float* part, void* stream);
+/* conv_last's whole backward in one pass (replaces the conv_last weight-gradient pass + the
+ * call above on the training path; custom.py:177-184 backward): du and the slope partials as
+ * fen_conv_last_dgrad, plus dw_part[rows][Co*C*9] (OIHW order) and db_part[rows][Co], whose
+ * column sums are conv_last's weight and bias gradients; rows = fen_conv_last_dgrad_part_rows.
+ * post is required (the stage's PReLU output is the weight gradient's operand).  16-bit, C = 64,
+ * Co <= 3, H and W multiples of 16 (fen_conv_last_bwd_supported); FEN_EUNSUPPORTED otherwise. */
+int fen_conv_last_bwd_supported(int dtype, int B, int H, int W, int C, int Co);
+int fen_conv_last_bwd(int dtype, int B, int H, int W, int C, int Co, const void* dout,
+                      const float* w, const void* pre, const void* post, const float* alpha,
+                      void* du, float* dal_part, float* dw_part, float* db_part, void* stream);
 
 /* Channel attention (blocks.py:44-92) forward: pool partials -> s = sigmoid(W2 relu(W1 mean)) */
 int fen_se_fwd(int B, int C, int Cr, int nparts, float inv_hw, const float* part,

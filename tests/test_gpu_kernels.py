@@ -603,12 +603,14 @@ def test_s2d_stride2_conv(dtype, B, H, W, Cin, Cout):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("B,H,W,C", [(2, 64, 64, 64), (1, 36, 20, 64), (1, 40, 24, 32), (1, 32, 32, 128)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 64, 64, 64), (1, 36, 20, 64), (1, 40, 24, 32), (1, 32, 32, 128),
+                                     (3, 256, 256, 64)])
 def test_conv_last_dgrad(dtype, B, H, W, C):
     """fen_conv_last_dgrad (conv_last^T 3 -> C + the last upsampler stage's PReLU backward +
     PixelShuffle inverse + dalpha partials) against torch autograd of conv(prelu(v)) in fp32;
-    16-bit at C <= 64 runs the LDS pre-activation tile, the rest the per-pixel reads; H = 36
-    leaves a partial tile row."""
+    16-bit at C = 64 runs the persistent pipelined kernel (k_cld_p) when the tiles are whole,
+    other 16-bit C <= 64 the LDS pre-activation tile, the rest the per-pixel reads; H = 36 leaves
+    a partial tile row; 3 x 256^2 has 768 tiles for 512 blocks (blocks take one or two tiles)."""
     from src.hip.program import ptr
     torch.manual_seed(21)
     Co = 3
@@ -641,6 +643,64 @@ def test_conv_last_dgrad(dtype, B, H, W, C):
     da = part.sum(0).cpu()
     rel = float((da - a.grad).norm() / a.grad.norm())
     assert rel <= (1e-5 if dtype == torch.float32 else 1e-4), rel
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("amode", ["pos", "mixed"])
+@pytest.mark.parametrize("B,H,W,Co", [(2, 64, 64, 3), (3, 256, 256, 3), (1, 16, 48, 1)])
+def test_conv_last_bwd(dtype, amode, B, H, W, Co):
+    """fen_conv_last_bwd (conv_last's data, slope, weight and bias gradients in one MFMA pass)
+    against torch autograd in fp32: du and dalpha of conv(prelu(v)) on the kernel's rounded v,
+    dW / db of conv(a) on the kernel's a.  pre is NaN in the groups whose slopes are all > 0
+    (read from post), post NaN in the others (read from pre, a rebuilt as rnd16(PReLU(v)))."""
+    from src.hip.program import ptr
+    torch.manual_seed(31)
+    C = 64
+    ctx = _ctx(dtype)
+    assert ctx.lib.fen_conv_last_bwd_supported(ctx.code, B, H, W, C, Co)
+    alpha = torch.rand(C) * 0.4 + 0.05
+    if amode == "mixed":
+        alpha[5], alpha[9], alpha[40] = -0.2, 0.0, -0.05
+    mixed = torch.zeros(C, dtype=torch.bool)
+    for c in range(0, C, 4):
+        mixed[c:c + 4] = bool((alpha[c:c + 4] <= 0).any())
+    v = torch.randn(B, H, W, C).to(dtype).float()                 # the stored pre-activation
+    a = O.prelu(v.permute(0, 3, 1, 2), alpha).permute(0, 2, 3, 1).to(dtype).float()   # rnd16(PReLU(v))
+    pre = v.to(DEV, dtype)
+    pre[..., ~mixed.to(DEV)] = float("nan")
+    post = a.to(DEV, dtype)
+    post[..., mixed.to(DEV)] = float("nan")
+    w = torch.randn(Co, C, 3, 3) * 0.05
+    g = torch.randn(B, Co, H, W)
+    dout = torch.zeros(B, H, W, 16)
+    dout[..., :Co] = g.permute(0, 2, 3, 1)
+    gq = dout.to(DEV, dtype)
+    gg = gq[..., :Co].float().cpu().permute(0, 3, 1, 2)
+    rows = ctx.lib.fen_conv_last_dgrad_part_rows(B, H, W)
+    du = ctx.alloc((B, H // 2, W // 2, 4 * C))
+    dal = ctx.alloc((rows, C), torch.float32)
+    dwp = ctx.alloc((rows, Co * C * 9), torch.float32)
+    dbp = ctx.alloc((rows, Co), torch.float32)
+    wd, ad = w.to(DEV).contiguous(), alpha.to(DEV)
+    ctx.emit("conv_last_bwd", ctx.lib.fen_conv_last_bwd, ctx.code, B, H, W, C, Co, ptr(gq), ptr(wd), ptr(pre),
+             ptr(post), ptr(ad), ptr(du), ptr(dal), ptr(dwp), ptr(dbp))
+    torch.cuda.synchronize()
+    vv = v.permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    al = alpha.clone().requires_grad_(True)
+    F.conv2d(O.prelu(vv, al), w, None, padding=1).mul(gg).sum().backward()
+    ref = vv.grad.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 3, 5, 2, 4).reshape(B, 4 * C, H // 2, W // 2)
+    assert bool(torch.isfinite(du.float()).all())
+    assert (nchw(du) - ref).abs().max() <= _tol(dtype, ref)
+    rel = float((dal.sum(0).cpu() - al.grad).norm() / al.grad.norm())
+    assert rel <= (1e-3 if amode == "pos" else 1e-2), rel
+    aa = a.permute(0, 3, 1, 2).contiguous()
+    wr = w.clone().requires_grad_(True)
+    br = torch.zeros(Co, requires_grad=True)
+    F.conv2d(aa, wr, br, padding=1).mul(gg).sum().backward()
+    dw = dwp.sum(0).cpu().reshape(Co, C, 3, 3)
+    db = dbp.sum(0).cpu()
+    assert float((dw - wr.grad).norm() / wr.grad.norm()) <= 1e-4
+    assert float((db - br.grad).abs().max()) <= 1e-4 * max(1.0, float(br.grad.abs().max()))
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
