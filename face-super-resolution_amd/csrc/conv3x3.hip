@@ -26,6 +26,8 @@
 // conv_last the bicubic skip + eval clamp + L1-loss gradient.
 #include "fen_common.h"
 
+#include <type_traits>
+
 namespace {
 
 // Diagnostic build only (-DFEN_STAMPS, tools/stamp_conv.py): per-block s_memrealtime /
@@ -937,6 +939,10 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
 // ------------------------------------------------------------------------------------
 // k_conv3x3_s: streamed per-tap weights, register-staged halo (f32 / bf16 / fp16, any Cin panel)
 // ------------------------------------------------------------------------------------
+// halo chunks of the next Cin panel loaded during the current panel's taps (the rest after it)
+#ifndef CONV_S_PFN
+#define CONV_S_PFN 11
+#endif
 template <typename T, int COT>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -965,7 +971,6 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + q * 4);   // latency hidden by the main loop
 
     // a last partial panel (Cin % CK: FaceEnhanceNetLite's 32 channels in 16-bit) reads zeros
     // past Cin, in the halo and in the filter
@@ -983,28 +988,37 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
         return m;
     };
     const unsigned mask_out = d.s2d_out > 0 ? live_taps(co0 / d.s2d_out, true) : 0x1ffu;
-    for (int pn = 0; pn < npan; ++pn) {
-        const unsigned mask = d.s2d_in > 0 ? live_taps(pn * CK / d.s2d_in, false) : mask_out;
-        // ---- stage the input halo of panel pn (zero padding outside the image) ----
-        constexpr int HPT = (HP * 8 + 255) / 256;   // 11 chunks per thread: loads first, then writes
-        uint4 hv[HPT];
-#pragma unroll
-        for (int j = 0; j < HPT; ++j) {
-            const int i = tid + j * 256;
-            hv[j] = make_uint4(0, 0, 0, 0);
-            if (i < HP * 8) {
-                const int p = i >> 3, ch = i & 7;
-                const int hr = p / HALO, hc = p - hr * HALO;
-                const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-                if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W && pn * 128 + ch * 16 < (int)xrow)
-                    hv[j] = *(const uint4*)(xb + ((size_t)(b * H + gh) * W + gw) * xrow + pn * 128 + ch * 16);
-            }
+    // ---- the input halo of a panel (zero padding outside the image), through registers ----
+    constexpr int HPT = (HP * 8 + 255) / 256;   // 11 chunks per thread
+    uint4 hv[HPT];
+    auto halo_load = [&](int pn, int j) {
+        int t = tid;
+        asm volatile("" : "+v"(t));             // addresses per call: not hoisted across the panels
+        const int i = t + j * 256;
+        hv[j] = make_uint4(0, 0, 0, 0);
+        if (i < HP * 8) {
+            const int p = i >> 3, ch = i & 7;
+            const int hr = p / HALO, hc = p - hr * HALO;
+            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+            if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W && pn * 128 + ch * 16 < (int)xrow)
+                hv[j] = *(const uint4*)(xb + ((size_t)(b * H + gh) * W + gw) * xrow + pn * 128 + ch * 16);
         }
+    };
+    auto halo_store = [&]() {
 #pragma unroll
         for (int j = 0; j < HPT; ++j) {
             const int i = tid + j * 256;
             if (i < HP * 8) *(uint4*)(halo + hswz(i >> 3, i & 7)) = hv[j];
         }
+    };
+#pragma unroll
+    for (int j = 0; j < HPT; ++j) halo_load(0, j);
+    // one Cin panel; NEXT: the next panel's halo loads are issued during this one (their
+    // registers are free in the last panel, which loads the epilogue constants instead)
+    auto run_panel = [&](int pn, auto NEXT) {
+        constexpr bool next = decltype(NEXT)::value;
+        const unsigned mask = d.s2d_in > 0 ? live_taps(pn * CK / d.s2d_in, false) : mask_out;
+        halo_store();                           // panel pn (the loads were issued one panel ahead)
         uint4 wr[WPT];
         // every thread loads WPT chunks (chunk index wrapped, duplicates are harmless): no
         // per-load branch, so hipcc keeps the prefetch in flight across the tap's MFMAs
@@ -1025,6 +1039,33 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
                 *(uint4*)(dst + swz(i >> 3, i & 7)) = wr[j];
             }
         };
+#ifndef CONV_S_NOPF
+        if (mask == 0x1ffu) {
+            // all 9 taps: the next panel's halo loads ride under this panel's MFMAs, one or two
+            // per tap, each issued after that tap's weight loads (the next tap's wait on the
+            // weights, which are older, leaves them in flight; the tap after covers them)
+            load_w(0);
+            store_w(wbuf);
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < 9; ++it) {
+                if (it < 8) load_w(it + 1);
+                if (next) {
+#pragma unroll
+                    for (int j = 0; j < CONV_S_PFN; ++j)
+                        if (j * 9 / CONV_S_PFN == it) halo_load(pn + 1, j);
+                }
+                conv_tap<T, MT, 4>(acc, wbuf + (it & 1) * COT * 128, halo, it, wave, 0, q, c16);
+                if (it < 8) store_w(wbuf + ((it + 1) & 1) * COT * 128);
+                __syncthreads();
+            }
+            if (next) {
+#pragma unroll
+                for (int j = CONV_S_PFN; j < HPT; ++j) halo_load(pn + 1, j);
+            }
+            return;
+        }
+#endif
         // live taps in order (mask is block-uniform: scalar bit walk)
         unsigned rem = mask;
         int tap = __builtin_ctz(rem);
@@ -1043,7 +1084,14 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
             rem &= rem - 1;
             tap = ntap;
         }
-    }
+        if (next) {
+#pragma unroll
+            for (int j = 0; j < HPT; ++j) halo_load(pn + 1, j);
+        }
+    };
+    for (int pn = 0; pn + 1 < npan; ++pn) run_panel(pn, std::true_type{});
+    const EpiConst<MT> ec = epi_consts<MT>(d, co0 + q * 4);   // latency hidden by the last panel
+    run_panel(npan - 1, std::false_type{});
     float* red = (float*)wbuf;     // LDS is free after the loop
     char* stage = (sizeof(T) == 2 && COT == 64) ? halo : nullptr;
     conv_epilogue<T, COT, 4, 1>(d, acc, b, tb, h0, w0, co0, stage, red, ec);

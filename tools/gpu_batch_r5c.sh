@@ -1,10 +1,10 @@
-# round-5 batch c: the fused conv_last backward (k_cl_bwd) and the persistent conv_last dgrad
-# (k_cld_p) parity first, then the strip-backward per-strip dalpha and training-path tests, the
+# round-5 batch c: the kernel tests first (the fused conv_last backward k_cl_bwd, the persistent
+# conv_last dgrad k_cld_p, the streamed conv's next-panel halo prefetch), then the strip-backward per-strip dalpha and training-path tests, the
 # fc2e variant's forward parity, then the training A/B (fused tail backward vs FEN_CL_BWD=0) and
 # the inference A/B (fc2e), op times
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_kernels.py -k "conv_last_dgrad or conv_last_bwd or pre_elide" > gpurun_out/t_cl.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_kernels.py > gpurun_out/t_cl.log 2>&1
 rc=$?; echo "conv_last tests rc=$rc"; tail -3 gpurun_out/t_cl.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/t_cl.log | head -20; exit 1; }
 timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_group_strip_bwd.py tests/test_gpu_train64.py tests/test_gpu_strip_status.py tests/test_gpu_rccl.py > gpurun_out/t_prod.log 2>&1
 rc=$?; echo "product tests rc=$rc"; tail -2 gpurun_out/t_prod.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/t_prod.log | head -20; exit 1; }
@@ -17,7 +17,7 @@ for rep in 1 2 3; do
     echo "CL_BWD=$v   $(tail -1 gpurun_out/ab_t.log)"
   done
 done
-INF=1 REPS=3 bash tools/gpu_ab_r5.sh
+INF=1 REPS=2 bash tools/gpu_ab_r5.sh
 timeout -k 10 200 python tools/op_times.py > gpurun_out/ops_inf.txt 2>&1
 TRAIN=1 timeout -k 10 300 python tools/op_times.py > gpurun_out/ops_train.txt 2>&1
 echo "op_times rc=$?"
