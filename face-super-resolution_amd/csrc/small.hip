@@ -891,8 +891,8 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
 #pragma unroll
         for (int n = 0; n < 4; ++n) acw[km][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bsum[3] = {0.f, 0.f, 0.f};
-    // ---- the im2col builder's role: pixel pair (2 p2, 2 p2 + 1) in r order, k half kh2
-    const int p2 = tid & 127, kh2 = tid >> 7;
+    // ---- the im2col builder's role: pixel pair (2 p2, 2 p2 + 1) in r order
+    const int p2 = tid & 127;
     const int Hh = H >> 1, Wh = W >> 1;
     int t = blockIdx.x;
     if (t < ntiles) load(t);
@@ -918,8 +918,12 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
         }
         __syncthreads();                                   // (B) halo and P^T written
         if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);   // the next tile, under this one's work
-        {
-            // X rows r0, r0 + 1 (k half kh2) and the matching X^T words; bias partials
+        // X rows r0, r0 + 1 (k half KH, wave-uniform: waves 0-1 k 0..15, waves 2-3 k 16..31) and
+        // the matching X^T words; bias partials.  KH a template constant: every k, co and tap
+        // below is compile-time, the 9 halo words stay in registers (a runtime index into them
+        // went to scratch, whose loads wait on the whole vmcnt queue: the prefetch)
+        auto build = [&](auto KHC) {
+            constexpr int KH = decltype(KHC)::value;
             const int r0 = 2 * p2;
             unsigned short xv[2][16];
 #pragma unroll
@@ -931,31 +935,32 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
                 for (int tap = 0; tap < 9; ++tap) g[tap] = hd[(sh - tap / 3 + 2) * 18 + (sw - tap % 3 + 2)];
 #pragma unroll
                 for (int kk = 0; kk < 16; ++kk) {
-                    const int k = 16 * kh2 + kk, co = k / 9, tap = k - 9 * co;
+                    const int k = 16 * KH + kk, co = k / 9, tap = k - 9 * co;
                     unsigned short v = 0;
-                    if (co < 3 && co < Co) {
-                        const uint2 gg = g[tap < 9 ? tap : 0];
-                        const unsigned wd = co < 2 ? gg.x : gg.y;
-                        v = (unsigned short)((co == 1) ? (wd >> 16) : (wd & 0xffffu));
+                    if (co < 3) {
+                        const unsigned wd = co < 2 ? g[tap].x : g[tap].y;
+                        v = co < Co ? (unsigned short)((co == 1) ? (wd >> 16) : (wd & 0xffffu)) : (unsigned short)0;
                     }
                     xv[e][kk] = v;
                 }
                 // bias: the centre tap (k = 9 co + 4) of the pixel's own dout
 #pragma unroll
                 for (int co = 0; co < 3; ++co)
-                    if ((9 * co + 4) / 16 == kh2) bsum[co] += tof<T>(__builtin_bit_cast(T, xv[e][(9 * co + 4) % 16]));
+                    if ((9 * co + 4) / 16 == KH) bsum[co] += tof<T>(__builtin_bit_cast(T, xv[e][(9 * co + 4) % 16]));
                 uint4 u0, u1;
                 u0.x = xv[e][0] | ((unsigned)xv[e][1] << 16);   u0.y = xv[e][2] | ((unsigned)xv[e][3] << 16);
                 u0.z = xv[e][4] | ((unsigned)xv[e][5] << 16);   u0.w = xv[e][6] | ((unsigned)xv[e][7] << 16);
                 u1.x = xv[e][8] | ((unsigned)xv[e][9] << 16);   u1.y = xv[e][10] | ((unsigned)xv[e][11] << 16);
                 u1.z = xv[e][12] | ((unsigned)xv[e][13] << 16); u1.w = xv[e][14] | ((unsigned)xv[e][15] << 16);
-                *(uint4*)(X + r * XS + 16 * kh2) = u0;
-                *(uint4*)(X + r * XS + 16 * kh2 + 8) = u1;
+                *(uint4*)(X + r * XS + 16 * KH) = u0;
+                *(uint4*)(X + r * XS + 16 * KH + 8) = u1;
             }
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk)
-                *(unsigned*)(XT + (16 * kh2 + kk) * TS + r0) = xv[0][kk] | ((unsigned)xv[1][kk] << 16);
-        }
+                *(unsigned*)(XT + (16 * KH + kk) * TS + r0) = xv[0][kk] | ((unsigned)xv[1][kk] << 16);
+        };
+        if (wave < 2) build(std::integral_constant<int, 0>{});
+        else build(std::integral_constant<int, 1>{});
         __syncthreads();                                   // (C) X, X^T written
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
