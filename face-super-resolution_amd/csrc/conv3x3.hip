@@ -991,24 +991,30 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     // ---- the input halo of a panel (zero padding outside the image), through registers ----
     constexpr int HPT = (HP * 8 + 255) / 256;   // 11 chunks per thread
     uint4 hv[HPT];
+    unsigned hok = 0;                           // bit j: chunk j in range (else stored as zeros)
     auto halo_load = [&](int pn, int j) {
         int t = tid;
         asm volatile("" : "+v"(t));             // addresses per call: not hoisted across the panels
         const int i = t + j * 256;
-        hv[j] = make_uint4(0, 0, 0, 0);
-        if (i < HP * 8) {
-            const int p = i >> 3, ch = i & 7;
-            const int hr = p / HALO, hc = p - hr * HALO;
-            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-            if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W && pn * 128 + ch * 16 < (int)xrow)
-                hv[j] = *(const uint4*)(xb + ((size_t)(b * H + gh) * W + gw) * xrow + pn * 128 + ch * 16);
-        }
+        const int p = i >> 3, ch = i & 7;
+        const int hr = p / HALO, hc = p - hr * HALO;
+        const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+        const bool ok = i < HP * 8 && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W &&
+                        pn * 128 + ch * 16 < (int)xrow;
+        // branch-free: an out-of-range chunk loads the image's first one and is zeroed after, so
+        // the vmcnt bookkeeping sees the same loads on every path (a branch makes hipcc wait for
+        // all of them at the next use of any)
+        // the zeroing waits for the store (a select right behind the load would wait for it)
+        const size_t off = ok ? ((size_t)(b * H + gh) * W + gw) * xrow + pn * 128 + ch * 16 : 0;
+        hv[j] = *(const uint4*)(xb + off);
+        hok = ok ? hok | (1u << j) : hok & ~(1u << j);
     };
     auto halo_store = [&]() {
 #pragma unroll
         for (int j = 0; j < HPT; ++j) {
             const int i = tid + j * 256;
-            if (i < HP * 8) *(uint4*)(halo + hswz(i >> 3, i & 7)) = hv[j];
+            const uint4 v = ((hok >> j) & 1u) ? hv[j] : make_uint4(0, 0, 0, 0);
+            if (i < HP * 8) *(uint4*)(halo + hswz(i >> 3, i & 7)) = v;
         }
     };
 #pragma unroll
@@ -1039,33 +1045,6 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
                 *(uint4*)(dst + swz(i >> 3, i & 7)) = wr[j];
             }
         };
-#ifndef CONV_S_NOPF
-        if (mask == 0x1ffu) {
-            // all 9 taps: the next panel's halo loads ride under this panel's MFMAs, one or two
-            // per tap, each issued after that tap's weight loads (the next tap's wait on the
-            // weights, which are older, leaves them in flight; the tap after covers them)
-            load_w(0);
-            store_w(wbuf);
-            __syncthreads();
-#pragma unroll
-            for (int it = 0; it < 9; ++it) {
-                if (it < 8) load_w(it + 1);
-                if (next) {
-#pragma unroll
-                    for (int j = 0; j < CONV_S_PFN; ++j)
-                        if (j * 9 / CONV_S_PFN == it) halo_load(pn + 1, j);
-                }
-                conv_tap<T, MT, 4>(acc, wbuf + (it & 1) * COT * 128, halo, it, wave, 0, q, c16);
-                if (it < 8) store_w(wbuf + ((it + 1) & 1) * COT * 128);
-                __syncthreads();
-            }
-            if (next) {
-#pragma unroll
-                for (int j = CONV_S_PFN; j < HPT; ++j) halo_load(pn + 1, j);
-            }
-            return;
-        }
-#endif
         // live taps in order (mask is block-uniform: scalar bit walk)
         unsigned rem = mask;
         int tap = __builtin_ctz(rem);
@@ -1089,9 +1068,75 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
             for (int j = 0; j < HPT; ++j) halo_load(pn + 1, j);
         }
     };
-    for (int pn = 0; pn + 1 < npan; ++pn) run_panel(pn, std::true_type{});
+#ifndef CONV_S_NOPF
+    // Every tap live (no space-to-depth): the (panel, tap) steps as one pipeline.  Weights two
+    // steps ahead (two register sets, step s + 2 issued during step s) into a
+    // 3-slot LDS ring (step s in slot s % 3, 9 % 3 == 0: the slot is the tap's), so an L2 round
+    // trip has two steps of MFMAs to land in and no panel starts on an exposed weight load; the
+    // next panel's halo chunks ride under this panel's taps, one or two per tap, after that
+    // tap's weight loads (a wait on the older weights leaves them in flight).
+    const bool fast = d.s2d_in <= 0 && mask_out == 0x1ffu;
+#else
+    const bool fast = false;
+#endif
+    uint4 w2[2][WPT];   // step s + 1 in w2[(it + 1) & 1], step s + 2 loaded into w2[it & 1]
+    auto ldw = [&](int pn, int tap, uint4 (&w)[WPT]) {
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int i = (tid + j * 256) % WCH;
+            const int r = i >> 3, ch = i & 7;
+            // branch-free as halo_load; a chunk past Cin (a last partial panel) re-reads chunk 0
+            // of the row and is zeroed by stw
+            const bool ok = pn * 128 + ch * 16 < (int)xrow;
+            w[j] = *(const uint4*)(wb + (size_t)(tap * coutp + co0 + r) * xrow + (ok ? pn * 128 + ch * 16 : 0));
+        }
+    };
+    auto stw = [&](const uint4 (&w)[WPT], char* dst, int pn) {
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const int i = (tid + j * 256) % WCH;
+            const bool ok = pn * 128 + (i & 7) * 16 < (int)xrow;
+            *(uint4*)(dst + swz(i >> 3, i & 7)) = ok ? w[j] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto fast_panel = [&](int pn, auto NEXT) {
+        constexpr bool next = decltype(NEXT)::value;
+#pragma unroll
+        for (int it = 0; it < 9; ++it) {
+            if (it + 2 < 9) ldw(pn, it + 2, w2[it & 1]);
+            else if (next) ldw(pn + 1, it - 7, w2[it & 1]);
+            if (next) {
+#pragma unroll
+                for (int j = 0; j < CONV_S_PFN; ++j)
+                    if (j * 9 / CONV_S_PFN == it) halo_load(pn + 1, j);
+            }
+            conv_tap<T, MT, 4>(acc, wbuf + (it % 3) * COT * 128, halo, it, wave, 0, q, c16);
+            if (it < 8 || next) stw(w2[(it + 1) & 1], wbuf + ((it + 1) % 3) * COT * 128, it < 8 ? pn : pn + 1);
+            __syncthreads();
+        }
+        if (next) {
+#pragma unroll
+            for (int j = CONV_S_PFN; j < HPT; ++j) halo_load(pn + 1, j);
+            halo_store();
+            // 9 steps per panel (odd): the next panel's tap 1 came into w2[0], its entry wants w2[1]
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) w2[1][j] = w2[0][j];
+            __syncthreads();
+        }
+    };
+    if (fast) {
+        ldw(0, 0, w2[0]);
+        ldw(0, 1, w2[1]);
+        halo_store();
+        stw(w2[0], wbuf, 0);
+        __syncthreads();
+        for (int pn = 0; pn + 1 < npan; ++pn) fast_panel(pn, std::true_type{});
+    } else {
+        for (int pn = 0; pn + 1 < npan; ++pn) run_panel(pn, std::true_type{});
+    }
     const EpiConst<MT> ec = epi_consts<MT>(d, co0 + q * 4);   // latency hidden by the last panel
-    run_panel(npan - 1, std::false_type{});
+    if (fast) fast_panel(npan - 1, std::false_type{});
+    else run_panel(npan - 1, std::false_type{});
     float* red = (float*)wbuf;     // LDS is free after the loop
     char* stage = (sizeof(T) == 2 && COT == 64) ? halo : nullptr;
     conv_epilogue<T, COT, 4, 1>(d, acc, b, tb, h0, w0, co0, stage, red, ec);
@@ -1169,7 +1214,12 @@ int launch_s(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int coutp = (d->Cout + 15) & ~15;
     dim3 grid(d->B * tpi, coutp / COT);
-    const size_t lds = HALO_BYTES + 2 * COT * 128;
+    const size_t lds = HALO_BYTES + 3 * COT * 128;   // > 64 KB at COT = 64: opt in once
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_s<T, COT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+    }
     hipLaunchKernelGGL((k_conv3x3_s<T, COT>), grid, dim3(256), lds, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
