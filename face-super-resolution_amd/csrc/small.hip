@@ -824,7 +824,12 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
     uint2* hd = (uint2*)smem;                                        // dout halo, channels 0..3
     unsigned short* X = (unsigned short*)(smem + 18 * 18 * 8);       // [256 r][XS]
     unsigned short* XT = X + 256 * XS;                               // [32 k][TS]
-    unsigned short* PT = XT + 32 * TS;                               // [64 c][TS]
+    unsigned short* PT = XT + 32 * TS;                               // [64 c][TS], 8-element chunks swizzled
+    // P^T element (c, r): the 16-B chunk r >> 3 of row c XOR (c >> 3) & 7.  The transposed
+    // writes (32 lanes of one ds_write_b32: 8 channel rows 8 apart x 4 pixel pairs) then fall on
+    // 16 banks instead of 4 (every row of a channel group hit the same one: 8-way); the reads
+    // (16 B at r % 8 == 0, 8 B at r % 4 == 0) stay inside one chunk
+    auto pt = [&](int c, int r) { return PT + c * TS + (((r >> 3) ^ ((c >> 3) & 7)) << 3) + (r & 7); };
     const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lq = lane >> 4;
     const int wave = wave_id();
     const int twn = W >> 4, tpi = twn * (H >> 4), ntiles = B * tpi;
@@ -912,7 +917,7 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const unsigned wd = __builtin_amdgcn_perm(a1[i >> 1], a0[i >> 1], (i & 1) ? 0x07060302u : 0x05040100u);
-                    *(unsigned*)(PT + (8 * pcq + i) * TS + r) = wd;
+                    *(unsigned*)pt(8 * pcq + i, r) = wd;
                 }
             }
         }
@@ -973,7 +978,7 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
             for (int km = 0; km < 2; ++km) A[km] = *(const uint4*)(XT + (16 * km + l16) * TS + rb);
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
-                uint4 Bv = *(const uint4*)(PT + (16 * n + l16) * TS + rb);
+                uint4 Bv = *(const uint4*)pt(16 * n + l16, rb);
                 if (!rec[n]) {                             // P holds v: a = PReLU(v) in 16 bits
                     float f[8];
                     unpack16<T>(Bv, f);
@@ -997,7 +1002,7 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
                 mma16<T>(acc, A, whi[n]);
                 mma16<T>(acc, A, wlo[n]);
                 const int c = 16 * n + l16;
-                const uint2 pw = *(const uint2*)(PT + c * TS + 4 * dp);
+                const uint2 pw = *(const uint2*)pt(c, 4 * dp);
                 const float pq[4] = {lo16<T>(pw.x), hi16<T>(pw.x), lo16<T>(pw.y), hi16<T>(pw.y)};
                 float ov[4];
 #pragma unroll
