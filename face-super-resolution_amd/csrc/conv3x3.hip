@@ -208,6 +208,27 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
     bool rec4[MT];                                        // PRELU_BWD from post_in (see fen.h)
 #pragma unroll
     for (int m = 0; m < MT; ++m) rec4[m] = (epi & FEN_EPI_PRELU_BWD) && d.post_in && all_pos4(ec.alpha[m]);
+    // the PRELU_BWD / DOT operands of the whole tile issued together, branch-free (an invalid
+    // pixel re-reads offset 0 and is not used), before pass 1 consumes any: one memory round
+    // trip per tile instead of one per (m, n) -- a load under the per-pixel branch with its use
+    // right behind it waited for each in turn
+    typedef typename std::conditional<sizeof(T) == 2, uint2, uint4>::type RawV;
+    const bool pin = epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT);
+    RawV pvr[MT][NT];
+    if (pin) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const int cob = co0 + wc * CW + m * 16 + q * 4;
+            const char* src = (const char*)(((epi & FEN_EPI_PRELU_BWD) && rec4[m]) ? d.post_in : d.pre_in);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int h = h0 + wr * NT + n;
+                const bool valid = (full || (h < H && w_ < W)) && cob < Cout;
+                const size_t oi = valid ? ((size_t)(b * H + h) * W + w_) * Cout + cob : 0;
+                pvr[m][n] = *(const RawV*)(src + oi * sizeof(T));
+            }
+        }
+    }
     // pass 1: elementwise epilogue in registers (acc <- pre-activation value)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -236,7 +257,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                     // post_in (every slope of the group > 0): the PReLU output has the
                     // pre-activation's sign; the slope partials are rescaled by 1 / alpha below
                     float pv[4];
-                    ld4<T>((const char*)(rec4[m] ? d.post_in : d.pre_in) + oi * sizeof(T), pv);
+                    ld4<T>(&pvr[m][n], pv);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         psum[m][r] += prelu_dalpha_f(v[r], pv[r]);
@@ -245,7 +266,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                 }
                 if (epi & FEN_EPI_DOT) {
                     float pv[4];
-                    ld4<T>((const char*)d.pre_in + oi * sizeof(T), pv);
+                    ld4<T>(&pvr[m][n], pv);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) psum[m][r] += rnd16<T>(v[r]) * pv[r];
                 }
