@@ -387,9 +387,10 @@ def time_gan_step(steps, B=16):
 
 
 def time_ssim(eng, reps=50):
-    """The stage-2 SSIM launch of a training engine (fwd map + tile sums + gradient added to
-    dL/dsr), timed with HIP events on the current stream, against the HBM roofline:
-    algorithmic bytes = pred + target (fp32 NCHW) read + dL/dsr (NHWC16 bf16) read + write."""
+    """The stage-2 SSIM op of a training engine (fwd map + tile sums + gradient added to dL/dsr;
+    fen_ssim_ex's two launches), timed with HIP events on the current stream, against the HBM
+    roofline: algorithmic bytes = pred + target (fp32 NCHW) read + dL/dsr (NHWC16 bf16) read +
+    write (the a / b / c workspace is the implementation's, not counted)."""
     name, fn, fargs = next(op for op in eng.ctx.ops if op[0] == "ssim")
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(5):
@@ -403,7 +404,8 @@ def time_ssim(eng, reps=50):
     us = e0.elapsed_time(e1) * 1e3 / reps
     B, C, H, W = eng.B, 3, eng.H, eng.W
     nbytes = 2 * B * C * H * W * 4 + 2 * B * H * W * 16 * 2
-    return {"kernel": "k_ssim<GRAD> (csrc/ssim.hip)", "us": round(us, 2), "bytes": nbytes,
+    return {"kernel": "k_ssim + k_ssim_g2 (csrc/ssim.hip, fen_ssim_ex: map + a/b/c, then the gradient)",
+            "us": round(us, 2), "bytes": nbytes,
             "achieved_GBs": round(nbytes / us / 1e3, 1), "peak_GBs": 8000.0,
             "frac": round(nbytes / us / 1e3 / 8000.0, 4), "bound": "hbm"}
 

@@ -62,7 +62,7 @@ template <bool GRAD, typename T, int CB>
 __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const float* __restrict__ pred,
                                               const float* __restrict__ target, const SsimWin win, float C1,
                                               float C2, float* __restrict__ part, void* __restrict__ grad,
-                                              float grad_scale, int grad_mode) {
+                                              float grad_scale, int grad_mode, float* __restrict__ maps) {
     constexpr int E1 = GRAD ? ST + 2 * SR : ST;   // where the map (and a, b, c) is needed
     constexpr int E2 = E1 + 2 * SR;               // where the inputs are needed
     constexpr int O1 = GRAD ? SR : 0;             // tile offset inside E1
@@ -193,6 +193,13 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
                 abc[0][r][c] = in ? 2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (r1 - r2) : 0.f;
                 abc[1][r][c] = in ? -S * r2 : 0.f;
                 abc[2][r][c] = in ? 2.f * A1 * iB : 0.f;
+            } else if (maps && in) {
+                // the two-launch form's first half: the same a, b, c of the tile's own pixels
+                // to the maps (k_ssim_g2 filters them over the tile + halo)
+                const size_t np = (size_t)B * C * H * W, e = (size_t)plane * H * W + (size_t)gy * W + gx;
+                maps[e] = 2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (r1 - r2);
+                maps[np + e] = -S * r2;
+                maps[2 * np + e] = 2.f * A1 * iB;
             }
         }
     }
@@ -296,6 +303,145 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     }
 }
 
+// The two-launch form's second half (grad_mode 2, C <= CB): per 32x32 tile, every channel in
+// turn, a / b / c of the tile + 5 px read back from the maps written by k_ssim<false> (zero
+// outside the image, as the fused kernel's), then the fused kernel's gradient passes unchanged
+// (horizontal a, b packed + c; vertical; d = G*a + 2 p G*b + t G*c) and the NHWC16 read-modify-
+// write of channels 0..3 once per pixel.  The split trades 75 MB of fp32 maps (write + read) for
+// the fused kernel's 10-px input halo: its map passes ran on 52 x 42 and 42 x 42 per 32 x 32
+// tile (2.1x and 1.7x the tile), here on 42 x 32 and 32 x 32 -- the kernel was VALU-bound.
+template <typename T, int CB>
+__global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, const float* __restrict__ pred,
+                                                 const float* __restrict__ target, const SsimWin win,
+                                                 const float* __restrict__ maps, void* __restrict__ grad,
+                                                 float grad_scale) {
+    constexpr int E1 = ST + 2 * SR;                   // 42: the maps on the tile + halo
+    constexpr int CW2 = 8, NCH2 = ST / CW2;
+    constexpr int RV = 4, NRV = ST / RV;
+    static_assert(ST * NRV == 256, "one vertical item per thread");
+    __shared__ float abc[3][E1][E1 + 1];
+    __shared__ float hp[3][E1][ST + 1];
+    __shared__ float dg[CB][ST][ST + 1];
+    const int tid = threadIdx.x;
+    const int h0 = blockIdx.y * ST, w0 = blockIdx.x * ST;
+    const int b = blockIdx.z;
+    const size_t np = (size_t)B * C * H * W;
+    constexpr int NLD = (E1 * E1 + 255) / 256;        // 7
+    float la[NLD], lb[NLD], lc[NLD];
+    auto load_maps = [&](int ch) {
+        const size_t pl = (size_t)(b * C + ch) * H * W;
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int i = tid + k * 256;
+            const int r = i / E1, c = i % E1, gy = h0 - SR + r, gx = w0 - SR + c;
+            const bool in = i < E1 * E1 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+            const size_t e = in ? pl + (size_t)gy * W + gx : 0;
+            const float va = maps[e], vb = maps[np + e], vc = maps[2 * np + e];
+            la[k] = in ? va : 0.f;
+            lb[k] = in ? vb : 0.f;
+            lc[k] = in ? vc : 0.f;
+        }
+    };
+    typedef typename std::conditional<sizeof(T) == 2, uint2, float4>::type GV;
+    GV gv[4];
+    auto grad_ptr = [&](int k) -> GV* {
+        const int pix = tid + 256 * k, gy = h0 + pix / ST, gx = w0 + pix % ST;
+        return (gy < H && gx < W) ? (GV*)((T*)grad + (((size_t)b * H + gy) * W + gx) * 16) : nullptr;
+    };
+    load_maps(0);
+#pragma unroll
+    for (int cc = 0; cc < CB; ++cc) {
+        if (cc >= C) break;
+        const float* pp = pred + (size_t)(b * C + cc) * H * W;
+        const float* tp = target + (size_t)(b * C + cc) * H * W;
+        if (cc > 0) __syncthreads();                  // the previous channel's reads of abc / hp done
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int i = tid + k * 256;
+            if (i < E1 * E1) {
+                const int r = i / E1, c = i % E1;
+                abc[0][r][c] = la[k];
+                abc[1][r][c] = lb[k];
+                abc[2][r][c] = lc[k];
+            }
+        }
+        __syncthreads();
+        if (cc + 1 < CB && cc + 1 < C) load_maps(cc + 1);
+        if (cc + 1 == CB || cc + 1 == C) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const GV* q = grad_ptr(k);
+                if (q) gv[k] = *q;
+            }
+        }
+        for (int i = tid; i < E1 * NCH2; i += 256) {          // horizontal pass of a, b (packed) and c
+            const int r = i / NCH2, c0 = (i % NCH2) * CW2;
+            f32x2 vab[CW2 + 2 * SR];
+            float vc[CW2 + 2 * SR];
+#pragma unroll
+            for (int q = 0; q < CW2 + 2 * SR; ++q) vab[q] = f32x2{abc[0][r][c0 + q], abc[1][r][c0 + q]}, vc[q] = abc[2][r][c0 + q];
+#pragma unroll
+            for (int c = 0; c < CW2; ++c) {
+                f32x2 sab = {0.f, 0.f};
+                float sc = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2 * SR + 1; ++j) {
+                    sab = pfma(f32x2{win.g[j], win.g[j]}, vab[c + j], sab);
+                    sc = fmaf(win.g[j], vc[c + j], sc);
+                }
+                hp[0][r][c0 + c] = sab.x;
+                hp[1][r][c0 + c] = sab.y;
+                hp[2][r][c0 + c] = sc;
+            }
+        }
+        __syncthreads();
+        {                                                     // vertical pass + the gradient
+            const int c = tid % ST, r0 = (tid / ST) * RV, gx = w0 + c;
+            float pr[RV], tr[RV];
+#pragma unroll
+            for (int o = 0; o < RV; ++o) {
+                const int gy = min(h0 + r0 + o, H - 1);
+                const bool in = gx < W;
+                pr[o] = in ? pp[(size_t)gy * W + gx] : 0.f;
+                tr[o] = in ? tp[(size_t)gy * W + gx] : 0.f;
+            }
+            f32x2 mab[RV];
+            float mc[RV];
+#pragma unroll
+            for (int o = 0; o < RV; ++o) mab[o] = f32x2{0.f, 0.f}, mc[o] = 0.f;
+#pragma unroll
+            for (int rr = 0; rr < RV + 2 * SR; ++rr) {
+                const f32x2 vab = {hp[0][r0 + rr][c], hp[1][r0 + rr][c]};
+                const float vc = hp[2][r0 + rr][c];
+#pragma unroll
+                for (int o = 0; o < RV; ++o) {
+                    const int j = rr - o;
+                    if (j >= 0 && j <= 2 * SR) {
+                        mab[o] = pfma(f32x2{win.g[j], win.g[j]}, vab, mab[o]);
+                        mc[o] = fmaf(win.g[j], vc, mc[o]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < RV; ++o)
+                dg[cc][r0 + o][c] = grad_scale * (mab[o].x + 2.f * pr[o] * mab[o].y + tr[o] * mc[o]);
+        }
+    }
+    __syncthreads();                                          // every channel's dg tile written
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        GV* q = grad_ptr(k);
+        if (!q) continue;
+        const int pix = tid + 256 * k, r = pix / ST, c = pix % ST;
+        GV u = gv[k];
+        T* v = (T*)&u;
+#pragma unroll
+        for (int kk = 0; kk < CB && kk < 4; ++kk)
+            if (kk < C) v[kk] = fromf<T>(tof<T>(v[kk]) + dg[kk][r][c]);
+        *q = u;
+    }
+}
+
 }  // namespace
 
 #define STREAM ((hipStream_t)stream)
@@ -316,26 +462,54 @@ extern "C" int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred
     const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);      // CB: channels looped in the block
     if (grad_mode == 0) {
         hipLaunchKernelGGL((k_ssim<false, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
-                           part, nullptr, 0.f, 0);
+                           part, nullptr, 0.f, 0, nullptr);
     } else if (grad_mode == 1) {
         hipLaunchKernelGGL((k_ssim<true, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
-                           part, grad, grad_scale, grad_mode);
+                           part, grad, grad_scale, grad_mode, nullptr);
     } else if (C <= 3 && (dtype == FEN_F32 || dtype == FEN_BF16)) {
         if (dtype == FEN_F32)
             hipLaunchKernelGGL((k_ssim<true, float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
-                               C2, part, grad, grad_scale, grad_mode);
+                               C2, part, grad, grad_scale, grad_mode, nullptr);
         else
             hipLaunchKernelGGL((k_ssim<true, bf16, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
-                               C2, part, grad, grad_scale, grad_mode);
+                               C2, part, grad, grad_scale, grad_mode, nullptr);
     } else if (dtype == FEN_F32) {
         hipLaunchKernelGGL((k_ssim<true, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
-                           part, grad, grad_scale, grad_mode);
+                           part, grad, grad_scale, grad_mode, nullptr);
     } else if (dtype == FEN_BF16) {
         hipLaunchKernelGGL((k_ssim<true, bf16, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
-                           part, grad, grad_scale, grad_mode);
+                           part, grad, grad_scale, grad_mode, nullptr);
     } else {
         return FEN_EINVAL;
     }
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" size_t fen_ssim_work_floats(int B, int C, int H, int W) { return (size_t)3 * B * C * H * W; }
+
+extern "C" int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* pred, const float* target,
+                           const float* window1d, int window_size, float C1, float C2, float* part, void* grad,
+                           float grad_scale, int grad_mode, float* work, void* stream) {
+    const bool two = work && grad_mode == 2 && C <= 3 && (dtype == FEN_F32 || dtype == FEN_BF16);
+    if (!two)
+        return fen_ssim(dtype, B, C, H, W, pred, target, window1d, window_size, C1, C2, part, grad, grad_scale,
+                        grad_mode, stream);
+    if (!pred || !target || !window1d || !part || !grad || B <= 0 || H <= 0 || W <= 0) return FEN_EINVAL;
+    if (window_size != 2 * SR + 1) return FEN_EUNSUPPORTED;
+    SsimWin w;
+    for (int j = 0; j < 2 * SR + 1; ++j) w.g[j] = window1d[j];
+    const dim3 grid((W + ST - 1) / ST, (H + ST - 1) / ST, B * C);
+    const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);
+    // first half: the map, its tile sums and a / b / c (the fused kernel's non-gradient geometry)
+    hipLaunchKernelGGL((k_ssim<false, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
+                       part, nullptr, 0.f, 0, work);
+    if (dtype == FEN_F32)
+        hipLaunchKernelGGL((k_ssim_g2<float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work, grad,
+                           grad_scale);
+    else
+        hipLaunchKernelGGL((k_ssim_g2<bf16, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work, grad,
+                           grad_scale);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

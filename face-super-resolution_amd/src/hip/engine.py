@@ -170,8 +170,12 @@ class FENEngine:
         part = ctx.scratch("ssim_part", (rows * B,), torch.float32)
         per = ctx.scratch("ssim_img", (B,), torch.float32)
         n = B * C * H * W
-        ctx.emit("ssim", ctx.lib.fen_ssim, ctx.code, B, C, H, W, ptr(self.out), ptr(self.hr), ptr(self.ssim_win), 11,
-                 0.01 ** 2, 0.03 ** 2, ptr(part), ptr(self.saved_tail["dout"]), -self.ssim_weight / (n * self.world * self.accum), 2)
+        # two launches (the map + its gradient coefficients a, b, c to a workspace, then their
+        # filtering into dL/dsr): fen_ssim_ex, equal results to the one-launch fen_ssim
+        work = ctx.scratch("ssim_work", (int(ctx.lib.fen_ssim_work_floats(B, C, H, W)),), torch.float32)
+        ctx.emit("ssim", ctx.lib.fen_ssim_ex, ctx.code, B, C, H, W, ptr(self.out), ptr(self.hr), ptr(self.ssim_win), 11,
+                 0.01 ** 2, 0.03 ** 2, ptr(part), ptr(self.saved_tail["dout"]), -self.ssim_weight / (n * self.world * self.accum), 2,
+                 ptr(work))
         ctx.emit("ssim_img", ctx.lib.fen_colsum, rows, B, ptr(part), 1.0 / (C * H * W), ptr(per), 0)
         ctx.emit("ssim_mean", ctx.lib.fen_colsum, B, 1, ptr(per), 1.0 / B, ptr(self.ssim_val), 0)
 

@@ -184,6 +184,9 @@ _SIGS = {
     "fen_feat_loss_parts": (c_int, []),
     "fen_feat_loss": (c_int, [c_int, c_size_t, c_void_p, c_int, c_float, c_void_p, c_int, c_void_p, c_void_p]),
     "fen_ssim_parts": (c_size_t, [c_int] * 4),
+    "fen_ssim_work_floats": (c_size_t, [c_int] * 4),
+    "fen_ssim_ex": (c_int, [c_int] * 5 + [c_void_p] * 3 + [c_int, c_float, c_float, c_void_p, c_void_p, c_float, c_int,
+                                                          c_void_p, c_void_p]),
     "fen_ssim": (c_int, [c_int] * 5 + [c_void_p] * 3 + [c_int, c_float, c_float, c_void_p, c_void_p, c_float, c_int,
                                                         c_void_p]),
     "fen_augment_u8": (c_int, [c_int, c_int] + [c_void_p] * 5),

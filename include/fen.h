@@ -557,6 +557,14 @@ size_t fen_ssim_parts(int B, int C, int H, int W);
 int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred, const float* target, const float* window1d,
              int window_size, float C1, float C2, float* part, void* grad, float grad_scale, int grad_mode,
              void* stream);
+/* The same with a workspace of fen_ssim_work_floats() floats: grad_mode 2 (C <= 3, fp32 / bf16
+ * gradient buffer) runs as two launches -- the map, its tile sums and the per-pixel gradient
+ * coefficients a, b, c to the workspace, then their Gaussian filtering into the gradient --
+ * with results equal to the one-launch form's; any other case (or work = NULL) is fen_ssim. */
+size_t fen_ssim_work_floats(int B, int C, int H, int W);
+int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* pred, const float* target,
+                const float* window1d, int window_size, float C1, float C2, float* part, void* grad,
+                float grad_scale, int grad_mode, float* work, void* stream);
 
 /* ---- HR batch preparation (src/data/transforms.py:173-279 + to_tensor 260-279) ----
  * src_u8: B uint8 HWC crops [B,P,P,3] (RGB, P even); params: B records {int flip, int

@@ -77,6 +77,36 @@ def test_ssim_grad_accumulates_into_nhwc16(dtype):
     assert bool((buf[..., C:].float().cpu() == base_q).all())
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,H,W", [(2, 3, 40, 36), (3, 3, 256, 256), (1, 1, 64, 96)])
+def test_ssim_two_launch_matches_fused(dtype, B, C, H, W):
+    """fen_ssim_ex with a workspace (grad_mode 2: the map + a / b / c maps, then their filtering
+    into the gradient) against the one-launch fen_ssim on the same buffers: the gradient
+    bit-identical (same per-pixel operation order), the tile sums to fp32 summation order."""
+    from src.hip import lib as L
+    from src.hip.program import ptr
+    from src.losses.ssim import _window1d
+    torch.manual_seed(9)
+    p = torch.rand(B, C, H, W, device=DEV)
+    t = (p + 0.1 * torch.randn(B, C, H, W, device=DEV)).clamp(0, 1)
+    lib = L.load()
+    rows = lib.fen_ssim_parts(B, C, H, W)
+    win = _window1d(11, 1.5).to(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    out = []
+    for two in (False, True):
+        buf = torch.full((B, H, W, 16), 3e-4, device=DEV, dtype=dtype)
+        part = torch.empty(rows * B, device=DEV)
+        work = torch.empty(lib.fen_ssim_work_floats(B, C, H, W), device=DEV) if two else None
+        L.check(lib.fen_ssim_ex(L.dtype_code(dtype), B, C, H, W, ptr(p), ptr(t), ptr(win), 11, 1e-4, 9e-4,
+                                ptr(part), ptr(buf), -0.2 / (B * C * H * W), 2, ptr(work) if two else None, s),
+                "ssim_ex")
+        torch.cuda.synchronize()
+        out.append((buf.clone(), part.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.allclose(out[0][1], out[1][1], rtol=1e-5, atol=1e-3)
+
+
 def test_engine_step_with_ssim_fp32(golden):
     """FENEngine(ssim_weight=0.2) fp32: generator grads of L1 + 0.2 (1 - SSIM) vs oracle autograd."""
     from src.hip.engine import FENEngine
