@@ -213,7 +213,11 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
     // trip per tile instead of one per (m, n) -- a load under the per-pixel branch with its use
     // right behind it waited for each in turn
     typedef typename std::conditional<sizeof(T) == 2, uint2, uint4>::type RawV;
+#ifndef EPI_NOPF
     const bool pin = epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT);
+#else   // A/B only: the operands loaded per fragment in pass 1
+    const bool pin = false;
+#endif
     RawV pvr[MT][NT];
     if (pin) {
 #pragma unroll
@@ -257,7 +261,11 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                     // post_in (every slope of the group > 0): the PReLU output has the
                     // pre-activation's sign; the slope partials are rescaled by 1 / alpha below
                     float pv[4];
+#ifndef EPI_NOPF
                     ld4<T>(&pvr[m][n], pv);
+#else
+                    ld4<T>((const char*)(rec4[m] ? d.post_in : d.pre_in) + oi * sizeof(T), pv);
+#endif
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         psum[m][r] += prelu_dalpha_f(v[r], pv[r]);
@@ -266,7 +274,11 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                 }
                 if (epi & FEN_EPI_DOT) {
                     float pv[4];
+#ifndef EPI_NOPF
                     ld4<T>(&pvr[m][n], pv);
+#else
+                    ld4<T>((const char*)d.pre_in + oi * sizeof(T), pv);
+#endif
 #pragma unroll
                     for (int r = 0; r < 4; ++r) psum[m][r] += rnd16<T>(v[r]) * pv[r];
                 }

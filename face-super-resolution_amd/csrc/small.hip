@@ -829,7 +829,11 @@ __global__ __launch_bounds__(256, 2) void k_cl_bwd(int B, int H, int W, int Co, 
     // writes (32 lanes of one ds_write_b32: 8 channel rows 8 apart x 4 pixel pairs) then fall on
     // 16 banks instead of 4 (every row of a channel group hit the same one: 8-way); the reads
     // (16 B at r % 8 == 0, 8 B at r % 4 == 0) stay inside one chunk
+#ifndef CLB_NOSWZ
     auto pt = [&](int c, int r) { return PT + c * TS + (((r >> 3) ^ ((c >> 3) & 7)) << 3) + (r & 7); };
+#else   // A/B only: the unswizzled layout
+    auto pt = [&](int c, int r) { return PT + c * TS + r; };
+#endif
     const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lq = lane >> 4;
     const int wave = wave_id();
     const int twn = W >> 4, tpi = twn * (H >> 4), ntiles = B * tpi;

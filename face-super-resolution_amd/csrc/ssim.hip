@@ -68,6 +68,9 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     constexpr int O1 = GRAD ? SR : 0;             // tile offset inside E1
     constexpr int CW = GRAD ? 7 : 8;              // register block of the map passes (E1 = 6 or 4 of them)
     constexpr int NCH = E1 / CW;
+    // the vertical pass's row block: without GRAD, 4 rows (32 x 8 = 256 items, one per thread;
+    // 8 rows left half the block idle)
+    constexpr int CWV = GRAD ? CW : 4, NCHV = E1 / CWV;
     constexpr int CW2 = 8, NCH2 = ST / CW2;       // horizontal gradient pass: 8-column chunks
     constexpr int RV = 4, NRV = ST / RV;          // vertical gradient pass: 4-row chunks (ST * NRV = 256 items)
     constexpr int PS = E2 + 1;
@@ -152,19 +155,19 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     // vertical pass: thread = (column, CW-row chunk), the chunk's CW + 10 rows read once; the
     // (mp, mt) and (E[p^2], E[t^2]) sums packed
     float acc = 0.f;
-    for (int i = tid; i < E1 * NCH; i += 256) {
-        const int c = i % E1, r0 = (i / E1) * CW;
-        f32x2 m01[CW], m23[CW];
-        float m4[CW];
+    for (int i = tid; i < E1 * NCHV; i += 256) {
+        const int c = i % E1, r0 = (i / E1) * CWV;
+        f32x2 m01[CWV], m23[CWV];
+        float m4[CWV];
 #pragma unroll
-        for (int o = 0; o < CW; ++o) m01[o] = m23[o] = f32x2{0.f, 0.f}, m4[o] = 0.f;
+        for (int o = 0; o < CWV; ++o) m01[o] = m23[o] = f32x2{0.f, 0.f}, m4[o] = 0.f;
 #pragma unroll
-        for (int rr = 0; rr < CW + 2 * SR; ++rr) {
+        for (int rr = 0; rr < CWV + 2 * SR; ++rr) {
             const f32x2 v01 = {hp[0][r0 + rr][c], hp[1][r0 + rr][c]};
             const f32x2 v23 = {hp[2][r0 + rr][c], hp[3][r0 + rr][c]};
             const float v4 = hp[4][r0 + rr][c];
 #pragma unroll
-            for (int o = 0; o < CW; ++o) {
+            for (int o = 0; o < CWV; ++o) {
                 const int j = rr - o;
                 if (j >= 0 && j <= 2 * SR) {
                     const f32x2 g2 = {win.g[j], win.g[j]};
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
             }
         }
 #pragma unroll
-        for (int o = 0; o < CW; ++o) {
+        for (int o = 0; o < CWV; ++o) {
             const int r = r0 + o;
             const float mp = m01[o].x, mt = m01[o].y;
             const float spp = m23[o].x - mp * mp, stt = m23[o].y - mt * mt, spt = m4[o] - mp * mt;
