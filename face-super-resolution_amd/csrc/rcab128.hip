@@ -173,8 +173,37 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
         // ---------------- the input image ----------------
         if constexpr (COMB) {
             // x_j = x_{j-1} + rs * s * t_{j-1} over the tile + halo: x and t chunks in flight while
-            // the gate is computed
+            // the gate is computed.  The gate's operands (the image's tile sums, FC1, FC2) are
+            // loaded FIRST: vmcnt retires in issue order, so gate operands issued behind the
+            // 26 x / t chunks made the gate wait for the whole 198-KB staging before it could
+            // start; issued ahead, the gate's reductions and FCs run while the staging lands
             constexpr int KU = (NUNIT + 511) / 512;   // 13
+            const bool newimg = b != prev_b;
+            // the gate's operands -- the image's tile sums (tpi x 512 B), FC1 and FC2 (Cr x 512 B
+            // each) -- by LDS-DMA into the image area (free: the previous tile ended on a barrier),
+            // ahead of the x / t chunks; the gate reads them from there
+            const int sums_b = tpi * CC * 4, fc_b = A.Cr * CC * 4;
+            const bool gate_lds = sums_b + 2 * fc_b <= IMG;
+            const int c = tid & (CC - 1), g = tid >> 7;
+            const int k1 = tid >> 4, j8 = (tid & 15) * 8;
+            // FC2 lane layout: channel c2 = tid >> 2, hidden units k8 .. k8 + 7 (a quad per channel)
+            const int c2 = tid >> 2, k8 = (tid & 3) * 8;
+            if (newimg && gate_lds) {
+                const i32x4 pr = make_rsrc(A.pp + (size_t)b * tpi * CC, (unsigned)sums_b);
+                const i32x4 f1 = make_rsrc(A.pfc1, (unsigned)fc_b);
+                const i32x4 f2 = make_rsrc(A.pfc2, (unsigned)fc_b);
+                const int n0 = (sums_b + 1023) / 1024, n1 = (fc_b + 1023) / 1024;
+                for (int piece = wave; piece < n0 + 2 * n1; piece += 8) {
+                    int ll = lane;
+                    asm volatile("" : "+v"(ll));
+                    const bool s_ = piece < n0, a_ = !s_ && piece < n0 + n1;
+                    const int loc = s_ ? piece : a_ ? piece - n0 : piece - n0 - n1;
+                    char* dst = img + (s_ ? 0 : a_ ? sums_b : sums_b + fc_b) + loc * 1024;
+                    dma16(s_ ? pr : a_ ? f1 : f2, __builtin_amdgcn_readfirstlane(lds_addr(dst)), (loc * 64 + ll) * 16);
+                }
+            }
+            // the x / t chunks are the last KU * 2 vector-memory ops before the gate's wait
+            asm volatile("" ::: "memory");
             const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, (int)act_bytes, 0x00020000);
             const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc((void*)A.tp, 0, (int)act_bytes, 0x00020000);
             uint4 xv[KU], tv[KU];
@@ -190,34 +219,50 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
                 xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)offs[k], 0, 0));
                 tv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trs, (int)offs[k], 0, 0));
             }
-            if (b != prev_b) {
+            asm volatile("" ::: "memory");
+            if (newimg) {
                 // the gate of image b (blocks.py:83-92): mean of t_{j-1} from its tile sums (fixed
                 // order: tiles g, g + 4, ... per quarter, quarters in order), FC1 -> ReLU -> FC2 ->
-                // sigmoid.  Every operand load is issued before the first reduction.
-                const int c = tid & (CC - 1), g = tid >> 7;
-                const int k1 = tid >> 4, j8 = (tid & 15) * 8;
-                // FC2 lane layout: channel c2 = tid >> 2, hidden units k8 .. k8 + 7 (a quad per channel)
-                const int c2 = tid >> 2, k8 = (tid & 3) * 8;
+                // sigmoid.  Waits for the gate operands only: the 2 KU x / t chunks stay in flight
                 float w1[8], w2[8];
                 {
-                    const float* w1p = A.pfc1 + (size_t)(k1 < A.Cr ? k1 : 0) * CC + j8;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) w1[e] = k1 < A.Cr ? w1p[e] : 0.f;
-                    const float* w2p = A.pfc2 + (size_t)c2 * A.Cr;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) w2[e] = k8 + e < A.Cr ? w2p[k8 + e] : 0.f;
-                }
-                {
-                    const float* pb = A.pp + (size_t)b * tpi * CC + c;
                     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-                    int k = g;
-                    for (; k + 12 < tpi; k += 16) {
-                        s0 += pb[(size_t)k * CC];
-                        s1 += pb[(size_t)(k + 4) * CC];
-                        s2 += pb[(size_t)(k + 8) * CC];
-                        s3 += pb[(size_t)(k + 12) * CC];
+                    if (gate_lds) {
+                        asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+                        static_assert(2 * KU == 26, "the wait above counts the x / t chunks");
+                        __syncthreads();                     // every wave's pieces landed
+                        const float* pb = (const float*)img + c;
+                        int k = g;
+                        for (; k + 12 < tpi; k += 16) {
+                            s0 += pb[k * CC];
+                            s1 += pb[(k + 4) * CC];
+                            s2 += pb[(k + 8) * CC];
+                            s3 += pb[(k + 12) * CC];
+                        }
+                        for (; k < tpi; k += 4) s0 += pb[k * CC];
+                        const float* w1p = (const float*)(img + sums_b) + (size_t)(k1 < A.Cr ? k1 : 0) * CC + j8;
+                        const float* w2p = (const float*)(img + sums_b + fc_b) + (size_t)c2 * A.Cr;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) w1[e] = k1 < A.Cr ? w1p[e] : 0.f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) w2[e] = k8 + e < A.Cr ? w2p[k8 + e] : 0.f;
+                    } else {
+                        const float* pb = A.pp + (size_t)b * tpi * CC + c;
+                        int k = g;
+                        for (; k + 12 < tpi; k += 16) {
+                            s0 += pb[(size_t)k * CC];
+                            s1 += pb[(size_t)(k + 4) * CC];
+                            s2 += pb[(size_t)(k + 8) * CC];
+                            s3 += pb[(size_t)(k + 12) * CC];
+                        }
+                        for (; k < tpi; k += 4) s0 += pb[(size_t)k * CC];
+                        const float* w1p = A.pfc1 + (size_t)(k1 < A.Cr ? k1 : 0) * CC + j8;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) w1[e] = k1 < A.Cr ? w1p[e] : 0.f;
+                        const float* w2p = A.pfc2 + (size_t)c2 * A.Cr;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) w2[e] = k8 + e < A.Cr ? w2p[k8 + e] : 0.f;
                     }
-                    for (; k < tpi; k += 4) s0 += pb[(size_t)k * CC];
                     red[g * CC + c] = (s0 + s1) + (s2 + s3);
                 }
                 __syncthreads();
