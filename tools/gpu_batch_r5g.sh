@@ -11,3 +11,19 @@ for rep in 1 2 3; do
     echo "$(echo $l | sed 's|.*/||')   $(tail -1 gpurun_out/st.log)"
   done
 done
+# per-launch durations of the stress forward (the three upsampler stages apart)
+STEPS=2 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/stprof -o st --output-format csv -- python tools/stress_step.py > gpurun_out/stprof.log 2>&1
+echo "stress trace rc=$?"
+f=$(find gpurun_out/stprof -name '*kernel_trace.csv' | head -1)
+python - "$f" <<'PY'
+import csv, sys, collections
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r['Start_Timestamp']))
+last = collections.defaultdict(list)
+for r in rows:
+    n = r['Kernel_Name']
+    if 'rcab128' in n and 'Li4E' in n or 'conv3x3_s' in n or 'conv_first' in n:
+        last[n[:60]].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
+for k, v in last.items():
+    print(k, [round(x, 1) for x in v[-8:]])
+PY
