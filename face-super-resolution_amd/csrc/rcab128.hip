@@ -183,7 +183,11 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
             // each) -- by LDS-DMA into the image area (free: the previous tile ended on a barrier),
             // ahead of the x / t chunks; the gate reads them from there
             const int sums_b = tpi * CC * 4, fc_b = A.Cr * CC * 4;
+#ifndef C128_GATE_REG
             const bool gate_lds = sums_b + 2 * fc_b <= IMG;
+#else   // A/B only: the gate's operands through registers, issued behind the staging
+            const bool gate_lds = false;
+#endif
             const int c = tid & (CC - 1), g = tid >> 7;
             const int k1 = tid >> 4, j8 = (tid & 15) * 8;
             // FC2 lane layout: channel c2 = tid >> 2, hidden units k8 .. k8 + 7 (a quad per channel)

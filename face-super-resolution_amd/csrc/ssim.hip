@@ -463,7 +463,12 @@ extern "C" int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred
     for (int j = 0; j < 2 * SR + 1; ++j) w.g[j] = window1d[j];
     const dim3 grid((W + ST - 1) / ST, (H + ST - 1) / ST, B * C);
     const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);      // CB: channels looped in the block
-    if (grad_mode == 0) {
+    if (grad_mode == 0 && C <= 3) {
+        // one block per tile walks the channels, the next channel's inputs in flight under the
+        // current one's passes
+        hipLaunchKernelGGL((k_ssim<false, float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
+                           C2, part, nullptr, 0.f, 0, nullptr);
+    } else if (grad_mode == 0) {
         hipLaunchKernelGGL((k_ssim<false, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
                            part, nullptr, 0.f, 0, nullptr);
     } else if (grad_mode == 1) {
@@ -502,10 +507,10 @@ extern "C" int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* p
     if (window_size != 2 * SR + 1) return FEN_EUNSUPPORTED;
     SsimWin w;
     for (int j = 0; j < 2 * SR + 1; ++j) w.g[j] = window1d[j];
-    const dim3 grid((W + ST - 1) / ST, (H + ST - 1) / ST, B * C);
     const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);
-    // first half: the map, its tile sums and a / b / c (the fused kernel's non-gradient geometry)
-    hipLaunchKernelGGL((k_ssim<false, float, 1>), grid, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
+    // first half: the map, its tile sums and a / b / c (the fused kernel's non-gradient geometry),
+    // one block per tile over the channels with the next channel's inputs prefetched
+    hipLaunchKernelGGL((k_ssim<false, float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
                        part, nullptr, 0.f, 0, work);
     if (dtype == FEN_F32)
         hipLaunchKernelGGL((k_ssim_g2<float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work, grad,
