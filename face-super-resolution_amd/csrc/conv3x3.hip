@@ -976,7 +976,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
 #ifndef CONV_S_PFN
 #define CONV_S_PFN 11
 #endif
-template <typename T, int COT>
+template <typename T, int COT, int EPIC = -1>
 __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* halo = smem;
@@ -1172,7 +1172,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     else run_panel(npan - 1, std::false_type{});
     float* red = (float*)wbuf;     // LDS is free after the loop
     char* stage = (sizeof(T) == 2 && COT == 64) ? halo : nullptr;
-    conv_epilogue<T, COT, 4, 1>(d, acc, b, tb, h0, w0, co0, stage, red, ec);
+    conv_epilogue<T, COT, 4, 1, EPIC>(d, acc, b, tb, h0, w0, co0, stage, red, ec);
 }
 
 int g_num_cus = 0;
@@ -1242,7 +1242,7 @@ int launch_g(const fen_conv_desc* d, hipStream_t s) {
     return FEN_OK;
 }
 
-template <typename T, int COT>
+template <typename T, int COT, int EPIC = -1>
 int launch_s(const fen_conv_desc* d, hipStream_t s) {
     const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
     const int coutp = (d->Cout + 15) & ~15;
@@ -1250,10 +1250,11 @@ int launch_s(const fen_conv_desc* d, hipStream_t s) {
     const size_t lds = HALO_BYTES + 3 * COT * 128;   // > 64 KB at COT = 64: opt in once
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_conv3x3_s<T, COT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_s<T, COT, EPIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_conv3x3_s<T, COT>), grid, dim3(256), lds, s, *d);
+    hipLaunchKernelGGL((k_conv3x3_s<T, COT, EPIC>), grid, dim3(256), lds, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }
@@ -1324,6 +1325,17 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
                     default: return launch_p<T, 64, 4, 2, -1>(d, s);
                 }
             }
+        }
+        if constexpr (H16) {
+            // the upsampler dgrads (Cin = 4C): their epilogue modes as compile-time constants (no
+            // residual loads or other modes' code in the epilogue's register budget)
+#ifndef CONV_S_GENERIC   // A/B only: every streamed conv on the runtime-mode epilogue
+            if (!d->res[0] && !d->res[1] && !d->res[2] && !s2d) {
+                if (epi == (FEN_EPI_PRELU_BWD | FEN_EPI_UNSHUFFLE))
+                    return launch_s<T, 64, FEN_EPI_PRELU_BWD | FEN_EPI_UNSHUFFLE>(d, s);
+                if (epi == 0) return launch_s<T, 64, 0>(d, s);
+            }
+#endif
         }
         return launch_s<T, 64>(d, s);
     }

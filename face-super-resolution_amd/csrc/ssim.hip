@@ -369,6 +369,17 @@ __global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, con
             }
         }
         __syncthreads();
+        // this channel's pred / target at the thread's 4 output pixels, for the gradient formula
+        // after the passes (not L2-hot here, unlike the fused kernel's: issued now, under them)
+        const int vc_ = tid % ST, vr0 = (tid / ST) * RV, vgx = w0 + vc_;
+        float pr[RV], tr[RV];
+#pragma unroll
+        for (int o = 0; o < RV; ++o) {
+            const int gy = min(h0 + vr0 + o, H - 1);
+            const size_t e = vgx < W ? (size_t)gy * W + vgx : 0;
+            pr[o] = pp[e];
+            tr[o] = tp[e];
+        }
         if (cc + 1 < CB && cc + 1 < C) load_maps(cc + 1);
         if (cc + 1 == CB || cc + 1 == C) {
 #pragma unroll
@@ -399,15 +410,7 @@ __global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, con
         }
         __syncthreads();
         {                                                     // vertical pass + the gradient
-            const int c = tid % ST, r0 = (tid / ST) * RV, gx = w0 + c;
-            float pr[RV], tr[RV];
-#pragma unroll
-            for (int o = 0; o < RV; ++o) {
-                const int gy = min(h0 + r0 + o, H - 1);
-                const bool in = gx < W;
-                pr[o] = in ? pp[(size_t)gy * W + gx] : 0.f;
-                tr[o] = in ? tp[(size_t)gy * W + gx] : 0.f;
-            }
+            const int c = vc_, r0 = vr0;
             f32x2 mab[RV];
             float mc[RV];
 #pragma unroll
