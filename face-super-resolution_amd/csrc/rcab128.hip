@@ -182,9 +182,11 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
             // the gate's operands -- the image's tile sums (tpi x 512 B), FC1 and FC2 (Cr x 512 B
             // each) -- by LDS-DMA into the image area (free: the previous tile ended on a barrier),
             // ahead of the x / t chunks; the gate reads them from there
+            // regions 1-KB aligned: a DMA piece writes whole KB (zeros past a region's end)
             const int sums_b = tpi * CC * 4, fc_b = A.Cr * CC * 4;
+            const int o_w1 = (sums_b + 1023) & ~1023, o_w2 = o_w1 + ((fc_b + 1023) & ~1023);
 #ifndef C128_GATE_REG
-            const bool gate_lds = sums_b + 2 * fc_b <= IMG;
+            const bool gate_lds = o_w2 + ((fc_b + 1023) & ~1023) <= IMG;
 #else   // A/B only: the gate's operands through registers, issued behind the staging
             const bool gate_lds = false;
 #endif
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
                     asm volatile("" : "+v"(ll));
                     const bool s_ = piece < n0, a_ = !s_ && piece < n0 + n1;
                     const int loc = s_ ? piece : a_ ? piece - n0 : piece - n0 - n1;
-                    char* dst = img + (s_ ? 0 : a_ ? sums_b : sums_b + fc_b) + loc * 1024;
+                    char* dst = img + (s_ ? 0 : a_ ? o_w1 : o_w2) + loc * 1024;
                     dma16(s_ ? pr : a_ ? f1 : f2, __builtin_amdgcn_readfirstlane(lds_addr(dst)), (loc * 64 + ll) * 16);
                 }
             }
@@ -244,8 +246,8 @@ __global__ __launch_bounds__(512, 1) void k_rcab128(const K128 A) {
                             s3 += pb[(k + 12) * CC];
                         }
                         for (; k < tpi; k += 4) s0 += pb[k * CC];
-                        const float* w1p = (const float*)(img + sums_b) + (size_t)(k1 < A.Cr ? k1 : 0) * CC + j8;
-                        const float* w2p = (const float*)(img + sums_b + fc_b) + (size_t)c2 * A.Cr;
+                        const float* w1p = (const float*)(img + o_w1) + (size_t)(k1 < A.Cr ? k1 : 0) * CC + j8;
+                        const float* w2p = (const float*)(img + o_w2) + (size_t)c2 * A.Cr;
 #pragma unroll
                         for (int e = 0; e < 8; ++e) w1[e] = k1 < A.Cr ? w1p[e] : 0.f;
 #pragma unroll
