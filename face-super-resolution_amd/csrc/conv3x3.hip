@@ -441,41 +441,6 @@ __device__ __forceinline__ void conv_tap(f32x4 (&acc)[MT][NT], const char* wt, c
     }
 }
 
-// conv_tap with its reads in flight under MFMAs (the streamed kernel's every-tap pipeline): the
-// caller holds B = this tap's k-half-0 halo fragments; k-half 1's A and B are read during k-half
-// 0's MFMAs, and the next tap's k-half-0 halo fragments (the halo is constant within a panel;
-// ntap < 0: none) during k-half 1's, returned in B.  Only the weight fragments wait on the
-// step's barrier (the ring slot was written in the previous step).
-template <typename T, int MT, int NT>
-__device__ __forceinline__ void conv_tap_pipe(f32x4 (&acc)[MT][NT], const char* wt, const char* halo, int tap,
-                                              int ntap, int wr, int q, int c16, uint4 (&B)[NT]) {
-    const int kh = tap / 3, kw = tap - kh * 3;
-    uint4 A0[MT], A1[MT], B1[NT];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) A0[m] = *(const uint4*)(wt + swz(m * 16 + c16, q));
-    {
-        const char* hb = halo + hcol(c16 + kw, 4 + q);
-#pragma unroll
-        for (int m = 0; m < MT; ++m) A1[m] = *(const uint4*)(wt + swz(m * 16 + c16, 4 + q));
-#pragma unroll
-        for (int n = 0; n < NT; ++n) B1[n] = *(const uint4*)(hb + (wr * NT + n + kh) * (HALO * 128));
-    }
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A0[m], B[n]);
-    if (ntap >= 0) {
-        const int nkh = ntap / 3, nkw = ntap - nkh * 3;
-        const char* hb = halo + hcol(c16 + nkw, q);
-#pragma unroll
-        for (int n = 0; n < NT; ++n) B[n] = *(const uint4*)(hb + (wr * NT + n + nkh) * (HALO * 128));
-    }
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A1[m], B1[n]);
-}
-
 // All 9 taps x 2 k-halves of one tile from an LDS-resident filter, software-pipelined:
 // the fragments of step s+1 are read while the MFMAs of step s run (two register sets).
 // per_tap(tap) runs once per tap between the MFMA groups (the next tile's halo DMA).
@@ -1167,16 +1132,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
             *(uint4*)(dst + swz(i >> 3, i & 7)) = ok ? w[j] : make_uint4(0, 0, 0, 0);
         }
     };
-    uint4 bf[4];                                  // conv_tap_pipe's carried halo fragments
     auto fast_panel = [&](int pn, auto NEXT) {
         constexpr bool next = decltype(NEXT)::value;
-#ifdef CONV_S_PIPE
-        {   // tap 0's k-half-0 halo fragments (the panel's halo is in LDS: the caller's barrier)
-            const char* hb = halo + hcol(c16, q);
-#pragma unroll
-            for (int n = 0; n < 4; ++n) bf[n] = *(const uint4*)(hb + (wave * 4 + n) * (HALO * 128));
-        }
-#endif
 #pragma unroll
         for (int it = 0; it < 9; ++it) {
             if (it + 2 < 9) ldw(pn, it + 2, w2[it & 1]);
@@ -1186,11 +1143,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
                 for (int j = 0; j < CONV_S_PFN; ++j)
                     if (j * 9 / CONV_S_PFN == it) halo_load(pn + 1, j);
             }
-#ifdef CONV_S_PIPE
-            conv_tap_pipe<T, MT, 4>(acc, wbuf + (it % 3) * COT * 128, halo, it, it < 8 ? it + 1 : -1, wave, q, c16, bf);
-#else
             conv_tap<T, MT, 4>(acc, wbuf + (it % 3) * COT * 128, halo, it, wave, 0, q, c16);
-#endif
             if (it < 8 || next) stw(w2[(it + 1) & 1], wbuf + ((it + 1) % 3) * COT * 128, it < 8 ? pn : pn + 1);
             __syncthreads();
         }
