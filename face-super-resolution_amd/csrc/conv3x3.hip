@@ -860,13 +860,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                     }
                 }
             }
-#ifdef G_NOWAIT
-            // A/B: without operand loads (no residual, no pre_in) the epilogue need not wait for
-            // the halo DMA just issued; the phase-end wait covers it
-            if constexpr (NRES > 0 || PIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
             if (ret) {
                 float psum[MT][4];
 #pragma unroll
