@@ -88,6 +88,10 @@ static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignmen
 #define GS_VMCNT_SAVES(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #endif
 
+#ifndef GS_SAVE_AUX
+#define GS_SAVE_AUX 0
+#endif
+
 // workspace: control words, counters, pool partials, boundary rows
 struct Ws {
     size_t cnt, flg, part, bx, bt, ba, bo, stamp, total;
@@ -329,16 +333,18 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
             for (int mp = 0; mp < 2; ++mp) {
                 const uint4 u = pair16(v[2 * mp][p], v[2 * mp + 1][p]);
                 const int off = lb + p * 2048 + mp * 64;
-                if (aux) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 16);
+                if (aux == 16) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 16);
+                else if (aux == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 2);
                 else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 0);
             }
     };
-    // training: the wave's row of a saved activation (plain stores; the backward reads it)
+    // training: the wave's row of a saved activation (the backward reads it ~ms later);
+    // GS_SAVE_AUX: the stores' cache-policy bits (A/B: 2 = non-temporal)
     auto save_row = [&](void* base, const uint2 (&v)[4][4]) {
         void* bp = base;
         asm volatile("" : "+s"(bp));
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, 0, (int)act_bytes, 0x00020000);
-        store_row(rs, (int)((size_t)(im * H + r0 + wave) * SW * 128), v, 0);
+        store_row(rs, (int)((size_t)(im * H + r0 + wave) * SW * 128), v, GS_SAVE_AUX);
     };
     // a boundary row (16-B chunks, lane handles chunks lane + 64 k) -> LDS image row lrow
     auto halo_to_lds = [&](int lrow, const uint4 (&v)[8]) {
