@@ -88,8 +88,11 @@ static_assert(O_FILT % 16 == 0 && O_RED % 16 == 0 && O_GATE % 16 == 0, "alignmen
 #define GS_VMCNT_SAVES(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #endif
 
+// the training saves' cache-policy bits: non-temporal (the backward reads them ~ms later; plain
+// stores allocated them in L2 / MALL beside the hand-off rows and filter taps): stage-1 step
+// 5.349 / 5.374 / 5.375 vs 5.445 / 5.462 / 5.442 ms (same box)
 #ifndef GS_SAVE_AUX
-#define GS_SAVE_AUX 0
+#define GS_SAVE_AUX 2
 #endif
 
 // workspace: control words, counters, pool partials, boundary rows
@@ -338,8 +341,8 @@ __global__ __launch_bounds__(512, 1) void k_group_strip(const GsArgs A) {
                 else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 0);
             }
     };
-    // training: the wave's row of a saved activation (the backward reads it ~ms later);
-    // GS_SAVE_AUX: the stores' cache-policy bits (A/B: 2 = non-temporal)
+    // training: the wave's row of a saved activation (the backward reads it ~ms later), stored
+    // non-temporal (GS_SAVE_AUX)
     auto save_row = [&](void* base, const uint2 (&v)[4][4]) {
         void* bp = base;
         asm volatile("" : "+s"(bp));

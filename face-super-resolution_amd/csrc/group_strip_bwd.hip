@@ -25,6 +25,13 @@
 // format where the per-RCAB backward (fen_rcab_bwd + fen_se_bwd_fused) rounds them.  The SE
 // backward's sums run over strips (not 16x16 tiles), so results match that path to rounding,
 // not bit for bit.
+// cache-policy bits of the saved-operand loads (t, z1 / a1: read once here); A/B: 2 = non-temporal
+#ifndef GSB_LOAD_AUX
+#define GSB_LOAD_AUX 0
+#endif
+#ifndef GSB_SAVE_AUX
+#define GSB_SAVE_AUX 0
+#endif
 #include "strip_common.h"
 
 namespace {
@@ -206,7 +213,7 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int p = 0; p < 4; ++p)
-                v[m][p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, lb + p * 2048 + m * 32, 0, 0));
+                v[m][p] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, lb + p * 2048 + m * 32, 0, GSB_LOAD_AUX));
     };
     auto write_row_lds = [&](int lrow, const uint2 (&v)[4][4]) {
         int qq = q, cc = c16;
@@ -230,15 +237,18 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             for (int mp = 0; mp < 2; ++mp) {
                 const uint4 u = pair16(v[2 * mp][p], v[2 * mp + 1][p]);
                 const int off = lb + p * 2048 + mp * 64;
-                if (aux) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 16);
+                if (aux == 16) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 16);
+                else if (aux == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 2);
                 else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u), rs, off, 0, 0);
             }
     };
+    // dt / dz1 for the group's weight gradients (the next launch); GSB_SAVE_AUX: their stores'
+    // cache-policy bits (A/B: 2 = non-temporal)
     auto save_row = [&](void* base, const uint2 (&v)[4][4]) {
         void* bp = base;
         asm volatile("" : "+s"(bp));
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, 0, (int)act_bytes, 0x00020000);
-        store_row(rs, (int)((size_t)(im * H + r0 + wave) * SW * 128), v, 0);
+        store_row(rs, (int)((size_t)(im * H + r0 + wave) * SW * 128), v, GSB_SAVE_AUX);
     };
     auto halo_to_lds = [&](int lrow, const uint4 (&v)[8]) {
         int ll = lane;
