@@ -287,6 +287,19 @@ __device__ __forceinline__ void dma16(const i32x4& rsrc, unsigned lds_base, int 
         : "s"(lds_base), "v"(voff), "s"(rsrc)
         : "memory");
 }
+// the same with the non-temporal cache policy (operands read once: no L2 / MALL allocation)
+__device__ __forceinline__ void dma16_nt(const i32x4& rsrc, unsigned lds_base, int voff) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, 0 offen nt lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(lds_base), "v"(voff), "s"(rsrc)
+        : "memory");
+}
 // 4 B per lane (buffer_load_dword ... lds) written to lds_base + lane*4: gathers with
 // per-element addresses (border-clamped patches)
 __device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned lds_base, int voff) {

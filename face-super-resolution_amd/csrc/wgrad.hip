@@ -14,6 +14,13 @@
 // the reference OIHW layout.
 #include "fen_common.h"
 
+// the persistent wgrad's operand DMA (x halo, dy tile: read once per job); A/B: WG_LOAD_NT
+#ifdef WG_LOAD_NT
+#define WG_DMA dma16_nt
+#else
+#define WG_DMA dma16
+#endif
+
 namespace {
 
 constexpr int PANEL_HALO = HP * 128;   // 41472 B
@@ -328,9 +335,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_p(const fen_wgrad_desc d, cons
                 const int gh = h0 + (ppos[k] >> 16), gw = w0 + ((ppos[k] << 16) >> 16);
                 const bool in = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
                 if (i < HALO_DMA)
-                    dma16(xr, __builtin_amdgcn_readfirstlane(hbase + i * 1024), in ? xb + prel[k] : 0x7ffffff0);
+                    WG_DMA(xr, __builtin_amdgcn_readfirstlane(hbase + i * 1024), in ? xb + prel[k] : 0x7ffffff0);
                 else
-                    dma16(yr, __builtin_amdgcn_readfirstlane(ybase + (i - HALO_DMA) * 1024),
+                    WG_DMA(yr, __builtin_amdgcn_readfirstlane(ybase + (i - HALO_DMA) * 1024),
                           in ? yb + prel[k] : 0x7ffffff0);
             }
         }
