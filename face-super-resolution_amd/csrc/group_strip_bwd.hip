@@ -25,14 +25,15 @@
 // format where the per-RCAB backward (fen_rcab_bwd + fen_se_bwd_fused) rounds them.  The SE
 // backward's sums run over strips (not 16x16 tiles), so results match that path to rounding,
 // not bit for bit.
-// cache-policy bits of the saved-operand loads and of the dt / dz1 stores (2 = non-temporal);
-// non-temporal both: the saved operands (t, z1 / a1) are read once here, dt / dz1 once by the
-// weight gradients (stage-1 step 5.575-5.627 (loads) and 5.596-5.611 (stores) vs 5.639-5.659 ms)
+// cache-policy bits of the saved-operand loads and of the dt / dz1 stores (2 = non-temporal):
+// default policy both.  Each alone measured faster on one box (5.575-5.627 / 5.596-5.611 vs
+// 5.639-5.659 ms), but a 5-way factorial on another (batch m) put saves-nt-only at 5.758-5.770,
+// + nt stores 5.783-5.786, + nt loads 5.826-5.845, all three 5.928-5.938 ms: not adopted
 #ifndef GSB_LOAD_AUX
-#define GSB_LOAD_AUX 2
+#define GSB_LOAD_AUX 0
 #endif
 #ifndef GSB_SAVE_AUX
-#define GSB_SAVE_AUX 2
+#define GSB_SAVE_AUX 0
 #endif
 #include "strip_common.h"
 
