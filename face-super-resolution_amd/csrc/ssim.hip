@@ -16,6 +16,9 @@
 namespace {
 
 constexpr int SR = 5;       // window radius (window 11)
+#ifndef SSIM_G2_WAVES
+#define SSIM_G2_WAVES 4     // k_ssim_g2, 16-bit gradient: 4 waves per SIMD (<= 128 VGPRs, no spill; 38 KB of LDS)
+#endif
 constexpr int ST = 32;      // output tile
 struct SsimWin {
     float g[2 * SR + 1];
@@ -27,6 +30,12 @@ inline int nblk(size_t n, int t = 256) { return (int)((n + t - 1) / t); }
 // its chunk in registers and reads each LDS element once.  Packed fp32 (v_pk_fma_f32): the
 // (p, t) and (p^2, t^2) sums two at a time, p t alone -- 3 FMA instructions per tap, not 5.
 __device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// G*a + 2 p G*b + t G*c with the contraction spelled out: the fused kernel and k_ssim_g2 round
+// it identically whatever the surrounding code lets the compiler fuse
+__device__ __forceinline__ float ssim_dcomb(f32x2 mab, float mc, float p, float t) {
+    return __builtin_fmaf(t, mc, __builtin_fmaf(2.f * p, mab.y, mab.x));
+}
 
 template <int CW>
 __device__ __forceinline__ void hrow(const SsimWin& win, const float* p, const float* t, float (&o)[5][CW]) {
@@ -258,7 +267,8 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
             }
 #pragma unroll
             for (int o = 0; o < RV; ++o) {
-                const float d = grad_scale * (mab[o].x + 2.f * pr[o] * mab[o].y + tr[o] * mc[o]);
+                float d = grad_scale * ssim_dcomb(mab[o], mc[o], pr[o], tr[o]);
+                asm volatile("" : "+v"(d));                 // rounded as in k_ssim_g2
                 const int gy = h0 + r0 + o;
                 if constexpr (LDSG) {
                     dg[cc][r0 + o][c] = d;
@@ -314,7 +324,7 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
 // the fused kernel's 10-px input halo: its map passes ran on 52 x 42 and 42 x 42 per 32 x 32
 // tile (2.1x and 1.7x the tile), here on 42 x 32 and 32 x 32 -- the kernel was VALU-bound.
 template <typename T, int CB>
-__global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, const float* __restrict__ pred,
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? SSIM_G2_WAVES : 3) void k_ssim_g2(int B, int C, int H, int W, const float* __restrict__ pred,
                                                  const float* __restrict__ target, const SsimWin win,
                                                  const float* __restrict__ maps, void* __restrict__ grad,
                                                  float grad_scale) {
@@ -322,9 +332,11 @@ __global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, con
     constexpr int CW2 = 8, NCH2 = ST / CW2;
     constexpr int RV = 4, NRV = ST / RV;
     static_assert(ST * NRV == 256, "one vertical item per thread");
+    // no gradient tile in LDS: each thread keeps its vertical item's pixels (4 rows of one column)
+    // of every channel in registers and read-modify-writes exactly those (38 KB of LDS: 4 blocks
+    // per CU, was 51 KB: 3)
     __shared__ float abc[3][E1][E1 + 1];
     __shared__ float hp[3][E1][ST + 1];
-    __shared__ float dg[CB][ST][ST + 1];
     const int tid = threadIdx.x;
     const int h0 = blockIdx.y * ST, w0 = blockIdx.x * ST;
     const int b = blockIdx.z;
@@ -346,10 +358,13 @@ __global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, con
         }
     };
     typedef typename std::conditional<sizeof(T) == 2, uint2, float4>::type GV;
-    GV gv[4];
-    auto grad_ptr = [&](int k) -> GV* {
-        const int pix = tid + 256 * k, gy = h0 + pix / ST, gx = w0 + pix % ST;
-        return (gy < H && gx < W) ? (GV*)((T*)grad + (((size_t)b * H + gy) * W + gx) * 16) : nullptr;
+    // the thread's vertical item: column vc_, rows vr0 .. vr0 + RV - 1 of the tile
+    const int vc_ = tid % ST, vr0 = (tid / ST) * RV, vgx = w0 + vc_;
+    GV gv[RV];
+    float dv[CB][RV];
+    auto grad_ptr = [&](int o) -> GV* {
+        const int gy = h0 + vr0 + o;
+        return (gy < H && vgx < W) ? (GV*)((T*)grad + (((size_t)b * H + gy) * W + vgx) * 16) : nullptr;
     };
     load_maps(0);
 #pragma unroll
@@ -369,9 +384,48 @@ __global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, con
             }
         }
         __syncthreads();
+#ifndef SSIM_G2_LATE_PF
+        if (cc + 1 < CB && cc + 1 < C) load_maps(cc + 1);
+#endif
+        if (cc + 1 == CB || cc + 1 == C) {
+#pragma unroll
+            for (int o = 0; o < RV; ++o) {
+                const GV* q = grad_ptr(o);
+                if (q) gv[o] = *q;
+            }
+        }
+        for (int i = tid; i < E1 * NCH2; i += 256) {          // horizontal pass of a, b (packed) and c
+            const int r = i / NCH2, c0 = (i % NCH2) * CW2;
+            // a, b (packed), then c: one operand row live at a time (register peak)
+            {
+                f32x2 vab[CW2 + 2 * SR];
+#pragma unroll
+                for (int q = 0; q < CW2 + 2 * SR; ++q) vab[q] = f32x2{abc[0][r][c0 + q], abc[1][r][c0 + q]};
+#pragma unroll
+                for (int c = 0; c < CW2; ++c) {
+                    f32x2 sab = {0.f, 0.f};
+#pragma unroll
+                    for (int j = 0; j < 2 * SR + 1; ++j) sab = pfma(f32x2{win.g[j], win.g[j]}, vab[c + j], sab);
+                    hp[0][r][c0 + c] = sab.x;
+                    hp[1][r][c0 + c] = sab.y;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                float vc[CW2 + 2 * SR];
+#pragma unroll
+                for (int q = 0; q < CW2 + 2 * SR; ++q) vc[q] = abc[2][r][c0 + q];
+#pragma unroll
+                for (int c = 0; c < CW2; ++c) {
+                    float sc = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 2 * SR + 1; ++j) sc = fmaf(win.g[j], vc[c + j], sc);
+                    hp[2][r][c0 + c] = sc;
+                }
+            }
+        }
         // this channel's pred / target at the thread's 4 output pixels, for the gradient formula
-        // after the passes (not L2-hot here, unlike the fused kernel's: issued now, under them)
-        const int vc_ = tid % ST, vr0 = (tid / ST) * RV, vgx = w0 + vc_;
+        // after the vertical pass (issued behind the horizontal pass: its registers are free)
         float pr[RV], tr[RV];
 #pragma unroll
         for (int o = 0; o < RV; ++o) {
@@ -380,34 +434,11 @@ __global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, con
             pr[o] = pp[e];
             tr[o] = tp[e];
         }
+#ifdef SSIM_G2_LATE_PF
+        // the next channel's maps issued after the horizontal pass (its registers free), in
+        // flight under the vertical pass
         if (cc + 1 < CB && cc + 1 < C) load_maps(cc + 1);
-        if (cc + 1 == CB || cc + 1 == C) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const GV* q = grad_ptr(k);
-                if (q) gv[k] = *q;
-            }
-        }
-        for (int i = tid; i < E1 * NCH2; i += 256) {          // horizontal pass of a, b (packed) and c
-            const int r = i / NCH2, c0 = (i % NCH2) * CW2;
-            f32x2 vab[CW2 + 2 * SR];
-            float vc[CW2 + 2 * SR];
-#pragma unroll
-            for (int q = 0; q < CW2 + 2 * SR; ++q) vab[q] = f32x2{abc[0][r][c0 + q], abc[1][r][c0 + q]}, vc[q] = abc[2][r][c0 + q];
-#pragma unroll
-            for (int c = 0; c < CW2; ++c) {
-                f32x2 sab = {0.f, 0.f};
-                float sc = 0.f;
-#pragma unroll
-                for (int j = 0; j < 2 * SR + 1; ++j) {
-                    sab = pfma(f32x2{win.g[j], win.g[j]}, vab[c + j], sab);
-                    sc = fmaf(win.g[j], vc[c + j], sc);
-                }
-                hp[0][r][c0 + c] = sab.x;
-                hp[1][r][c0 + c] = sab.y;
-                hp[2][r][c0 + c] = sc;
-            }
-        }
+#endif
         __syncthreads();
         {                                                     // vertical pass + the gradient
             const int c = vc_, r0 = vr0;
@@ -429,21 +460,26 @@ __global__ __launch_bounds__(256) void k_ssim_g2(int B, int C, int H, int W, con
                 }
             }
 #pragma unroll
-            for (int o = 0; o < RV; ++o)
-                dg[cc][r0 + o][c] = grad_scale * (mab[o].x + 2.f * pr[o] * mab[o].y + tr[o] * mc[o]);
+            for (int o = 0; o < RV; ++o) {
+                // the product rounded (opaque: not contracted into the final add, which the fused
+                // kernel's LDS round trip rounds apart)
+                float d = grad_scale * ssim_dcomb(mab[o], mc[o], pr[o], tr[o]);
+                asm volatile("" : "+v"(d));
+                dv[cc][o] = d;
+            }
         }
     }
-    __syncthreads();                                          // every channel's dg tile written
+    // channels 0..3 of each of the thread's pixels in one read-modify-write (channels >= C
+    // written back as read)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        GV* q = grad_ptr(k);
+    for (int o = 0; o < RV; ++o) {
+        GV* q = grad_ptr(o);
         if (!q) continue;
-        const int pix = tid + 256 * k, r = pix / ST, c = pix % ST;
-        GV u = gv[k];
+        GV u = gv[o];
         T* v = (T*)&u;
 #pragma unroll
         for (int kk = 0; kk < CB && kk < 4; ++kk)
-            if (kk < C) v[kk] = fromf<T>(tof<T>(v[kk]) + dg[kk][r][c]);
+            if (kk < C) v[kk] = fromf<T>(tof<T>(v[kk]) + dv[kk][o]);
         *q = u;
     }
 }

@@ -1,6 +1,7 @@
 """The stage-2 SSIM launch alone (fen_ssim, grad_mode 2: map + tile sums + gradient added to the
 NHWC16 bf16 dL/dsr), B=32, 3 x 256 x 256, REPS back-to-back launches, for rocprofv3 passes and
-A/B timing (HIP events, printed as us per launch)."""
+A/B timing (HIP events, printed as us per launch).  MODE=ex: fen_ssim_ex's two launches (the
+map kernel writing a / b / c to a workspace, then k_ssim_g2)."""
 import os
 import sys
 
@@ -21,9 +22,15 @@ win = _window1d(11, 1.5).cuda()
 part = torch.zeros(int(lib.fen_ssim_parts(B, C, H, W)) * B, device="cuda")
 grad = torch.zeros(B, H, W, 16, dtype=torch.bfloat16, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
+EX = os.environ.get("MODE", "") == "ex"
+work = torch.empty(int(lib.fen_ssim_work_floats(B, C, H, W)), device="cuda") if EX else None
 
 
 def launch():
+    if EX:
+        L.check(lib.fen_ssim_ex(1, B, C, H, W, pred.data_ptr(), target.data_ptr(), win.data_ptr(), 11, 1e-4, 9e-4,
+                                part.data_ptr(), grad.data_ptr(), -1e-6, 2, work.data_ptr(), s), "ssim_ex")
+        return
     L.check(lib.fen_ssim(1, B, C, H, W, pred.data_ptr(), target.data_ptr(), win.data_ptr(), 11, 1e-4, 9e-4,
                          part.data_ptr(), grad.data_ptr(), -1e-6, 2, s), "ssim")
 
