@@ -37,6 +37,8 @@
 #endif
 #include "strip_common.h"
 
+#include <type_traits>
+
 namespace {
 
 using namespace gs;
@@ -598,20 +600,30 @@ __global__ __launch_bounds__(512, 1) void k_group_strip_bwd(const GsbArgs A) {
             const int po = (int)(L.part + ((size_t)(im * 2 + par) * S) * 512) + ll * 8;   // this image's granules
             float asum = 0.f;
             bool got = false;
+            // the strips' granules swept 8 at a time (one round of 8 loads when S <= 8, two in
+            // order when S <= 16): 8 live granules on this wave's path instead of 16 (GSB_POLL16:
+            // all 16 loads in flight at once, strips past S re-reading strip 0)
+#ifndef GSB_POLL16
+            constexpr int NSW = 8;
+#else
+            constexpr int NSW = 16;
+#endif
             for (int it = 0; it < SPIN_MAX && ok; ++it) {
-                asm volatile("" ::: "memory");              // a fresh sc1 load per poll
-                uint2 gv[16];
-#pragma unroll
-                for (int s_ = 0; s_ < 16; ++s_)
-                    gv[s_] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
-                                                           wsr, po + (s_ < S ? s_ : 0) * 512, 0, 16));
                 unsigned bad = 0u;
-                float ms = 0.f;
+                float ms = 0.f;                             // in strip order
+                for (int s0 = 0; s0 < S; s0 += NSW) {
+                    asm volatile("" ::: "memory");          // a fresh sc1 load per poll
+                    uint2 gv[NSW];
 #pragma unroll
-                for (int s_ = 0; s_ < 16; ++s_) {
-                    const bool in = s_ < S;
-                    ms += in ? __uint_as_float(gv[s_].x) : 0.f;
-                    bad |= (unsigned)(in & (gv[s_].y != tg));
+                    for (int s_ = 0; s_ < NSW; ++s_)
+                        gv[s_] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                               wsr, po + (s0 + s_ < S ? s0 + s_ : 0) * 512, 0, 16));
+#pragma unroll
+                    for (int s_ = 0; s_ < NSW; ++s_) {
+                        const bool in = s0 + s_ < S;
+                        ms += in ? __uint_as_float(gv[s_].x) : 0.f;
+                        bad |= (unsigned)(in & (gv[s_].y != tg));
+                    }
                 }
                 asum = ms;
                 if (__all(bad == 0u)) {

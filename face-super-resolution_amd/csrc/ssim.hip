@@ -67,7 +67,10 @@ __device__ __forceinline__ void hrow(const SsimWin& win, const float* p, const f
 // per 8-B (16-bit) / 16-B (fp32) read-modify-write per pixel, every thread 4 pixels, the reads
 // issued before the last channel's passes; instead of C blocks each rewriting one 2-byte
 // channel of every pixel row.
-template <bool GRAD, typename T, int CB>
+// MT: the type of the two-launch form's a / b / c maps (k_ssim<false> writes them when `maps`
+// is given): fp16 for a 16-bit gradient (half the bytes of fp32; its 2^-11 relative rounding is
+// 8x below the bf16 rounding of the sum the gradient lands in), fp32 for an fp32 gradient
+template <bool GRAD, typename T, int CB, typename MT = float>
 __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const float* __restrict__ pred,
                                               const float* __restrict__ target, const SsimWin win, float C1,
                                               float C2, float* __restrict__ part, void* __restrict__ grad,
@@ -209,9 +212,10 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
                 // the two-launch form's first half: the same a, b, c of the tile's own pixels
                 // to the maps (k_ssim_g2 filters them over the tile + halo)
                 const size_t np = (size_t)B * C * H * W, e = (size_t)plane * H * W + (size_t)gy * W + gx;
-                maps[e] = 2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (r1 - r2);
-                maps[np + e] = -S * r2;
-                maps[2 * np + e] = 2.f * A1 * iB;
+                MT* mq = (MT*)maps;
+                mq[e] = (MT)(2.f * mt * (A2 - A1) * iB - 2.f * mp * S * (r1 - r2));
+                mq[np + e] = (MT)(-S * r2);
+                mq[2 * np + e] = (MT)(2.f * A1 * iB);
             }
         }
     }
@@ -320,8 +324,9 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
 // turn, a / b / c of the tile + 5 px read back from the maps written by k_ssim<false> (zero
 // outside the image, as the fused kernel's), then the fused kernel's gradient passes unchanged
 // (horizontal a, b packed + c; vertical; d = G*a + 2 p G*b + t G*c) and the NHWC16 read-modify-
-// write of channels 0..3 once per pixel.  The split trades 75 MB of fp32 maps (write + read) for
-// the fused kernel's 10-px input halo: its map passes ran on 52 x 42 and 42 x 42 per 32 x 32
+// write of channels 0..3 once per pixel.  The maps are fp16 for a 16-bit gradient (37.5 MB
+// written + read at B = 32, 3 x 256^2: the pair takes 103 us where fp32 maps took 115), fp32 for
+// an fp32 one.  The split trades them for the fused kernel's 10-px input halo: its map passes ran on 52 x 42 and 42 x 42 per 32 x 32
 // tile (2.1x and 1.7x the tile), here on 42 x 32 and 32 x 32 -- the kernel was VALU-bound.
 template <typename T, int CB>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? SSIM_G2_WAVES : 3) void k_ssim_g2(int B, int C, int H, int W, const float* __restrict__ pred,
@@ -341,6 +346,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? SSIM_G2_WAVES : 3) void k_ssi
     const int h0 = blockIdx.y * ST, w0 = blockIdx.x * ST;
     const int b = blockIdx.z;
     const size_t np = (size_t)B * C * H * W;
+    typedef typename std::conditional<sizeof(T) == 2, _Float16, float>::type MT;   // k_ssim<false, float, 3, MT>'s maps
     constexpr int NLD = (E1 * E1 + 255) / 256;        // 7
     float la[NLD], lb[NLD], lc[NLD];
     auto load_maps = [&](int ch) {
@@ -351,7 +357,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? SSIM_G2_WAVES : 3) void k_ssi
             const int r = i / E1, c = i % E1, gy = h0 - SR + r, gx = w0 - SR + c;
             const bool in = i < E1 * E1 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
             const size_t e = in ? pl + (size_t)gy * W + gx : 0;
-            const float va = maps[e], vb = maps[np + e], vc = maps[2 * np + e];
+            const MT* mq = (const MT*)maps;
+            const float va = (float)mq[e], vb = (float)mq[np + e], vc = (float)mq[2 * np + e];
             la[k] = in ? va : 0.f;
             lb[k] = in ? vb : 0.f;
             lc[k] = in ? vc : 0.f;
@@ -549,8 +556,12 @@ extern "C" int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* p
     const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);
     // first half: the map, its tile sums and a / b / c (the fused kernel's non-gradient geometry),
     // one block per tile over the channels with the next channel's inputs prefetched
-    hipLaunchKernelGGL((k_ssim<false, float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1, C2,
-                       part, nullptr, 0.f, 0, work);
+    if (dtype == FEN_F32)
+        hipLaunchKernelGGL((k_ssim<false, float, 3, float>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
+                           C2, part, nullptr, 0.f, 0, work);
+    else
+        hipLaunchKernelGGL((k_ssim<false, float, 3, _Float16>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w,
+                           C1, C2, part, nullptr, 0.f, 0, work);
     if (dtype == FEN_F32)
         hipLaunchKernelGGL((k_ssim_g2<float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work, grad,
                            grad_scale);

@@ -559,8 +559,9 @@ int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred, const flo
              void* stream);
 /* The same with a workspace of fen_ssim_work_floats() floats: grad_mode 2 (C <= 3, fp32 / bf16
  * gradient buffer) runs as two launches -- the map, its tile sums and the per-pixel gradient
- * coefficients a, b, c to the workspace, then their Gaussian filtering into the gradient --
- * with results equal to the one-launch form's; any other case (or work = NULL) is fen_ssim. */
+ * coefficients a, b, c to the workspace (fp32 for an fp32 gradient: results bit-identical to
+ * the one-launch form's; fp16 for a bf16 gradient: within one bf16 ulp of them), then their
+ * Gaussian filtering into the gradient; any other case (or work = NULL) is fen_ssim. */
 size_t fen_ssim_work_floats(int B, int C, int H, int W);
 int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* pred, const float* target,
                 const float* window1d, int window_size, float C1, float C2, float* part, void* grad,

@@ -81,8 +81,13 @@ def test_ssim_grad_accumulates_into_nhwc16(dtype):
 @pytest.mark.parametrize("B,C,H,W", [(2, 3, 40, 36), (3, 3, 256, 256), (1, 1, 64, 96)])
 def test_ssim_two_launch_matches_fused(dtype, B, C, H, W):
     """fen_ssim_ex with a workspace (grad_mode 2: the map + a / b / c maps, then their filtering
-    into the gradient) against the one-launch fen_ssim on the same buffers: the gradient
-    bit-identical (same per-pixel operation order), the tile sums to fp32 summation order."""
+    into the gradient) against the one-launch fen_ssim on the same buffers: the fp32 gradient
+    bit-identical (fp32 maps, same per-pixel operation order).  The bf16 one (fp16 maps: each of
+    G*a, 2p G*b, t G*c off by ~2^-11 of ITSELF, and they cancel where the gradient is small) per
+    element within one bf16 ulp of the fused result plus 2e-3 of the tensor's largest magnitude
+    (below the 2^-9 relative rounding that bf16 storage already puts on the largest elements),
+    checked on a zeroed buffer (the raw gradient) and on one holding 3e-4 (the accumulation);
+    the tile sums to fp32 summation order."""
     from src.hip import lib as L
     from src.hip.program import ptr
     from src.losses.ssim import _window1d
@@ -94,8 +99,8 @@ def test_ssim_two_launch_matches_fused(dtype, B, C, H, W):
     win = _window1d(11, 1.5).to(DEV)
     s = torch.cuda.current_stream().cuda_stream
     out = []
-    for two in (False, True):
-        buf = torch.full((B, H, W, 16), 3e-4, device=DEV, dtype=dtype)
+    for two, base in ((False, 3e-4), (True, 3e-4), (False, 0.0), (True, 0.0)):
+        buf = torch.full((B, H, W, 16), base, device=DEV, dtype=dtype)
         part = torch.empty(rows * B, device=DEV)
         work = torch.empty(lib.fen_ssim_work_floats(B, C, H, W), device=DEV) if two else None
         L.check(lib.fen_ssim_ex(L.dtype_code(dtype), B, C, H, W, ptr(p), ptr(t), ptr(win), 11, 1e-4, 9e-4,
@@ -103,11 +108,19 @@ def test_ssim_two_launch_matches_fused(dtype, B, C, H, W):
                 "ssim_ex")
         torch.cuda.synchronize()
         out.append((buf.clone(), part.clone()))
-    d = (out[0][0].float() - out[1][0].float()).abs()
-    bad = (d > 0).nonzero()
-    assert bad.numel() == 0, (f"{bad.shape[0]} gradient elements differ, max {d.max().item():.3e}; "
-                              f"first (b, y, x, ch): {bad[:8].tolist()}")
-    assert torch.allclose(out[0][1], out[1][1], rtol=1e-5, atol=1e-3)
+    for i in (0, 2):
+        ref, got = out[i][0].float(), out[i + 1][0].float()
+        d = (ref - got).abs()
+        if dtype == torch.float32:
+            allowed = torch.zeros_like(d)
+        else:   # one bf16 ulp of the larger magnitude: 2^(floor(log2 |x|) - 7)
+            mag = torch.maximum(ref.abs(), got.abs()).clamp_min(1e-30)
+            allowed = torch.exp2(torch.floor(torch.log2(mag)) - 7) + 2e-3 * float(ref.abs().max())
+        bad = (d > allowed).nonzero()
+        print(f"{dtype} base {i // 2}: max |diff| {d.max().item():.3e}, max |grad| {ref.abs().max().item():.3e}")
+        assert bad.numel() == 0, (f"{bad.shape[0]} gradient elements differ, max {d.max().item():.3e}; "
+                                  f"first (b, y, x, ch): {bad[:8].tolist()}")
+        assert torch.allclose(out[i][1], out[i + 1][1], rtol=1e-5, atol=1e-3)
 
 
 def test_engine_step_with_ssim_fp32(golden):
