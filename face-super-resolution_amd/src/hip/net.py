@@ -242,6 +242,12 @@ GROUP_STRIP_BWD = os.environ.get("FEN_GROUP_STRIP_BWD", "1") != "0"
 # stage's output (16-bit, 64 ch, whole 16x16 tiles, PRE_ELIDE); FEN_CL_BWD=0: the separate
 # weight-gradient pass + fen_conv_last_dgrad
 CL_BWD_FUSED = os.environ.get("FEN_CL_BWD", "1") != "0"
+# FEN_CS_SIDE=1 (A/B only): a recorded strip-backward group issues its PReLU / SE column sums on a
+# side stream, forked after the strip launch and joined before the group's end (its DP bucket
+# mark, the next group's strip launch), beside the group's batched weight gradients instead of
+# after them.  Measured slower: stage-1 step 5.603-5.623 vs 5.579-5.590 ms in line (the sums'
+# blocks slow the weight gradients they share the CUs with by more than the 10 us they hide)
+CS_SIDE = os.environ.get("FEN_CS_SIDE", "0") == "1"
 # test-only fault injection for the strip kernels' bounded waits (fen_group_strip_desc.fault):
 # bit 0 = the forward launches, bit 1 = the backward launches skip one hand-off flag in one
 # strip, so its neighbour's wait times out and the launch reports through the status word
@@ -304,14 +310,19 @@ class ColsumBatch:
         if len(self.jobs) == self.MAX:
             self.flush()
 
-    def flush(self) -> None:
+    def flush(self, stream=None) -> None:
+        """stream: a torch stream to launch on instead of the program's (recorded programs)."""
         if not self.jobs:
             return
         arr = (L.ColsumJob * len(self.jobs))()
         for i, (part, rows, cols, out, scale) in enumerate(self.jobs):
             arr[i].part, arr[i].out, arr[i].rows, arr[i].cols = ptr(part), ptr(out), rows, cols
             arr[i].scale, arr[i].accumulate = scale, 0
-        self.ctx.emit("colsum_multi", self.ctx.lib.fen_colsum_multi, len(self.jobs), ctypes.cast(arr, ctypes.c_void_p))
+        fn = self.ctx.lib.fen_colsum_multi
+        if stream is not None:
+            h, lib_fn = stream.cuda_stream, fn
+            fn = lambda n, a, _s: lib_fn(n, a, h)      # noqa: E731  (the op's stream argument ignored)
+        self.ctx.emit("colsum_multi", fn, len(self.jobs), ctypes.cast(arr, ctypes.c_void_p))
         self.ctx.keep(arr)
         self.jobs = []
 
@@ -741,6 +752,9 @@ class Backward:
     def __init__(self, spec: NetSpec, ctx: Ctx, Wt: Weights, G: Dict[str, torch.Tensor]):
         self.s, self.ctx, self.Wt, self.G = spec, ctx, Wt, G
         self.cs = ColsumBatch(ctx)   # flushed at the end of every group / the tail
+        # the side stream of the strip-backward groups' column sums (recorded programs only)
+        self.side = (torch.cuda.Stream(device=ctx.device) if (CS_SIDE and ctx.record and torch.cuda.is_available())
+                     else None)
         self.wb = WgradBatch(ctx)    # RCAB conv weight gradients; flushed with self.cs
         self._rc = 0                 # RCAB backward counter: rotates the dt / dz1 buffers
         # (partials, parts per image) of sum dy*t for the next rcab(), computed by the epilogue
@@ -907,20 +921,31 @@ class Backward:
         if size is not None:   # this group's weight gradients in one batch
             wb.flush()
             wb.size = WGRAD_STRIP_BATCH
-        wb.add(sv["x_last"], dy, B, H, W, C, C, G[pre + "conv.weight"], G[pre + "conv.bias"])
+        # the column sums read only the strip launch's partials: on the side stream (when
+        # recording, nothing else queued on self.cs) beside the weight gradients below
+        side = self.side if (self.side is not None and not self.cs.jobs) else None
         for b in reversed(range(s.NB)):
             q = f"{pre}blocks.{b}."
             ca = q + "channel_attention.fc."
-            blk, o = sv["blocks"][b], outs[b]
-            wb.add(blk["a1"], o["dt"], B, H, W, C, C, G[q + "conv2.weight"], G[q + "conv2.bias"])
-            wb.add(blk["x"], o["dz1"], B, H, W, C, C, G[q + "conv1.weight"], G[q + "conv1.bias"])
+            o = outs[b]
             self.cs.add(o["dal"], drows, C, G[q + "prelu.weight"])
             self.cs.add(o["dw1p"], B, s.Cr * C, G[ca + "0.weight"])
             self.cs.add(o["dw2p"], B, s.Cr * C, G[ca + "2.weight"])
+        if side is not None:
+            ctx.mark("cs_fork", lambda: side.wait_stream(torch.cuda.current_stream(ctx.device)))
+            self.cs.flush(stream=side)
+        wb.add(sv["x_last"], dy, B, H, W, C, C, G[pre + "conv.weight"], G[pre + "conv.bias"])
+        for b in reversed(range(s.NB)):
+            q = f"{pre}blocks.{b}."
+            blk, o = sv["blocks"][b], outs[b]
+            wb.add(blk["a1"], o["dt"], B, H, W, C, C, G[q + "conv2.weight"], G[q + "conv2.bias"])
+            wb.add(blk["x"], o["dz1"], B, H, W, C, C, G[q + "conv1.weight"], G[q + "conv1.bias"])
         wb.flush()
         if size is not None:
             wb.size = size
         self.flush()
+        if side is not None:   # the group's gradients complete on the compute stream from here
+            ctx.mark("cs_join", lambda: torch.cuda.current_stream(ctx.device).wait_stream(side))
         return dx
 
     def group(self, sv: dict, dy: torch.Tensor, g: int, extra_res: Sequence = (), dx_out=None,

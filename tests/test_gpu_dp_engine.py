@@ -124,8 +124,14 @@ def test_dp_marks_follow_bucket_writers(precision):
     base = eng.flat_g.data_ptr()
     spans = {t: (base + lo * el, base + hi * el) for t, lo, hi in eng.exchange.plan}
     marks, last_writer = {}, {t: -1 for t in spans}
+    forked = False                       # a strip-backward group's column sums on the side stream
     for i, (name, fn, args) in enumerate(eng.ctx.ops):
+        if fn is None and name in ("cs_fork", "cs_join"):
+            assert forked == (name == "cs_join"), (i, name)     # fork, join, fork, join ...
+            forked = name == "cs_fork"
+            continue
         if fn is None:
+            assert not forked, (i, name)                        # joined before any bucket's exchange
             assert name.startswith("allreduce_"), name
             tag = name[len("allreduce_"):]
             assert tag not in marks, tag
