@@ -88,8 +88,19 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
     constexpr int PS = E2 + 1;
     constexpr bool LDSG = GRAD && CB > 1;         // the gradient tiles kept in LDS
     // sb: p, t on E2 x E2; after the first pass, a / b / c on E1 x E1 (3 E1 (E1+1) <= 2 E2 PS)
-    __shared__ float sb[2 * E2 * PS];
-    __shared__ float hp[5][E2][E1 + 1];           // horizontal sums (reused for a, b, c)
+    // without GRAD the horizontal sums overwrite the staged inputs -- every item takes its input
+    // window into registers before a barrier, then writes its sums (one item per thread:
+    // E2 * NCH <= 256) -- 27.7 KB of LDS instead of 42 KB: with one channel per block (92 VGPRs)
+    // 5 blocks per CU, was 3 (SSIM_NO_ALIAS: separate arrays, A/B)
+#ifndef SSIM_NO_ALIAS
+    constexpr bool ALIAS = !GRAD;
+#else
+    constexpr bool ALIAS = false;
+#endif
+    constexpr int NSB = 2 * E2 * PS, NHP = 5 * E2 * (E1 + 1);
+    __shared__ float sbuf[ALIAS ? (NSB > NHP ? NSB : NHP) : NSB + NHP];
+    float* sb = sbuf;
+    float (*hp)[E2][E1 + 1] = (float (*)[E2][E1 + 1])(ALIAS ? sbuf : sbuf + NSB);   // horizontal sums (reused for a, b, c)
     __shared__ float dg[LDSG ? CB : 1][LDSG ? ST : 1][LDSG ? ST + 1 : 1];   // per channel d(sum S)/dp
     __shared__ float red[4];
     static_assert(3 * E1 * (E1 + 1) <= 2 * E2 * PS, "a/b/c alias");
@@ -154,14 +165,34 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
             if (q) gv[k] = *q;
         }
     }
-    for (int i = tid; i < E2 * NCH; i += 256) {
-        const int r = i / NCH, c0 = (i % NCH) * CW;
-        float o[5][CW];
-        hrow<CW>(win, sp + r * PS + c0, st + r * PS + c0, o);
+    if constexpr (ALIAS) {
+        static_assert(E2 * NCH <= 256, "one horizontal item per thread");
+        const int r = tid / NCH, c0 = (tid % NCH) * CW;
+        const bool item = tid < E2 * NCH;
+        float pw[CW + 2 * SR], tw[CW + 2 * SR];
+        if (item) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k)
+            for (int k = 0; k < CW + 2 * SR; ++k) pw[k] = sp[r * PS + c0 + k], tw[k] = st[r * PS + c0 + k];
+        }
+        __syncthreads();                                    // every window in registers: sb is hp's now
+        if (item) {
+            float o[5][CW];
+            hrow<CW>(win, pw, tw, o);
 #pragma unroll
-            for (int c = 0; c < CW; ++c) hp[k][r][c0 + c] = o[k][c];
+            for (int k = 0; k < 5; ++k)
+#pragma unroll
+                for (int c = 0; c < CW; ++c) hp[k][r][c0 + c] = o[k][c];
+        }
+    } else {
+        for (int i = tid; i < E2 * NCH; i += 256) {
+            const int r = i / NCH, c0 = (i % NCH) * CW;
+            float o[5][CW];
+            hrow<CW>(win, sp + r * PS + c0, st + r * PS + c0, o);
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+#pragma unroll
+                for (int c = 0; c < CW; ++c) hp[k][r][c0 + c] = o[k][c];
+        }
     }
     __syncthreads();
     // vertical pass: thread = (column, CW-row chunk), the chunk's CW + 10 rows read once; the
@@ -325,7 +356,7 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
 // outside the image, as the fused kernel's), then the fused kernel's gradient passes unchanged
 // (horizontal a, b packed + c; vertical; d = G*a + 2 p G*b + t G*c) and the NHWC16 read-modify-
 // write of channels 0..3 once per pixel.  The maps are fp16 for a 16-bit gradient (37.5 MB
-// written + read at B = 32, 3 x 256^2: the pair takes 103 us where fp32 maps took 115), fp32 for
+// written + read at B = 32, 3 x 256^2: the pair takes 97-98 us, 115 with fp32 maps), fp32 for
 // an fp32 one.  The split trades them for the fused kernel's 10-px input halo: its map passes ran on 52 x 42 and 42 x 42 per 32 x 32
 // tile (2.1x and 1.7x the tile), here on 42 x 32 and 32 x 32 -- the kernel was VALU-bound.
 template <typename T, int CB>
@@ -554,14 +585,23 @@ extern "C" int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* p
     SsimWin w;
     for (int j = 0; j < 2 * SR + 1; ++j) w.g[j] = window1d[j];
     const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);
-    // first half: the map, its tile sums and a / b / c (the fused kernel's non-gradient geometry),
-    // one block per tile over the channels with the next channel's inputs prefetched
+    // first half: the map, its tile sums and a / b / c (the fused kernel's non-gradient geometry)
+#ifdef SSIM_EX_CB3   // A/B: one block per tile over the channels (3 blocks per CU)
     if (dtype == FEN_F32)
         hipLaunchKernelGGL((k_ssim<false, float, 3, float>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
                            C2, part, nullptr, 0.f, 0, work);
     else
         hipLaunchKernelGGL((k_ssim<false, float, 3, _Float16>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w,
                            C1, C2, part, nullptr, 0.f, 0, work);
+#else   // one block per (tile, channel): 5 blocks per CU (97-98 us for the pair vs 102-104)
+    const dim3 gridc((W + ST - 1) / ST, (H + ST - 1) / ST, B * C);
+    if (dtype == FEN_F32)
+        hipLaunchKernelGGL((k_ssim<false, float, 1, float>), gridc, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
+                           C2, part, nullptr, 0.f, 0, work);
+    else
+        hipLaunchKernelGGL((k_ssim<false, float, 1, _Float16>), gridc, dim3(256), 0, STREAM, B, C, H, W, pred, target, w,
+                           C1, C2, part, nullptr, 0.f, 0, work);
+#endif
     if (dtype == FEN_F32)
         hipLaunchKernelGGL((k_ssim_g2<float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work, grad,
                            grad_scale);
