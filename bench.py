@@ -253,6 +253,78 @@ def conv_flop(cin, cout, h, w, k=3):
     return 2.0 * cin * cout * k * k * h * w
 
 
+# ---- algorithmic FLOPs of the training legs (every 3x3 conv counted as
+# 2 Cin Cout 9 Hout Wout; a data or weight gradient costs what its forward costs; SE, PReLU, BN,
+# pools, bicubic and the elementwise work are excluded) ----
+def gen_fwd_flop(hw=64, C=64, G=6, R=10, scale=4):
+    """One image through FaceEnhanceNet (custom.py:147-190): conv_first, G x (2R + 1) body
+    convs, conv_after_body, log2(scale) conv + PixelShuffle stages, conv_last."""
+    f = conv_flop(3, C, hw, hw) + (G * (2 * R + 1) + 1) * conv_flop(C, C, hw, hw)
+    s = hw
+    while s < hw * scale:
+        f += conv_flop(C, 4 * C, s, s)
+        s *= 2
+    return f + conv_flop(C, 3, s, s)
+
+
+def gen_train_flop(hw=64):
+    """forward + data gradients + weight gradients, less conv_first's data gradient (no gradient
+    flows to the LR input): 133.9 GFLOP per image at the bench shape."""
+    return 3.0 * gen_fwd_flop(hw) - conv_flop(3, 64, hw, hw)
+
+
+def vgg_flops(hr_hw=256, last="conv3_4"):
+    """VGG19 up to the feature layer (perceptual.py:13-169): (forward FLOPs per image, data-
+    gradient FLOPs per image of the pred half, conv1_1's included -- the gradient reaches sr)."""
+    from src.hip.vgg import LAYER_MAP, vgg19_convs
+    fwd = bwd = 0.0
+    s = hr_hw
+    for c in vgg19_convs():
+        if c["idx"] > LAYER_MAP[last]:
+            break
+        fwd += conv_flop(c["cin"], c["cout"], s, s)
+        bwd += conv_flop(c["cin"], c["cout"], s, s)
+        if c["pool_after"]:
+            s //= 2
+    return fwd, bwd
+
+
+def disc_flops(hw=256, bc=64):
+    """VGGStyleDiscriminator (discriminator.py:58-90) per image: (forward FLOPs, the first conv's
+    forward FLOPs); the stride-2 convs at their output resolution; the classifier's two GEMMs."""
+    cfg = [(3, bc, 1), (bc, bc, 2), (bc, 2 * bc, 1), (2 * bc, 2 * bc, 2), (2 * bc, 4 * bc, 1), (4 * bc, 4 * bc, 2),
+           (4 * bc, 8 * bc, 1), (8 * bc, 8 * bc, 2), (8 * bc, 8 * bc, 1), (8 * bc, 8 * bc, 2)]
+    f, s, first = 0.0, hw, None
+    for cin, cout, st in cfg:
+        s //= st
+        f += conv_flop(cin, cout, s, s)
+        first = first if first is not None else conv_flop(cin, cout, s, s)
+    f += 2.0 * 8 * bc * s * s * 1024 + 2.0 * 1024
+    return f, first
+
+
+def gan_iteration_flop(B=16, hw=64):
+    """One Trainer._gan_step (trainer.py:424-485, d_updates_per_g = 1): D step = G forward (no
+    grad) + D forward on real and fake + D backward of both (weight gradients, data gradients
+    but the first conv's); G step = G training pass + VGG19 conv3_4 perceptual (forward on
+    [sr; hr], backward on sr) + D forward on sr + D backward (weight and data gradients, the
+    first conv's data gradient included: it reaches sr)."""
+    g_fwd = gen_fwd_flop(hw)
+    d_fwd, d_first = disc_flops(4 * hw)
+    v_fwd, v_bwd = vgg_flops(4 * hw)
+    d_step = g_fwd + 2 * d_fwd + 2 * (2 * d_fwd - d_first)
+    g_step = gen_train_flop(hw) + 2 * v_fwd + v_bwd + d_fwd + 2 * d_fwd
+    return B * (d_step + g_step)
+
+
+def step_roofline(flop, ms, note):
+    """roofline object of a whole training step: algorithmic FLOPs / the step's wall time."""
+    tf = flop / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_BF16_TFLOPS, 4), "flop_per_step": flop, "traffic": None,
+            "basis": "whole step wall time (graph replay), " + note}
+
+
 def time_stress(steps=3, warmup=1, B=4, hw=128, precision="fp16"):
     """BASELINE configs[4]: the 128-ch / 10x20 RCAB x8 stress variant, inference, 128x128 ->
     1024x1024 (x8 from a 128 input), in its stated fp16; the body,
@@ -376,7 +448,11 @@ def time_gan_step(steps, B=16):
 
     el_e, _ = run(tr._gan_step)
     el, loss = run(tr._gan_iteration)
-    return {"metric": "training images/sec (stage-3 GAN iteration: D update + G update, L1 0.01 + perceptual 1 + "
+    flop = gan_iteration_flop(B)
+    return {"roofline": step_roofline(flop, 1000.0 * el / steps,
+                                      "algorithmic FLOPs of one iteration (bench.gan_iteration_flop: G fwd + D fwd x2 + "
+                                      "D bwd x2; G train + VGG19 conv3_4 fwd x2 + dgrad + D fwd + D bwd) at B=16"),
+            "metric": "training images/sec (stage-3 GAN iteration: D update + G update, L1 0.01 + perceptual 1 + "
                       "adversarial 0.005) at batch 16/GPU", "value": round(B * steps / el, 2),
             "ms_per_step": round(1000.0 * el / steps, 3), "steps": steps, "loss": loss,
             "path": ("Trainer iteration replayed from a captured hipGraph (capture_gan_step; module autograd "
@@ -408,6 +484,18 @@ def time_ssim(eng, reps=50):
             "us": round(us, 2), "bytes": nbytes,
             "achieved_GBs": round(nbytes / us / 1e3, 1), "peak_GBs": 8000.0,
             "frac": round(nbytes / us / 1e3 / 8000.0, 4), "bound": "hbm"}
+
+
+def exchange_label(backend, world):
+    """what carries a training leg's gradient all-reduce (src/training/dp.py)"""
+    if world <= 1:
+        return "none"
+    from src.training.dp import use_direct_rccl
+    if backend != "nccl":
+        return f"torch.distributed {backend}, per-group buckets, overlapped with backward"
+    path = ("RCCL called directly (fen_rccl_allreduce_bucket, include/fen.h)" if use_direct_rccl()
+            else "RCCL through torch.distributed (ProcessGroupNCCL)")
+    return path + ", per-group buckets on a side stream, overlapped with backward"
 
 
 def load_traffic(label):
@@ -528,8 +616,9 @@ def main():
         out["train"] = {"metric": "training images/sec (stage-1 L1 generator step) at batch 32/GPU",
                         "value": round(B * world * args.train_steps / tt, 2),
                         "ms_per_step": round(1000.0 * tt / args.train_steps, 3), "steps": args.train_steps,
-                        "loss": float(teng.loss), "path": tpath, "allreduce": (("RCCL (torch.distributed nccl backend)" if backend == "nccl" else backend)
-                                      + ", 8 buckets, overlapped with backward") if world > 1 else "none"}
+                        "loss": float(teng.loss), "path": tpath, "allreduce": exchange_label(backend, world),
+                        "roofline": step_roofline(B * gen_train_flop(), 1000.0 * tt / args.train_steps,
+                                                  "generator fwd + dgrad + wgrad (133.9 GFLOP/img) x B")}
         del teng
         torch.cuda.empty_cache()
         if not args.no_perceptual:
@@ -546,13 +635,17 @@ def main():
                              perceptual=spec)
             peng.hr.copy_(hr_t)
             fn, ppath = captured_or_eager(peng, world)
+            vf, vb = vgg_flops()
             tp = timed(fn, args.train_steps, 3, world)
             out["train_perceptual"] = {
                 "metric": "training images/sec (stage-1 step: L1 + VGG19 conv3_4 perceptual) at batch 32/GPU",
                 "value": round(B * world * args.train_steps / tp, 2),
                 "ms_per_step": round(1000.0 * tp / args.train_steps, 3), "steps": args.train_steps,
                 "loss": float(peng.total_loss()), "vgg": "random-init VGG19 (no ImageNet weights offline)",
-                "path": ppath}
+                "path": ppath, "allreduce": exchange_label(backend, world),
+                "roofline": step_roofline(B * (gen_train_flop() + 2 * vf + vb), 1000.0 * tp / args.train_steps,
+                                          "generator train (133.9 GFLOP/img) + VGG19 conv3_4 fwd on [sr; hr] + dgrad "
+                                          "on sr (%.1f GFLOP/img) x B" % ((2 * vf + vb) / 1e9))}
             del peng
             torch.cuda.empty_cache()
             # stage 2 (stage2_ssim_config.yaml:40-50): L1 x 1 + perceptual x 0.5 + (1 - SSIM) x 0.2
@@ -568,7 +661,9 @@ def main():
                 "metric": "training images/sec (stage-2 step: L1 + 0.5 perceptual + 0.2 (1 - SSIM)) at batch 32/GPU",
                 "value": round(B * world * args.train_steps / ts, 2),
                 "ms_per_step": round(1000.0 * ts / args.train_steps, 3), "steps": args.train_steps,
-                "loss": float(seng.total_loss()), "path": spath}
+                "loss": float(seng.total_loss()), "path": spath, "allreduce": exchange_label(backend, world),
+                "roofline": step_roofline(B * (gen_train_flop() + 2 * vf + vb), 1000.0 * ts / args.train_steps,
+                                          "as train_perceptual (SSIM is HBM-bound: aux.ssim_loss_grad)")}
             if world == 1:
                 out["aux"] = {"ssim_loss_grad": time_ssim(seng)}
             del seng
@@ -599,6 +694,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        from src.training.dp import RcclComm
+        RcclComm.destroy_all()
         dist.destroy_process_group()
 
 

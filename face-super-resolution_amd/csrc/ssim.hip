@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void k_ssim(int B, int C, int H, int W, const 
 // written + read at B = 32, 3 x 256^2: the pair takes 97-98 us, 115 with fp32 maps), fp32 for
 // an fp32 one.  The split trades them for the fused kernel's 10-px input halo: its map passes ran on 52 x 42 and 42 x 42 per 32 x 32
 // tile (2.1x and 1.7x the tile), here on 42 x 32 and 32 x 32 -- the kernel was VALU-bound.
-template <typename T, int CB>
+template <typename T, int CB, typename MT = typename std::conditional<sizeof(T) == 2, _Float16, float>::type>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? SSIM_G2_WAVES : 3) void k_ssim_g2(int B, int C, int H, int W, const float* __restrict__ pred,
                                                  const float* __restrict__ target, const SsimWin win,
                                                  const float* __restrict__ maps, void* __restrict__ grad,
@@ -377,7 +377,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? SSIM_G2_WAVES : 3) void k_ssi
     const int h0 = blockIdx.y * ST, w0 = blockIdx.x * ST;
     const int b = blockIdx.z;
     const size_t np = (size_t)B * C * H * W;
-    typedef typename std::conditional<sizeof(T) == 2, _Float16, float>::type MT;   // k_ssim<false, float, 3, MT>'s maps
     constexpr int NLD = (E1 * E1 + 255) / 256;        // 7
     float la[NLD], lb[NLD], lc[NLD];
     auto load_maps = [&](int ch) {
@@ -585,6 +584,12 @@ extern "C" int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* p
     SsimWin w;
     for (int j = 0; j < 2 * SR + 1; ++j) w.g[j] = window1d[j];
     const dim3 gridb((W + ST - 1) / ST, (H + ST - 1) / ST, B);
+    // fp16 maps for a bf16 gradient only where a, b, c stay far inside fp16's range: |c| <= 2/C2,
+    // |b| <= |S|/C2, |a| <= (2|mt| + 2|mp|)/C2 + 1/sqrt(C1) (B2 >= C2, A1 <= B1, |A2| <= B2); with
+    // pixel values in [-1.5, 2.5] that is <= 8/C2 + 1/sqrt(C1).  Smaller constants than that
+    // bound allows (the default C2 = 0.03^2 gives 8/C2 = 8.9e3) take fp32 maps: the same
+    // gradient, 115 instead of 98 us at the bench shape (fen.h, fen_ssim_ex)
+    const bool f16maps = dtype == FEN_BF16 && C1 > 0.f && C2 > 0.f && 8.f / C2 + 1.f / sqrtf(C1) <= 16384.f;
     // first half: the map, its tile sums and a / b / c (the fused kernel's non-gradient geometry)
 #ifdef SSIM_EX_CB3   // A/B: one block per tile over the channels (3 blocks per CU)
     if (dtype == FEN_F32)
@@ -595,7 +600,7 @@ extern "C" int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* p
                            C1, C2, part, nullptr, 0.f, 0, work);
 #else   // one block per (tile, channel): 5 blocks per CU (97-98 us for the pair vs 102-104)
     const dim3 gridc((W + ST - 1) / ST, (H + ST - 1) / ST, B * C);
-    if (dtype == FEN_F32)
+    if (!f16maps)
         hipLaunchKernelGGL((k_ssim<false, float, 1, float>), gridc, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, C1,
                            C2, part, nullptr, 0.f, 0, work);
     else
@@ -605,9 +610,12 @@ extern "C" int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* p
     if (dtype == FEN_F32)
         hipLaunchKernelGGL((k_ssim_g2<float, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work, grad,
                            grad_scale);
-    else
+    else if (f16maps)
         hipLaunchKernelGGL((k_ssim_g2<bf16, 3>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work, grad,
                            grad_scale);
+    else
+        hipLaunchKernelGGL((k_ssim_g2<bf16, 3, float>), gridb, dim3(256), 0, STREAM, B, C, H, W, pred, target, w, work,
+                           grad, grad_scale);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

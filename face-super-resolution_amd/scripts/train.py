@@ -196,6 +196,8 @@ def main(argv=None):
     except KeyboardInterrupt:
         trainer._save_checkpoint("interrupted.pth")
     if dist.is_initialized():
+        from src.training.dp import RcclComm
+        RcclComm.destroy_all()          # before the group whose ranks they span goes away
         dist.destroy_process_group()
 
 

@@ -22,7 +22,8 @@ Under torch.distributed every rank reads its own shard of the images -- files or
 indices alike -- with DistributedSampler's counts (`rank_shard`): train drops the remainder so
 every rank has n // world images (and, with drop_last batching, the same number of steps: a
 rank with one more step would pair its gradient all-reduce with another rank's end-of-epoch
-reduction), other modes pad by wrapping round to ceil(n / world).  Per-sample augmentation
+reduction); other modes take the exact disjoint split rank::world (validation metrics are
+reduced as sums and counts, so no image may be counted twice).  Per-sample augmentation
 draws are seeded by (seed, rank) so the ranks' draws are independent.
 """
 from __future__ import annotations
@@ -129,7 +130,11 @@ class SyntheticU8Images:
 def rank_shard(n: int, train: bool, rank: Optional[int] = None, world: Optional[int] = None):
     """This rank's item indices out of n, DistributedSampler-style (no shuffle: the loaders
     shuffle within the shard): indices rank, rank + world, ...; train keeps n // world of them
-    (equal step counts on every rank), other modes ceil(n / world), wrapping round.  Without
+    (equal step counts on every rank: a rank with one more step would pair its gradient
+    all-reduce with another rank's end-of-epoch reduction).  Other modes take the exact
+    disjoint split (rank::world): validation has no per-batch collective, its metrics are
+    reduced as sums and counts, so unequal shard lengths are fine and no image is counted
+    twice (the global val loss / PSNR / SSIM equal the one-rank values).  Without
     torch.distributed: all of range(n)."""
     if rank is None or world is None:
         if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
@@ -137,10 +142,12 @@ def rank_shard(n: int, train: bool, rank: Optional[int] = None, world: Optional[
         rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
     if world <= 1:
         return list(range(n))
-    m = n // world if train else -(-n // world)
+    if not train:
+        return list(range(rank, n, world))
+    m = n // world
     if m == 0:
         raise ValueError(f"{n} images cannot give each of {world} ranks one")
-    return [(rank + world * j) % n for j in range(m)]
+    return [rank + world * j for j in range(m)]
 
 
 def _rank() -> int:

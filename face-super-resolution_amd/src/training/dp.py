@@ -16,17 +16,23 @@ Callers pre-scale the loss gradient by 1/world, so SUM = the gradient of the glo
 mean loss, exactly the DDP semantics; clip and AdamW run after the join on every rank on
 identical data (`trainer.py:490-503` ordering).
 
-On the GPU the collectives are RCCL called directly through the C-ABI (`RcclComm`:
-`fen_rccl_allreduce_bucket`, include/fen.h): one ncclAllReduce per bucket on a side stream,
-no c10d Work object, no HIP events, no watchdog -- torch.distributed only carries the
-communicator's unique id.  That is what makes a capture of collectives issued from autograd's
-device thread (the module path's post-accumulate hooks) safe: ProcessGroupNCCL hands a work
-issued outside the capturing thread's view to its watchdog, whose event queries then fail
-with hipErrorCapturedEvent and abort the process (round 4).  `FEN_DP_COMM=torch`
-keeps the torch.distributed collectives (gloo always uses them).
+Two collective paths on the GPU, chosen by `FEN_DP_COMM`:
+- `rccl`: RCCL called directly through the C-ABI (`RcclComm`: `fen_rccl_allreduce_bucket`,
+  include/fen.h): one ncclAllReduce per bucket on a side stream, no c10d Work object, no HIP
+  events, no watchdog -- torch.distributed only carries the communicator's unique id.  That is
+  what makes a capture of collectives issued from autograd's device thread (the module path's
+  post-accumulate hooks) safe: ProcessGroupNCCL hands a work issued outside the capturing
+  thread's view to its watchdog, whose event queries then fail with hipErrorCapturedEvent and
+  abort the process (round 4).
+- `torch`: torch.distributed's collectives (ProcessGroupNCCL = RCCL; gloo always uses them).
+The default (`auto`) is the direct path on a one-rank communicator (what the one-GPU tests
+exercise) and torch's collectives at world size > 1: the direct path has not yet run with
+two or more GPUs, so a multi-GPU job takes the collective path torch itself validates until
+it has (`FEN_DP_COMM=rccl` opts in).
 """
 from __future__ import annotations
 
+import collections
 from typing import Iterable, List, Sequence, Tuple
 
 import torch
@@ -78,14 +84,20 @@ def _rccl_capture_ok(group=None) -> bool:
 
 
 def use_direct_rccl(group=None) -> bool:
-    """The exchange's collectives go through `RcclComm` (the C-ABI) unless FEN_DP_COMM=torch:
-    on CUDA with a process group whose backend is nccl (RCCL), or none (one rank)."""
+    """Whether the exchange's collectives go through `RcclComm` (the C-ABI): FEN_DP_COMM=rccl
+    on a process group whose backend is nccl (RCCL); FEN_DP_COMM=torch never; the default
+    (auto) only on a one-rank group or without one (see the module docstring)."""
     import os
-    if os.environ.get("FEN_DP_COMM", "rccl") == "torch":
+    mode = os.environ.get("FEN_DP_COMM", "auto")
+    if mode not in ("auto", "rccl", "torch"):
+        raise ValueError(f"FEN_DP_COMM={mode!r}: expected auto, rccl or torch")
+    if mode == "torch":
         return False
     if not (dist.is_available() and dist.is_initialized()):
         return True
-    return dist.get_backend(group) == "nccl"
+    if dist.get_backend(group) != "nccl":
+        return False
+    return mode == "rccl" or dist.get_world_size(group) == 1
 
 
 class RcclComm:
@@ -120,14 +132,26 @@ class RcclComm:
         self.handle = h.value
         self.library = lib.fen_rccl_library().decode()
 
+    @staticmethod
+    def _key(device: torch.device, group=None):
+        """(device, group, world, rank, backend): a communicator made before
+        init_process_group (one rank) or under a destroyed and re-created default group is
+        never handed to an exchange over a different set of ranks."""
+        dist_on = dist.is_available() and dist.is_initialized()
+        return (str(torch.device(device)), id(group),
+                dist.get_world_size(group) if dist_on else 1, dist.get_rank(group) if dist_on else 0,
+                str(dist.get_backend(group)) if dist_on else None)
+
     @classmethod
     def get(cls, device: torch.device, group=None) -> "RcclComm":
-        """One communicator per (device, group) for the process (the engines, the module-path
-        exchanges and the trainer share it)."""
-        key = (str(torch.device(device)), id(group))
+        """One communicator per (device, group, world, rank, backend) for the process (the
+        engines, the module-path exchanges and the trainer share it)."""
+        key = cls._key(device, group)
         c = cls._cache.get(key)
         if c is None:
             c = cls._cache[key] = cls(device, group)
+        if c.world != key[2] or c.rank != key[3]:
+            raise RuntimeError(f"RcclComm cache: communicator of world {c.world} rank {c.rank} under key {key}")
         return c
 
     def allreduce(self, t: torch.Tensor, stream: torch.cuda.Stream) -> None:
@@ -210,7 +234,8 @@ class BucketExchange:
         self.works: List = []
         self._forked = False
         self.base = None              # the stream launches fork from (default: the current one)
-        self.captured_launches: List[bool] = []   # per launch: was the fork inside a capture
+        # per launch: was the fork inside a capture (the last 256 launches; replays add none)
+        self.captured_launches = collections.deque(maxlen=256)
 
     def launch(self, tag: str) -> None:
         if not self.active:

@@ -315,12 +315,13 @@ class Trainer:
         return loss.detach()
 
     def _capture_gan(self) -> bool:
-        """Captured at any world size: with an exchange (N > 1, or the tests' forced one-rank
-        group) the module path's bucket all-reduces are direct RCCL calls (dp.RcclComm, the
-        C-ABI's fen_rccl_allreduce_bucket) that record into the graph from autograd's hook thread
-        like any kernel -- no ProcessGroupNCCL work, event or watchdog is involved (the round-4
-        watchdog abort).  FEN_DP_COMM=torch (torch's collectives) captures only
-        with FEN_GAN_CAPTURE_DP=1; gloo never captures."""
+        """Captured at world size 1, and with an exchange whose bucket all-reduces are direct
+        RCCL calls (dp.RcclComm, the C-ABI's fen_rccl_allreduce_bucket: the tests' forced one-rank
+        group, or N > 1 with FEN_DP_COMM=rccl) -- they record into the graph from autograd's hook
+        thread like any kernel, no ProcessGroupNCCL work, event or watchdog involved (the round-4
+        watchdog abort).  With torch's collectives (the default at N > 1 until the
+        direct path has run on two or more GPUs, dp.use_direct_rccl) the iteration runs eagerly
+        unless FEN_GAN_CAPTURE_DP=1; gloo never captures."""
         import os
         from .dp import _rccl_capture_ok, use_direct_rccl
         if not (bool(self.config.capture_gan_step) and torch.cuda.is_available() and self._accum() == 1):

@@ -561,7 +561,10 @@ int fen_ssim(int dtype, int B, int C, int H, int W, const float* pred, const flo
  * gradient buffer) runs as two launches -- the map, its tile sums and the per-pixel gradient
  * coefficients a, b, c to the workspace (fp32 for an fp32 gradient: results bit-identical to
  * the one-launch form's; fp16 for a bf16 gradient: within one bf16 ulp of them), then their
- * Gaussian filtering into the gradient; any other case (or work = NULL) is fen_ssim. */
+ * Gaussian filtering into the gradient; any other case (or work = NULL) is fen_ssim.  fp16
+ * coefficients only while they stay inside fp16's range: |a|, |b|, |c| <= 8/C2 + 1/sqrt(C1)
+ * for pixel values in [-1.5, 2.5], so a bf16 gradient takes fp32 coefficients when that
+ * exceeds 16384 (C2 below ~5e-4 -- the default (0.03)^2 = 9e-4 keeps fp16). */
 size_t fen_ssim_work_floats(int B, int C, int H, int W);
 int fen_ssim_ex(int dtype, int B, int C, int H, int W, const float* pred, const float* target,
                 const float* window1d, int window_size, float C1, float C2, float* part, void* grad,

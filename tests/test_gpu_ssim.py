@@ -150,3 +150,38 @@ def test_engine_step_with_ssim_fp32(golden):
         if not e <= 1e-4:
             bad[k] = e
     assert not bad, bad
+
+
+def test_ssim_two_launch_small_constants_bf16():
+    """fen_ssim_ex's fp16 a / b / c maps overflow for small C1 / C2 (|c| <= 2 / C2,
+    |a| up to ~8 / C2 + 1 / sqrt(C1)); below the bound in fen.h the bf16 gradient takes fp32
+    maps.  At C1 = 1e-8, C2 = 1e-6 (8 / C2 = 8e6) the two-launch bf16 gradient is finite and
+    within one bf16 ulp of the one-launch fen_ssim's."""
+    from src.hip import lib as L
+    from src.hip.program import ptr
+    from src.losses.ssim import _window1d
+    B, C, H, W = 2, 3, 64, 64
+    torch.manual_seed(3)
+    p = torch.rand(B, C, H, W, device=DEV)
+    t = (p + 0.05 * torch.randn(B, C, H, W, device=DEV)).clamp(0, 1)
+    p[:, :, :8, :8] = 0.25                       # flat patches: variances ~0, the coefficients ~1/C2
+    t[:, :, :8, :8] = 0.25
+    lib = L.load()
+    rows = lib.fen_ssim_parts(B, C, H, W)
+    win = _window1d(11, 1.5).to(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    out = []
+    for two in (False, True):
+        buf = torch.zeros((B, H, W, 16), device=DEV, dtype=torch.bfloat16)
+        part = torch.empty(rows * B, device=DEV)
+        work = torch.empty(lib.fen_ssim_work_floats(B, C, H, W), device=DEV)
+        L.check(lib.fen_ssim_ex(L.dtype_code(torch.bfloat16), B, C, H, W, ptr(p), ptr(t), ptr(win), 11, 1e-8, 1e-6,
+                                ptr(part), ptr(buf), 1.0 / (B * C * H * W), 2, ptr(work) if two else None, s),
+                "ssim_ex")
+        torch.cuda.synchronize()
+        out.append(buf.float())
+    ref, got = out
+    assert bool(torch.isfinite(got).all())
+    mag = torch.maximum(ref.abs(), got.abs()).clamp_min(1e-30)
+    allowed = torch.exp2(torch.floor(torch.log2(mag)) - 7)
+    assert bool(((ref - got).abs() <= allowed).all()), float((ref - got).abs().max())
