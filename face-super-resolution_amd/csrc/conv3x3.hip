@@ -1175,6 +1175,196 @@ __global__ __launch_bounds__(256, 2) void k_conv3x3_s(const fen_conv_desc d) {
     conv_epilogue<T, COT, 4, 1, EPIC>(d, acc, b, tb, h0, w0, co0, stage, red, ec);
 }
 
+// ------------------------------------------------------------------------------------
+// k_conv3x3_v: persistent, LDS-DMA-fed (16-bit, Cin % 64 == 0, Cin >= 128, Cout % 128 == 0):
+// the wide convs of VGG19's perceptual extractor (perceptual.py:13-169: conv2_2 .. conv3_4 and
+// their data gradients) and of the discriminator (discriminator.py:58-90), where the filter slab
+// (9 x Cin x Cout) is far larger than the LDS, so it streams.
+// 512 threads = 8 waves; a block owns 128 output channels (co-tile fixed per block, tiles
+// strided over the blocks, XCD-aware); wave (wr, wc) = 4 output rows x 16 columns x 64 channels
+// of the 16 x 16 tile (16 accumulators, the streamed kernel's wave shape).  The K loop of a tile
+// is npan x 9 steps (64-channel Cin panel, tap), and the steps of consecutive tiles run as ONE
+// pipeline.  Operands arrive by LDS-DMA only (nothing through VGPRs or ds_write): step s's 16-KB
+// weight slab (128 co x 64 ci) into slot s % 4 of a ring, three steps ahead, issued by waves 4-7;
+// each panel's 18 x 18 halo into one of two slots, a whole panel ahead, issued by waves 0-3.
+// vmcnt counts a wave's own loads in issue order, so the split keeps a weight wave's wait for
+// the next step's slab from also waiting for a halo that is not due for eight more steps.  One
+// s_barrier per step certifies the NEXT step's operands (each wave first waits for its own
+// pieces of them), so a step reads the next step's first k-half fragments under its own
+// second-half MFMAs and its MFMAs start right behind the barrier.  Taps are unrolled: every LDS
+// address is a per-lane constant plus a scalar slot base.
+// LDS: ring 4 x 16 KB | halo 2 x 44 KB | epilogue partials 2 KB = 154 KB.
+// ------------------------------------------------------------------------------------
+constexpr int V_COT = 128;
+constexpr int V_WSLOT = V_COT * 128;       // one (tap, panel) weight slab
+constexpr int V_RING = 4;
+constexpr int V_HPIECES = 44;              // 41 halo pieces rounded up to 11 per halo wave
+constexpr int V_HSLOT = V_HPIECES * 1024;
+constexpr int V_LDS = V_RING * V_WSLOT + 2 * V_HSLOT + 4 * V_COT * 4;
+constexpr int V_BAD = 0x7f000000;          // a voffset past any buffer fen_conv3x3 routes here (loads 0)
+
+template <typename T, int EPIC>
+__global__ __launch_bounds__(512, 1) void k_conv3x3_v(const fen_conv_desc d) {
+    constexpr int MT = 4, NT = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* wring = smem;
+    char* hbuf = smem + V_RING * V_WSLOT;
+    float* red = (float*)(hbuf + 2 * V_HSLOT);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wv = wave_id();                                // the same, scalar: role branches are real branches
+    const bool hwave = wv < 4;                               // halo DMA (0-3) / weight DMA (4-7)
+    const int wl = wv & 3;
+    const int wr = wave & 3, wc = wave >> 2;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
+    const int ncot = Cout / V_COT;
+    const int bid = xcd_block();
+    const int cot = bid % ncot, co0 = cot * V_COT;
+    const int nslot = gridDim.x / ncot, slot = bid / ncot;
+    const int twn = (W + 15) >> 4, tpi = twn * ((H + 15) >> 4);
+    const int ntiles = d.B * tpi;
+    const int nmine = slot < ntiles ? (ntiles - slot + nslot - 1) / nslot : 0;
+    const int npan = Cin >> 6;
+    const int nsteps = nmine * npan * 9;
+    if (nsteps == 0) return;                                 // block-uniform
+    const i32x4 xr4 = make_rsrc(d.x, (unsigned)((size_t)d.B * H * W * Cin * 2));
+    const i32x4 wr4 = make_rsrc(d.w, (unsigned)((size_t)9 * Cout * Cin * 2));
+
+    // weight waves: per-lane source offsets of their 4 pieces (i = 4 wl + k) of a slab, less the
+    // (tap, panel) term; the LDS slot is lane-linear, the XOR swizzle on the source chunk
+    auto issue_w = [&](int slot_i, int tap, int pn) {
+        const unsigned base = lds_addr(wring + slot_i * V_WSLOT) + 4 * wl * 1024;
+        const int so = (tap * Cout + co0) * Cin * 2 + pn * 128;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sl = (4 * wl + k) * 64 + lane;
+            const int r = sl >> 3, pc = sl & 7;
+#ifndef CVX_NOW
+            dma16(wr4, base + k * 1024, so + (r * Cin + (pc ^ ((r >> 1) & 7)) * 8) * 2);
+#endif
+        }
+    };
+    // halo waves: their 11 pieces (i = wl + 4 k) of tile t's halo, Cin panel pn, into slot par
+    // (zero padding: a voffset past the buffer outside the image / past the 18 x 18 pixels)
+    auto issue_h = [&](int par, int t, int pn) {
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const unsigned base = lds_addr(hbuf + par * V_HSLOT) + wl * 1024;
+#pragma unroll 1
+        for (int k = 0; k < 11; ++k) {
+            const int sl = (wl + 4 * k) * 64 + lane;
+            const int p = sl >> 3, pc = sl & 7;
+            const int hr = p / HALO, hc = p - hr * HALO;
+            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+            const bool in = p < HP && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            const int voff = in ? (((b * H + gh) * W + gw) * Cin + (pc ^ (hc & 7)) * 8) * 2 + pn * 128 : V_BAD;
+#ifndef CVX_NOH
+            dma16(xr4, __builtin_amdgcn_readfirstlane(base + k * 4096), voff);
+#endif
+        }
+    };
+    // per-lane LDS read offsets: A rows wc*64 + m*16 + c16 of a slab (the swizzle key (row >> 1) & 7
+    // does not depend on m or wc: m steps are immediates), B at halo column c16 + kw, row wr*4 + kh + n
+    const int aoff0 = swz(wc * 64 + c16, q), aoff1 = swz(wc * 64 + c16, 4 + q);
+    auto load = [&](int wslot, int par, int kh, int kw, int kk, uint4 (&A)[MT], uint4 (&Bf)[NT]) {
+        const char* pa = wring + wslot * V_WSLOT + (kk ? aoff1 : aoff0);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) A[m] = *(const uint4*)(pa + m * 2048);
+        const char* pb = hbuf + par * V_HSLOT + hcol(c16 + kw, kk * 4 + q) + (wr * NT + kh) * (HALO * 128);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) Bf[n] = *(const uint4*)(pb + n * (HALO * 128));
+    };
+    f32x4 acc[MT][NT];
+    auto mma = [&](const uint4 (&A)[MT], const uint4 (&Bf)[NT]) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A[m], Bf[n]);
+    };
+
+    // prologue: tile 0's panel-0 halo; slabs of steps 0..2
+    if (hwave) {
+        issue_h(0, slot, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        for (int s = 0; s < 3 && s < nsteps; ++s) issue_w(s, s, 0);
+        if (nsteps > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (nsteps > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    uint4 A0[MT], B0[NT], A1[MT], B1[NT];
+    load(0, 0, 0, 0, 0, A0, B0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int s = 0, gp = 0;                                       // global step / panel counters
+    for (int j = 0; j < nmine; ++j) {
+        for (int pn = 0; pn < npan; ++pn, ++gp) {
+            const int par = gp & 1;
+            // the step 3 ahead: (tap + 3) % 9 of this panel or the next (of the next tile)
+            const int pn3 = pn + 1 < npan ? pn + 1 : 0;
+#pragma unroll 1
+            for (int kh = 0; kh < 3; ++kh) {
+#ifdef CV_KWU
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+            for (int kw = 0; kw < 3; ++kw, ++s) {
+                const int tap = kh * 3 + kw;
+                if (s + 1 < nsteps) {
+                    // certify step s + 1 (its slab; at tap 8 the next panel's halo)
+                    if (!hwave) {
+                        if (s + 2 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    } else if (kw == 2 && kh == 2) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();            // and: every wave is done with step s - 1
+                    if (hwave) {
+                        if (kw == 0 && kh == 0 && gp + 1 < nmine * npan) {  // the next panel's halo, into the slot gp - 1 used
+                            if (pn + 1 < npan) issue_h(par ^ 1, slot + j * nslot, pn + 1);
+                            else issue_h(par ^ 1, slot + (j + 1) * nslot, 0);
+                        }
+                    } else if (s + 3 < nsteps) {
+                        issue_w((s + 3) & 3, (tap + 3) % 9, tap + 3 < 9 ? pn : pn3);   // into slot (s - 1) % 4
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                load(s & 3, par, kh, kw, 1, A1, B1);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(A0, B0);
+                __builtin_amdgcn_sched_barrier(0);
+                // the next step's first-half fragments (not across a tile end: the epilogue's
+                // registers come first, the next tile's first fragments are read after it)
+                if (kw < 2) load((s + 1) & 3, par, kh, kw + 1, 0, A0, B0);
+                else if (kh < 2) load((s + 1) & 3, par, kh + 1, 0, 0, A0, B0);
+                else if (pn + 1 < npan) load((s + 1) & 3, par ^ 1, 0, 0, 0, A0, B0);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(A1, B1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            }
+        }
+        // tile done: epilogue from registers (direct stores)
+        const int t = slot + j * nslot;
+        const int b = t / tpi, tile = t - b * tpi;
+        const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
+        const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * 64 + q * 4);   // (per tile: 32 VGPRs less in the loop)
+        conv_epilogue<T, V_COT, 4, 2, EPIC, true>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (s < nsteps) load(s & 3, gp & 1, 0, 0, 0, A0, B0);   // the next tile's step 0 (certified)
+    }
+}
+
 int g_num_cus = 0;
 
 // kernel-variant selector for A/B runs (FEN_CONV_VARIANT): 0 default (ping-pong persistent
@@ -1240,6 +1430,45 @@ int launch_g(const fen_conv_desc* d, hipStream_t s) {
     hipLaunchKernelGGL((k_conv3x3_g<T, EPIC>), dim3(grid), dim3(512), G_LDS, s, *d);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
+}
+
+template <typename T, int EPIC>
+int launch_v(const fen_conv_desc* d, hipStream_t s) {
+    const int tpi = ((d->W + 15) >> 4) * ((d->H + 15) >> 4);
+    const int ntiles = d->B * tpi;
+    const int ncot = d->Cout / V_COT;
+    if (g_num_cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    int grid = g_num_cus;
+    grid -= grid % ncot;
+    if (grid < ncot) grid = ncot;
+    const int maxg = ntiles * ncot;
+    if (grid > maxg) grid = maxg;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_conv3x3_v<T, EPIC>, hipFuncAttributeMaxDynamicSharedMemorySize, V_LDS);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_conv3x3_v<T, EPIC>), dim3(grid), dim3(512), V_LDS, s, *d);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+// the DMA-fed wide conv: 16-bit, Cin a multiple of 64 above 64, Cout of 128, stride 1, no
+// (un)shuffle / conv_last, 32-bit buffer offsets (FEN_CONV_V=0: the streamed kernel instead)
+bool conv_v_ok(const fen_conv_desc* d) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("FEN_CONV_V");
+        on = e ? atoi(e) : 1;
+    }
+    return on && conv_variant() != 1 && d->Cin % 64 == 0 && d->Cin >= 128 && d->Cout % V_COT == 0 &&
+           d->s2d_in == 0 && d->s2d_out == 0 && !(d->epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE | FEN_EPI_LAST)) &&
+           (size_t)d->B * d->H * d->W * d->Cin * 2 < (size_t)V_BAD && (size_t)9 * d->Cout * d->Cin * 2 < (size_t)V_BAD;
 }
 
 template <typename T, int COT, int EPIC = -1>
@@ -1323,6 +1552,21 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
                     case 2 << 8: return launch_p<T, 64, 4, 2, 2 << 8>(d, s);
                     case 3 << 8: return launch_p<T, 64, 4, 2, 3 << 8>(d, s);
                     default: return launch_p<T, 64, 4, 2, -1>(d, s);
+                }
+            }
+        }
+        if constexpr (H16) {
+            if (conv_v_ok(d)) {
+                const int nres = d->res[0] ? (d->res[1] ? (d->res[2] ? 3 : 2) : 1) : 0;
+                bool dense = true;
+                for (int k = nres; k < 3; ++k) dense = dense && !d->res[k];
+                constexpr int B_ = FEN_EPI_BIAS;
+                switch (dense ? (epi | (nres << 8)) : -1) {
+                    case B_ | FEN_EPI_PRELU: return launch_v<T, B_ | FEN_EPI_PRELU>(d, s);
+                    case B_: return launch_v<T, B_>(d, s);
+                    case FEN_EPI_PRELU_BWD: return launch_v<T, FEN_EPI_PRELU_BWD>(d, s);
+                    case 0: return launch_v<T, 0>(d, s);
+                    default: break;   // (the runtime-mode epilogue spills at this wave shape: streamed kernel)
                 }
             }
         }

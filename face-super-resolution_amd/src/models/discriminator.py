@@ -283,13 +283,18 @@ class VGGStyleDiscriminator(nn.Module):
         if x.shape[1] != 3 or x.shape[2] % 32 or x.shape[3] % 32:
             raise ValueError("input must be (B, 3, H, W) with H, W multiples of 32")
         feats = _DFeatures.apply(x, self, *self._feature_params())
-        h = feats.flatten(1)
-        lin1, lin2 = self.classifier[1], self.classifier[3]
-        h = F.leaky_relu(F.linear(h, lin1.weight, lin1.bias), 0.2)
+        h = F.leaky_relu(self.head_preactivation(feats.flatten(1)), 0.2)
+        lin2 = self.classifier[3]
         out = F.linear(h, lin2.weight, lin2.bias)
         if self.use_sigmoid:
             out = torch.sigmoid(out)
         return out
+
+    def head_preactivation(self, h: torch.Tensor) -> torch.Tensor:
+        """The classifier's hidden layer before its LeakyReLU, Linear(32768, 1024) of the
+        flattened features, exactly as forward computes it (tests read its branches)."""
+        lin1 = self.classifier[1]
+        return F.linear(h, lin1.weight, lin1.bias)
 
     def get_model_info(self) -> dict:
         total_params = sum(p.numel() for p in self.parameters())

@@ -287,6 +287,40 @@ def perceptual_loss(p: Params, pred: torch.Tensor, target: torch.Tensor, layer_i
 
 
 # ---------------------------------------------------------------------------------------
+# VGGStyleDiscriminator forward (reference src/models/discriminator.py:58-90 tree, 118-136
+# forward), functional, train-mode BatchNorm (batch statistics, eps 1e-5), for gradient replays.
+D_STRIDES = (1, 2, 1, 2, 1, 2, 1, 2, 1, 2)
+
+
+def disc_forward(p: Params, x: torch.Tensor, masks=None, record=None, slope: float = 0.2) -> torch.Tensor:
+    """Scores [B,1] of the discriminator with parameters p (its state_dict keys) on x, in x's
+    dtype.  The 11 LeakyReLUs (10 feature blocks, the classifier's hidden layer) take their
+    branch from `masks[i]` (bool, the activation's shape) when given -- the derivative of the
+    piecewise-linear net on the linear piece another run (the HIP discriminator) took: an
+    element whose pre-activation sits within rounding of 0 flips sides between precisions and
+    moves every gradient below it by a finite step -- else from the sign of the pre-activation;
+    `record` (a list) collects the masks this run took."""
+    h = x
+    for i, st in enumerate(D_STRIDES):
+        b = p.get(f"features.{i}.0.bias")
+        h = F.conv2d(h, p[f"features.{i}.0.weight"].to(h.dtype), None if b is None else b.to(h.dtype), stride=st,
+                     padding=1)
+        if i > 0:
+            mu = h.mean((0, 2, 3), keepdim=True)
+            var = h.var((0, 2, 3), unbiased=False, keepdim=True)
+            h = ((h - mu) / torch.sqrt(var + 1e-5) * p[f"features.{i}.1.weight"].to(h.dtype).view(1, -1, 1, 1)
+                 + p[f"features.{i}.1.bias"].to(h.dtype).view(1, -1, 1, 1))
+        if record is not None:
+            record.append((h > 0).detach())
+        h = torch.where(h > 0 if masks is None else masks[i], h, slope * h)
+    h = F.linear(h.flatten(1), p["classifier.1.weight"].to(h.dtype), p["classifier.1.bias"].to(h.dtype))
+    if record is not None:
+        record.append((h > 0).detach())
+    h = torch.where(h > 0 if masks is None else masks[10], h, slope * h)
+    return F.linear(h, p["classifier.3.weight"].to(h.dtype), p["classifier.3.bias"].to(h.dtype))
+
+
+# ---------------------------------------------------------------------------------------
 # SSIM (reference src/losses/ssim_loss.py:14-98,174-226); pinned by tests/golden/g7_ssim.npz
 # (made by importing the reference module, tests/golden/make_golden_ssim.py)
 def gaussian_window(window_size: int = 11, sigma: float = 1.5) -> torch.Tensor:

@@ -155,7 +155,7 @@ def test_gan_iteration_over_rccl(tmp_path):
         assert cap._g_ex is not None and cap._d_ex is not None
         assert len(cap._g_ex.ranges) == 2 + 1 and len(cap._d_ex.ranges) == 2   # tail, rg0, head
         assert cap._g_ex.ex.comm is not None and cap._d_ex.ex.comm is not None     # direct RCCL
-        g, d = cap._g_ex.ex.captured_launches, cap._d_ex.ex.captured_launches
+        g, d = list(cap._g_ex.ex.captured_launches), list(cap._d_ex.ex.captured_launches)
         # 2 eager iterations + the captured one went through Python; replays do not
         assert g == [False] * 6 + [True] * 3, g
         nd = cap.config.d_updates_per_g * 2

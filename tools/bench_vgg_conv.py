@@ -37,4 +37,15 @@ for name, N, hw, cin, cout in [("c1_2", 64, 256, 64, 64), ("c2_1", 64, 128, 64, 
     us = timeit(lambda: net.conv(ctx, x, wp, N, hw, hw, cin, cout, bias=b, epi=L.EPI_PRELU, alpha=torch.zeros(cout, device='cuda'), y=y))
     fl = 2 * N * hw * hw * cin * cout * 9
     res[name] = [round(us, 1), round(fl / us / 1e6, 1)]
+    if cin >= 128:     # its data gradient at B = 32 through the ReLU mask (mode-2 weights: Cout <-> Cin)
+        n2 = N // 2
+        d = torch.randn(n2, hw, hw, cout, device='cuda', dtype=dt)
+        pre = torch.randn(n2, hw, hw, cin, device='cuda', dtype=dt)
+        dz = torch.empty(n2, hw, hw, cin, device='cuda', dtype=dt)
+        part = torch.empty(n2 * ((hw + 15) // 16) ** 2, cin, device='cuda')
+        wp2 = pack(w, 2)
+        if cin % 128 == 0:
+            us = timeit(lambda: net.conv(ctx, d, wp2, n2, hw, hw, cout, cin, epi=L.EPI_PRELU_BWD,
+                                         alpha=torch.zeros(cin, device='cuda'), pre_in=pre, y=dz, part=part))
+            res[name + "_dg"] = [round(us, 1), round(fl / 2 / us / 1e6, 1)]
 print(json.dumps(res))
