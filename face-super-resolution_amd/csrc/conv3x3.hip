@@ -1309,23 +1309,23 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_v(const fen_conv_desc d) {
             const int pn3 = pn + 1 < npan ? pn + 1 : 0;
 #pragma unroll 1
             for (int kh = 0; kh < 3; ++kh) {
-#ifdef CV_KWU
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
+#pragma unroll   // (kw unrolled: 302 vs 327 us on VGG conv3_2, A/B r6)
             for (int kw = 0; kw < 3; ++kw, ++s) {
                 const int tap = kh * 3 + kw;
                 if (s + 1 < nsteps) {
                     // certify step s + 1 (its slab; at tap 8 the next panel's halo)
                     if (!hwave) {
+                        // (after a tile's epilogue this also waits for its stores: letting them stay
+                        // in flight took a runtime count whose registers spilled -- slower, A/B r6)
                         if (s + 2 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     } else if (kw == 2 && kh == 2) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef CVX_NOBAR   // (diagnostic variants: timing only, wrong results)
                     __builtin_amdgcn_s_barrier();            // and: every wave is done with step s - 1
+#endif
                     if (hwave) {
                         if (kw == 0 && kh == 0 && gp + 1 < nmine * npan) {  // the next panel's halo, into the slot gp - 1 used
                             if (pn + 1 < npan) issue_h(par ^ 1, slot + j * nslot, pn + 1);
@@ -1356,7 +1356,11 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_v(const fen_conv_desc d) {
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const EpiConst<MT> ec = epi_consts<MT>(d, co0 + wc * 64 + q * 4);   // (per tile: 32 VGPRs less in the loop)
+#ifndef CVX_NOEPI
         conv_epilogue<T, V_COT, 4, 2, EPIC, true>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
+#else
+        if (acc[0][0][0] == 12345.f) conv_epilogue<T, V_COT, 4, 2, EPIC, true>(d, acc, b, t, h0, w0, co0, nullptr, red, ec);
+#endif
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -1466,7 +1470,18 @@ bool conv_v_ok(const fen_conv_desc* d) {
         const char* e = getenv("FEN_CONV_V");
         on = e ? atoi(e) : 1;
     }
-    return on && conv_variant() != 1 && d->Cin % 64 == 0 && d->Cin >= 128 && d->Cout % V_COT == 0 &&
+    // (and enough 16 x 16 x 128 work items to fill the CUs: a long K loop on a quarter of the
+    // chip lost to the streamed kernel's 2-blocks-per-CU grid -- the discriminator's 16 x 16 layers)
+    const int items = d->B * ((d->H + 15) >> 4) * ((d->W + 15) >> 4) * (d->Cout / V_COT);
+    int ncu = g_num_cus;
+    if (ncu == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (ncu <= 0) ncu = 256;
+        g_num_cus = ncu;
+    }
+    return on && conv_variant() != 1 && items >= ncu && d->Cin % 64 == 0 && d->Cin >= 128 && d->Cout % V_COT == 0 &&
            d->s2d_in == 0 && d->s2d_out == 0 && !(d->epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE | FEN_EPI_LAST)) &&
            (size_t)d->B * d->H * d->W * d->Cin * 2 < (size_t)V_BAD && (size_t)9 * d->Cout * d->Cin * 2 < (size_t)V_BAD;
 }

@@ -65,6 +65,9 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_finalize(int nblocks, siz
     const int c = blockIdx.x * 64 + lane;
     double s = 0.0, q = 0.0;
     if (c < C) {
+        // (unrolled: the partials' loads in flight together, summed in the same order -- the
+        // rolled loop waited one L2 round trip per partial, ~12 us per finalize)
+#pragma unroll 8
         for (int b = w; b < nblocks; b += FIN_WAVES) {
             s += part[(size_t)b * 2 * C + c];
             q += part[(size_t)b * 2 * C + C + c];
@@ -190,6 +193,7 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_bwd_finalize(int nblocks,
     const int c = blockIdx.x * 64 + lane;
     float s = 0.f, q = 0.f;
     if (c < C) {
+#pragma unroll 8
         for (int b = w; b < nblocks; b += FIN_WAVES) {
             s += part[(size_t)b * 2 * C + c];
             q += part[(size_t)b * 2 * C + C + c];
@@ -462,6 +466,266 @@ extern "C" int fen_s2d_filter(int Cout, int C, const float* src, float* dst, int
     const size_t n = (size_t)Cout * C * 9 * (gather ? 1 : 4);
     if (gather) hipLaunchKernelGGL(k_s2d_filter<true>, dim3(nblk(n)), dim3(256), 0, STREAM, Cout, C, src, dst);
     else hipLaunchKernelGGL(k_s2d_filter<false>, dim3(nblk(n)), dim3(256), 0, STREAM, Cout, C, src, dst);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The classifier head (discriminator.py:85-90: Flatten -> Linear(K, N) -> LeakyReLU(0.2) ->
+// Linear(N, 1), optional sigmoid 131-132), fp32 as the reference.  K = 512 x 8 x 8 = 32768,
+// N = 1024: the first layer's 128-MB weight is the whole cost -- one read in the forward, one read
+// (for d(x)) and one write (its gradient) in the backward; everything else is small.
+//   forward   k_dhead_mm: per k-split s, part[s][b][n] = sum_k x[b][k] w1[n][k] on fp32 MFMAs
+//             (v_mfma_f32_16x16x4f32, a wave = 16 rows n x 16 samples, the weight row read as
+//             float4 along k); k_dhead_fin: pre = b1 + sum_s part (fixed order), the LeakyReLU, the
+//             second layer's dot (fixed-order block reduction), + b2 (and the sigmoid).
+//   backward  k_dhead_bvec: dpre = g w2 LeakyReLU'(pre), db1, dw2, db2; k_dhead_bw: one wave per
+//             256 k x N/G rows -- dw1[n][k] = sum_b dpre[b][n] x[b][k] (written once) and the
+//             d(x) partial sum_n dpre[b][n] w1[n][k] over its rows (w1 read once), G row groups
+//             summed by k_dhead_dxfin in fixed order.  Deterministic run to run.
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int DH_SPLIT = 32;    // k-splits of the forward GEMM
+constexpr int DH_G = 8;         // row groups of the backward's d(x)
+constexpr int DH_BC = 16;       // samples per pass of the backward kernel
+constexpr int DH_UNR = 8;       // forward: k-steps of loads in flight per wave
+constexpr int DH_RUN = 4;       // backward: rows of loads in flight per wave
+
+// the head's weight and its gradient are streamed once per launch: non-temporal (no L2 / MALL
+// allocation for 128 MB that will not be re-read before it is evicted)
+__device__ __forceinline__ float4 ld_nt4(const float* p) {
+    const f32x4 v = __builtin_nontemporal_load((const f32x4*)p);
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st_nt4(float* p, const float4& v) {
+    __builtin_nontemporal_store((f32x4){v.x, v.y, v.z, v.w}, (f32x4*)p);
+}
+
+__global__ __launch_bounds__(256) void k_dhead_mm(int B, int K, int N, int kc, const float* __restrict__ x,
+                                                  const float* __restrict__ w1, float* __restrict__ part) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, q = lane >> 4;
+    const int n0 = (blockIdx.x * 4 + wave) * 16;
+    const int s = blockIdx.y;
+    const int k0 = s * kc;
+    const int nbb = (B + 15) >> 4;
+    const float* wrow = w1 + (size_t)(n0 + r) * K + k0 + 4 * q;
+    for (int bb = 0; bb < nbb; ++bb) {
+        const int b = bb * 16 + r;
+        const float* xrow = x + (size_t)(b < B ? b : 0) * K + k0 + 4 * q;
+        const float xm = b < B ? 1.f : 0.f;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        // 8 k-steps of loads in flight per wave (the weight streams from HBM once)
+        for (int k = 0; k < kc; k += 16 * DH_UNR) {
+            float4 wv[DH_UNR], xv[DH_UNR];
+#pragma unroll
+            for (int u = 0; u < DH_UNR; ++u) {
+                wv[u] = ld_nt4(wrow + k + 16 * u);
+                xv[u] = *(const float4*)(xrow + k + 16 * u);
+            }
+#pragma unroll
+            for (int u = 0; u < DH_UNR; ++u) {
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].x, xv[u].x * xm, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].y, xv[u].y * xm, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].z, xv[u].z * xm, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].w, xv[u].w * xm, acc, 0, 0, 0);
+            }
+        }
+        // lane holds D[n0 + 4q + t][b] for t = 0..3
+        if (b < B) *(float4*)(part + ((size_t)s * B + b) * N + n0 + 4 * q) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    }
+}
+
+// one block per sample, one thread per output unit n (N <= 1024): the DH_SPLIT partials in
+// fixed order (all loads in flight), the LeakyReLU, the second layer's dot by a fixed-order tree
+__global__ __launch_bounds__(1024) void k_dhead_fin(int B, int N, int S, const float* __restrict__ part,
+                                                    const float* __restrict__ b1, const float* __restrict__ w2,
+                                                    const float* __restrict__ b2, float slope, int sigmoid,
+                                                    float* __restrict__ pre, float* __restrict__ y) {
+    __shared__ float red[1024];
+    const int b = blockIdx.x, n = threadIdx.x;
+    float acc = 0.f;
+    if (n < N) {
+        float pv[DH_SPLIT];
+#pragma unroll
+        for (int s = 0; s < DH_SPLIT; ++s) pv[s] = s < S ? part[((size_t)s * B + b) * N + n] : 0.f;
+        float v = b1[n];
+#pragma unroll
+        for (int s = 0; s < DH_SPLIT; ++s)
+            if (s < S) v += pv[s];
+        pre[(size_t)b * N + n] = v;
+        acc = (v > 0.f ? v : slope * v) * w2[n];
+    }
+    red[n] = acc;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (n < o) red[n] += red[n + o];
+        __syncthreads();
+    }
+    if (n == 0) {
+        const float sc = red[0] + b2[0];
+        y[b] = sigmoid ? 1.f / (1.f + expf(-sc)) : sc;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dhead_bvec(int B, int N, const float* __restrict__ gy,
+                                                    const float* __restrict__ pre, const float* __restrict__ w2,
+                                                    const float* __restrict__ y, float slope, int sigmoid,
+                                                    float* __restrict__ dpre, float* __restrict__ db1,
+                                                    float* __restrict__ dw2, float* __restrict__ db2) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n < N) {
+        const float w = w2[n];
+        float sdb = 0.f, sdw = 0.f;
+        for (int b = 0; b < B; ++b) {
+            const float g = sigmoid ? gy[b] * y[b] * (1.f - y[b]) : gy[b];
+            const float p = pre[(size_t)b * N + n];
+            const float dp = g * w * (p > 0.f ? 1.f : slope);
+            dpre[(size_t)n * B + b] = dp;                     // [n][b]: the backward kernel's rows
+            sdb += dp;
+            sdw = fmaf(g, p > 0.f ? p : slope * p, sdw);
+        }
+        db1[n] = sdb;
+        dw2[n] = sdw;
+    }
+    if (n == 0) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += sigmoid ? gy[b] * y[b] * (1.f - y[b]) : gy[b];
+        db2[0] = s;
+    }
+}
+
+// block = 4 waves over one 256-k column block and one group of N / DH_G rows (the waves take every
+// 4th row): dw1[n][k] = sum_b dpre[n][b] x[b][k] written once, each wave's d(x) partial over its
+// rows summed across the waves in LDS (fixed order) into dxpart[g]; dpre of the rows staged in
+// LDS (read as broadcast float4s); samples [b0, b0 + nb) of this pass (accumulate: dw1 +=)
+__global__ __launch_bounds__(256) void k_dhead_bw(int B, int K, int N, int b0, int nb, const float* __restrict__ x,
+                                                  const float* __restrict__ w1, const float* __restrict__ dpre,
+                                                  int accumulate, float* __restrict__ dw1, float* __restrict__ dxpart) {
+    __shared__ __attribute__((aligned(16))) float sdp[1024 / DH_G * DH_BC];   // [row][b]
+    __shared__ __attribute__((aligned(16))) float4 sdx[3][DH_BC][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int k4 = blockIdx.x * 256 + lane * 4;
+    const int g = blockIdx.y;
+    const int rows = N / DH_G, n0 = g * rows;
+    for (int i = threadIdx.x; i < rows * DH_BC; i += 256) {
+        const int rr = i / DH_BC, b = i % DH_BC;
+        sdp[i] = b < nb ? dpre[(size_t)(n0 + rr) * B + b0 + b] : 0.f;
+    }
+    float4 xv[DH_BC], dx[DH_BC];
+#pragma unroll
+    for (int b = 0; b < DH_BC; ++b) {
+        xv[b] = b < nb ? *(const float4*)(x + (size_t)(b0 + b) * K + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        dx[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    for (int rr = wave; rr < rows; rr += 4 * DH_RUN) {
+        float4 wv[DH_RUN], dw[DH_RUN];
+#pragma unroll
+        for (int u = 0; u < DH_RUN; ++u) {
+            const int n = n0 + rr + 4 * u;
+            wv[u] = ld_nt4(w1 + (size_t)n * K + k4);
+            dw[u] = accumulate ? *(const float4*)(dw1 + (size_t)n * K + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < DH_RUN; ++u) {
+            const float4* dp4 = (const float4*)(sdp + (rr + 4 * u) * DH_BC);
+#pragma unroll
+            for (int b4 = 0; b4 < DH_BC / 4; ++b4) {
+                const float4 p = dp4[b4];
+                const float pb[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int b = 4 * b4 + j;
+                    const float dp = pb[j];
+                    dx[b].x = fmaf(dp, wv[u].x, dx[b].x), dx[b].y = fmaf(dp, wv[u].y, dx[b].y);
+                    dx[b].z = fmaf(dp, wv[u].z, dx[b].z), dx[b].w = fmaf(dp, wv[u].w, dx[b].w);
+                    dw[u].x = fmaf(dp, xv[b].x, dw[u].x), dw[u].y = fmaf(dp, xv[b].y, dw[u].y);
+                    dw[u].z = fmaf(dp, xv[b].z, dw[u].z), dw[u].w = fmaf(dp, xv[b].w, dw[u].w);
+                }
+            }
+            st_nt4(dw1 + (size_t)(n0 + rr + 4 * u) * K + k4, dw[u]);
+        }
+    }
+    if (!dxpart) return;
+    // the 4 waves' partials, summed in wave order
+    if (wave > 0) {
+#pragma unroll
+        for (int b = 0; b < DH_BC; ++b) sdx[wave - 1][b][lane] = dx[b];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int b = 0; b < DH_BC; ++b) {
+            if (b >= nb) continue;
+            float4 v = dx[b];
+#pragma unroll
+            for (int w = 0; w < 3; ++w) {
+                const float4 o = sdx[w][b][lane];
+                v.x += o.x, v.y += o.y, v.z += o.z, v.w += o.w;
+            }
+            *(float4*)(dxpart + ((size_t)g * B + b0 + b) * K + k4) = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dhead_dxfin(size_t n, const float* __restrict__ dxpart, float* __restrict__ dx) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < DH_G; ++g) v += dxpart[(size_t)g * n + i];
+    dx[i] = v;
+}
+}  // namespace
+
+extern "C" size_t fen_dhead_work_floats(int B, int K, int N) {
+    if (B <= 0 || K <= 0 || N <= 0) return 0;
+    const size_t fwd = (size_t)DH_SPLIT * B * N;
+    const size_t bwd = (size_t)B * N + (size_t)DH_G * B * K;
+    return fwd > bwd ? fwd : bwd;
+}
+
+// k-splits of the forward: the largest power of two <= DH_SPLIT whose chunks are whole unrolled steps
+static int dhead_split(int K) {
+    int S = DH_SPLIT;
+    while (S > 1 && K % (16 * DH_UNR * S)) S >>= 1;
+    return S;
+}
+static bool dhead_shape_ok(int B, int K, int N) {
+    return B > 0 && K % (16 * DH_UNR) == 0 && K % 256 == 0 && N % 64 == 0 && N <= 1024 && (N / DH_G) % (4 * DH_RUN) == 0;
+}
+
+extern "C" int fen_dhead_fwd(int B, int K, int N, const float* x, const float* w1, const float* b1, const float* w2,
+                             const float* b2, float slope, int sigmoid, float* pre, float* y, float* work,
+                             void* stream) {
+    if (!x || !w1 || !b1 || !w2 || !b2 || !pre || !y || !work || B <= 0 || K <= 0 || N <= 0) return FEN_EINVAL;
+    if (!dhead_shape_ok(B, K, N)) return FEN_EUNSUPPORTED;
+    const int S = dhead_split(K), kc = K / S;
+    hipLaunchKernelGGL(k_dhead_mm, dim3(N / 64, S), dim3(256), 0, STREAM, B, K, N, kc, x, w1, work);
+    hipLaunchKernelGGL(k_dhead_fin, dim3(B), dim3(1024), 0, STREAM, B, N, S, work, b1, w2, b2, slope, sigmoid, pre, y);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_dhead_bwd(int B, int K, int N, const float* x, const float* w1, const float* pre, const float* w2,
+                             const float* y, const float* gy, float slope, int sigmoid, float* dx, float* dw1,
+                             float* db1, float* dw2, float* db2, float* work, void* stream) {
+    if (!x || !w1 || !pre || !w2 || !gy || !dw1 || !db1 || !dw2 || !db2 || !work || (sigmoid && !y)) return FEN_EINVAL;
+    if (!dhead_shape_ok(B, K, N)) return FEN_EUNSUPPORTED;
+    float* dpre = work;
+    float* dxpart = dx ? work + (size_t)B * N : nullptr;
+    hipLaunchKernelGGL(k_dhead_bvec, dim3((N + 255) / 256), dim3(256), 0, STREAM, B, N, gy, pre, w2, y, slope, sigmoid,
+                       dpre, db1, dw2, db2);
+    for (int b0 = 0; b0 < B; b0 += DH_BC) {
+        const int nb = B - b0 < DH_BC ? B - b0 : DH_BC;
+        hipLaunchKernelGGL(k_dhead_bw, dim3(K / 256, DH_G), dim3(256), 0, STREAM, B, K, N, b0, nb, x, w1, dpre,
+                           b0 > 0 ? 1 : 0, dw1, dxpart);
+    }
+    if (dx) {
+        const size_t n = (size_t)B * K;
+        hipLaunchKernelGGL(k_dhead_dxfin, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, STREAM, n, dxpart, dx);
+    }
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

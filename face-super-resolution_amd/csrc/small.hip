@@ -1845,6 +1845,52 @@ __global__ void k_adamw(size_t n, float* __restrict__ p, const float* __restrict
     pi = pi - step_size * mi / denom;
     p[i] = pi; m[i] = mi; v[i] = vi;
 }
+// torch.optim.AdamW over a list of separate tensors (the discriminator's optimizer_d,
+// trainer.py:230-250, 446-451): per tensor its own device step count (torch's capturable form),
+// incremented by k_adamw_steps before the update reads it.  Blocks map to jobs by a prefix of
+// block offsets; each thread updates 4 consecutive elements (a tensor's tail by element).
+constexpr int ADAMW_MAXJ = 48;
+struct AdamJobK {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    float* step;
+    long long n;
+    int blk0;
+};
+struct AdamJobs {
+    int n;
+    float lr, b1, b2, eps, wd, omb1, omb2;   // 1 - b1, 1 - b2 rounded from double (torch's lerp weight)
+    AdamJobK j[ADAMW_MAXJ];
+};
+__global__ void k_adamw_steps(const AdamJobs jobs) {
+    const int i = threadIdx.x;
+    if (i < jobs.n) jobs.j[i].step[0] += 1.f;
+}
+__global__ __launch_bounds__(256) void k_adamw_multi(const AdamJobs jobs) {
+    int ji = 0;
+    while (ji + 1 < jobs.n && (int)blockIdx.x >= jobs.j[ji + 1].blk0) ++ji;
+    const AdamJobK& jb = jobs.j[ji];
+    const long long i0 = ((long long)(blockIdx.x - jb.blk0) * 256 + threadIdx.x) * 4;
+    if (i0 >= jb.n) return;
+    const float step = jb.step[0];
+    const float lr = jobs.lr, b1 = jobs.b1, b2 = jobs.b2;
+    const float decay = 1.f - lr * jobs.wd;
+    const float step_size = lr / (1.f - powf(b1, step));
+    const float rbc2 = 1.f / sqrtf(1.f - powf(b2, step));
+    const int cnt = jb.n - i0 >= 4 ? 4 : (int)(jb.n - i0);
+    for (int e = 0; e < cnt; ++e) {
+        const long long i = i0 + e;
+        const float gi = jb.g[i];
+        const float mi = jb.m[i] + jobs.omb1 * (gi - jb.m[i]);    // lerp
+        const float vi = jb.v[i] * b2 + jobs.omb2 * gi * gi;
+        const float denom = sqrtf(vi) * rbc2 + jobs.eps;
+        jb.p[i] = jb.p[i] * decay - step_size * mi / denom;
+        jb.m[i] = mi;
+        jb.v[i] = vi;
+    }
+}
 __global__ void k_scale(size_t n, float* y, float s) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) y[i] *= s;
@@ -2359,6 +2405,26 @@ extern "C" int fen_adamw(size_t n, float* p, const float* g, float* m, float* v,
                          float beta2, float eps, void* stream) {
     if (!p || !g || !m || !v || !scal) return FEN_EINVAL;
     hipLaunchKernelGGL(k_adamw, dim3(nblk(n)), dim3(256), 0, STREAM, n, p, g, m, v, scal, beta1, beta2, eps);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_adamw_multi(int njobs, const fen_adamw_job* jobs, float lr, float beta1, float beta2, float eps,
+                               float weight_decay, void* stream) {
+    if (njobs <= 0 || njobs > ADAMW_MAXJ || !jobs) return FEN_EINVAL;
+    AdamJobs k;
+    k.n = njobs, k.lr = lr, k.b1 = beta1, k.b2 = beta2, k.eps = eps, k.wd = weight_decay;
+    k.omb1 = (float)(1.0 - (double)beta1), k.omb2 = (float)(1.0 - (double)beta2);
+    long long blk = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const fen_adamw_job& j = jobs[i];
+        if (!j.p || !j.g || !j.m || !j.v || !j.step || j.n <= 0) return FEN_EINVAL;
+        k.j[i] = AdamJobK{j.p, j.g, j.m, j.v, j.step, (long long)j.n, (int)blk};
+        blk += ((long long)j.n + 1023) / 1024;
+        if (blk >= (1ll << 30)) return FEN_EUNSUPPORTED;
+    }
+    hipLaunchKernelGGL(k_adamw_steps, dim3(1), dim3(64), 0, STREAM, k);
+    hipLaunchKernelGGL(k_adamw_multi, dim3((unsigned)blk), dim3(256), 0, STREAM, k);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

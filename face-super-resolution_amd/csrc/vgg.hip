@@ -159,6 +159,37 @@ extern "C" int fen_maxpool2_bwd_relu(int dtype, int B, int H, int W, int C, cons
     return FEN_OK;
 }
 
+// mean |pred - target| over fp32 tensors (nn.L1Loss, combined.py:38-47 / the trainer's fallback
+// F.l1_loss): part[blk] = sum |p - t| of the block's elements (fixed order); with grad:
+// grad = scale * (gs ? *gs : 1) * sign(p - t) (gs: the upstream gradient, read on the device)
+__global__ __launch_bounds__(256) void k_l1(size_t n, const float* __restrict__ p, const float* __restrict__ t,
+                                            const float* __restrict__ gs, float scale, float* __restrict__ g,
+                                            float* __restrict__ part) {
+    __shared__ float red[256];
+    const float sc = g ? scale * (gs ? gs[0] : 1.f) : 0.f;
+    float acc = 0.f;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float d = p[i] - t[i];
+        acc += fabsf(d);
+        if (g) g[i] = d > 0.f ? sc : (d < 0.f ? -sc : 0.f);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+extern "C" int fen_l1_loss(size_t n, const float* pred, const float* target, const float* gscale, float scale,
+                           float* grad, float* part, void* stream) {
+    if (!pred || !target || !part || n == 0) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_l1, dim3(FL_BLOCKS), dim3(256), 0, STREAM, n, pred, target, gscale, scale, grad, part);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
 extern "C" int fen_feat_loss_parts(void) { return FL_BLOCKS; }
 
 extern "C" int fen_feat_loss(int dtype, size_t n, const void* f, int l2, float scale, void* g, int accumulate,

@@ -25,6 +25,11 @@ EPI_LAST = 64
 EPI_DOT = 128
 
 
+class AdamwJob(Structure):
+    _fields_ = [("p", c_void_p), ("g", c_void_p), ("m", c_void_p), ("v", c_void_p), ("step", c_void_p),
+                ("n", c_size_t)]
+
+
 class ConvDesc(Structure):
     _fields_ = [
         ("dtype", c_int), ("B", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
@@ -199,6 +204,11 @@ _SIGS = {
     "fen_s2d2": (c_int, [c_int] * 5 + [c_void_p] * 2 + [c_int, c_void_p]),
     "fen_s2d_filter": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
+    "fen_adamw_multi": (c_int, [c_int, c_void_p] + [c_float] * 5 + [c_void_p]),
+    "fen_l1_loss": (c_int, [c_size_t] + [c_void_p] * 3 + [c_float] + [c_void_p] * 3),
+    "fen_dhead_work_floats": (c_size_t, [c_int] * 3),
+    "fen_dhead_fwd": (c_int, [c_int] * 3 + [c_void_p] * 5 + [c_float, c_int] + [c_void_p] * 4),
+    "fen_dhead_bwd": (c_int, [c_int] * 3 + [c_void_p] * 6 + [c_float, c_int] + [c_void_p] * 7),
     "fen_status_word": (c_int, [POINTER(c_void_p), POINTER(c_void_p)]),
     "fen_status_take": (c_int, [c_void_p]),
     "fen_rccl_unique_id": (c_int, [c_void_p]),

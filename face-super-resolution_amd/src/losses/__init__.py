@@ -32,14 +32,53 @@ class LossConfig:
     vgg_weights: Optional[str] = None      # local torchvision VGG19 state dict (no download offline)
 
 
+class _L1(torch.autograd.Function):
+    """mean |pred - target| on fen_l1_loss (fixed-order partial sums, fen_colsum); the gradient
+    sign(pred - target) / n x the upstream gradient, read on the device.  No gradient to target
+    (the reference's HR images never require one; asking for it raises)."""
+
+    @staticmethod
+    def forward(fctx, pred, target):
+        from ..hip import lib as L
+        from ..hip.program import ptr
+        if target.requires_grad:
+            raise NotImplementedError("HIP L1Loss: no gradient with respect to the target")
+        p, t = pred.detach().float().contiguous(), target.detach().float().contiguous()
+        lib, s = L.load(), torch.cuda.current_stream().cuda_stream
+        nparts = lib.fen_feat_loss_parts()
+        part = torch.empty(nparts, device=p.device)
+        loss = torch.empty((), device=p.device)
+        L.check(lib.fen_l1_loss(p.numel(), ptr(p), ptr(t), None, 0.0, None, ptr(part), s), "l1_loss")
+        L.check(lib.fen_colsum(nparts, 1, ptr(part), 1.0 / p.numel(), ptr(loss), 0, s), "l1_loss sum")
+        fctx.save_for_backward(p, t)
+        fctx.dtype = pred.dtype
+        return loss
+
+    @staticmethod
+    def backward(fctx, gout):
+        from ..hip import lib as L
+        from ..hip.program import ptr
+        p, t = fctx.saved_tensors
+        lib, s = L.load(), torch.cuda.current_stream().cuda_stream
+        g = torch.empty_like(p)
+        part = torch.empty(lib.fen_feat_loss_parts(), device=p.device)
+        gout = gout.detach().float().contiguous()
+        L.check(lib.fen_l1_loss(p.numel(), ptr(p), ptr(t), ptr(gout), 1.0 / p.numel(), ptr(g), ptr(part), s),
+                "l1_loss grad")
+        return g.to(fctx.dtype), None
+
+
 class L1Loss(nn.Module):
-    """mean |pred - target| (combined.py:38-47)."""
+    """mean |pred - target| (combined.py:38-47), on the HIP kernel for GPU tensors ('mean'; the
+    other reductions and CPU tensors through torch, which the HIP path never hands it)."""
 
     def __init__(self, reduction: str = "mean"):
         super().__init__()
         self.reduction = reduction
 
     def forward(self, pred, target):
+        if self.reduction == "mean" and pred.is_cuda and pred.shape == target.shape:
+            return _L1.apply(pred, target)
         return F.l1_loss(pred, target, reduction=self.reduction)
 
 

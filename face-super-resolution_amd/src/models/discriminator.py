@@ -19,9 +19,11 @@ dtype:
              gradients on fen_wgrad3x3 / fen_conv_first_wgrad, data gradients on mode-2 convs
              (block 2's epilogue applies block 1's LeakyReLU mask), and d(input) -- needed by
              the generator's adversarial step -- through a 64->16 conv (3 valid channels).
-The classifier head (Flatten -> Linear(32768,1024) -> LeakyReLU -> Linear(1024,1)) is two
-plain GEMMs on hipBLASLt through torch.nn.functional.linear.  use_bn=False is not wired on
-the HIP path (the reference's factory always builds use_bn=True).
+The classifier head (Flatten -> Linear(32768,1024) -> LeakyReLU -> Linear(1024,1), and the
+optional sigmoid) is one autograd Function over fen_dhead_fwd / fen_dhead_bwd (disc.hip): the
+first layer on fp32 MFMAs in k-splits summed in fixed order, its backward one pass over the
+weight (d(input) and the weight gradient together).  use_bn=False is not wired on the HIP path
+(the reference's factory always builds use_bn=True).
 """
 from __future__ import annotations
 
@@ -30,7 +32,6 @@ from typing import List
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 _DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
 _SLOPE = 0.2
@@ -182,6 +183,53 @@ class _DFeatures(torch.autograd.Function):
         return (dx, None, *out)
 
 
+def _dhead_forward(h, w1, b1, w2, b2, sigmoid):
+    """fen_dhead_fwd: (pre-activation [B, N], score [B, 1]) of the classifier head."""
+    from ..hip import lib as L
+    from ..hip.program import ptr
+    B, K = h.shape
+    N = w1.shape[0]
+    pre = torch.empty(B, N, device=h.device)
+    y = torch.empty(B, 1, device=h.device)
+    work = torch.empty(L.load().fen_dhead_work_floats(B, K, N), device=h.device)
+    L.check(L.load().fen_dhead_fwd(B, K, N, ptr(h), ptr(w1.detach()), ptr(b1.detach()), ptr(w2.detach()),
+                                   ptr(b2.detach()), _SLOPE, int(sigmoid), ptr(pre), ptr(y), ptr(work),
+                                   torch.cuda.current_stream().cuda_stream), "dhead_fwd")
+    return pre, y
+
+
+class _DHead(torch.autograd.Function):
+    """The classifier head on the C-ABI's fen_dhead_fwd / fen_dhead_bwd (discriminator.py:85-90,
+    131-132): Linear(K, N) -> LeakyReLU(0.2) -> Linear(N, 1) (-> sigmoid), fp32."""
+
+    @staticmethod
+    def forward(fctx, h, w1, b1, w2, b2, sigmoid):
+        h = h.detach().contiguous()
+        pre, y = _dhead_forward(h, w1, b1, w2, b2, sigmoid)
+        fctx.save_for_backward(h, w1, w2, pre, y)
+        fctx.sigmoid = bool(sigmoid)
+        return y
+
+    @staticmethod
+    def backward(fctx, gy):
+        from ..hip import lib as L
+        from ..hip.program import ptr
+        h, w1, w2, pre, y = fctx.saved_tensors
+        B, K = h.shape
+        N = w1.shape[0]
+        gy = gy.detach().float().contiguous()
+        dx = torch.empty_like(h) if fctx.needs_input_grad[0] else None
+        dw1 = torch.empty_like(w1)
+        db1 = torch.empty(N, device=h.device)
+        dw2 = torch.empty_like(w2)
+        db2 = torch.empty(1, device=h.device)
+        work = torch.empty(L.load().fen_dhead_work_floats(B, K, N), device=h.device)
+        L.check(L.load().fen_dhead_bwd(B, K, N, ptr(h), ptr(w1.detach()), ptr(pre), ptr(w2.detach()), ptr(y), ptr(gy),
+                                       _SLOPE, int(fctx.sigmoid), ptr(dx), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2),
+                                       ptr(work), torch.cuda.current_stream().cuda_stream), "dhead_bwd")
+        return dx, dw1, db1, dw2, db2, None
+
+
 class VGGStyleDiscriminator(nn.Module):
     """VGG-style discriminator for 256x256 images (discriminator.py:12-151)."""
 
@@ -283,18 +331,16 @@ class VGGStyleDiscriminator(nn.Module):
         if x.shape[1] != 3 or x.shape[2] % 32 or x.shape[3] % 32:
             raise ValueError("input must be (B, 3, H, W) with H, W multiples of 32")
         feats = _DFeatures.apply(x, self, *self._feature_params())
-        h = F.leaky_relu(self.head_preactivation(feats.flatten(1)), 0.2)
-        lin2 = self.classifier[3]
-        out = F.linear(h, lin2.weight, lin2.bias)
-        if self.use_sigmoid:
-            out = torch.sigmoid(out)
-        return out
+        lin1, lin2 = self.classifier[1], self.classifier[3]
+        return _DHead.apply(feats.flatten(1), lin1.weight, lin1.bias, lin2.weight, lin2.bias, self.use_sigmoid)
 
     def head_preactivation(self, h: torch.Tensor) -> torch.Tensor:
         """The classifier's hidden layer before its LeakyReLU, Linear(32768, 1024) of the
-        flattened features, exactly as forward computes it (tests read its branches)."""
-        lin1 = self.classifier[1]
-        return F.linear(h, lin1.weight, lin1.bias)
+        flattened features, exactly as forward computes it (the same fen_dhead_fwd launch;
+        tests read its branches)."""
+        lin1, lin2 = self.classifier[1], self.classifier[3]
+        return _dhead_forward(h.detach().float().contiguous(), lin1.weight, lin1.bias, lin2.weight, lin2.bias,
+                              self.use_sigmoid)[0]
 
     def get_model_info(self) -> dict:
         total_params = sum(p.numel() for p in self.parameters())

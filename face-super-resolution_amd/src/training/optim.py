@@ -114,3 +114,54 @@ class FusedAdamW:
         self.scal[2] = step
         if sd.get("param_groups"):
             self.set_lr(sd["param_groups"][0]["lr"])
+
+
+class HipAdamW(torch.optim.AdamW):
+    """torch.optim.AdamW whose step runs as two HIP launches over every parameter tensor
+    (fen_adamw_multi) instead of torch's multi-tensor passes: the discriminator's optimizer_d
+    (reference trainer.py:230-250, 446-451).  Same constructor, param_groups, per-parameter state
+    (exp_avg, exp_avg_sq, a float32 step tensor on the device: torch's capturable form) and
+    state_dict, so schedulers, checkpoints and the captured GAN iteration see a torch AdamW.
+    amsgrad / maximize / differentiable groups fall back to torch's own step."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, **kw):
+        kw.setdefault("capturable", True)
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, **kw)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            if group.get("amsgrad") or group.get("maximize") or group.get("differentiable"):
+                raise NotImplementedError("HipAdamW: amsgrad / maximize / differentiable groups")
+            jobs = []
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse or p.dtype != torch.float32 or not p.is_cuda:
+                    raise RuntimeError("HipAdamW: dense fp32 GPU parameters only")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                elif not (torch.is_tensor(st["step"]) and st["step"].is_cuda):
+                    st["step"] = torch.tensor(float(st["step"]), dtype=torch.float32, device=p.device)
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                for t in (p, st["exp_avg"], st["exp_avg_sq"]):
+                    if not t.is_contiguous():
+                        raise RuntimeError("HipAdamW: contiguous parameters and moments only")
+                jobs.append(L.AdamwJob(ptr(p), ptr(g), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), ptr(st["step"]),
+                                       p.numel()))
+            b1, b2 = group["betas"]
+            lib = L.load()
+            for i in range(0, len(jobs), 48):
+                chunk = jobs[i:i + 48]
+                arr = (L.AdamwJob * len(chunk))(*chunk)
+                L.check(lib.fen_adamw_multi(len(chunk), arr, float(group["lr"]), float(b1), float(b2),
+                                            float(group["eps"]), float(group["weight_decay"]),
+                                            torch.cuda.current_stream().cuda_stream), "adamw_multi")
+        return loss

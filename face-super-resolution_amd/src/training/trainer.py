@@ -36,7 +36,7 @@ from ..hip.engine import FENEngine, flatten_params
 from ..hip.lib import check_strip_status
 from ..hip.program import Ctx, ptr
 from .dp import broadcast_arena
-from .optim import FusedAdamW, adamw_state, bump_versions, state_view
+from .optim import FusedAdamW, HipAdamW, adamw_state, bump_versions, state_view
 
 
 @dataclass
@@ -178,8 +178,9 @@ class Trainer:
             from ..models.discriminator import GANLoss
             self.discriminator = discriminator.to(self.device)
             self.gan_loss = gan_loss.to(self.device) if gan_loss is not None else GANLoss(self.config.gan_type)
-            self.optimizer_d = torch.optim.AdamW(self.discriminator.parameters(), lr=self.config.d_learning_rate,
-                                                 weight_decay=self.config.d_weight_decay)
+            # torch.optim.AdamW's state and format, its step on the HIP multi-tensor kernel
+            self.optimizer_d = HipAdamW(self.discriminator.parameters(), lr=self.config.d_learning_rate,
+                                        weight_decay=self.config.d_weight_decay)
             self._make_d_capturable()
         self._gan_graph: Optional[dict] = None
         self._gan_eager_left = 2
@@ -279,7 +280,8 @@ class Trainer:
         """The content loss: CombinedLoss returns (loss, components) (combined.py:158-203), a
         plain criterion a tensor; L1 without a loss function."""
         if self.loss_fn is None:
-            return F.l1_loss(sr, hr)
+            from ..losses import L1Loss
+            return L1Loss()(sr, hr)
         out = self.loss_fn(sr, hr)
         return out[0] if isinstance(out, tuple) else out
 

@@ -528,6 +528,21 @@ int fen_adamw(size_t n, float* p, const float* g, float* m, float* v, const floa
               float beta1, float beta2, float eps, void* stream);
 /* y[i] *= s  (DP gradient averaging helper)                                                 */
 int fen_scale(size_t n, float* y, float s, void* stream);
+/* torch.optim.AdamW.step (amsgrad / maximize off) over up to 48 separate fp32 tensors in two
+ * launches -- the discriminator's optimizer_d (reference trainer.py:230-250, 446-451): per
+ * tensor p, its gradient g, exp_avg m, exp_avg_sq v (n elements each) and a device step count
+ * (torch's capturable state, incremented first).  p = p (1 - lr wd) - lr / (1 - b1^t) m' /
+ * (sqrt(v') / sqrt(1 - b2^t) + eps), m' = lerp(m, g, 1 - b1), v' = b2 v + (1 - b2) g^2.       */
+typedef struct {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    float* step;
+    size_t n;
+} fen_adamw_job;
+int fen_adamw_multi(int njobs, const fen_adamw_job* jobs, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, void* stream);
 
 /* ---- VGG19 perceptual loss (src/losses/perceptual.py:13-169), frozen feature extractor ----
  * The convs run on fen_conv3x3 (ReLU = FEN_EPI_PRELU with zero slopes; its backward =
@@ -543,6 +558,12 @@ int fen_maxpool2_bwd_relu(int dtype, int B, int H, int W, int C, const void* dy,
  * |p - t| (l2 = 0: nn.L1Loss) or (p - t)^2 (l2 = 1: nn.MSELoss); g (n elements) =
  * (accumulate ? g : 0) + scale * d/dp (sign(p - t) or 2 (p - t)); scale = weight / n.       */
 int fen_feat_loss_parts(void);
+/* mean |pred - target| over n fp32 elements (nn.L1Loss, losses/combined.py:38-47): part
+ * [fen_feat_loss_parts()] = per-block sums of |p - t| (fen_colsum with scale 1/n gives the loss);
+ * grad (NULL: none) = scale * (gscale ? *gscale : 1) * sign(p - t), gscale a device scalar (the
+ * upstream gradient of the loss: no host sync).                                              */
+int fen_l1_loss(size_t n, const float* pred, const float* target, const float* gscale, float scale, float* grad,
+                float* part, void* stream);
 int fen_feat_loss(int dtype, size_t n, const void* f, int l2, float scale, void* g, int accumulate, float* part,
                   void* stream);
 
@@ -606,6 +627,22 @@ int fen_s2d2(int dtype, int B, int H, int W, int C, const void* x, void* y, int 
  * zeros where no tap lands) and the OIHW gradient back from the phase-major one (gather = 1)  */
 int fen_s2d_filter(int Cout, int C, const float* src, float* dst, int gather, void* stream);
 int fen_zero_insert2(int dtype, int B, int Ho, int Wo, int C, const void* dy, void* out, void* stream);
+
+/* The discriminator's classifier head (discriminator.py:85-90, replaces its two nn.Linear and the
+ * LeakyReLU between them; use_sigmoid 131-132), fp32: x [B][K] (the flattened NCHW features),
+ * w1 [N][K], b1 [N], w2 [N] (= classifier.3.weight [1][N]), b2 [1].
+ * fwd: pre [B][N] = x w1^T + b1 (kept for the backward), y [B] = LeakyReLU(pre, slope) w2 + b2
+ *      (sigmoid = 1: its sigmoid).
+ * bwd: gy [B] = dL/dy -> dx [B][K] (NULL: skipped), dw1 [N][K], db1 [N], dw2 [N], db2 [1], all
+ *      written (not accumulated).
+ * K a multiple of 256, N a multiple of 128 up to 1024 (else FEN_EUNSUPPORTED); work: fen_dhead_work_floats()
+ * floats.  Fixed-order reductions: deterministic.                                             */
+size_t fen_dhead_work_floats(int B, int K, int N);
+int fen_dhead_fwd(int B, int K, int N, const float* x, const float* w1, const float* b1, const float* w2,
+                  const float* b2, float slope, int sigmoid, float* pre, float* y, float* work, void* stream);
+int fen_dhead_bwd(int B, int K, int N, const float* x, const float* w1, const float* pre, const float* w2,
+                  const float* y, const float* gy, float slope, int sigmoid, float* dx, float* dw1, float* db1,
+                  float* dw2, float* db2, float* work, void* stream);
 
 /* A status word for fen_group_strip / fen_group_strip_bwd `status`: one zeroed int in
  * host-mapped, coherent pinned memory (hipHostMalloc, 64 B), allocated on the first call for

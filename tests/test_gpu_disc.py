@@ -66,3 +66,40 @@ def test_discriminator_vs_reference(golden, precision):
     with torch.no_grad():
         oe = d(torch.from_numpy(g["x"]).to(DEV))
     assert _rel(oe.cpu(), g["out_eval"]) <= (1e-4 if fp32 else 5e-2)
+
+
+@pytest.mark.parametrize("B,sigmoid", [(2, False), (16, False), (20, True)])
+def test_classifier_head_vs_float64(B, sigmoid):
+    """The HIP classifier head (fen_dhead_fwd / fen_dhead_bwd: Linear(32768, 1024) -> LeakyReLU(0.2)
+    -> Linear(1024, 1) [-> sigmoid], discriminator.py:85-90,131-132) against torch float64 on the
+    same fp32 operands, at the bench's D input (256: K = 512 x 8 x 8); B = 20 takes two sample
+    chunks in the backward.  Score, input gradient and every parameter gradient within rel 1e-5;
+    two runs bit-identical."""
+    import torch.nn.functional as F
+    from src.models.discriminator import _DHead
+    K, N = 32768, 1024
+    g = torch.Generator().manual_seed(11)
+    h = (torch.randn(B, K, generator=g) * 0.5).to(DEV)
+    w1 = (torch.randn(N, K, generator=g) * (2.0 / K) ** 0.5).to(DEV)
+    b1 = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    w2 = (torch.randn(1, N, generator=g) * (2.0 / N) ** 0.5).to(DEV)
+    b2 = (torch.randn(1, generator=g) * 0.1).to(DEV)
+    r = torch.randn(B, 1, generator=g).to(DEV)
+    outs = []
+    for _ in range(2):
+        leaves = [t.clone().requires_grad_(True) for t in (h, w1, b1, w2, b2)]
+        y = _DHead.apply(*leaves, sigmoid)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        outs.append([y.detach()] + [t.grad for t in leaves])
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    l64 = [t.detach().double().cpu().requires_grad_(True) for t in (h, w1, b1, w2, b2)]
+    y64 = F.linear(F.leaky_relu(F.linear(l64[0], l64[1], l64[2]), 0.2), l64[3], l64[4])
+    if sigmoid:
+        y64 = torch.sigmoid(y64)
+    (y64 * r.double().cpu()).sum().backward()
+    ref = [y64.detach()] + [t.grad for t in l64]
+    for name, a, b in zip(("y", "dh", "dw1", "db1", "dw2", "db2"), outs[0], ref):
+        e = _rel(a.cpu().numpy(), b.numpy())
+        assert e <= 1e-5, (name, e)

@@ -9,7 +9,7 @@ for l in ${VARIANTS:-}; do
   FEN_HIP_LIB=$V/libfen_hip_$l.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_conv_wide.py > gpurun_out/convv/t_wide_$l.log 2>&1
   rc=$?; echo "$l wide tests rc=$rc: $(tail -1 gpurun_out/convv/t_wide_$l.log)"
 done
-timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_vgg.py tests/test_gpu_perceptual_train.py tests/test_gpu_disc.py tests/test_gpu_gan_step.py tests/test_gpu_bench_legs.py > gpurun_out/convv/t_legs.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_vgg.py tests/test_gpu_perceptual_train.py tests/test_gpu_disc.py tests/test_gpu_gan_step.py tests/test_gpu_gan_capture.py tests/test_gpu_rccl.py tests/test_gpu_bench_legs.py > gpurun_out/convv/t_legs.log 2>&1
 rc=$?; echo "leg tests rc=$rc: $(tail -1 gpurun_out/convv/t_legs.log)"; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|error" gpurun_out/convv/t_legs.log | head -20; exit $rc; }
 for rep in 1 2; do
   for l in prod ${VARIANTS:-} ${TIMEONLY:-}; do
