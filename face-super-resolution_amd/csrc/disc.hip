@@ -294,6 +294,92 @@ __global__ __launch_bounds__(256) void k_zero_insert2(int B, int Ho, int Wo, int
     *(uint4*)(out + p * C + g * V) = v;
 }
 
+// The same two elementwise passes with each thread on one fixed 16-B channel group (G = C / V
+// groups, 256 / G pixel lanes, BN_PPT pixels per thread with their loads in flight): the group's
+// per-channel operands are loaded into registers once per thread, not per vector (the forms
+// above index them per vector with a 64-bit modulo).  Arithmetic unchanged: bit-identical.
+constexpr int BN_PPT = 4;
+template <typename T>
+__global__ __launch_bounds__(256) void k_bn_apply_g(size_t npx, int C, const T* __restrict__ y,
+                                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float slope, T* __restrict__ out) {
+    constexpr int V = 16 / sizeof(T);
+    const int G = C / V, lanes = 256 / G;
+    const int g = threadIdx.x % G, pl = threadIdx.x / G;
+    if (pl >= lanes) return;
+    float sm[V], sr[V], sg[V], sb[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const int c = g * V + j;
+        sm[j] = mean[c], sr[j] = rstd[c], sg[j] = gamma[c], sb[j] = beta[c];
+    }
+    const size_t p0 = (size_t)blockIdx.x * lanes * BN_PPT + pl;
+    uint4 d[BN_PPT];
+#pragma unroll
+    for (int k = 0; k < BN_PPT; ++k) {
+        const size_t p = p0 + (size_t)k * lanes;
+        if (p < npx) d[k] = *(const uint4*)(y + p * C + g * V);
+    }
+#pragma unroll
+    for (int k = 0; k < BN_PPT; ++k) {
+        const size_t p = p0 + (size_t)k * lanes;
+        if (p >= npx) break;
+        float v[V];
+        unpack16<T>(d[k], v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float z = (v[j] - sm[j]) * sr[j] * sg[j] + sb[j];
+            v[j] = z > 0.f ? z : slope * z;
+        }
+        *(uint4*)(out + p * C + g * V) = pack16<T>(v);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_g(size_t npx, int C, const T* __restrict__ da,
+                                                        const T* __restrict__ y, const float* __restrict__ stat,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        float slope, const float* __restrict__ red2,
+                                                        T* __restrict__ dy) {
+    constexpr int V = 16 / sizeof(T);
+    const int G = C / V, lanes = 256 / G;
+    const int g = threadIdx.x % G, pl = threadIdx.x / G;
+    if (pl >= lanes) return;
+    float mu[V], rs[V], ga[V], be[V], s0[V], s1[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const int c = g * V + j;
+        mu[j] = stat[c], rs[j] = stat[C + c], ga[j] = gamma[c], be[j] = beta[c], s0[j] = red2[c], s1[j] = red2[C + c];
+    }
+    const float inv_n = 1.f / (float)npx;
+    const size_t p0 = (size_t)blockIdx.x * lanes * BN_PPT + pl;
+    uint4 dd[BN_PPT], yy[BN_PPT];
+#pragma unroll
+    for (int k = 0; k < BN_PPT; ++k) {
+        const size_t p = p0 + (size_t)k * lanes;
+        if (p < npx) {
+            dd[k] = *(const uint4*)(da + p * C + g * V);
+            yy[k] = *(const uint4*)(y + p * C + g * V);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < BN_PPT; ++k) {
+        const size_t p = p0 + (size_t)k * lanes;
+        if (p >= npx) break;
+        float dv[V], yv[V];
+        unpack16<T>(dd[k], dv);
+        unpack16<T>(yy[k], yv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float xh = (yv[j] - mu[j]) * rs[j];
+            const float z = ga[j] * xh + be[j];
+            const float dz = z > 0.f ? dv[j] : slope * dv[j];
+            dv[j] = ga[j] * rs[j] * (dz - inv_n * s0[j] - xh * inv_n * s1[j]);
+        }
+        *(uint4*)(dy + p * C + g * V) = pack16<T>(dv);
+    }
+}
 }  // namespace
 
 #define STREAM ((hipStream_t)stream)
@@ -328,6 +414,21 @@ extern "C" int fen_bn_apply(int dtype, size_t npx, int C, const void* y, const f
                             const float* gamma, const float* beta, float slope, void* out, void* stream) {
     if (!y || !mean || !rstd || !gamma || !beta || !out || C % 8) return FEN_EINVAL;
     if (C > 1024) return FEN_EUNSUPPORTED;
+    {
+        const int G = C / (dtype == FEN_F32 ? 4 : 8);
+        if (G <= 256 && 256 % G == 0 && (dtype == FEN_BF16 || dtype == FEN_F32)) {
+            const size_t per = (size_t)(256 / G) * BN_PPT;
+            const unsigned nb = (unsigned)((npx + per - 1) / per);
+            if (dtype == FEN_BF16)
+                hipLaunchKernelGGL(k_bn_apply_g<bf16>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const bf16*)y, mean, rstd,
+                                   gamma, beta, slope, (bf16*)out);
+            else
+                hipLaunchKernelGGL(k_bn_apply_g<float>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const float*)y, mean,
+                                   rstd, gamma, beta, slope, (float*)out);
+            FEN_CHECK_LAUNCH();
+            return FEN_OK;
+        }
+    }
     if (dtype == FEN_BF16) {
         const size_t nv = npx * C / 8;
         hipLaunchKernelGGL(k_bn_apply<bf16>, dim3(nblk(nv, 256 * BN_NPT)), dim3(256), 0, STREAM, nv, C, (const bf16*)y,
@@ -362,6 +463,21 @@ extern "C" int fen_bn_bwd(int dtype, size_t npx, int C, const void* da, const vo
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, C, work, dgamma, dbeta, red2,
                        accumulate);
     FEN_CHECK_LAUNCH();
+    {
+        const int G = C / (dtype == FEN_F32 ? 4 : 8);
+        if (G <= 256 && 256 % G == 0) {
+            const size_t per = (size_t)(256 / G) * BN_PPT;
+            const unsigned nb = (unsigned)((npx + per - 1) / per);
+            if (dtype == FEN_BF16)
+                hipLaunchKernelGGL(k_bn_bwd_apply_g<bf16>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const bf16*)da,
+                                   (const bf16*)y, stat, gamma, beta, slope, red2, (bf16*)dy);
+            else
+                hipLaunchKernelGGL(k_bn_bwd_apply_g<float>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const float*)da,
+                                   (const float*)y, stat, gamma, beta, slope, red2, (float*)dy);
+            FEN_CHECK_LAUNCH();
+            return FEN_OK;
+        }
+    }
     if (dtype == FEN_BF16) {
         const size_t nv = npx * C / 8;
         hipLaunchKernelGGL(k_bn_bwd_apply<bf16>, dim3(nblk(nv)), dim3(256), 0, STREAM, nv, npx, C, (const bf16*)da,

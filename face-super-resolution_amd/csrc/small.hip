@@ -1858,15 +1858,22 @@ struct AdamJobK {
     float* step;
     long long n;
     int blk0;
+    int vec;                                 // all four 16-B aligned
 };
 struct AdamJobs {
     int n;
-    float lr, b1, b2, eps, wd, omb1, omb2;   // 1 - b1, 1 - b2 rounded from double (torch's lerp weight)
+    float lr, b1, b2, eps, wd, omb1, omb2;   // 1 - b1, 1 - b2 as the caller rounds them (torch: from the Python doubles)
     AdamJobK j[ADAMW_MAXJ];
 };
 __global__ void k_adamw_steps(const AdamJobs jobs) {
     const int i = threadIdx.x;
     if (i < jobs.n) jobs.j[i].step[0] += 1.f;
+}
+__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v, float decay, float step_size, float rbc2,
+                                           const AdamJobs& jobs) {
+    m = m + jobs.omb1 * (g - m);                                   // lerp
+    v = v * jobs.b2 + jobs.omb2 * g * g;
+    p = p * decay - step_size * m / (sqrtf(v) * rbc2 + jobs.eps);
 }
 __global__ __launch_bounds__(256) void k_adamw_multi(const AdamJobs jobs) {
     int ji = 0;
@@ -1875,20 +1882,29 @@ __global__ __launch_bounds__(256) void k_adamw_multi(const AdamJobs jobs) {
     const long long i0 = ((long long)(blockIdx.x - jb.blk0) * 256 + threadIdx.x) * 4;
     if (i0 >= jb.n) return;
     const float step = jb.step[0];
-    const float lr = jobs.lr, b1 = jobs.b1, b2 = jobs.b2;
+    const float lr = jobs.lr;
     const float decay = 1.f - lr * jobs.wd;
-    const float step_size = lr / (1.f - powf(b1, step));
-    const float rbc2 = 1.f / sqrtf(1.f - powf(b2, step));
+    const float step_size = lr / (1.f - powf(jobs.b1, step));
+    const float rbc2 = 1.f / sqrtf(1.f - powf(jobs.b2, step));
+    if (jb.n - i0 >= 4 && jb.vec) {
+        // 16-B accesses (every tensor of the job 16-B aligned: fen_adamw_multi checks)
+        float4 p = *(const float4*)(jb.p + i0), g = *(const float4*)(jb.g + i0);
+        float4 m = *(const float4*)(jb.m + i0), v = *(const float4*)(jb.v + i0);
+        adamw_elem(p.x, g.x, m.x, v.x, decay, step_size, rbc2, jobs);
+        adamw_elem(p.y, g.y, m.y, v.y, decay, step_size, rbc2, jobs);
+        adamw_elem(p.z, g.z, m.z, v.z, decay, step_size, rbc2, jobs);
+        adamw_elem(p.w, g.w, m.w, v.w, decay, step_size, rbc2, jobs);
+        *(float4*)(jb.p + i0) = p;
+        *(float4*)(jb.m + i0) = m;
+        *(float4*)(jb.v + i0) = v;
+        return;
+    }
     const int cnt = jb.n - i0 >= 4 ? 4 : (int)(jb.n - i0);
     for (int e = 0; e < cnt; ++e) {
         const long long i = i0 + e;
-        const float gi = jb.g[i];
-        const float mi = jb.m[i] + jobs.omb1 * (gi - jb.m[i]);    // lerp
-        const float vi = jb.v[i] * b2 + jobs.omb2 * gi * gi;
-        const float denom = sqrtf(vi) * rbc2 + jobs.eps;
-        jb.p[i] = jb.p[i] * decay - step_size * mi / denom;
-        jb.m[i] = mi;
-        jb.v[i] = vi;
+        float p = jb.p[i], m = jb.m[i], v = jb.v[i];
+        adamw_elem(p, jb.g[i], m, v, decay, step_size, rbc2, jobs);
+        jb.p[i] = p, jb.m[i] = m, jb.v[i] = v;
     }
 }
 __global__ void k_scale(size_t n, float* y, float s) {
@@ -2409,17 +2425,19 @@ extern "C" int fen_adamw(size_t n, float* p, const float* g, float* m, float* v,
     return FEN_OK;
 }
 
-extern "C" int fen_adamw_multi(int njobs, const fen_adamw_job* jobs, float lr, float beta1, float beta2, float eps,
-                               float weight_decay, void* stream) {
+extern "C" int fen_adamw_multi(int njobs, const fen_adamw_job* jobs, float lr, float beta1, float beta2,
+                               float one_minus_beta1, float one_minus_beta2, float eps, float weight_decay,
+                               void* stream) {
     if (njobs <= 0 || njobs > ADAMW_MAXJ || !jobs) return FEN_EINVAL;
     AdamJobs k;
     k.n = njobs, k.lr = lr, k.b1 = beta1, k.b2 = beta2, k.eps = eps, k.wd = weight_decay;
-    k.omb1 = (float)(1.0 - (double)beta1), k.omb2 = (float)(1.0 - (double)beta2);
+    k.omb1 = one_minus_beta1, k.omb2 = one_minus_beta2;
     long long blk = 0;
     for (int i = 0; i < njobs; ++i) {
         const fen_adamw_job& j = jobs[i];
         if (!j.p || !j.g || !j.m || !j.v || !j.step || j.n <= 0) return FEN_EINVAL;
-        k.j[i] = AdamJobK{j.p, j.g, j.m, j.v, j.step, (long long)j.n, (int)blk};
+        const bool vec = !(((uintptr_t)j.p | (uintptr_t)j.g | (uintptr_t)j.m | (uintptr_t)j.v) & 15);
+        k.j[i] = AdamJobK{j.p, j.g, j.m, j.v, j.step, (long long)j.n, (int)blk, vec ? 1 : 0};
         blk += ((long long)j.n + 1023) / 1024;
         if (blk >= (1ll << 30)) return FEN_EUNSUPPORTED;
     }

@@ -158,10 +158,13 @@ class HipAdamW(torch.optim.AdamW):
                                        p.numel()))
             b1, b2 = group["betas"]
             lib = L.load()
+            # the kernel writes the parameters behind torch's version counters: bump them, so
+            # the packed-weight caches keyed on p._version (the discriminator's) re-pack
+            bump_versions([p for p in group["params"] if p.grad is not None])
             for i in range(0, len(jobs), 48):
                 chunk = jobs[i:i + 48]
                 arr = (L.AdamwJob * len(chunk))(*chunk)
-                L.check(lib.fen_adamw_multi(len(chunk), arr, float(group["lr"]), float(b1), float(b2),
+                L.check(lib.fen_adamw_multi(len(chunk), arr, float(group["lr"]), float(b1), float(b2), 1.0 - b1, 1.0 - b2,
                                             float(group["eps"]), float(group["weight_decay"]),
                                             torch.cuda.current_stream().cuda_stream), "adamw_multi")
         return loss

@@ -532,7 +532,8 @@ int fen_scale(size_t n, float* y, float s, void* stream);
  * launches -- the discriminator's optimizer_d (reference trainer.py:230-250, 446-451): per
  * tensor p, its gradient g, exp_avg m, exp_avg_sq v (n elements each) and a device step count
  * (torch's capturable state, incremented first).  p = p (1 - lr wd) - lr / (1 - b1^t) m' /
- * (sqrt(v') / sqrt(1 - b2^t) + eps), m' = lerp(m, g, 1 - b1), v' = b2 v + (1 - b2) g^2.       */
+ * (sqrt(v') / sqrt(1 - b2^t) + eps), m' = lerp(m, g, 1 - b1), v' = b2 v + (1 - b2) g^2; 1 - b1
+ * and 1 - b2 passed as the caller rounds them (torch: float(1 - beta) of the Python doubles).  */
 typedef struct {
     float* p;
     const float* g;
@@ -541,8 +542,8 @@ typedef struct {
     float* step;
     size_t n;
 } fen_adamw_job;
-int fen_adamw_multi(int njobs, const fen_adamw_job* jobs, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, void* stream);
+int fen_adamw_multi(int njobs, const fen_adamw_job* jobs, float lr, float beta1, float beta2, float one_minus_beta1,
+                    float one_minus_beta2, float eps, float weight_decay, void* stream);
 
 /* ---- VGG19 perceptual loss (src/losses/perceptual.py:13-169), frozen feature extractor ----
  * The convs run on fen_conv3x3 (ReLU = FEN_EPI_PRELU with zero slopes; its backward =

@@ -3,6 +3,8 @@ torch.optim.AdamW itself -- the discriminator's optimizer_d (reference trainer.p
 446-451).  Several steps with weight decay on tensors of mixed sizes (a tail of 1..3 elements,
 one larger than a block), parameters without a gradient skipped; every tensor within fp32
 rounding of torch's; state_dict interchangeable both ways; captured in a hipGraph it replays."""
+import copy
+
 import pytest
 import torch
 
@@ -47,7 +49,9 @@ def test_hip_adamw_matches_torch(wd):
     with torch.no_grad():
         for pc, pa in zip(c, a):
             pc.copy_(pa)
-    oc.load_state_dict(oa.state_dict())
+    # (a copy, as a checkpoint is: torch's load_state_dict keeps same-device tensors as they are,
+    # so a live state_dict would alias oa's moments)
+    oc.load_state_dict(copy.deepcopy(oa.state_dict()))
     _grads(a, 7)
     _grads(c, 7)
     oa.step()
