@@ -67,6 +67,19 @@ static void conv_refusals() {
     EXPECT(fen_conv3x3(&d, nullptr) == FEN_EINVAL);
     d.s2d_in = 0, d.dtype = 7;
     EXPECT(fen_conv3x3(&d, nullptr) == FEN_EINVAL);
+    d.dtype = FEN_BF16, d.pre_in = nullptr, d.part = nullptr;
+    d.epi = FEN_EPI_RELU_BWD;
+    EXPECT(fen_conv3x3(&d, nullptr) == FEN_EINVAL);                      // no pre_in
+    d.pre_in = fake(1), d.part = (float*)fake(2);
+    d.epi = FEN_EPI_RELU_BWD | FEN_EPI_PRELU_BWD;
+    d.alpha = (const float*)fake(3);
+    EXPECT(fen_conv3x3(&d, nullptr) == FEN_EUNSUPPORTED);
+    d.epi = 1 << 20;
+    EXPECT(fen_conv3x3(&d, nullptr) == FEN_EINVAL);                      // unknown flag
+    d.epi = 0, d.y_images = 1;
+    EXPECT(fen_conv3x3(&d, nullptr) == FEN_EINVAL);                      // y_images without y_pool
+    d.y_images = 0, d.y_pool = fake(4);
+    EXPECT(fen_conv3x3(&d, nullptr) == FEN_EUNSUPPORTED);                // y_pool without PReLU
 }
 
 static void wgrad_tables() {

@@ -28,6 +28,8 @@
 
 #include <type_traits>
 
+extern "C" int fen_maxpool2(int dtype, int B, int H, int W, int C, const void* x, void* y, void* stream);   // vgg.hip
+
 namespace {
 
 // Diagnostic build only (-DFEN_STAMPS, tools/stamp_conv.py): per-block s_memrealtime /
@@ -108,6 +110,35 @@ __device__ __forceinline__ EpiConst<MT> epi_consts(const fen_conv_desc& d, int c
     return e;
 }
 
+// fen_conv_desc.y_pool: the 2x2 max pool fused into the store (compile-time key bit of the
+// persistent kernels' epilogue instantiations; VGG19's conv -> ReLU -> 'M', perceptual.py:50-53).
+constexpr int EPIC_MPOOL = 1 << 13;
+// A wave's tile piece: rows h0w + n (n < 4, h0w even) x columns w0 + c16 x channels cob0 + m*16
+// + 4q + r; o(m, n, r) = the stored activation.  Rows pool inside a lane, columns across lanes
+// c16 ^ 1 (DPP): the even lane of a pair keeps pooled row 0 and sends row 1, the odd lane the
+// reverse, so every lane stores one pooled pixel's 4 channels.  max commutes with the monotone
+// rounding to T, so this equals pooling the stored y (k_maxpool2).
+template <typename T, int MT, typename F>
+__device__ __forceinline__ void pool2_store(const fen_conv_desc& d, int b, int h0w, int w0, int cob0, int c16,
+                                            bool full, F&& o) {
+    const int H = d.H, W = d.W, Cout = d.Cout, Hp = H >> 1, Wp = W >> 1;
+    const bool odd = c16 & 1;
+    const int hp = (h0w >> 1) + (odd ? 1 : 0), wp = (w0 + c16) >> 1;
+    const bool ok = full || (2 * hp < H && 2 * wp < W);
+    char* base = (char*)d.y_pool + ((((size_t)b * Hp + hp) * Wp + wp) * Cout + cob0) * sizeof(T);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        float res[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float a0 = fmaxf(o(m, 0, r), o(m, 1, r)), a1 = fmaxf(o(m, 2, r), o(m, 3, r));
+            const float recv = dpp_f<0xB1>(odd ? a0 : a1);
+            res[r] = fmaxf(odd ? a1 : a0, recv);
+        }
+        if (ok && cob0 + m * 16 < Cout) st4<T>(base + m * 16 * sizeof(T), res);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // epilogue (shared by both kernels).  acc[m][n][r] = D[co = co0 + m*16 + 4q + r][pixel
 // (h0 + wave*4 + n, w0 + c16)].  `stage` (>= 32 KB LDS) enables the 16-bit LDS-staged
@@ -138,12 +169,13 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
     // EPIC >= 0: the epilogue mode is a compile-time constant (flags | residual count << 8),
     // so every branch on it folds away; -1: read it from the descriptor.
     constexpr bool CT = EPIC >= 0;
-    constexpr int NRES = CT ? (EPIC >> 8) : 3;
+    constexpr int NRES = CT ? ((EPIC >> 8) & 3) : 3;
+    constexpr bool MPOOL = CT && (EPIC & EPIC_MPOOL);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave % WR, wc = wave / WR;
     const int q = lane >> 4, c16 = lane & 15;
     const int H = d.H, W = d.W, Cout = d.Cout;
-    const int epi = CT ? (EPIC & 0xff) : d.epi;
+    const int epi = CT ? (EPIC & ~(0x300 | EPIC_MPOOL)) : d.epi;
     const int w_ = w0 + c16;
     const bool full = h0 + 16 <= H && w0 + 16 <= W;
 
@@ -214,7 +246,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
     // right behind it waited for each in turn
     typedef typename std::conditional<sizeof(T) == 2, uint2, uint4>::type RawV;
 #ifndef EPI_NOPF
-    const bool pin = epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT);
+    const bool pin = epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT | FEN_EPI_RELU_BWD);
 #else   // A/B only: the operands loaded per fragment in pass 1
     const bool pin = false;
 #endif
@@ -271,6 +303,16 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                         psum[m][r] += prelu_dalpha_f(v[r], pv[r]);
                         v[r] = prelu_bwd_f(v[r], pv[r], al4[r]);
                     }
+                }
+                if (epi & FEN_EPI_RELU_BWD) {
+                    float pv[4];
+#ifndef EPI_NOPF
+                    ld4<T>(&pvr[m][n], pv);
+#else
+                    ld4<T>((const char*)d.pre_in + oi * sizeof(T), pv);
+#endif
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = pv[r] > 0.f ? v[r] : 0.f;
                 }
                 if (epi & FEN_EPI_DOT) {
                     float pv[4];
@@ -388,6 +430,7 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
     for (int k = 0; k < 2; ++k) {
         void* dst = k == 0 ? d.y_pre : d.y;
         if (k == 0 && (!prelu || !dst)) continue;
+        if (MPOOL && d.y_images > 0 && b >= d.y_images) continue;   // (block-uniform)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
             const int cob = co0 + wc * CW + m * 16 + q * 4;
@@ -415,6 +458,11 @@ __device__ __forceinline__ int conv_epilogue(const fen_conv_desc& d, f32x4 (&acc
                 ++nst;
             }
         }
+    }
+    if constexpr (MPOOL) {
+        static_assert(NT == 4, "pool2_store: 4 rows per wave");
+        pool2_store<T, MT>(d, b, h0 + wr * NT, w0, co0 + wc * CW + q * 4, c16, full,
+                           [&](int m, int n, int r) { return final_v(acc[m][n][r], m, r, 1); });
     }
     return (full && !unshuf && co0 + COT <= Cout) ? nst : 0;
 }
@@ -721,12 +769,14 @@ constexpr int G_LDS = G_WBYTES + 2 * HALO_SLOT + 2 * 4 * 64 * 4 + 2 * 64 * 4;
 template <typename T, int EPIC>
 __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
     constexpr int MT = 4, NT = 4;
-    constexpr int NRES = EPIC >> 8;
-    constexpr int EPI = EPIC & 0xff;
+    constexpr int NRES = (EPIC >> 8) & 3;
+    constexpr int EPI = EPIC & ~(0x300 | EPIC_MPOOL);
+    constexpr bool MPOOL = EPIC & EPIC_MPOOL;
     constexpr bool PRELU = EPI & FEN_EPI_PRELU, PBWD = EPI & FEN_EPI_PRELU_BWD, POOL = EPI & FEN_EPI_POOL;
+    constexpr bool RBWD = EPI & FEN_EPI_RELU_BWD;
     constexpr bool SHUF = EPI & FEN_EPI_SHUFFLE, DOT = EPI & FEN_EPI_DOT;
     constexpr bool PART = POOL || PBWD || DOT;                // per-tile channel partials
-    constexpr bool PIN = PBWD || DOT;                         // reads pre_in
+    constexpr bool PIN = PBWD || DOT || RBWD;                 // reads pre_in
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* wts = smem;
     float* red = (float*)(smem + G_WBYTES + 2 * HALO_SLOT);   // [grp][wr][64]
@@ -904,6 +954,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                                 psum[m][r] += okf * prelu_dalpha_f(v, pr);
                                 v = prelu_bwd_f(v, pr, al4[r]);
                             }
+                            if constexpr (RBWD) v = pf[r] > 0.f ? v : 0.f;
                             if constexpr (POOL) psum[m][r] += okf * v;
                             if constexpr (DOT) psum[m][r] += okf * rnd16<T>(v) * pf[r];
                             acc[m][n][r] = v;
@@ -933,6 +984,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                         } else {
                             off = ((size_t)(b * H + h) * W + w) * Cout + cob;
                         }
+                        if (MPOOL && d.y_images > 0 && b >= d.y_images) continue;   // (block-uniform)
                         if (wpre) {
                             st4<T>((char*)d.y_pre + off * 2, v);
                             ++nst;
@@ -940,6 +992,11 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_g(const fen_conv_desc d) {
                         st4<T>((char*)d.y + off * 2, o);
                         ++nst;
                     }
+                }
+                if constexpr (MPOOL) {
+                    pool2_store<T, MT>(d, b, h0 + wr * NT, w0, co0 + 4 * q, c16, full, [&](int m, int n, int r) {
+                        return PRELU ? prelu_f(acc[m][n][r], cst[64 + m * 16 + 4 * q + r]) : acc[m][n][r];
+                    });
                 }
                 if constexpr (PART) {
                     float* rg = red + grp * 256 + wr * 64;
@@ -1525,6 +1582,24 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
             return FEN_EUNSUPPORTED;
     }
     if ((epi & FEN_EPI_UNSHUFFLE) && ((d->H | d->W) & 1)) return FEN_EINVAL;
+    if (d->y_pool) {
+        // the fused 2x2 max pool: bias + ReLU/PReLU stores of the persistent kernels; any other
+        // route stores every image of y and pools it in a k_maxpool2 pass
+        if constexpr (H16) {
+            constexpr int B_ = FEN_EPI_BIAS;
+            const bool dense = !d->res[0] && !d->res[1] && !d->res[2];
+            if (dense && epi == (B_ | FEN_EPI_PRELU) && d->Cout % 64 == 0 && conv_variant() == 0) {
+                if (persist) return launch_g<T, B_ | FEN_EPI_PRELU | EPIC_MPOOL>(d, s);
+                if (conv_v_ok(d)) return launch_v<T, B_ | FEN_EPI_PRELU | EPIC_MPOOL>(d, s);
+            }
+        }
+        fen_conv_desc d2 = *d;
+        d2.y_pool = nullptr;
+        d2.y_images = 0;
+        const int rc = conv_dispatch<T>(&d2, s);
+        if (rc != FEN_OK) return rc;
+        return fen_maxpool2(d->dtype, d->B, d->H, d->W, d->Cout, d->y, d->y_pool, s);
+    }
     if (d->Cout % 64 == 0) {
         if constexpr (H16) {
             if (persist) {
@@ -1546,6 +1621,7 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
                         case B_ | (1 << 8): return launch_g<T, B_ | (1 << 8)>(d, s);
                         case B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE: return launch_g<T, B_ | FEN_EPI_PRELU | FEN_EPI_SHUFFLE>(d, s);
                         case FEN_EPI_PRELU_BWD: return launch_p<T, 64, 4, 2, FEN_EPI_PRELU_BWD>(d, s);
+                        case FEN_EPI_RELU_BWD: return launch_g<T, FEN_EPI_RELU_BWD>(d, s);
                         case 0: return launch_g<T, 0>(d, s);
                         case 1 << 8: return launch_g<T, 1 << 8>(d, s);
                         case 2 << 8: return launch_g<T, 2 << 8>(d, s);
@@ -1580,6 +1656,7 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
                     case B_ | FEN_EPI_PRELU: return launch_v<T, B_ | FEN_EPI_PRELU>(d, s);
                     case B_: return launch_v<T, B_>(d, s);
                     case FEN_EPI_PRELU_BWD: return launch_v<T, FEN_EPI_PRELU_BWD>(d, s);
+                    case FEN_EPI_RELU_BWD: return launch_v<T, FEN_EPI_RELU_BWD>(d, s);
                     case 0: return launch_v<T, 0>(d, s);
                     default: break;   // (the runtime-mode epilogue spills at this wave shape: streamed kernel)
                 }
@@ -1613,8 +1690,16 @@ extern "C" int fen_conv3x3(const fen_conv_desc* d, void* stream) {
     const int epi = d->epi;
     if ((epi & FEN_EPI_BIAS) && !d->bias) return FEN_EINVAL;
     if ((epi & (FEN_EPI_PRELU | FEN_EPI_PRELU_BWD)) && !d->alpha) return FEN_EINVAL;
-    if ((epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT)) && !d->pre_in) return FEN_EINVAL;
+    if ((epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT | FEN_EPI_RELU_BWD)) && !d->pre_in) return FEN_EINVAL;
+    if (epi & ~0x10ff) return FEN_EINVAL;
+    if ((epi & FEN_EPI_RELU_BWD) &&
+        (epi & (FEN_EPI_PRELU_BWD | FEN_EPI_DOT | FEN_EPI_LAST | FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE)))
+        return FEN_EUNSUPPORTED;
     if ((epi & (FEN_EPI_POOL | FEN_EPI_PRELU_BWD | FEN_EPI_DOT)) && !d->part) return FEN_EINVAL;
+    if (d->y_images < 0 || d->y_images > d->B || (d->y_images && !d->y_pool)) return FEN_EINVAL;
+    if (d->y_pool && (!(epi & FEN_EPI_PRELU) || ((d->H | d->W) & 1) || d->s2d_in || d->s2d_out ||
+                      (epi & (FEN_EPI_SHUFFLE | FEN_EPI_UNSHUFFLE | FEN_EPI_LAST | FEN_EPI_POOL | FEN_EPI_DOT))))
+        return FEN_EUNSUPPORTED;
     // one partial-sum stream per launch
     {
         const int np = !!(epi & FEN_EPI_POOL) + !!(epi & FEN_EPI_PRELU_BWD) + !!(epi & FEN_EPI_DOT);

@@ -23,6 +23,7 @@ EPI_UNSHUFFLE = 16
 EPI_POOL = 32
 EPI_LAST = 64
 EPI_DOT = 128
+EPI_RELU_BWD = 4096
 
 
 class AdamwJob(Structure):
@@ -38,7 +39,7 @@ class ConvDesc(Structure):
         ("part", c_void_p), ("lr", c_void_p), ("scale", c_int), ("clamp", c_int), ("hr", c_void_p),
         ("dout", c_void_p), ("l1_scale", c_float), ("loss_part", c_void_p), ("debug", c_int),
         ("s2d_in", c_int), ("s2d_out", c_int),
-        ("pre_elide", c_int), ("post_in", c_void_p),
+        ("pre_elide", c_int), ("post_in", c_void_p), ("y_pool", c_void_p), ("y_images", c_int),
     ]
 
 

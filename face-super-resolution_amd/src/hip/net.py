@@ -161,7 +161,8 @@ class Weights:
 # --------------------------------------------------------------------------------------
 def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, y=None, y_pre=None,
          res: Sequence = (), pre_in=None, part=None, lr=None, scale=0, clamp=0, hr=None, dout=None,
-         l1_scale=0.0, loss_part=None, debug=0, s2d_in=0, s2d_out=0, pre_elide=0, post_in=None) -> None:
+         l1_scale=0.0, loss_part=None, debug=0, s2d_in=0, s2d_out=0, pre_elide=0, post_in=None,
+         y_pool=None, y_images=0) -> None:
     d = L.ConvDesc()
     d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = ctx.code, B, H, W, Cin, Cout
     d.x, d.w, d.bias = ptr(x), ptr(wpk), ptr(bias)
@@ -175,6 +176,7 @@ def conv(ctx: Ctx, x, wpk, B, H, W, Cin, Cout, *, bias=None, epi=0, alpha=None, 
     d.debug = debug
     d.s2d_in, d.s2d_out = s2d_in, s2d_out
     d.pre_elide, d.post_in = int(pre_elide), ptr(post_in)
+    d.y_pool, d.y_images = ptr(y_pool), int(y_images)
     ctx.emit("conv3x3", ctx.lib.fen_conv3x3, byref(d))
 
 

@@ -7,8 +7,8 @@ with bias + ReLU fused (PReLU epilogue with zero slopes; a feature layer keeps i
 pre-ReLU output through y_pre); max pools on fen_maxpool2.  The loss
 (weight x nn.L1Loss / nn.MSELoss of each requested layer, perceptual.py:155-167) and its
 gradient come from fen_feat_loss, and the backward runs on the pred half only: mode-2
-data gradients whose epilogue applies the ReLU mask (PReLU backward, zero slopes, pre_in =
-the saved ReLU output), fen_maxpool2_bwd_relu through the pools, and conv1_1's data
+data gradients whose epilogue applies the ReLU mask (FEN_EPI_RELU_BWD, pre_in = the saved
+ReLU output; no slope partials), fen_maxpool2_bwd_relu through the pools, and conv1_1's data
 gradient (weights pre-divided by the ImageNet std, so it yields d(pred)) added straight into
 the generator's dL/dsr buffer.  No weight gradients: the extractor is frozen
 (perceptual.py:60-64).
@@ -18,6 +18,7 @@ configs' conv3_4 / conv4_4) except conv1_1.  relu / pool names raise NotImplemen
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -41,6 +42,9 @@ VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512,
              512, 512, 512, 512, "M"]
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
+# A/B switch only: FEN_VGG_LEGACY=1 records round 5's form (PReLU-backward epilogues with slope
+# partials, k_maxpool2 passes) instead of FEN_EPI_RELU_BWD and the fused y_pool stores
+_LEGACY = os.environ.get("FEN_VGG_LEGACY", "0") == "1"
 
 
 def vgg19_convs() -> List[dict]:
@@ -129,10 +133,14 @@ class VGGPerceptual:
         return out
 
     # ------------------------------------------------------------------ program
-    def forward(self, x: torch.Tensor, ctx: Optional[Ctx] = None, upto: Optional[int] = None):
+    def forward(self, x: torch.Tensor, ctx: Optional[Ctx] = None, upto: Optional[int] = None,
+                keep_images: int = 0):
         """Record the extractor over NCHW fp32 x [N,3,H,W] up to conv index `upto` (default:
         the deepest feature).  Returns (acts, feats): per conv its ReLU output and geometry,
-        and {feature index: NHWC [N,h,w,C] pre-ReLU conv output}."""
+        and {feature index: NHWC [N,h,w,C] pre-ReLU conv output}.  A conv followed by a max pool
+        stores the pooled map from its epilogue (fen_conv_desc.y_pool, no k_maxpool2 pass) and
+        its own ReLU output only for the first `keep_images` images (0: all) -- the pred half,
+        whose pool masks the backward reads."""
         ctx = ctx or self.ctx
         N, _, H, W = x.shape
         last_idx = self.convs[-1]["idx"] if upto is None else upto
@@ -141,6 +149,7 @@ class VGGPerceptual:
         h, hh, ww = None, H, W
         for c in convs:
             i, cin, cout = c["idx"], c["cin"], c["cout"]
+            fuse = False
             is_feat, is_last = i in self.idx, i == last_idx
             if i == 0:
                 a = ctx.alloc((N, hh, ww, cout))
@@ -153,17 +162,24 @@ class VGGPerceptual:
                 conv(ctx, h, self.packed[(i, 0)], N, hh, ww, cin, cout, bias=self.p[f"features.{i}.bias"], y=z)
                 a = None
             else:
+                # (fen_conv3x3 fuses the pool into the 16-bit persistent kernels' store and pools
+                # in a k_maxpool2 pass everywhere else)
+                pool = c["pool_after"] and not is_last and not (hh | ww) & 1
+                fuse = pool and not _LEGACY
                 a = ctx.alloc((N, hh, ww, cout))
                 z = ctx.alloc((N, hh, ww, cout)) if is_feat else None
+                pooled = ctx.alloc((N, hh // 2, ww // 2, cout)) if pool else None
                 conv(ctx, h, self.packed[(i, 0)], N, hh, ww, cin, cout, bias=self.p[f"features.{i}.bias"],
-                     epi=L.EPI_PRELU, alpha=self._zeros(cout), y=a, y_pre=z)
+                     epi=L.EPI_PRELU, alpha=self._zeros(cout), y=a, y_pre=z, y_pool=pooled if fuse else None,
+                     y_images=keep_images if fuse and not is_feat else 0)
             if is_feat:
                 feats[i] = z
             acts.append(dict(c=c, a=a, H=hh, W=ww))
             h = a
             if c["pool_after"] and not is_last:
-                pooled = ctx.alloc((N, hh // 2, ww // 2, cout))
-                ctx.emit("vgg_pool", ctx.lib.fen_maxpool2, ctx.code, N, hh, ww, cout, ptr(a), ptr(pooled))
+                if not fuse:
+                    pooled = ctx.alloc((N, hh // 2, ww // 2, cout))
+                    ctx.emit("vgg_pool", ctx.lib.fen_maxpool2, ctx.code, N, hh, ww, cout, ptr(a), ptr(pooled))
                 h, hh, ww = pooled, hh // 2, ww // 2
         return acts, feats
 
@@ -175,8 +191,8 @@ class VGGPerceptual:
         ctx = ctx or self.ctx
         N = x2.shape[0]
         B = N // 2
-        acts, feats = self.forward(x2, ctx)
         train = dpred is not None
+        acts, feats = self.forward(x2, ctx, keep_images=B if train else 0)
         nparts = ctx.lib.fen_feat_loss_parts()
         order = sorted(self.idx, reverse=True)
         first = [True]
@@ -219,8 +235,12 @@ class VGGPerceptual:
                          pc["cout"], ptr(dp), ptr(prev["a"]), ptr(dz))
             else:
                 dz = ctx.alloc((B, hh, ww, c["cin"]))
-                part = ctx.scratch("vgg_dal", (B * ((hh + 15) // 16) * ((ww + 15) // 16), c["cin"]), torch.float32)
-                conv(ctx, d, self.packed[(i, 2)], B, hh, ww, c["cout"], c["cin"], epi=L.EPI_PRELU_BWD,
-                     alpha=self._zeros(c["cin"]), pre_in=prev["a"], y=dz, part=part)
+                if _LEGACY:
+                    part = ctx.scratch("vgg_dal", (B * ((hh + 15) // 16) * ((ww + 15) // 16), c["cin"]), torch.float32)
+                    conv(ctx, d, self.packed[(i, 2)], B, hh, ww, c["cout"], c["cin"], epi=L.EPI_PRELU_BWD,
+                         alpha=self._zeros(c["cin"]), pre_in=prev["a"], y=dz, part=part)
+                else:
+                    conv(ctx, d, self.packed[(i, 2)], B, hh, ww, c["cout"], c["cin"], epi=L.EPI_RELU_BWD,
+                         pre_in=prev["a"], y=dz)
             d = dz
         return feats

@@ -42,7 +42,10 @@ enum {
     FEN_EPI_UNSHUFFLE = 16, /* inverse PixelShuffle(2) store: y is [B,H/2,W/2,4*Cout]           */
     FEN_EPI_POOL = 32,      /* part[b][tile][co] = sum over the tile's pixels of the stored v   */
     FEN_EPI_LAST = 64,      /* conv_last: + bicubic skip, eval clamp, NCHW fp32 out, L1 grad    */
-    FEN_EPI_DOT = 128       /* part[b][tile][co] = sum over the tile of (stored v) * pre_in      */
+    FEN_EPI_DOT = 128,      /* part[b][tile][co] = sum over the tile of (stored v) * pre_in      */
+    FEN_EPI_RELU_BWD = 4096 /* y = pre_in>0 ? v : 0 (ReLU backward through the ReLU output pre_in;
+                               no partial sums: the frozen VGG19 extractor's data gradients,
+                               perceptual.py:60-64).  Not with PRELU_BWD / DOT / LAST / SHUFFLE.  */
 };
 
 /* 3x3, stride 1, pad 1 convolution as an implicit GEMM on MFMA.
@@ -92,6 +95,16 @@ typedef struct {
      * every other group reads pre_in.  (The upsampler stages, blocks.py:225-226.)              */
     int pre_elide;
     const void* post_in;
+    /* The 2x2 max pool of the output (the VGG19 conv -> ReLU -> 'M' layers of the perceptual
+     * extractor, perceptual.py:50-53): y_pool (or NULL) = max over each 2x2 window of y, NHWC
+     * [B,H/2,W/2,Cout]; needs FEN_EPI_PRELU without SHUFFLE / UNSHUFFLE / LAST / POOL / DOT and
+     * H, W even.  The 16-bit persistent kernels (bias + PReLU, no residuals) fuse it into their
+     * store; every other route stores y and pools it in a second launch.  y_images > 0 (needs
+     * y_pool): the kernel MAY skip storing y (and y_pre) for images b >= y_images -- the target
+     * half of VGG's [pred; target] batch, whose activations no backward reads; y_pool is
+     * written for every image.  0: y for every image.                                         */
+    void* y_pool;
+    int y_images;
 } fen_conv_desc;
 
 int fen_conv3x3(const fen_conv_desc* d, void* stream);

@@ -113,6 +113,33 @@ def test_conv_dot_epilogue_validation_without_gpu():
     assert lib.fen_conv3x3(d, None) == -2
 
 
+def test_conv_relu_bwd_and_pool_validation_without_gpu():
+    """FEN_EPI_RELU_BWD needs pre_in and excludes the other pre_in modes; y_images needs y_pool;
+    y_pool needs the PReLU epilogue and even H, W (all refused before any launch)."""
+    from src.hip import lib as L
+    lib = L.load()
+    d = L.ConvDesc()
+    d.dtype, d.B, d.H, d.W, d.Cin, d.Cout = L.BF16, 2, 16, 16, 64, 64
+    d.x = d.w = d.y = 16
+    d.epi = L.EPI_RELU_BWD
+    assert lib.fen_conv3x3(d, None) == -1            # no pre_in
+    d.pre_in = d.part = d.alpha = 16
+    d.epi = L.EPI_RELU_BWD | L.EPI_PRELU_BWD
+    assert lib.fen_conv3x3(d, None) == -2
+    d.epi = L.EPI_RELU_BWD | L.EPI_SHUFFLE
+    assert lib.fen_conv3x3(d, None) == -2
+    d.epi = 1 << 20
+    assert lib.fen_conv3x3(d, None) == -1            # unknown flag
+    d.epi, d.y_images = L.EPI_PRELU, 1
+    assert lib.fen_conv3x3(d, None) == -1            # y_images without y_pool
+    d.y_pool, d.y_images = 16, 3
+    assert lib.fen_conv3x3(d, None) == -1            # y_images > B
+    d.epi, d.y_images = 0, 0
+    assert lib.fen_conv3x3(d, None) == -2            # y_pool without PReLU
+    d.epi, d.H = L.EPI_PRELU, 15
+    assert lib.fen_conv3x3(d, None) == -2            # odd H
+
+
 def test_group_strip_chain_validation_without_gpu():
     """fen_group_strip_chain's host checks run before any copy or launch: a broken chain, too many
     step tags and a tail aliasing the body's buffers are refused on CPU (a launch without a
