@@ -1303,22 +1303,23 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_v(const fen_conv_desc d) {
     };
     // halo waves: their 11 pieces (i = wl + 4 k) of tile t's halo, Cin panel pn, into slot par
     // (zero padding: a voffset past the buffer outside the image / past the 18 x 18 pixels)
-    auto issue_h = [&](int par, int t, int pn) {
+    auto issue_hk = [&](int par, int t, int pn, int k) {     // piece k (< 11) of this wave's share
         const int b = t / tpi, tile = t - b * tpi;
         const int h0 = (tile / twn) << 4, w0 = (tile % twn) << 4;
         const unsigned base = lds_addr(hbuf + par * V_HSLOT) + wl * 1024;
-#pragma unroll 1
-        for (int k = 0; k < 11; ++k) {
-            const int sl = (wl + 4 * k) * 64 + lane;
-            const int p = sl >> 3, pc = sl & 7;
-            const int hr = p / HALO, hc = p - hr * HALO;
-            const int gh = h0 + hr - 1, gw = w0 + hc - 1;
-            const bool in = p < HP && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-            const int voff = in ? (((b * H + gh) * W + gw) * Cin + (pc ^ (hc & 7)) * 8) * 2 + pn * 128 : V_BAD;
+        const int sl = (wl + 4 * k) * 64 + lane;
+        const int p = sl >> 3, pc = sl & 7;
+        const int hr = p / HALO, hc = p - hr * HALO;
+        const int gh = h0 + hr - 1, gw = w0 + hc - 1;
+        const bool in = p < HP && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+        const int voff = in ? (((b * H + gh) * W + gw) * Cin + (pc ^ (hc & 7)) * 8) * 2 + pn * 128 : V_BAD;
 #ifndef CVX_NOH
-            dma16(xr4, __builtin_amdgcn_readfirstlane(base + k * 4096), voff);
+        dma16(xr4, __builtin_amdgcn_readfirstlane(base + k * 4096), voff);
 #endif
-        }
+    };
+    auto issue_h = [&](int par, int t, int pn) {
+#pragma unroll 1
+        for (int k = 0; k < 11; ++k) issue_hk(par, t, pn, k);
     };
     // per-lane LDS read offsets: A rows wc*64 + m*16 + c16 of a slab (the swizzle key (row >> 1) & 7
     // does not depend on m or wc: m steps are immediates), B at halo column c16 + kw, row wr*4 + kh + n
@@ -1384,10 +1385,24 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_v(const fen_conv_desc d) {
                     __builtin_amdgcn_s_barrier();            // and: every wave is done with step s - 1
 #endif
                     if (hwave) {
-                        if (kw == 0 && kh == 0 && gp + 1 < nmine * npan) {  // the next panel's halo, into the slot gp - 1 used
+                        // the next panel's halo, into the slot panel gp - 1 used (free since this
+                        // panel's first barrier): the wave's 11 pieces in three bursts, at taps 0,
+                        // 3 and 6 (4 + 4 + 3; all 11 at tap 0 held the halo waves for one long step
+                        // while the barrier kept the other waves waiting), landed by tap 8's vmcnt(0)
+#ifndef CVX_HALO_BURST
+                        if (kw == 0 && gp + 1 < nmine * npan) {
+                            const int tn = pn + 1 < npan ? slot + j * nslot : slot + (j + 1) * nslot;
+                            const int pnn = pn + 1 < npan ? pn + 1 : 0;
+                            const int k1 = kh < 2 ? 4 * kh + 4 : 11;
+#pragma unroll 1
+                            for (int k = 4 * kh; k < k1; ++k) issue_hk(par ^ 1, tn, pnn, k);
+                        }
+#else   // A/B: round 6's first form, every piece at tap 0
+                        if (kw == 0 && kh == 0 && gp + 1 < nmine * npan) {
                             if (pn + 1 < npan) issue_h(par ^ 1, slot + j * nslot, pn + 1);
                             else issue_h(par ^ 1, slot + (j + 1) * nslot, 0);
                         }
+#endif
                     } else if (s + 3 < nsteps) {
                         issue_w((s + 3) & 3, (tap + 3) % 9, tap + 3 < 9 ? pn : pn3);   // into slot (s - 1) % 4
                     }
@@ -1675,6 +1690,9 @@ int conv_dispatch(const fen_conv_desc* d, hipStream_t s) {
         }
         return launch_s<T, 64>(d, s);
     }
+    // (Cout 16 from Cin 64 -- VGG conv1_1's data gradient -- on the one-group persistent kernel
+    // with a 16-row resident filter measured 149 us vs the streamed kernel's 123 at B = 32, 256^2:
+    // its per-tile residual loads and halo wait are exposed; r6)
     if (d->Cout % 16 == 0) return launch_s<T, 16>(d, s);
     return FEN_EUNSUPPORTED;
 }

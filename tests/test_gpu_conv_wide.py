@@ -193,3 +193,17 @@ def test_fused_maxpool_refusals():
         net.conv(ctx, x, wp, 2, 16, 16, 64, 64, epi=L.EPI_PRELU, alpha=z, y=y, y_pool=yp, y_images=3)
     with pytest.raises(L.FenError):
         net.conv(ctx, x[:, :15].contiguous(), wp, 2, 15, 16, 64, 64, epi=L.EPI_PRELU, alpha=z, y=y, y_pool=yp)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,H,W,res", [(2, 64, 48, True), (3, 40, 24, False), (1, 16, 16, True)])
+def test_thin_conv_cout16(dtype, B, H, W, res):
+    """Cin 64 -> Cout 16 on the one-group persistent kernel with a 16-row resident filter: VGG
+    conv1_1's data gradient added into dL/dsr (perceptual.py:84-95; residual = the L1 term)."""
+    from src.hip import net
+    ctx, x, wp, ref = _setup(dtype, B, H, W, 64, 16, seed=5)
+    r = torch.randn(B, H, W, 16).to(dtype)
+    y = torch.empty(B, H, W, 16, device=DEV, dtype=dtype)
+    net.conv(ctx, x, wp, B, H, W, 64, 16, y=y, res=(r.to(DEV),) if res else ())
+    torch.cuda.synchronize()
+    _close(y, ref + (r.float() if res else 0), dtype)

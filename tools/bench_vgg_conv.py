@@ -34,7 +34,9 @@ for name, N, hw, cin, cout in [("c1_2", 64, 256, 64, 64), ("c2_1", 64, 128, 64, 
     w = torch.randn(cout, cin, 3, 3, device='cuda') * 0.05; b = torch.zeros(cout, device='cuda')
     y = torch.empty(N, hw, hw, cout, device='cuda', dtype=dt)
     wp = pack(w, 0)
-    us = timeit(lambda: net.conv(ctx, x, wp, N, hw, hw, cin, cout, bias=b, epi=L.EPI_PRELU, alpha=torch.zeros(cout, device='cuda'), y=y))
+    yp = torch.empty(N, hw // 2, hw // 2, cout, device='cuda', dtype=dt) if name in ("c1_2", "c2_2") else None
+    us = timeit(lambda: net.conv(ctx, x, wp, N, hw, hw, cin, cout, bias=b, epi=L.EPI_PRELU, alpha=torch.zeros(cout, device='cuda'), y=y,
+                                 y_pool=yp, y_images=N // 2 if yp is not None else 0))
     fl = 2 * N * hw * hw * cin * cout * 9
     res[name] = [round(us, 1), round(fl / us / 1e6, 1)]
     if cin >= 128:     # its data gradient at B = 32 through the ReLU mask (mode-2 weights: Cout <-> Cin)
@@ -45,7 +47,6 @@ for name, N, hw, cin, cout in [("c1_2", 64, 256, 64, 64), ("c2_1", 64, 128, 64, 
         part = torch.empty(n2 * ((hw + 15) // 16) ** 2, cin, device='cuda')
         wp2 = pack(w, 2)
         if cin % 128 == 0:
-            us = timeit(lambda: net.conv(ctx, d, wp2, n2, hw, hw, cout, cin, epi=L.EPI_PRELU_BWD,
-                                         alpha=torch.zeros(cin, device='cuda'), pre_in=pre, y=dz, part=part))
+            us = timeit(lambda: net.conv(ctx, d, wp2, n2, hw, hw, cout, cin, epi=L.EPI_RELU_BWD, pre_in=pre, y=dz))
             res[name + "_dg"] = [round(us, 1), round(fl / 2 / us / 1e6, 1)]
 print(json.dumps(res))

@@ -1,6 +1,6 @@
 """One VGG19 conv shape through fen_conv3x3 (bf16), repeated -- for rocprofv3 counter passes of
 the streamed conv kernel.  SHAPE=c3_2 (N=64, 64x64, 256->256, bias+ReLU) by default; others as in
-bench_vgg_conv.py; DGRAD=1: the data-gradient form (N=32, PReLU-backward epilogue)."""
+bench_vgg_conv.py; DGRAD=1: the data-gradient form (N=32, ReLU-backward epilogue)."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'face-super-resolution_amd'))
 import torch
@@ -24,8 +24,7 @@ pre = torch.randn(N, hw, hw, cout, device='cuda', dtype=dt)
 part = torch.empty(N * ((hw + 15) // 16) ** 2, cout, device='cuda')
 for _ in range(int(os.environ.get("REPS", "10"))):
     if dg:
-        net.conv(ctx, x, wp, N, hw, hw, cin, cout, epi=L.EPI_PRELU_BWD, alpha=torch.zeros(cout, device='cuda'),
-                 pre_in=pre, y=y, part=part)
+        net.conv(ctx, x, wp, N, hw, hw, cin, cout, epi=L.EPI_RELU_BWD, pre_in=pre, y=y)
     else:
         net.conv(ctx, x, wp, N, hw, hw, cin, cout, bias=b, epi=L.EPI_PRELU, alpha=torch.zeros(cout, device='cuda'), y=y)
 torch.cuda.synchronize()
