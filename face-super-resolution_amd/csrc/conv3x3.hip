@@ -1340,6 +1340,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_v(const fen_conv_desc d) {
             for (int n = 0; n < NT; ++n) mma16<T>(acc[m][n], A[m], Bf[n]);
     };
 
+
     // prologue: tile 0's panel-0 halo; slabs of steps 0..2
     if (hwave) {
         issue_h(0, slot, 0);
@@ -1390,6 +1391,8 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_v(const fen_conv_desc d) {
                         // 3 and 6 (4 + 4 + 3; all 11 at tap 0 held the halo waves for one long step
                         // while the barrier kept the other waves waiting), landed by tap 8's vmcnt(0)
 #ifndef CVX_HALO_BURST
+                        // (each piece issued between the MFMAs of the step's first half instead, the
+                        // weight waves' too: conv3_2 343 vs 313-321 us, dgrad 180-183 vs 166-170, A/B r6)
                         if (kw == 0 && gp + 1 < nmine * npan) {
                             const int tn = pn + 1 < npan ? slot + j * nslot : slot + (j + 1) * nslot;
                             const int pnn = pn + 1 < npan ? pn + 1 : 0;
