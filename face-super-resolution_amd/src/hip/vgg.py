@@ -4,7 +4,8 @@ The frozen feature extractor runs ONCE over [pred; target] stacked in one batch 
 (pred = the generator output, target = HR): conv1_1 on the K=27 input kernel with the
 ImageNet normalisation fused (perceptual.py:67-72,84-95); every later conv on fen_conv3x3
 with bias + ReLU fused (PReLU epilogue with zero slopes; a feature layer keeps its
-pre-ReLU output through y_pre); max pools on fen_maxpool2.  The loss
+pre-ReLU output through y_pre); the max pools from the store of the conv before them
+(fen_conv_desc.y_pool, which also keeps that conv's ReLU output for the pred half only).  The loss
 (weight x nn.L1Loss / nn.MSELoss of each requested layer, perceptual.py:155-167) and its
 gradient come from fen_feat_loss, and the backward runs on the pred half only: mode-2
 data gradients whose epilogue applies the ReLU mask (FEN_EPI_RELU_BWD, pre_in = the saved
@@ -228,6 +229,9 @@ class VGGPerceptual:
             prev = acts[k - 1]
             pc = prev["c"]
             if pc["pool_after"]:
+                # (the pool's backward in the dgrad's epilogue instead -- 2x2 scatter of 8-B stores
+                # and window loads -- measured slower: 189 vs 82 + 45 us at conv3_1, 274 vs 93 + 92 at
+                # conv2_1, r6)
                 dp = ctx.alloc((B, hh, ww, c["cin"]))
                 conv(ctx, d, self.packed[(i, 2)], B, hh, ww, c["cout"], c["cin"], y=dp)
                 dz = ctx.alloc((B, prev["H"], prev["W"], pc["cout"]))
