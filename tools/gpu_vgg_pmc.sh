@@ -1,4 +1,4 @@
-# round 6b: full GPU suite + smoke + bench line on the current tree, then the VGG wide conv's
+# full GPU suite + smoke + bench line on the current tree, then the VGG wide conv's
 # SQ counters (c3_2 forward, 64 x 64 x 256 -> 256 at N = 64) and the perceptual step's kernel stats
 set -e
 export TMPDIR=/tmp
