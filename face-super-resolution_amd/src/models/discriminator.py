@@ -115,6 +115,9 @@ class _DFeatures(torch.autograd.Function):
         d = g.permute(0, 2, 3, 1).contiguous().to(dt)            # NHWC
         blocks = mod._hip_blocks()
         grads = {}
+        # the parameters' gradients only when autograd wants them (the trainer's generator step
+        # passes D frozen: its data gradient alone, TrainerConfig.freeze_d_in_g_step)
+        pgrad = any(fctx.needs_input_grad[2:])
         for k in range(len(fctx.saved_blocks) - 1, -1, -1):
             sv = fctx.saved_blocks[k]
             blk, bn = sv["blk"], sv["blk"]["bn"]
@@ -133,11 +136,12 @@ class _DFeatures(torch.autograd.Function):
             if sv["xs"] is not None:
                 # stride 2 over the space-to-depth input: the phase-major filter's gradients
                 ho, wo, c4 = sv["Ho"], sv["Wo"], 4 * cin
-                dw4 = torch.empty(cout, c4, 3, 3, device=g.device)
-                wgrad(ctx, sv["xs"], dz, B, ho, wo, c4, cout, dw4, None)
-                dw = torch.empty_like(blk["conv"].weight)
-                s2d_filter_grad(dw4, dw)
-                grads[blk["conv"].weight] = dw
+                if pgrad:
+                    dw4 = torch.empty(cout, c4, 3, 3, device=g.device)
+                    wgrad(ctx, sv["xs"], dz, B, ho, wo, c4, cout, dw4, None)
+                    dw = torch.empty_like(blk["conv"].weight)
+                    s2d_filter_grad(dw4, dw)
+                    grads[blk["conv"].weight] = dw
                 dxs = ctx.alloc((B, ho, wo, c4))
                 if k == 0:
                     part = ctx.alloc((B * tiles(ho, wo), c4), torch.float32)
@@ -153,9 +157,10 @@ class _DFeatures(torch.autograd.Function):
                 dzf = ctx.alloc((B, sv["H"], sv["W"], cout))
                 ctx.emit("d_zins", lib.fen_zero_insert2, ctx.code, B, sv["Ho"], sv["Wo"], cout, ptr(dz), ptr(dzf))
                 dz = dzf
-            dw = torch.empty_like(blk["conv"].weight)
-            wgrad(ctx, sv["a_in"], dz, B, sv["H"], sv["W"], cin, cout, dw, None)
-            grads[blk["conv"].weight] = dw
+            if pgrad:
+                dw = torch.empty_like(blk["conv"].weight)
+                wgrad(ctx, sv["a_in"], dz, B, sv["H"], sv["W"], cin, cout, dw, None)
+                grads[blk["conv"].weight] = dw
             da = ctx.alloc((B, sv["H"], sv["W"], cin))
             if k == 0:
                 # block 1's LeakyReLU mask on the way down: a1 > 0 <=> its pre-activation > 0
@@ -167,19 +172,20 @@ class _DFeatures(torch.autograd.Function):
             d = da
         # block 1: conv 3->64 weight / bias gradient, and d(input) when asked for
         c0 = blocks[0]
-        dw0 = torch.empty_like(c0["conv"].weight)
-        db0 = torch.empty_like(c0["conv"].bias)
-        work = ctx.alloc((lib.fen_conv_first_work_floats(B, 3, H, W, c0["cout"]),), torch.float32)
-        ctx.emit("d_conv1_wgrad", lib.fen_conv_first_wgrad, ctx.code, B, 3, H, W, c0["cout"], ptr(fctx.xin), ptr(d),
-                 ptr(dw0), ptr(db0), 0, ptr(work))
-        grads[c0["conv"].weight] = dw0
-        grads[c0["conv"].bias] = db0
+        if pgrad:
+            dw0 = torch.empty_like(c0["conv"].weight)
+            db0 = torch.empty_like(c0["conv"].bias)
+            work = ctx.alloc((lib.fen_conv_first_work_floats(B, 3, H, W, c0["cout"]),), torch.float32)
+            ctx.emit("d_conv1_wgrad", lib.fen_conv_first_wgrad, ctx.code, B, 3, H, W, c0["cout"], ptr(fctx.xin), ptr(d),
+                     ptr(dw0), ptr(db0), 0, ptr(work))
+            grads[c0["conv"].weight] = dw0
+            grads[c0["conv"].bias] = db0
         dx = None
         if fctx.x_needs_grad:
             d16 = ctx.alloc((B, H, W, 16))
             conv(ctx, d, mod._packed(ctx, c0, 2), B, H, W, c0["cout"], 16, y=d16)
             dx = d16[..., :3].float().permute(0, 3, 1, 2).contiguous()
-        out = [grads.get(p) for p in mod._feature_params()]
+        out = [grads.get(p) if pgrad else None for p in mod._feature_params()]
         return (dx, None, *out)
 
 

@@ -74,6 +74,12 @@ class TrainerConfig:
     # warm-up iterations -- world size 1; re-captured when the batch shape or a learning rate
     # changes; results identical to the eager iteration (tests/test_gpu_gan_capture.py)
     capture_gan_step: bool = True
+    # (HIP extension) the generator step's pass through D takes no gradient for D's parameters:
+    # the reference computes them (trainer.py:458-475) and never uses them -- optimizer_d has
+    # already stepped, and its next zero_grad() drops them before the next D update -- so every
+    # weight update is identical (tests/test_gpu_gan_step.py); only D's .grad after an
+    # iteration differs (the D step's gradients alone).  False: the reference's dead work too.
+    freeze_d_in_g_step: bool = True
 
 
 class EarlyStopping:
@@ -306,7 +312,17 @@ class Trainer:
             self.optimizer_d.step()
         sr = self.model(lr)
         content = self._content(sr, hr)
-        loss = content + self.config.gan_weight * gl(D(sr), True)
+        frozen = []
+        if getattr(self.config, "freeze_d_in_g_step", True):
+            frozen = [p for p in D.parameters() if p.requires_grad]
+            for p in frozen:
+                p.requires_grad_(False)
+        try:
+            adv = gl(D(sr), True)
+        finally:
+            for p in frozen:
+                p.requires_grad_(True)
+        loss = content + self.config.gan_weight * adv
         for p in self.model.parameters():
             p.grad = None
         if update and self._g_ex is not None:

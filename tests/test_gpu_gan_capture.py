@@ -53,3 +53,22 @@ def test_captured_gan_iteration_matches_eager(tmp_path):
         cap.model.eval()
         eager.model.eval()
         assert torch.equal(cap.model(x), eager.model(x))
+
+
+def test_frozen_d_in_g_step_same_updates(tmp_path):
+    """TrainerConfig.freeze_d_in_g_step (default): the generator step's pass through D computes
+    only D's data gradients -- the reference also computes D's parameter gradients there and never
+    uses them (optimizer_d has stepped; its next zero_grad drops them).  Every update is the
+    same bit for bit as with the dead work done, eager and captured; D's .grad after an
+    iteration holds the D step's gradients alone."""
+    ref = _trainer(False, tmp_path / "r")
+    ref.config.freeze_d_in_g_step = False
+    frz, cap = _trainer(False, tmp_path / "f"), _trainer(True, tmp_path / "c")
+    gen = torch.Generator().manual_seed(9)
+    for i in range(5):
+        hr = torch.rand(2, 3, 128, 128, generator=gen).to(DEV)
+        losses = [float(tr._gan_iteration(hr)) for tr in (ref, frz, cap)]
+        assert losses[0] == losses[1] == losses[2], (i, losses)
+        for a, b, c in zip(_state(ref), _state(frz), _state(cap)):
+            assert torch.equal(a, b) and torch.equal(a, c), i
+    assert all(p.requires_grad for p in frz.discriminator.parameters())
