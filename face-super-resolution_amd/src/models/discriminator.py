@@ -42,8 +42,14 @@ _S2D_MAX_CIN = int(os.environ.get("FEN_D_S2D_MAX_CIN", "256"))
 
 
 class _DFeatures(torch.autograd.Function):
+    """x [ng * Bg, 3, H, W]: ng independent batches of Bg images (forward_pair: ng = 2, the D
+    step's real and fake).  The convs, the LeakyReLUs and the head are per image, so the groups
+    run as one batch; train-mode BatchNorm takes each group's own statistics (and updates the
+    running ones group by group, in order), as separate calls would; the weight gradients come
+    out summed over the groups in one launch each."""
+
     @staticmethod
-    def forward(fctx, x, mod, *params):
+    def forward(fctx, x, mod, ng, *params):
         from ..hip import lib as L
         from ..hip.net import conv, wgrad  # noqa: F401
         from ..hip.program import Ctx, ptr
@@ -80,25 +86,29 @@ class _DFeatures(torch.autograd.Function):
                     ctx.emit("d_sub", lib.fen_subsample2, ctx.code, B, hh, ww, cout, ptr(z), ptr(zs))
                     z = zs
             bn = blk["bn"]
-            npx = B * ho * wo
-            stat = ctx.alloc((2 * cout,), torch.float32)
-            if mod.training:
-                work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
-                ctx.emit("d_bn_stats", lib.fen_bn_stats, ctx.code, npx, cout, ptr(z), float(bn.eps),
-                         float(bn.momentum), ptr(stat), ptr(bn.running_mean), ptr(bn.running_var), ptr(work))
-                with torch.no_grad():
-                    bn.num_batches_tracked += 1
-            else:
-                with torch.no_grad():
-                    stat[:cout] = bn.running_mean
-                    stat[cout:] = (bn.running_var + bn.eps).rsqrt()
             out = ctx.alloc((B, ho, wo, cout))
-            ctx.emit("d_bn_apply", lib.fen_bn_apply, ctx.code, npx, cout, ptr(z), ptr(stat), ptr(stat[cout:]),
-                     ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(out))
+            gs = ng if mod.training else 1
+            npx = (B // gs) * ho * wo                     # one BN group's pixels
+            stat = ctx.alloc((gs, 2 * cout), torch.float32)
+            for gi in range(gs):
+                zg, sg, og = z[gi * (B // gs):], stat[gi], out[gi * (B // gs):]
+                if mod.training:
+                    work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
+                    ctx.emit("d_bn_stats", lib.fen_bn_stats, ctx.code, npx, cout, ptr(zg), float(bn.eps),
+                             float(bn.momentum), ptr(sg), ptr(bn.running_mean), ptr(bn.running_var), ptr(work))
+                    with torch.no_grad():
+                        bn.num_batches_tracked += 1
+                else:
+                    with torch.no_grad():
+                        sg[:cout] = bn.running_mean
+                        sg[cout:] = (bn.running_var + bn.eps).rsqrt()
+                ctx.emit("d_bn_apply", lib.fen_bn_apply, ctx.code, npx, cout, ptr(zg), ptr(sg), ptr(sg[cout:]),
+                         ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(og))
             saved.append(dict(blk=blk, a_in=a, xs=xs, z=z, stat=stat, H=hh, W=ww, Ho=ho, Wo=wo))
             a, hh, ww = out, ho, wo
         fctx.saved_blocks, fctx.a1, fctx.xin, fctx.mod = saved, saved[0]["a_in"], xin, mod
         fctx.shape = (B, H, W)
+        fctx.ng = ng if mod.training else 1
         fctx.x_needs_grad = x.requires_grad
         return a.float().permute(0, 3, 1, 2).contiguous()        # NCHW for the Flatten
 
@@ -117,20 +127,24 @@ class _DFeatures(torch.autograd.Function):
         grads = {}
         # the parameters' gradients only when autograd wants them (the trainer's generator step
         # passes D frozen: its data gradient alone, TrainerConfig.freeze_d_in_g_step)
-        pgrad = any(fctx.needs_input_grad[2:])
+        pgrad = any(fctx.needs_input_grad[3:])
+        ng = fctx.ng
         for k in range(len(fctx.saved_blocks) - 1, -1, -1):
             sv = fctx.saved_blocks[k]
             blk, bn = sv["blk"], sv["blk"]["bn"]
             cin, cout = blk["cin"], blk["cout"]
-            npx = B * sv["Ho"] * sv["Wo"]
+            npx = (B // ng) * sv["Ho"] * sv["Wo"]
             dz = ctx.alloc((B, sv["Ho"], sv["Wo"], cout))
-            # (every gradient buffer below is written whole by its kernel: no zero fill)
+            # (every gradient buffer below is written whole by its kernel: no zero fill; the BN
+            # groups' dgamma / dbeta accumulate)
             dgam = torch.empty(cout, device=g.device)
             dbet = torch.empty(cout, device=g.device)
             work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
-            ctx.emit("d_bn_bwd", lib.fen_bn_bwd, ctx.code, npx, cout, ptr(d), ptr(sv["z"]), ptr(sv["stat"]),
-                     ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(dz), ptr(dgam), ptr(dbet), 0,
-                     ptr(work))
+            for gi in range(ng):
+                o = gi * (B // ng)
+                ctx.emit("d_bn_bwd", lib.fen_bn_bwd, ctx.code, npx, cout, ptr(d[o:]), ptr(sv["z"][o:]), ptr(sv["stat"][gi]),
+                         ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(dz[o:]), ptr(dgam), ptr(dbet),
+                         int(gi > 0), ptr(work))
             grads[bn.weight] = dgam
             grads[bn.bias] = dbet
             if sv["xs"] is not None:
@@ -186,7 +200,7 @@ class _DFeatures(torch.autograd.Function):
             conv(ctx, d, mod._packed(ctx, c0, 2), B, H, W, c0["cout"], 16, y=d16)
             dx = d16[..., :3].float().permute(0, 3, 1, 2).contiguous()
         out = [grads.get(p) if pgrad else None for p in mod._feature_params()]
-        return (dx, None, *out)
+        return (dx, None, None, *out)
 
 
 def _dhead_forward(h, w1, b1, w2, b2, sigmoid):
@@ -336,9 +350,30 @@ class VGGStyleDiscriminator(nn.Module):
             raise NotImplementedError("use_bn=False is not wired on the HIP path")
         if x.shape[1] != 3 or x.shape[2] % 32 or x.shape[3] % 32:
             raise ValueError("input must be (B, 3, H, W) with H, W multiples of 32")
-        feats = _DFeatures.apply(x, self, *self._feature_params())
+        feats = _DFeatures.apply(x, self, 1, *self._feature_params())
         lin1, lin2 = self.classifier[1], self.classifier[3]
         return _DHead.apply(feats.flatten(1), lin1.weight, lin1.bias, lin2.weight, lin2.bias, self.use_sigmoid)
+
+    def forward_pair(self, x1: torch.Tensor, x2: torch.Tensor):
+        """(self(x1), self(x2)) -- the D step's real and fake batches (trainer.py:433-434) -- as
+        one pass: the two batches' convs, LeakyReLUs and head run as one batch, train-mode
+        BatchNorm takes each batch's own statistics and updates the running ones x1 then x2,
+        exactly as the two calls do; the parameter gradients come out summed in one launch each
+        (no per-parameter accumulation of two gradients).  Same scores; gradients equal to the two
+        calls' up to fp32 summation order."""
+        if x1.shape != x2.shape or os.environ.get("FEN_D_PAIR", "1") == "0":
+            return self(x1), self(x2)
+        x = torch.cat([x1, x2])
+        if not x.is_cuda:
+            raise RuntimeError("the HIP discriminator runs on a ROCm GPU tensor (got CPU); there is no CPU path")
+        if not self.use_bn:
+            raise NotImplementedError("use_bn=False is not wired on the HIP path")
+        if x.shape[1] != 3 or x.shape[2] % 32 or x.shape[3] % 32:
+            raise ValueError("input must be (B, 3, H, W) with H, W multiples of 32")
+        feats = _DFeatures.apply(x, self, 2, *self._feature_params())
+        lin1, lin2 = self.classifier[1], self.classifier[3]
+        y = _DHead.apply(feats.flatten(1), lin1.weight, lin1.bias, lin2.weight, lin2.bias, self.use_sigmoid)
+        return y[:x1.shape[0]], y[x1.shape[0]:]
 
     def head_preactivation(self, h: torch.Tensor) -> torch.Tensor:
         """The classifier's hidden layer before its LeakyReLU, Linear(32768, 1024) of the

@@ -303,7 +303,10 @@ class Trainer:
             self.optimizer_d.zero_grad()
             with torch.no_grad():
                 sr_d = self.model(lr)
-            d_loss = (gl(D(hr), True) + gl(D(sr_d.detach()), False)) / 2
+            # (the HIP discriminator takes both batches in one pass, per-batch BatchNorm statistics)
+            d_real, d_fake = D.forward_pair(hr, sr_d.detach()) if hasattr(D, "forward_pair") else \
+                (D(hr), D(sr_d.detach()))
+            d_loss = (gl(d_real, True) + gl(d_fake, False)) / 2
             if self._d_ex is not None:
                 self._d_ex.arm()
             (d_loss / self.world).backward()

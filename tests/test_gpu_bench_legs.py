@@ -144,7 +144,7 @@ def _hip_d_masks(d0, x):
     D = VGGStyleDiscriminator(input_size=256, precision="fp32")
     D.load_state_dict(d0)
     D = D.to(DEV).train()
-    feats = _DFeatures.apply(x.to(DEV), D, *D._feature_params())
+    feats = _DFeatures.apply(x.to(DEV), D, 1, *D._feature_params())
     masks = [(s["a_in"] > 0).permute(0, 3, 1, 2).cpu() for s in feats.grad_fn.saved_blocks] + [(feats > 0).cpu()]
     masks.append((D.head_preactivation(feats.flatten(1)) > 0).cpu())
     return masks

@@ -103,3 +103,35 @@ def test_classifier_head_vs_float64(B, sigmoid):
     for name, a, b in zip(("y", "dh", "dw1", "db1", "dw2", "db2"), outs[0], ref):
         e = _rel(a.cpu().numpy(), b.numpy())
         assert e <= 1e-5, (name, e)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_forward_pair_matches_two_calls(precision):
+    """VGGStyleDiscriminator.forward_pair (the D step's real and fake batches as one pass,
+    trainer.py:433-434): the same scores as two calls (per-batch BatchNorm statistics; bit for bit
+    in fp32, where the kernels do not depend on the batch), the same running statistics and
+    num_batches_tracked (updated real then fake), parameter gradients of the summed loss equal
+    up to fp32 summation order (one weight-gradient launch over both batches vs two + add)."""
+    import copy
+    from src.models import VGGStyleDiscriminator
+    torch.manual_seed(4)
+    d1 = VGGStyleDiscriminator(input_size=64, precision=precision).to(DEV).train()
+    d2 = copy.deepcopy(d1)
+    g = torch.Generator().manual_seed(5)
+    xr, xf = torch.rand(3, 3, 64, 64, generator=g).to(DEV), torch.rand(3, 3, 64, 64, generator=g).to(DEV)
+    a1, b1 = d1(xr), d1(xf)
+    a2, b2 = d2.forward_pair(xr, xf)
+    ((a1 * 0.7).sum() - (b1 * 1.3).sum()).backward()
+    ((a2 * 0.7).sum() - (b2 * 1.3).sum()).backward()
+    torch.cuda.synchronize()
+    if precision == "fp32":
+        assert torch.equal(a1, a2) and torch.equal(b1, b2)
+    else:
+        assert float((a1 - a2).abs().max()) <= 2e-2 * float(a1.abs().max()) + 1e-3
+    for (k, t1), t2 in zip(d1.state_dict().items(), d2.state_dict().values()):
+        if "running" in k or "num_batches" in k:
+            assert torch.allclose(t1.float(), t2.float(), rtol=1e-5, atol=1e-6), k
+    tol = 1e-5 if precision == "fp32" else 3e-2
+    for (k, p1), p2 in zip(d1.named_parameters(), d2.parameters()):
+        e = float((p1.grad - p2.grad).norm() / max(float(p1.grad.norm()), 1e-30))
+        assert e <= tol, (k, e)
