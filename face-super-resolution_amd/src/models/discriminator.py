@@ -39,6 +39,8 @@ _S2D = os.environ.get("FEN_D_S2D", "1") != "0"
 # (the 64-channel stride-2 layer stays on the full-resolution persistent kernels)
 _S2D_MIN_CIN = int(os.environ.get("FEN_D_S2D_MIN_CIN", "128"))
 _S2D_MAX_CIN = int(os.environ.get("FEN_D_S2D_MAX_CIN", "256"))
+# A/B switch: FEN_D_PACK_MULTI=0 re-packs each stale filter copy in a launch of its own
+_PACK_MULTI = os.environ.get("FEN_D_PACK_MULTI", "1") != "0"
 
 
 class _DFeatures(torch.autograd.Function):
@@ -67,6 +69,7 @@ class _DFeatures(torch.autograd.Function):
                  ptr(c0["conv"].weight.detach().float().contiguous()), ptr(c0["conv"].bias.detach().float()), 0, 0,
                  _SLOPE, ptr(a))
         hh, ww = H, W
+        tracked = []                                  # BN counters to advance (one launch at the end)
         for blk in blocks[1:]:
             cin, cout, st = blk["cin"], blk["cout"], blk["stride"]
             xs = None
@@ -96,8 +99,7 @@ class _DFeatures(torch.autograd.Function):
                     work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
                     ctx.emit("d_bn_stats", lib.fen_bn_stats, ctx.code, npx, cout, ptr(zg), float(bn.eps),
                              float(bn.momentum), ptr(sg), ptr(bn.running_mean), ptr(bn.running_var), ptr(work))
-                    with torch.no_grad():
-                        bn.num_batches_tracked += 1
+                    tracked.append(bn.num_batches_tracked)
                 else:
                     with torch.no_grad():
                         sg[:cout] = bn.running_mean
@@ -106,6 +108,14 @@ class _DFeatures(torch.autograd.Function):
                          ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(og))
             saved.append(dict(blk=blk, a_in=a, xs=xs, z=z, stat=stat, H=hh, W=ww, Ho=ho, Wo=wo))
             a, hh, ww = out, ho, wo
+        if tracked:
+            # num_batches_tracked += its BN calls (ng per layer), every layer in one launch (a
+            # tensor once in the list: repeated entries would race inside the launch)
+            cnt = {}
+            for t in tracked:
+                cnt[id(t)] = (t, cnt.get(id(t), (t, 0))[1] + 1)
+            with torch.no_grad():
+                torch._foreach_add_([t for t, _ in cnt.values()], [n for _, n in cnt.values()])
         fctx.saved_blocks, fctx.a1, fctx.xin, fctx.mod = saved, saved[0]["a_in"], xin, mod
         fctx.shape = (B, H, W)
         fctx.ng = ng if mod.training else 1
@@ -289,6 +299,7 @@ class VGGStyleDiscriminator(nn.Module):
         self._initialize_weights()
         self.compute_dtype = _DTYPES[precision]
         self._packs = {}
+        self._pack_tab = {}                            # dtype code -> (device job table, njobs, total)
 
     def _initialize_weights(self):
         """discriminator.py:104-116."""
@@ -317,24 +328,83 @@ class VGGStyleDiscriminator(nn.Module):
         return [p for p in self.features.parameters()]
 
     def _packed(self, ctx, blk, mode, s2d=False):
+        """The packed copy of block blk's filter for fen_conv3x3 mode `mode` (phase-major for the
+        space-to-depth form).  A new copy is packed on its own; when the weights move (an
+        optimizer step bumps every version at once) the first stale lookup re-packs every known
+        copy in ONE fen_pack_multi launch (+ the space-to-depth scatters), not one launch per
+        (layer, mode).  (A captured GAN iteration records the re-packs its Python saw: the
+        optimizer steps bump the versions at capture time exactly as in every eager iteration.)"""
         from ..hip.net import s2d_filter
         from ..hip.program import ptr
         w = blk["conv"].weight
         key = (blk["i"], mode, ctx.code, s2d)
         ent = self._packs.get(key)
-        if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
-            # (a captured GAN iteration records the re-packs its Python saw: the optimizer
-            # steps bump the versions at capture time exactly as in every eager iteration)
+        if ent is None or ent[1] != w.data_ptr():
             cout, cin = w.shape[0], w.shape[1] * (4 if s2d else 1)
             n = ctx.lib.fen_packed_elems(mode, cout, cin)
-            buf = ent[2] if ent is not None and ent[1] == w.data_ptr() else \
-                torch.empty(n, dtype=ctx.tdtype, device=w.device)
-            src = s2d_filter(w.detach().float()) if s2d else w.detach().float().contiguous()
-            ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, cout, cin, ptr(src), ptr(buf))
-            ctx.keep(src)
-            ent = (w._version, w.data_ptr(), buf)
+            buf = torch.empty(n, dtype=ctx.tdtype, device=w.device)
+            src = self._s2d_src(blk, w) if s2d else w.detach()
+            if s2d:
+                self._s2d_scatter(blk, w)
+            ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, cout, cin, ptr(src.contiguous()), ptr(buf))
+            ent = (w._version, w.data_ptr(), buf, w, mode, cout, cin, src, blk, s2d)
             self._packs[key] = ent
+            self._pack_tab.pop(ctx.code, None)
+        elif ent[0] != w._version:
+            if _PACK_MULTI:
+                self._repack_all(ctx)
+            else:                                      # (A/B: one launch per stale copy)
+                if s2d:
+                    self._s2d_scatter(blk, w)
+                ctx.emit("d_pack", ctx.lib.fen_pack_conv_w, ctx.code, mode, ent[5], ent[6], ptr(ent[7]), ptr(ent[2]))
+                self._packs[key] = (w._version,) + ent[1:]
+            ent = self._packs[key]
         return ent[2]
+
+    def _s2d_src(self, blk, w):
+        """The persistent fp32 phase-major filter of a space-to-depth block (re-scattered from the
+        weights on every re-pack)."""
+        k = ("s2d_src", blk["i"])
+        if k not in self._packs:
+            self._packs[k] = torch.empty(w.shape[0], 4 * w.shape[1], 3, 3, device=w.device)
+        return self._packs[k]
+
+    def _s2d_scatter(self, blk, w):
+        from ..hip import lib as L
+        src = self._s2d_src(blk, w)
+        L.check(L.load().fen_s2d_filter(int(w.shape[0]), int(w.shape[1]), w.detach().contiguous().data_ptr(),
+                                        src.data_ptr(), 0, torch.cuda.current_stream().cuda_stream), "s2d_filter")
+
+    def _repack_all(self, ctx):
+        """Every packed copy of dtype ctx.code whose weights moved: the space-to-depth scatters,
+        then one fen_pack_multi over all of them (its job table built once per entry set)."""
+        import ctypes
+        from ..hip import lib as L
+        ents = [(k, e) for k, e in self._packs.items() if isinstance(k[0], int) and k[2] == ctx.code]
+        done = set()
+        for k, e in ents:
+            if e[9] and e[8]["i"] not in done:
+                self._s2d_scatter(e[8], e[3])
+                done.add(e[8]["i"])
+        tab = self._pack_tab.get(ctx.code)
+        if tab is None:
+            lib = ctx.lib
+            jobs = (L.PackJob * len(ents))()
+            for i, (k, e) in enumerate(ents):
+                jobs[i].w, jobs[i].out = e[7].data_ptr(), e[2].data_ptr()
+                jobs[i].mode, jobs[i].Cout, jobs[i].Cin = e[4], e[5], e[6]
+            nbytes = lib.fen_pack_table_bytes(len(ents))
+            host = (ctypes.c_uint8 * nbytes)()
+            total = ctypes.c_size_t(0)
+            L.check(lib.fen_pack_table(ctx.code, len(ents), ctypes.cast(jobs, ctypes.c_void_p),
+                                       ctypes.cast(host, ctypes.c_void_p), ctypes.byref(total)), "d_pack_table")
+            dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(ents[0][1][2].device)
+            tab = self._pack_tab[ctx.code] = (dev, len(ents), int(total.value))
+        dev, nj, total = tab
+        L.check(ctx.lib.fen_pack_multi(ctx.code, nj, dev.data_ptr(), total, torch.cuda.current_stream().cuda_stream),
+                "d_pack_multi")
+        for k, e in ents:
+            self._packs[k] = (e[3]._version,) + e[1:]
 
     def _slopes(self, n, dev):
         key = ("slopes", n, dev)
