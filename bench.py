@@ -303,18 +303,20 @@ def disc_flops(hw=256, bc=64):
     return f, first
 
 
-def gan_iteration_flop(B=16, hw=64, freeze_d=True):
+def gan_iteration_flop(B=16, hw=64, freeze_d=True, reuse_g=True):
     """One Trainer._gan_step (trainer.py:424-485, d_updates_per_g = 1): D step = G forward (no
     grad) + D forward on real and fake + D backward of both (weight gradients, data gradients
     but the first conv's); G step = G training pass + VGG19 conv3_4 perceptual (forward on
     [sr; hr], backward on sr) + D forward on sr + D's data gradients down to sr (the first
     conv's included).  D's weight gradients in the G step are counted only with
     freeze_d_in_g_step=False (the reference computes them and never uses them:
-    TrainerConfig.freeze_d_in_g_step skips them by default)."""
+    TrainerConfig.freeze_d_in_g_step skips them by default), the D step's own generator forward
+    only with reuse_g_forward=False (the reference recomputes the G step's forward there: same
+    input, same weights)."""
     g_fwd = gen_fwd_flop(hw)
     d_fwd, d_first = disc_flops(4 * hw)
     v_fwd, v_bwd = vgg_flops(4 * hw)
-    d_step = g_fwd + 2 * d_fwd + 2 * (2 * d_fwd - d_first)
+    d_step = (0 if reuse_g else g_fwd) + 2 * d_fwd + 2 * (2 * d_fwd - d_first)
     g_step = gen_train_flop(hw) + 2 * v_fwd + v_bwd + d_fwd + (d_fwd if freeze_d else 2 * d_fwd)
     return B * (d_step + g_step)
 
@@ -434,7 +436,8 @@ def time_gan_step(steps, B=16):
     cfg = TrainerConfig(learning_rate=1e-4, weight_decay=0.0, gradient_clip=0.5, gan_weight=0.005,
                         d_learning_rate=1e-4, use_wandb=False, scheduler_type="none",
                         checkpoint_dir="/tmp/fen_bench_ckpt",
-                        freeze_d_in_g_step=os.environ.get("FEN_GAN_FREEZE_D", "1") == "1")   # (A/B switch)
+                        freeze_d_in_g_step=os.environ.get("FEN_GAN_FREEZE_D", "1") == "1",   # (A/B switches)
+                        reuse_g_forward=os.environ.get("FEN_GAN_REUSE_G", "1") == "1")
     tr = Trainer(build_model("bf16"), [], None, loss_fn=loss_fn, config=cfg, discriminator=D,
                  gan_loss=GANLoss("vanilla"))
     hr = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(99)).cuda()
@@ -452,9 +455,11 @@ def time_gan_step(steps, B=16):
     el_e, _ = run(tr._gan_step)
     el, loss = run(tr._gan_iteration)
     frz = bool(getattr(tr.config, "freeze_d_in_g_step", True))
-    flop = gan_iteration_flop(B, freeze_d=frz)
+    reu = bool(getattr(tr.config, "reuse_g_forward", True))
+    flop = gan_iteration_flop(B, freeze_d=frz, reuse_g=reu)
     return {"roofline": step_roofline(flop, 1000.0 * el / steps,
-                                      "algorithmic FLOPs of one iteration (bench.gan_iteration_flop: G fwd + D fwd x2 + "
+                                      "algorithmic FLOPs of one iteration (bench.gan_iteration_flop: "
+                                      + ("" if reu else "G fwd + ") + "D fwd x2 + "
                                       "D bwd x2; G train + VGG19 conv3_4 fwd x2 + dgrad + D fwd + D "
                                       + ("data gradients (freeze_d_in_g_step: D's unused weight gradients not computed)"
                                          if frz else "bwd") + ") at B=16"),

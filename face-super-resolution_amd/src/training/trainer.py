@@ -80,6 +80,11 @@ class TrainerConfig:
     # weight update is identical (tests/test_gpu_gan_step.py); only D's .grad after an
     # iteration differs (the D step's gradients alone).  False: the reference's dead work too.
     freeze_d_in_g_step: bool = True
+    # (HIP extension) the iteration's generator forward runs once: the reference runs it twice
+    # on the same LR batch with the same weights -- under no_grad for the D step(s), again with
+    # grad for the G step (trainer.py:430-431, 461) -- so the D step takes the G step's output,
+    # detached (the same values; the G weights do not move in between).  False: both passes.
+    reuse_g_forward: bool = True
 
 
 class EarlyStopping:
@@ -299,10 +304,15 @@ class Trainer:
         self._dp_exchanges()
         lr = bicubic_down4(hr)
         D.train()
+        reuse = getattr(self.config, "reuse_g_forward", True)
+        sr = self.model(lr) if reuse else None
         for _ in range(self.config.d_updates_per_g):
             self.optimizer_d.zero_grad()
-            with torch.no_grad():
-                sr_d = self.model(lr)
+            if reuse:
+                sr_d = sr.detach()
+            else:
+                with torch.no_grad():
+                    sr_d = self.model(lr)
             # (the HIP discriminator takes both batches in one pass, per-batch BatchNorm statistics)
             d_real, d_fake = D.forward_pair(hr, sr_d.detach()) if hasattr(D, "forward_pair") else \
                 (D(hr), D(sr_d.detach()))
@@ -313,7 +323,8 @@ class Trainer:
             if self._d_ex is not None:
                 self._d_ex.wait()        # D's two buckets, all-reduced as the backward completed them
             self.optimizer_d.step()
-        sr = self.model(lr)
+        if not reuse:
+            sr = self.model(lr)
         content = self._content(sr, hr)
         frozen = []
         if getattr(self.config, "freeze_d_in_g_step", True):

@@ -72,3 +72,27 @@ def test_frozen_d_in_g_step_same_updates(tmp_path):
         for a, b, c in zip(_state(ref), _state(frz), _state(cap)):
             assert torch.equal(a, b) and torch.equal(a, c), i
     assert all(p.requires_grad for p in frz.discriminator.parameters())
+
+
+def test_reused_g_forward_same_updates(tmp_path):
+    """TrainerConfig.reuse_g_forward (default): the iteration's generator forward runs once and
+    the D step takes it detached -- the reference runs the same forward twice (no_grad for the D
+    step, with grad for the G step: same LR batch, same weights).  The training forward's output
+    equals the no-grad forward's bit for bit, so every update is the same as with both passes."""
+    a, b = _trainer(False, tmp_path / "a"), _trainer(False, tmp_path / "b")
+    a.config.reuse_g_forward = False
+    gen = torch.Generator().manual_seed(11)
+    hr0 = torch.rand(2, 3, 128, 128, generator=gen).to(DEV)
+    from src.training.trainer import bicubic_down4
+    lr = bicubic_down4(hr0)
+    with torch.no_grad():
+        y0 = a.model(lr)
+    y1 = a.model(lr)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1.detach())
+    for i in range(4):
+        hr = torch.rand(2, 3, 128, 128, generator=gen).to(DEV)
+        la, lb = float(a._gan_iteration(hr)), float(b._gan_iteration(hr))
+        assert la == lb, (i, la, lb)
+        for x, y in zip(_state(a), _state(b)):
+            assert torch.equal(x, y), i
