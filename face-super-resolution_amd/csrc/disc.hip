@@ -793,6 +793,46 @@ __global__ __launch_bounds__(256) void k_dhead_dxfin(size_t n, const float* __re
     for (int g = 0; g < DH_G; ++g) v += dxpart[(size_t)g * n + i];
     dx[i] = v;
 }
+// GANLoss (discriminator.py:154-206) against a constant label t, mean over n scores, one block
+// (fixed-order reduction: deterministic):
+//   mode 0 'vanilla': nn.BCEWithLogitsLoss, torch's stable form (1 - t) x + m + log(exp(-m) +
+//                     exp(-x - m)), m = max(-x, 0); d/dx = sigmoid(x) - t
+//   mode 1 'lsgan':   nn.MSELoss, (x - t)^2; d/dx = 2 (x - t)
+//   mode 2 'wgan':    t x (t = -1 real, +1 fake: -mean / +mean); d/dx = t
+// and the gradient gx = d/dx / n * gy, the upstream gradient gy read on the device.  n is the
+// batch (16-32 scores): one launch each way instead of the ~10 small aten kernels per call.
+__device__ __forceinline__ float gan_term(int mode, float v, float t) {
+    if (mode == 0) {
+        const float m = fmaxf(-v, 0.f);
+        return (1.f - t) * v + m + logf(expf(-m) + expf(-v - m));
+    }
+    if (mode == 1) return (v - t) * (v - t);
+    return t * v;
+}
+
+__global__ __launch_bounds__(256) void k_gan_loss(int mode, int n, const float* __restrict__ x, float t,
+                                                   float* __restrict__ loss) {
+    __shared__ float red[256];
+    float a = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) a += gan_term(mode, x[i], t);
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) loss[0] = red[0] / (float)n;
+}
+
+__global__ __launch_bounds__(256) void k_gan_loss_bwd(int mode, int n, const float* __restrict__ x, float t,
+                                                       const float* __restrict__ gy, float* __restrict__ gx) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float v = x[i];
+    const float d = mode == 0 ? 1.f / (1.f + expf(-v)) - t : mode == 1 ? 2.f * (v - t) : t;
+    gx[i] = d / (float)n * gy[0];
+}
+
 }  // namespace
 
 extern "C" size_t fen_dhead_work_floats(int B, int K, int N) {
@@ -842,6 +882,21 @@ extern "C" int fen_dhead_bwd(int B, int K, int N, const float* x, const float* w
         const size_t n = (size_t)B * K;
         hipLaunchKernelGGL(k_dhead_dxfin, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, STREAM, n, dxpart, dx);
     }
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_gan_loss(int mode, int n, const float* x, float target, float* loss, void* stream) {
+    if (mode < 0 || mode > 2 || n <= 0 || !x || !loss) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_gan_loss, dim3(1), dim3(256), 0, STREAM, mode, n, x, target, loss);
+    FEN_CHECK_LAUNCH();
+    return FEN_OK;
+}
+
+extern "C" int fen_gan_loss_bwd(int mode, int n, const float* x, float target, const float* gy, float* gx,
+                                void* stream) {
+    if (mode < 0 || mode > 2 || n <= 0 || !x || !gy || !gx) return FEN_EINVAL;
+    hipLaunchKernelGGL(k_gan_loss_bwd, dim3((n + 255) / 256), dim3(256), 0, STREAM, mode, n, x, target, gy, gx);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
 }

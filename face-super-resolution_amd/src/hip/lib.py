@@ -207,6 +207,8 @@ _SIGS = {
     "fen_zero_insert2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_adamw_multi": (c_int, [c_int, c_void_p] + [c_float] * 7 + [c_void_p]),
     "fen_l1_loss": (c_int, [c_size_t] + [c_void_p] * 3 + [c_float] + [c_void_p] * 3),
+    "fen_gan_loss": (c_int, [c_int, c_int, c_void_p, c_float, c_void_p, c_void_p]),
+    "fen_gan_loss_bwd": (c_int, [c_int, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
     "fen_dhead_work_floats": (c_size_t, [c_int] * 3),
     "fen_dhead_fwd": (c_int, [c_int] * 3 + [c_void_p] * 5 + [c_float, c_int] + [c_void_p] * 4),
     "fen_dhead_bwd": (c_int, [c_int] * 3 + [c_void_p] * 6 + [c_float, c_int] + [c_void_p] * 7),

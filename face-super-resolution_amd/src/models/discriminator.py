@@ -39,6 +39,8 @@ _S2D = os.environ.get("FEN_D_S2D", "1") != "0"
 # (the 64-channel stride-2 layer stays on the full-resolution persistent kernels)
 _S2D_MIN_CIN = int(os.environ.get("FEN_D_S2D_MIN_CIN", "128"))
 _S2D_MAX_CIN = int(os.environ.get("FEN_D_S2D_MAX_CIN", "256"))
+# FEN_GAN_LOSS=0: GANLoss on the torch criteria (A/B; CPU tensors always take them)
+_HIP_GAN_LOSS = os.environ.get("FEN_GAN_LOSS", "1") != "0"
 # A/B switch: FEN_D_PACK_MULTI=0 re-packs each stale filter copy in a launch of its own
 _PACK_MULTI = os.environ.get("FEN_D_PACK_MULTI", "1") != "0"
 
@@ -460,6 +462,35 @@ class VGGStyleDiscriminator(nn.Module):
                 'size_mb': total_params * 4 / (1024 ** 2)}
 
 
+_GAN_MODES = {'vanilla': 0, 'lsgan': 1, 'wgan': 2}
+
+
+class _GanLossFn(torch.autograd.Function):
+    """GANLoss's criterion on fen_gan_loss / fen_gan_loss_bwd: one launch each way (the module
+    losses take ~10 small aten kernels per call)."""
+
+    @staticmethod
+    def forward(fctx, x, mode, target):
+        from ..hip import lib as L
+        x = x.detach().float().contiguous()
+        loss = torch.empty((), device=x.device)
+        L.check(L.load().fen_gan_loss(mode, x.numel(), x.data_ptr(), float(target), loss.data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream), "gan_loss")
+        fctx.save_for_backward(x)
+        fctx.mode, fctx.target = mode, float(target)
+        return loss
+
+    @staticmethod
+    def backward(fctx, gy):
+        from ..hip import lib as L
+        (x,) = fctx.saved_tensors
+        gy = gy.detach().float().contiguous()
+        gx = torch.empty_like(x)
+        L.check(L.load().fen_gan_loss_bwd(fctx.mode, x.numel(), x.data_ptr(), fctx.target, gy.data_ptr(),
+                                          gx.data_ptr(), torch.cuda.current_stream().cuda_stream), "gan_loss_bwd")
+        return gx, None, None
+
+
 class GANLoss(nn.Module):
     """'vanilla' (BCE with logits), 'lsgan' (MSE), 'wgan' (raw scores) -- discriminator.py:154-206."""
 
@@ -481,6 +512,9 @@ class GANLoss(nn.Module):
         return torch.full_like(prediction, self.real_label if is_real else self.fake_label)
 
     def forward(self, prediction: torch.Tensor, is_real: bool) -> torch.Tensor:
+        if prediction.is_cuda and prediction.dtype == torch.float32 and _HIP_GAN_LOSS:
+            t = (-1.0 if is_real else 1.0) if self.gan_type == 'wgan' else (self.real_label if is_real else self.fake_label)
+            return _GanLossFn.apply(prediction, _GAN_MODES[self.gan_type], t)
         if self.gan_type == 'wgan':
             return -prediction.mean() if is_real else prediction.mean()
         return self.loss(prediction, self.get_target_tensor(prediction, is_real))

@@ -657,6 +657,12 @@ int fen_dhead_fwd(int B, int K, int N, const float* x, const float* w1, const fl
 int fen_dhead_bwd(int B, int K, int N, const float* x, const float* w1, const float* pre, const float* w2,
                   const float* y, const float* gy, float slope, int sigmoid, float* dx, float* dw1, float* db1,
                   float* dw2, float* db2, float* work, void* stream);
+/* GANLoss (discriminator.py:154-206) over n fp32 scores x against a constant label, mean
+ * reduction: mode 0 'vanilla' nn.BCEWithLogitsLoss (torch's stable form), 1 'lsgan' nn.MSELoss,
+ * 2 'wgan' target * x (target -1 for real, +1 for fake).  loss[0] = the mean; the gradient
+ * gx = d(term)/dx / n * gy[0], gy the upstream gradient on the device.  FEN_EINVAL: mode, n.  */
+int fen_gan_loss(int mode, int n, const float* x, float target, float* loss, void* stream);
+int fen_gan_loss_bwd(int mode, int n, const float* x, float target, const float* gy, float* gx, void* stream);
 
 /* A status word for fen_group_strip / fen_group_strip_bwd `status`: one zeroed int in
  * host-mapped, coherent pinned memory (hipHostMalloc, 64 B), allocated on the first call for

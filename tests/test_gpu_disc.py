@@ -135,3 +135,29 @@ def test_forward_pair_matches_two_calls(precision):
     for (k, p1), p2 in zip(d1.named_parameters(), d2.parameters()):
         e = float((p1.grad - p2.grad).norm() / max(float(p1.grad.norm()), 1e-30))
         assert e <= tol, (k, e)
+
+
+@pytest.mark.parametrize("gan_type", ["vanilla", "lsgan", "wgan"])
+@pytest.mark.parametrize("is_real", [True, False])
+def test_gan_loss_hip(gan_type, is_real):
+    """GANLoss on fen_gan_loss: the loss and d(loss)/d(scores) equal the reference criteria's
+    (nn.BCEWithLogitsLoss / nn.MSELoss / the signed mean, torch on the same device) within fp32
+    rounding, for large, small and zero scores."""
+    from src.models import GANLoss
+    x = torch.tensor([[-30.0], [-3.5], [-0.2], [0.0], [0.7], [4.0], [25.0]] * 3, device=DEV, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    gl = GANLoss(gan_type)
+    loss = gl(x, is_real) * 1.7
+    t = torch.full_like(xr, 1.0 if is_real else 0.0)
+    if gan_type == "vanilla":
+        ref = torch.nn.BCEWithLogitsLoss()(xr, t)
+    elif gan_type == "lsgan":
+        ref = torch.nn.MSELoss()(xr, t)
+    else:
+        ref = -xr.mean() if is_real else xr.mean()
+    ref = ref * 1.7
+    loss.backward()
+    ref.backward()
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)) + 1e-7
+    assert torch.allclose(x.grad, xr.grad, rtol=1e-5, atol=1e-8)
