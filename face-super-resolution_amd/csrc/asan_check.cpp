@@ -37,6 +37,16 @@ static void pure_queries() {
     EXPECT(fen_feat_loss_parts() > 0);
     EXPECT(fen_ssim_parts(2, 3, 64, 64) > 0 && fen_ssim_work_floats(2, 3, 64, 64) == (size_t)3 * 2 * 3 * 64 * 64);
     EXPECT(fen_bn_work_floats(64) > 0);
+    {   // grouped BN refusals (host checks only: no launch)
+        float f = 0.f;
+        EXPECT(fen_bn_stats_n(FEN_BF16, 0, 16, 64, &f, 1e-5f, 0.1f, &f, nullptr, nullptr, &f, nullptr) == FEN_EINVAL);
+        EXPECT(fen_bn_stats_n(FEN_BF16, 2, 16, 60, &f, 1e-5f, 0.1f, &f, nullptr, nullptr, &f, nullptr) == FEN_EINVAL);
+        EXPECT(fen_bn_stats_n(FEN_BF16, 2, 16, 64, &f, 1e-5f, 0.1f, &f, &f, nullptr, &f, nullptr) == FEN_EINVAL);
+        EXPECT(fen_bn_apply_n(FEN_BF16, 2, 16, 64, &f, &f, &f, 32, &f, &f, 0.2f, &f, nullptr) == FEN_EINVAL);
+        EXPECT(fen_bn_apply_n(FEN_BF16, 1, 16, 2048, &f, &f, &f, 0, &f, &f, 0.2f, &f, nullptr) == FEN_EUNSUPPORTED);
+        EXPECT(fen_bn_bwd_n(FEN_BF16, 0, 16, 64, &f, &f, &f, &f, &f, 0.2f, &f, &f, &f, 0, &f, nullptr) == FEN_EINVAL);
+        EXPECT(fen_bn_bwd_n(FEN_BF16, 2, 16, 64, &f, &f, &f, &f, &f, 0.2f, &f, &f, &f, 0, nullptr, nullptr) == FEN_EINVAL);
+    }
     EXPECT(fen_conv_first_work_floats(2, 3, 64, 64, 64) > 0);
     EXPECT(fen_conv_last_dgrad_part_rows(2, 256, 256) > 0);
     EXPECT(fen_group_strip_work_bytes(32, 64) > 0 && fen_group_strip_bwd_work_bytes(32, 64) > 0);

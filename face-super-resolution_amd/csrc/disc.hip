@@ -14,10 +14,13 @@ constexpr int BN_BLOCKS = 512;
 
 // part[blk][c] = (sum (y - shift_c), sum (y - shift_c)^2) over the block's pixels; thread =
 // (pixel lane, 8-channel group)
+// (blockIdx.y = group: groups of npx pixels one after another in y, partials [group][blk][2C])
 template <typename T>
 __global__ __launch_bounds__(256) void k_bn_stats(size_t npx, int C, const T* __restrict__ y,
                                                   float* __restrict__ part) {
     constexpr int V = 16 / sizeof(T);
+    y += (size_t)blockIdx.y * npx * C;
+    part += (size_t)blockIdx.y * gridDim.x * 2 * C;
     const int G = C / V;                     // channel groups (C % 8 == 0, C / V <= 256)
     const int lanes = 256 / G > 0 ? 256 / G : 1;
     const int g = threadIdx.x % G, pl = threadIdx.x / G;
@@ -55,44 +58,52 @@ __global__ __launch_bounds__(256) void k_bn_stats(size_t npx, int C, const T* __
 // 64 channels per block, 16 waves each summing every 16th partial (loads in flight across the
 // waves; one thread walking all BN_BLOCKS partials took ~130 us), fixed-order combine in LDS
 constexpr int FIN_WAVES = 16;
+// ng groups (partials [group][nblocks][2C], stat [group][2C]) one after another in this order,
+// so the running statistics move group by group exactly as ng separate calls move them
 template <typename T>
 __global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_finalize(int nblocks, size_t npx, int C, const T* __restrict__ y,
                                                               const float* __restrict__ part, float eps, float momentum,
                                                               float* __restrict__ stat, float* __restrict__ rmean,
-                                                              float* __restrict__ rvar) {
+                                                              float* __restrict__ rvar, int ng) {
     __shared__ double red[2][FIN_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
-    double s = 0.0, q = 0.0;
-    if (c < C) {
-        // (unrolled: the partials' loads in flight together, summed in the same order -- the
-        // rolled loop waited one L2 round trip per partial, ~12 us per finalize)
+    for (int gi = 0; gi < ng; ++gi) {
+        const float* pg = part + (size_t)gi * nblocks * 2 * C;
+        double s = 0.0, q = 0.0;
+        if (c < C) {
+            // (unrolled: the partials' loads in flight together, summed in the same order -- the
+            // rolled loop waited one L2 round trip per partial, ~12 us per finalize)
 #pragma unroll 8
-        for (int b = w; b < nblocks; b += FIN_WAVES) {
-            s += part[(size_t)b * 2 * C + c];
-            q += part[(size_t)b * 2 * C + C + c];
+            for (int b = w; b < nblocks; b += FIN_WAVES) {
+                s += pg[(size_t)b * 2 * C + c];
+                q += pg[(size_t)b * 2 * C + C + c];
+            }
         }
-    }
-    red[0][w][lane] = s;
-    red[1][w][lane] = q;
-    __syncthreads();
-    if (w != 0 || c >= C) return;
-    s = 0.0;
-    q = 0.0;
-    for (int k = 0; k < FIN_WAVES; ++k) {
-        s += red[0][k][lane];
-        q += red[1][k][lane];
-    }
-    const double n = (double)npx;
-    const double md = s / n;                                  // mean of (y - shift)
-    double var = q / n - md * md;
-    if (var < 0) var = 0;
-    const float mean = (float)(md + (double)tof<T>(y[c]));
-    stat[c] = mean;
-    stat[C + c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (rmean) {
-        rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-        rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(var * n / (n > 1 ? n - 1 : 1));
+        if (gi) __syncthreads();                             // the previous group's combine read red
+        red[0][w][lane] = s;
+        red[1][w][lane] = q;
+        __syncthreads();
+        if (w == 0 && c < C) {
+            s = 0.0;
+            q = 0.0;
+            for (int k = 0; k < FIN_WAVES; ++k) {
+                s += red[0][k][lane];
+                q += red[1][k][lane];
+            }
+            const double n = (double)npx;
+            const double md = s / n;                              // mean of (y - shift)
+            double var = q / n - md * md;
+            if (var < 0) var = 0;
+            const float mean = (float)(md + (double)tof<T>(y[(size_t)gi * npx * C + c]));
+            float* sg = stat + (size_t)gi * 2 * C;
+            sg[c] = mean;
+            sg[C + c] = (float)(1.0 / sqrt(var + (double)eps));
+            if (rmean) {
+                rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+                rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(var * n / (n > 1 ? n - 1 : 1));
+            }
+        }
     }
 }
 
@@ -148,6 +159,10 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(size_t npx, int C, const 
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float slope, float* __restrict__ part) {
     constexpr int V = 16 / sizeof(T);
+    da += (size_t)blockIdx.y * npx * C;                      // (blockIdx.y = group, as k_bn_stats)
+    y += (size_t)blockIdx.y * npx * C;
+    stat += (size_t)blockIdx.y * 2 * C;
+    part += (size_t)blockIdx.y * gridDim.x * 2 * C;
     const int G = C / V;
     const int lanes = 256 / G > 0 ? 256 / G : 1;
     const int g = threadIdx.x % G, pl = threadIdx.x / G;
@@ -184,35 +199,44 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(size_t npx, int C, const 
 }
 
 // dbeta = sum dz, dgamma = sum dz xh (fixed-order over the block partials); red2 = the same
-// for the data-gradient pass
+// for the data-gradient pass.  ng groups in order (partials [group][nblocks][2C], red2 [group][2C]):
+// group 0 sets or accumulates as `accumulate` says, every later group accumulates -- the sums of
+// ng separate calls, in their order
 __global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_bwd_finalize(int nblocks, int C, const float* __restrict__ part,
                                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                                  float* __restrict__ red2, int accumulate) {
+                                                                  float* __restrict__ red2, int accumulate, int ng) {
     __shared__ float red[2][FIN_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
-    float s = 0.f, q = 0.f;
-    if (c < C) {
+    for (int gi = 0; gi < ng; ++gi) {
+        const float* pg = part + (size_t)gi * nblocks * 2 * C;
+        float s = 0.f, q = 0.f;
+        if (c < C) {
 #pragma unroll 8
-        for (int b = w; b < nblocks; b += FIN_WAVES) {
-            s += part[(size_t)b * 2 * C + c];
-            q += part[(size_t)b * 2 * C + C + c];
+            for (int b = w; b < nblocks; b += FIN_WAVES) {
+                s += pg[(size_t)b * 2 * C + c];
+                q += pg[(size_t)b * 2 * C + C + c];
+            }
+        }
+        if (gi) __syncthreads();
+        red[0][w][lane] = s;
+        red[1][w][lane] = q;
+        __syncthreads();
+        if (w == 0 && c < C) {
+            s = 0.f;
+            q = 0.f;
+            for (int k = 0; k < FIN_WAVES; ++k) {
+                s += red[0][k][lane];
+                q += red[1][k][lane];
+            }
+            float* r2 = red2 + (size_t)gi * 2 * C;
+            r2[c] = s;
+            r2[C + c] = q;
+            const int acc = gi ? 1 : accumulate;
+            if (dbeta) dbeta[c] = acc ? dbeta[c] + s : s;
+            if (dgamma) dgamma[c] = acc ? dgamma[c] + q : q;
         }
     }
-    red[0][w][lane] = s;
-    red[1][w][lane] = q;
-    __syncthreads();
-    if (w != 0 || c >= C) return;
-    s = 0.f;
-    q = 0.f;
-    for (int k = 0; k < FIN_WAVES; ++k) {
-        s += red[0][k][lane];
-        q += red[1][k][lane];
-    }
-    red2[c] = s;
-    red2[C + c] = q;
-    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + s : s;
-    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + q : q;
 }
 
 // dy = gamma rstd / N (N dz - sum dz - xh sum dz xh)
@@ -299,12 +323,17 @@ __global__ __launch_bounds__(256) void k_zero_insert2(int B, int Ho, int Wo, int
 // per-channel operands are loaded into registers once per thread, not per vector (the forms
 // above index them per vector with a 64-bit modulo).  Arithmetic unchanged: bit-identical.
 constexpr int BN_PPT = 4;
+// (blockIdx.y = group: y / out advance npx pixels, mean / rstd `mstride` floats per group)
 template <typename T>
 __global__ __launch_bounds__(256) void k_bn_apply_g(size_t npx, int C, const T* __restrict__ y,
                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                    float slope, T* __restrict__ out) {
+                                                    float slope, T* __restrict__ out, int mstride) {
     constexpr int V = 16 / sizeof(T);
+    y += (size_t)blockIdx.y * npx * C;
+    out += (size_t)blockIdx.y * npx * C;
+    mean += (size_t)blockIdx.y * mstride;
+    rstd += (size_t)blockIdx.y * mstride;
     const int G = C / V, lanes = 256 / G;
     const int g = threadIdx.x % G, pl = threadIdx.x / G;
     if (pl >= lanes) return;
@@ -343,6 +372,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_g(size_t npx, int C, const
                                                         float slope, const float* __restrict__ red2,
                                                         T* __restrict__ dy) {
     constexpr int V = 16 / sizeof(T);
+    da += (size_t)blockIdx.y * npx * C;                      // (blockIdx.y = group)
+    y += (size_t)blockIdx.y * npx * C;
+    dy += (size_t)blockIdx.y * npx * C;
+    stat += (size_t)blockIdx.y * 2 * C;
+    red2 += (size_t)blockIdx.y * 2 * C;
     const int G = C / V, lanes = 256 / G;
     const int g = threadIdx.x % G, pl = threadIdx.x / G;
     if (pl >= lanes) return;
@@ -385,22 +419,25 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_g(size_t npx, int C, const
 #define STREAM ((hipStream_t)stream)
 extern "C" size_t fen_bn_work_floats(int C) { return (size_t)BN_BLOCKS * 2 * C + 2 * C; }
 
-// train-mode statistics of y (NHWC [npx][C]) -> stat [2C] (mean, rstd); running stats updated
-// when rmean != NULL.  work: fen_bn_work_floats(C) floats.
-extern "C" int fen_bn_stats(int dtype, size_t npx, int C, const void* y, float eps, float momentum, float* stat,
-                            float* rmean, float* rvar, float* work, void* stream) {
-    if (!y || !stat || !work || npx == 0 || C % 8 || C > 2048 || (rmean != nullptr) != (rvar != nullptr))
+// train-mode statistics of ng groups of npx pixels each, one after another in y (NHWC) -> stat
+// [ng][2C] (mean, rstd); running stats updated group by group in order when rmean != NULL.
+// work: ng * fen_bn_work_floats(C) floats.  Two launches whatever ng (the D step's real and fake
+// batches: half the launches of one call per batch, bit-identical results)
+extern "C" int fen_bn_stats_n(int dtype, int ng, size_t npx, int C, const void* y, float eps, float momentum,
+                              float* stat, float* rmean, float* rvar, float* work, void* stream) {
+    if (!y || !stat || !work || npx == 0 || ng < 1 || ng > 65535 || C % 8 || C > 2048 ||
+        (rmean != nullptr) != (rvar != nullptr))
         return FEN_EINVAL;
     if (dtype == FEN_BF16) {
-        hipLaunchKernelGGL(k_bn_stats<bf16>, dim3(BN_BLOCKS), dim3(256), 0, STREAM, npx, C, (const bf16*)y, work);
+        hipLaunchKernelGGL(k_bn_stats<bf16>, dim3(BN_BLOCKS, ng), dim3(256), 0, STREAM, npx, C, (const bf16*)y, work);
         FEN_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_bn_finalize<bf16>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C, (const bf16*)y,
-                           work, eps, momentum, stat, rmean, rvar);
+                           work, eps, momentum, stat, rmean, rvar, ng);
     } else if (dtype == FEN_F32) {
-        hipLaunchKernelGGL(k_bn_stats<float>, dim3(BN_BLOCKS), dim3(256), 0, STREAM, npx, C, (const float*)y, work);
+        hipLaunchKernelGGL(k_bn_stats<float>, dim3(BN_BLOCKS, ng), dim3(256), 0, STREAM, npx, C, (const float*)y, work);
         FEN_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C,
-                           (const float*)y, work, eps, momentum, stat, rmean, rvar);
+                           (const float*)y, work, eps, momentum, stat, rmean, rvar, ng);
     } else {
         return FEN_EINVAL;
     }
@@ -408,87 +445,118 @@ extern "C" int fen_bn_stats(int dtype, size_t npx, int C, const void* y, float e
     return FEN_OK;
 }
 
-// out = lrelu((y - mean) * rstd * gamma + beta); mean / rstd = stat (train) or the running
-// statistics turned into rstd by the caller (eval)
+// one group: stat [2C], work fen_bn_work_floats(C)
+extern "C" int fen_bn_stats(int dtype, size_t npx, int C, const void* y, float eps, float momentum, float* stat,
+                            float* rmean, float* rvar, float* work, void* stream) {
+    return fen_bn_stats_n(dtype, 1, npx, C, y, eps, momentum, stat, rmean, rvar, work, stream);
+}
+
+// out = lrelu((y - mean) * rstd * gamma + beta) for ng groups of npx pixels (y / out one group
+// after another; group g's mean / rstd at mean / rstd + g * mstride); mean / rstd = stat (train)
+// or the running statistics turned into rstd by the caller (eval)
+extern "C" int fen_bn_apply_n(int dtype, int ng, size_t npx, int C, const void* y, const float* mean, const float* rstd,
+                              int mstride, const float* gamma, const float* beta, float slope, void* out,
+                              void* stream) {
+    if (!y || !mean || !rstd || !gamma || !beta || !out || C % 8 || ng < 1 || ng > 65535 || (ng > 1 && mstride < C))
+        return FEN_EINVAL;
+    if (C > 1024) return FEN_EUNSUPPORTED;
+    if (dtype != FEN_BF16 && dtype != FEN_F32) return FEN_EINVAL;
+    const int G = C / (dtype == FEN_F32 ? 4 : 8);
+    if (G <= 256 && 256 % G == 0) {
+        const size_t per = (size_t)(256 / G) * BN_PPT;
+        const unsigned nb = (unsigned)((npx + per - 1) / per);
+        if (dtype == FEN_BF16)
+            hipLaunchKernelGGL(k_bn_apply_g<bf16>, dim3(nb, ng), dim3(256), 0, STREAM, npx, C, (const bf16*)y, mean, rstd,
+                               gamma, beta, slope, (bf16*)out, mstride);
+        else
+            hipLaunchKernelGGL(k_bn_apply_g<float>, dim3(nb, ng), dim3(256), 0, STREAM, npx, C, (const float*)y, mean,
+                               rstd, gamma, beta, slope, (float*)out, mstride);
+        FEN_CHECK_LAUNCH();
+        return FEN_OK;
+    }
+    const size_t esz = dtype == FEN_F32 ? 4 : 2;
+    for (int gi = 0; gi < ng; ++gi) {                        // other channel counts: a launch per group
+        const char* yg = (const char*)y + (size_t)gi * npx * C * esz;
+        char* og = (char*)out + (size_t)gi * npx * C * esz;
+        const float *mg = mean + (size_t)gi * mstride, *rg = rstd + (size_t)gi * mstride;
+        if (dtype == FEN_BF16) {
+            const size_t nv = npx * C / 8;
+            hipLaunchKernelGGL(k_bn_apply<bf16>, dim3(nblk(nv, 256 * BN_NPT)), dim3(256), 0, STREAM, nv, C, (const bf16*)yg,
+                               mg, rg, gamma, beta, slope, (bf16*)og);
+        } else {
+            const size_t nv = npx * C / 4;
+            hipLaunchKernelGGL(k_bn_apply<float>, dim3(nblk(nv, 256 * BN_NPT)), dim3(256), 0, STREAM, nv, C,
+                               (const float*)yg, mg, rg, gamma, beta, slope, (float*)og);
+        }
+        FEN_CHECK_LAUNCH();
+    }
+    return FEN_OK;
+}
+
 extern "C" int fen_bn_apply(int dtype, size_t npx, int C, const void* y, const float* mean, const float* rstd,
                             const float* gamma, const float* beta, float slope, void* out, void* stream) {
-    if (!y || !mean || !rstd || !gamma || !beta || !out || C % 8) return FEN_EINVAL;
-    if (C > 1024) return FEN_EUNSUPPORTED;
-    {
-        const int G = C / (dtype == FEN_F32 ? 4 : 8);
-        if (G <= 256 && 256 % G == 0 && (dtype == FEN_BF16 || dtype == FEN_F32)) {
-            const size_t per = (size_t)(256 / G) * BN_PPT;
-            const unsigned nb = (unsigned)((npx + per - 1) / per);
-            if (dtype == FEN_BF16)
-                hipLaunchKernelGGL(k_bn_apply_g<bf16>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const bf16*)y, mean, rstd,
-                                   gamma, beta, slope, (bf16*)out);
-            else
-                hipLaunchKernelGGL(k_bn_apply_g<float>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const float*)y, mean,
-                                   rstd, gamma, beta, slope, (float*)out);
-            FEN_CHECK_LAUNCH();
-            return FEN_OK;
-        }
-    }
-    if (dtype == FEN_BF16) {
-        const size_t nv = npx * C / 8;
-        hipLaunchKernelGGL(k_bn_apply<bf16>, dim3(nblk(nv, 256 * BN_NPT)), dim3(256), 0, STREAM, nv, C, (const bf16*)y,
-                           mean, rstd, gamma, beta, slope, (bf16*)out);
-    } else if (dtype == FEN_F32) {
-        const size_t nv = npx * C / 4;
-        hipLaunchKernelGGL(k_bn_apply<float>, dim3(nblk(nv, 256 * BN_NPT)), dim3(256), 0, STREAM, nv, C,
-                           (const float*)y, mean, rstd, gamma, beta, slope, (float*)out);
-    } else {
+    return fen_bn_apply_n(dtype, 1, npx, C, y, mean, rstd, 0, gamma, beta, slope, out, stream);
+}
+
+// backward of out = lrelu(BN_train(y)) for ng groups of npx pixels (da / y / dy one group after
+// another, stat [ng][2C]): dy from da; dgamma / dbeta = the groups' sums in order (group 0 set or
+// accumulated as `accumulate` says).  work: ng * fen_bn_work_floats(C) floats.  Three launches
+// whatever ng; bit-identical to ng calls of fen_bn_bwd with accumulate = (g > 0 || accumulate)
+extern "C" int fen_bn_bwd_n(int dtype, int ng, size_t npx, int C, const void* da, const void* y, const float* stat,
+                            const float* gamma, const float* beta, float slope, void* dy, float* dgamma, float* dbeta,
+                            int accumulate, float* work, void* stream) {
+    if (!da || !y || !stat || !gamma || !beta || !dy || !work || C % 8 || C > 2048 || ng < 1 || ng > 65535)
         return FEN_EINVAL;
-    }
+    if (dtype != FEN_BF16 && dtype != FEN_F32) return FEN_EINVAL;
+    float* red2 = work + (size_t)ng * BN_BLOCKS * 2 * C;
+    if (dtype == FEN_BF16)
+        hipLaunchKernelGGL(k_bn_bwd_reduce<bf16>, dim3(BN_BLOCKS, ng), dim3(256), 0, STREAM, npx, C, (const bf16*)da,
+                           (const bf16*)y, stat, gamma, beta, slope, work);
+    else
+        hipLaunchKernelGGL(k_bn_bwd_reduce<float>, dim3(BN_BLOCKS, ng), dim3(256), 0, STREAM, npx, C, (const float*)da,
+                           (const float*)y, stat, gamma, beta, slope, work);
     FEN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, C, work, dgamma, dbeta, red2,
+                       accumulate, ng);
+    FEN_CHECK_LAUNCH();
+    const int G = C / (dtype == FEN_F32 ? 4 : 8);
+    if (G <= 256 && 256 % G == 0) {
+        const size_t per = (size_t)(256 / G) * BN_PPT;
+        const unsigned nb = (unsigned)((npx + per - 1) / per);
+        if (dtype == FEN_BF16)
+            hipLaunchKernelGGL(k_bn_bwd_apply_g<bf16>, dim3(nb, ng), dim3(256), 0, STREAM, npx, C, (const bf16*)da,
+                               (const bf16*)y, stat, gamma, beta, slope, red2, (bf16*)dy);
+        else
+            hipLaunchKernelGGL(k_bn_bwd_apply_g<float>, dim3(nb, ng), dim3(256), 0, STREAM, npx, C, (const float*)da,
+                               (const float*)y, stat, gamma, beta, slope, red2, (float*)dy);
+        FEN_CHECK_LAUNCH();
+        return FEN_OK;
+    }
+    const size_t esz = dtype == FEN_F32 ? 4 : 2;
+    for (int gi = 0; gi < ng; ++gi) {                        // other channel counts: a launch per group
+        const size_t o = (size_t)gi * npx * C * esz;
+        const float* sg = stat + (size_t)gi * 2 * C;
+        const float* rg = red2 + (size_t)gi * 2 * C;
+        if (dtype == FEN_BF16) {
+            const size_t nv = npx * C / 8;
+            hipLaunchKernelGGL(k_bn_bwd_apply<bf16>, dim3(nblk(nv)), dim3(256), 0, STREAM, nv, npx, C,
+                               (const bf16*)((const char*)da + o), (const bf16*)((const char*)y + o), sg, gamma, beta, slope,
+                               rg, (bf16*)((char*)dy + o));
+        } else {
+            const size_t nv = npx * C / 4;
+            hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(nblk(nv)), dim3(256), 0, STREAM, nv, npx, C,
+                               (const float*)((const char*)da + o), (const float*)((const char*)y + o), sg, gamma, beta,
+                               slope, rg, (float*)((char*)dy + o));
+        }
+        FEN_CHECK_LAUNCH();
+    }
     return FEN_OK;
 }
 
-// backward of out = lrelu(BN_train(y)): dy (NHWC) from da; dgamma / dbeta (accumulate or set)
 extern "C" int fen_bn_bwd(int dtype, size_t npx, int C, const void* da, const void* y, const float* stat,
                           const float* gamma, const float* beta, float slope, void* dy, float* dgamma, float* dbeta,
                           int accumulate, float* work, void* stream) {
-    if (!da || !y || !stat || !gamma || !beta || !dy || !work || C % 8 || C > 2048) return FEN_EINVAL;
-    float* red2 = work + (size_t)BN_BLOCKS * 2 * C;
-    if (dtype == FEN_BF16) {
-        hipLaunchKernelGGL(k_bn_bwd_reduce<bf16>, dim3(BN_BLOCKS), dim3(256), 0, STREAM, npx, C, (const bf16*)da,
-                           (const bf16*)y, stat, gamma, beta, slope, work);
-    } else if (dtype == FEN_F32) {
-        hipLaunchKernelGGL(k_bn_bwd_reduce<float>, dim3(BN_BLOCKS), dim3(256), 0, STREAM, npx, C, (const float*)da,
-                           (const float*)y, stat, gamma, beta, slope, work);
-    } else {
-        return FEN_EINVAL;
-    }
-    FEN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, C, work, dgamma, dbeta, red2,
-                       accumulate);
-    FEN_CHECK_LAUNCH();
-    {
-        const int G = C / (dtype == FEN_F32 ? 4 : 8);
-        if (G <= 256 && 256 % G == 0) {
-            const size_t per = (size_t)(256 / G) * BN_PPT;
-            const unsigned nb = (unsigned)((npx + per - 1) / per);
-            if (dtype == FEN_BF16)
-                hipLaunchKernelGGL(k_bn_bwd_apply_g<bf16>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const bf16*)da,
-                                   (const bf16*)y, stat, gamma, beta, slope, red2, (bf16*)dy);
-            else
-                hipLaunchKernelGGL(k_bn_bwd_apply_g<float>, dim3(nb), dim3(256), 0, STREAM, npx, C, (const float*)da,
-                                   (const float*)y, stat, gamma, beta, slope, red2, (float*)dy);
-            FEN_CHECK_LAUNCH();
-            return FEN_OK;
-        }
-    }
-    if (dtype == FEN_BF16) {
-        const size_t nv = npx * C / 8;
-        hipLaunchKernelGGL(k_bn_bwd_apply<bf16>, dim3(nblk(nv)), dim3(256), 0, STREAM, nv, npx, C, (const bf16*)da,
-                           (const bf16*)y, stat, gamma, beta, slope, red2, (bf16*)dy);
-    } else {
-        const size_t nv = npx * C / 4;
-        hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(nblk(nv)), dim3(256), 0, STREAM, nv, npx, C, (const float*)da,
-                           (const float*)y, stat, gamma, beta, slope, red2, (float*)dy);
-    }
-    FEN_CHECK_LAUNCH();
-    return FEN_OK;
+    return fen_bn_bwd_n(dtype, 1, npx, C, da, y, stat, gamma, beta, slope, dy, dgamma, dbeta, accumulate, work, stream);
 }
 
 extern "C" int fen_subsample2(int dtype, int B, int H, int W, int C, const void* x, void* y, void* stream) {

@@ -201,6 +201,11 @@ _SIGS = {
     "fen_bn_apply": (c_int, [c_int, c_size_t, c_int] + [c_void_p] * 5 + [c_float, c_void_p, c_void_p]),
     "fen_bn_bwd": (c_int, [c_int, c_size_t, c_int] + [c_void_p] * 5 + [c_float] + [c_void_p] * 3 +
                    [c_int, c_void_p, c_void_p]),
+    "fen_bn_stats_n": (c_int, [c_int, c_int, c_size_t, c_int, c_void_p, c_float, c_float] + [c_void_p] * 5),
+    "fen_bn_apply_n": (c_int, [c_int, c_int, c_size_t, c_int] + [c_void_p] * 3 + [c_int] + [c_void_p] * 2 +
+                       [c_float, c_void_p, c_void_p]),
+    "fen_bn_bwd_n": (c_int, [c_int, c_int, c_size_t, c_int] + [c_void_p] * 5 + [c_float] + [c_void_p] * 3 +
+                     [c_int, c_void_p, c_void_p]),
     "fen_subsample2": (c_int, [c_int] * 5 + [c_void_p] * 3),
     "fen_s2d2": (c_int, [c_int] * 5 + [c_void_p] * 2 + [c_int, c_void_p]),
     "fen_s2d_filter": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),

@@ -43,6 +43,8 @@ _S2D_MAX_CIN = int(os.environ.get("FEN_D_S2D_MAX_CIN", "256"))
 _HIP_GAN_LOSS = os.environ.get("FEN_GAN_LOSS", "1") != "0"
 # A/B switch: FEN_D_PACK_MULTI=0 re-packs each stale filter copy in a launch of its own
 _PACK_MULTI = os.environ.get("FEN_D_PACK_MULTI", "1") != "0"
+# A/B switch: FEN_D_BN_MULTI=0 runs the pair pass's BatchNorm launches once per batch
+_BN_MULTI = os.environ.get("FEN_D_BN_MULTI", "1") != "0"
 
 
 class _DFeatures(torch.autograd.Function):
@@ -95,7 +97,16 @@ class _DFeatures(torch.autograd.Function):
             gs = ng if mod.training else 1
             npx = (B // gs) * ho * wo                     # one BN group's pixels
             stat = ctx.alloc((gs, 2 * cout), torch.float32)
-            for gi in range(gs):
+            if gs > 1 and _BN_MULTI:
+                # the groups' statistics (running stats moved group by group) and BN + LeakyReLU
+                # in the launches of one group (fen_bn_stats_n / fen_bn_apply_n: bit-identical)
+                work = ctx.alloc((gs * lib.fen_bn_work_floats(cout),), torch.float32)
+                ctx.emit("d_bn_stats", lib.fen_bn_stats_n, ctx.code, gs, npx, cout, ptr(z), float(bn.eps),
+                         float(bn.momentum), ptr(stat), ptr(bn.running_mean), ptr(bn.running_var), ptr(work))
+                tracked += [bn.num_batches_tracked] * gs
+                ctx.emit("d_bn_apply", lib.fen_bn_apply_n, ctx.code, gs, npx, cout, ptr(z), ptr(stat), ptr(stat[0, cout:]),
+                         2 * cout, ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(out))
+            for gi in range(gs if not (gs > 1 and _BN_MULTI) else 0):
                 zg, sg, og = z[gi * (B // gs):], stat[gi], out[gi * (B // gs):]
                 if mod.training:
                     work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
@@ -151,8 +162,16 @@ class _DFeatures(torch.autograd.Function):
             # groups' dgamma / dbeta accumulate)
             dgam = torch.empty(cout, device=g.device)
             dbet = torch.empty(cout, device=g.device)
-            work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
-            for gi in range(ng):
+            if ng > 1 and _BN_MULTI:
+                # every group in the launches of one (fen_bn_bwd_n; dgamma / dbeta summed in group
+                # order, as the per-group calls below accumulate them)
+                work = ctx.alloc((ng * lib.fen_bn_work_floats(cout),), torch.float32)
+                ctx.emit("d_bn_bwd", lib.fen_bn_bwd_n, ctx.code, ng, npx, cout, ptr(d), ptr(sv["z"]), ptr(sv["stat"]),
+                         ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(dz), ptr(dgam), ptr(dbet), 0,
+                         ptr(work))
+            else:
+                work = ctx.alloc((lib.fen_bn_work_floats(cout),), torch.float32)
+            for gi in range(ng if not (ng > 1 and _BN_MULTI) else 0):
                 o = gi * (B // ng)
                 ctx.emit("d_bn_bwd", lib.fen_bn_bwd, ctx.code, npx, cout, ptr(d[o:]), ptr(sv["z"][o:]), ptr(sv["stat"][gi]),
                          ptr(bn.weight.detach()), ptr(bn.bias.detach()), _SLOPE, ptr(dz[o:]), ptr(dgam), ptr(dbet),

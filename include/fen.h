@@ -619,6 +619,11 @@ int fen_augment_u8(int B, int P, const void* src_u8, const void* params, long lo
  * when rmean/rvar != NULL; work = fen_bn_work_floats(C) floats.
  * fen_bn_apply: out = lrelu((y - mean) * rstd * gamma + beta, slope) (eval: running stats).
  * fen_bn_bwd: dy from da for out = lrelu(BN_train(y)); dgamma / dbeta set or accumulated.
+ * The _n forms run ng groups of npx pixels (one after another in y / out / da / dy; stat
+ * [ng][2C]; work ng * fen_bn_work_floats(C)) in the same launches as one group -- each group its
+ * own statistics, the running statistics and dgamma / dbeta moved group by group in order:
+ * bit-identical to ng calls (the D step's real and fake batches, trainer.py:433-434).
+ * fen_bn_apply_n takes group g's mean / rstd at mean / rstd + g * mstride.
  * A stride-2 conv = fen_conv3x3 at full resolution + fen_subsample2; its gradients = the
  * stride-1 ones of fen_zero_insert2(dy).                                                  */
 size_t fen_bn_work_floats(int C);
@@ -629,6 +634,13 @@ int fen_bn_apply(int dtype, size_t npx, int C, const void* y, const float* mean,
 int fen_bn_bwd(int dtype, size_t npx, int C, const void* da, const void* y, const float* stat, const float* gamma,
                const float* beta, float slope, void* dy, float* dgamma, float* dbeta, int accumulate, float* work,
                void* stream);
+int fen_bn_stats_n(int dtype, int ng, size_t npx, int C, const void* y, float eps, float momentum, float* stat,
+                   float* rmean, float* rvar, float* work, void* stream);
+int fen_bn_apply_n(int dtype, int ng, size_t npx, int C, const void* y, const float* mean, const float* rstd,
+                   int mstride, const float* gamma, const float* beta, float slope, void* out, void* stream);
+int fen_bn_bwd_n(int dtype, int ng, size_t npx, int C, const void* da, const void* y, const float* stat,
+                 const float* gamma, const float* beta, float slope, void* dy, float* dgamma, float* dbeta,
+                 int accumulate, float* work, void* stream);
 int fen_subsample2(int dtype, int B, int H, int W, int C, const void* x, void* y, void* stream);
 /* space-to-depth by 2: y[b][i][j][(2a + c2) * C + c] = x[b][2i + a][2j + c2][c] (x [B,H,W,C] ->
  * y [B,H/2,W/2,4C]); inverse = 1 maps y back.  With the phase-major filter
