@@ -58,52 +58,46 @@ __global__ __launch_bounds__(256) void k_bn_stats(size_t npx, int C, const T* __
 // 64 channels per block, 16 waves each summing every 16th partial (loads in flight across the
 // waves; one thread walking all BN_BLOCKS partials took ~130 us), fixed-order combine in LDS
 constexpr int FIN_WAVES = 16;
-// ng groups (partials [group][nblocks][2C], stat [group][2C]) one after another in this order,
-// so the running statistics move group by group exactly as ng separate calls move them
+// (one group per launch: a form walking the groups inside one launch measured 19-42 us per
+// launch vs 6.2 per group -- the grouped entry points launch this once per group)
 template <typename T>
 __global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_finalize(int nblocks, size_t npx, int C, const T* __restrict__ y,
                                                               const float* __restrict__ part, float eps, float momentum,
                                                               float* __restrict__ stat, float* __restrict__ rmean,
-                                                              float* __restrict__ rvar, int ng) {
+                                                              float* __restrict__ rvar) {
     __shared__ double red[2][FIN_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
-    for (int gi = 0; gi < ng; ++gi) {
-        const float* pg = part + (size_t)gi * nblocks * 2 * C;
-        double s = 0.0, q = 0.0;
-        if (c < C) {
-            // (unrolled: the partials' loads in flight together, summed in the same order -- the
-            // rolled loop waited one L2 round trip per partial, ~12 us per finalize)
+    double s = 0.0, q = 0.0;
+    if (c < C) {
+        // (unrolled: the partials' loads in flight together, summed in the same order -- the
+        // rolled loop waited one L2 round trip per partial, ~12 us per finalize)
 #pragma unroll 8
-            for (int b = w; b < nblocks; b += FIN_WAVES) {
-                s += pg[(size_t)b * 2 * C + c];
-                q += pg[(size_t)b * 2 * C + C + c];
-            }
+        for (int b = w; b < nblocks; b += FIN_WAVES) {
+            s += part[(size_t)b * 2 * C + c];
+            q += part[(size_t)b * 2 * C + C + c];
         }
-        if (gi) __syncthreads();                             // the previous group's combine read red
-        red[0][w][lane] = s;
-        red[1][w][lane] = q;
-        __syncthreads();
-        if (w == 0 && c < C) {
-            s = 0.0;
-            q = 0.0;
-            for (int k = 0; k < FIN_WAVES; ++k) {
-                s += red[0][k][lane];
-                q += red[1][k][lane];
-            }
-            const double n = (double)npx;
-            const double md = s / n;                              // mean of (y - shift)
-            double var = q / n - md * md;
-            if (var < 0) var = 0;
-            const float mean = (float)(md + (double)tof<T>(y[(size_t)gi * npx * C + c]));
-            float* sg = stat + (size_t)gi * 2 * C;
-            sg[c] = mean;
-            sg[C + c] = (float)(1.0 / sqrt(var + (double)eps));
-            if (rmean) {
-                rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-                rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(var * n / (n > 1 ? n - 1 : 1));
-            }
-        }
+    }
+    red[0][w][lane] = s;
+    red[1][w][lane] = q;
+    __syncthreads();
+    if (w != 0 || c >= C) return;
+    s = 0.0;
+    q = 0.0;
+    for (int k = 0; k < FIN_WAVES; ++k) {
+        s += red[0][k][lane];
+        q += red[1][k][lane];
+    }
+    const double n = (double)npx;
+    const double md = s / n;                                  // mean of (y - shift)
+    double var = q / n - md * md;
+    if (var < 0) var = 0;
+    const float mean = (float)(md + (double)tof<T>(y[c]));
+    stat[c] = mean;
+    stat[C + c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) {
+        rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+        rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(var * n / (n > 1 ? n - 1 : 1));
     }
 }
 
@@ -199,44 +193,35 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(size_t npx, int C, const 
 }
 
 // dbeta = sum dz, dgamma = sum dz xh (fixed-order over the block partials); red2 = the same
-// for the data-gradient pass.  ng groups in order (partials [group][nblocks][2C], red2 [group][2C]):
-// group 0 sets or accumulates as `accumulate` says, every later group accumulates -- the sums of
-// ng separate calls, in their order
+// for the data-gradient pass
 __global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_bwd_finalize(int nblocks, int C, const float* __restrict__ part,
                                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                                  float* __restrict__ red2, int accumulate, int ng) {
+                                                                  float* __restrict__ red2, int accumulate) {
     __shared__ float red[2][FIN_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
-    for (int gi = 0; gi < ng; ++gi) {
-        const float* pg = part + (size_t)gi * nblocks * 2 * C;
-        float s = 0.f, q = 0.f;
-        if (c < C) {
+    float s = 0.f, q = 0.f;
+    if (c < C) {
 #pragma unroll 8
-            for (int b = w; b < nblocks; b += FIN_WAVES) {
-                s += pg[(size_t)b * 2 * C + c];
-                q += pg[(size_t)b * 2 * C + C + c];
-            }
-        }
-        if (gi) __syncthreads();
-        red[0][w][lane] = s;
-        red[1][w][lane] = q;
-        __syncthreads();
-        if (w == 0 && c < C) {
-            s = 0.f;
-            q = 0.f;
-            for (int k = 0; k < FIN_WAVES; ++k) {
-                s += red[0][k][lane];
-                q += red[1][k][lane];
-            }
-            float* r2 = red2 + (size_t)gi * 2 * C;
-            r2[c] = s;
-            r2[C + c] = q;
-            const int acc = gi ? 1 : accumulate;
-            if (dbeta) dbeta[c] = acc ? dbeta[c] + s : s;
-            if (dgamma) dgamma[c] = acc ? dgamma[c] + q : q;
+        for (int b = w; b < nblocks; b += FIN_WAVES) {
+            s += part[(size_t)b * 2 * C + c];
+            q += part[(size_t)b * 2 * C + C + c];
         }
     }
+    red[0][w][lane] = s;
+    red[1][w][lane] = q;
+    __syncthreads();
+    if (w != 0 || c >= C) return;
+    s = 0.f;
+    q = 0.f;
+    for (int k = 0; k < FIN_WAVES; ++k) {
+        s += red[0][k][lane];
+        q += red[1][k][lane];
+    }
+    red2[c] = s;
+    red2[C + c] = q;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + s : s;
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + q : q;
 }
 
 // dy = gamma rstd / N (N dz - sum dz - xh sum dz xh)
@@ -421,8 +406,8 @@ extern "C" size_t fen_bn_work_floats(int C) { return (size_t)BN_BLOCKS * 2 * C +
 
 // train-mode statistics of ng groups of npx pixels each, one after another in y (NHWC) -> stat
 // [ng][2C] (mean, rstd); running stats updated group by group in order when rmean != NULL.
-// work: ng * fen_bn_work_floats(C) floats.  Two launches whatever ng (the D step's real and fake
-// batches: half the launches of one call per batch, bit-identical results)
+// work: ng * fen_bn_work_floats(C) floats.  The statistics pass is one launch whatever ng (the D
+// step's real and fake batches), the finalize one per group; bit-identical to per-group calls
 extern "C" int fen_bn_stats_n(int dtype, int ng, size_t npx, int C, const void* y, float eps, float momentum,
                               float* stat, float* rmean, float* rvar, float* work, void* stream) {
     if (!y || !stat || !work || npx == 0 || ng < 1 || ng > 65535 || C % 8 || C > 2048 ||
@@ -431,13 +416,17 @@ extern "C" int fen_bn_stats_n(int dtype, int ng, size_t npx, int C, const void* 
     if (dtype == FEN_BF16) {
         hipLaunchKernelGGL(k_bn_stats<bf16>, dim3(BN_BLOCKS, ng), dim3(256), 0, STREAM, npx, C, (const bf16*)y, work);
         FEN_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_bn_finalize<bf16>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C, (const bf16*)y,
-                           work, eps, momentum, stat, rmean, rvar, ng);
+        for (int gi = 0; gi < ng; ++gi)                      // in group order: the running statistics
+            hipLaunchKernelGGL(k_bn_finalize<bf16>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C,
+                               (const bf16*)y + (size_t)gi * npx * C, work + (size_t)gi * BN_BLOCKS * 2 * C, eps, momentum,
+                               stat + (size_t)gi * 2 * C, rmean, rvar);
     } else if (dtype == FEN_F32) {
         hipLaunchKernelGGL(k_bn_stats<float>, dim3(BN_BLOCKS, ng), dim3(256), 0, STREAM, npx, C, (const float*)y, work);
         FEN_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C,
-                           (const float*)y, work, eps, momentum, stat, rmean, rvar, ng);
+        for (int gi = 0; gi < ng; ++gi)
+            hipLaunchKernelGGL(k_bn_finalize<float>, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, npx, C,
+                               (const float*)y + (size_t)gi * npx * C, work + (size_t)gi * BN_BLOCKS * 2 * C, eps, momentum,
+                               stat + (size_t)gi * 2 * C, rmean, rvar);
     } else {
         return FEN_EINVAL;
     }
@@ -500,8 +489,8 @@ extern "C" int fen_bn_apply(int dtype, size_t npx, int C, const void* y, const f
 
 // backward of out = lrelu(BN_train(y)) for ng groups of npx pixels (da / y / dy one group after
 // another, stat [ng][2C]): dy from da; dgamma / dbeta = the groups' sums in order (group 0 set or
-// accumulated as `accumulate` says).  work: ng * fen_bn_work_floats(C) floats.  Three launches
-// whatever ng; bit-identical to ng calls of fen_bn_bwd with accumulate = (g > 0 || accumulate)
+// accumulated as `accumulate` says).  work: ng * fen_bn_work_floats(C) floats.  The reduce and
+// apply passes one launch whatever ng, the finalize one per group; bit-identical to ng calls of fen_bn_bwd with accumulate = (g > 0 || accumulate)
 extern "C" int fen_bn_bwd_n(int dtype, int ng, size_t npx, int C, const void* da, const void* y, const float* stat,
                             const float* gamma, const float* beta, float slope, void* dy, float* dgamma, float* dbeta,
                             int accumulate, float* work, void* stream) {
@@ -516,8 +505,10 @@ extern "C" int fen_bn_bwd_n(int dtype, int ng, size_t npx, int C, const void* da
         hipLaunchKernelGGL(k_bn_bwd_reduce<float>, dim3(BN_BLOCKS, ng), dim3(256), 0, STREAM, npx, C, (const float*)da,
                            (const float*)y, stat, gamma, beta, slope, work);
     FEN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, C, work, dgamma, dbeta, red2,
-                       accumulate, ng);
+    for (int gi = 0; gi < ng; ++gi)                          // in group order: dgamma / dbeta accumulate
+        hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, STREAM, BN_BLOCKS, C,
+                           work + (size_t)gi * BN_BLOCKS * 2 * C, dgamma, dbeta, red2 + (size_t)gi * 2 * C,
+                           gi ? 1 : accumulate);
     FEN_CHECK_LAUNCH();
     const int G = C / (dtype == FEN_F32 ? 4 : 8);
     if (G <= 256 && 256 % G == 0) {
@@ -685,38 +676,54 @@ __device__ __forceinline__ void st_nt4(float* p, const float4& v) {
     __builtin_nontemporal_store((f32x4){v.x, v.y, v.z, v.w}, (f32x4*)p);
 }
 
-__global__ __launch_bounds__(256) void k_dhead_mm(int B, int K, int N, int kc, const float* __restrict__ x,
+// NBB sample blocks of 16 per pass (bb0 .. bb0 + NBB - 1), their accumulators side by side: the
+// weight rows stream from HBM once per pass -- once per launch for B <= 16 * DH_MAXBB (the D
+// step's real + fake batches: 32 samples; one pass per 16 samples read the 128-MB weight twice)
+constexpr int DH_MAXBB = 2;
+template <int NBB>
+__global__ __launch_bounds__(256) void k_dhead_mm(int B, int K, int N, int kc, int bb0, const float* __restrict__ x,
                                                   const float* __restrict__ w1, float* __restrict__ part) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 15, q = lane >> 4;
     const int n0 = (blockIdx.x * 4 + wave) * 16;
     const int s = blockIdx.y;
     const int k0 = s * kc;
-    const int nbb = (B + 15) >> 4;
     const float* wrow = w1 + (size_t)(n0 + r) * K + k0 + 4 * q;
-    for (int bb = 0; bb < nbb; ++bb) {
-        const int b = bb * 16 + r;
-        const float* xrow = x + (size_t)(b < B ? b : 0) * K + k0 + 4 * q;
-        const float xm = b < B ? 1.f : 0.f;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        // 8 k-steps of loads in flight per wave (the weight streams from HBM once)
-        for (int k = 0; k < kc; k += 16 * DH_UNR) {
-            float4 wv[DH_UNR], xv[DH_UNR];
+    const float* xrow[NBB];
+    float xm[NBB];
+    f32x4 acc[NBB];
 #pragma unroll
-            for (int u = 0; u < DH_UNR; ++u) {
-                wv[u] = ld_nt4(wrow + k + 16 * u);
-                xv[u] = *(const float4*)(xrow + k + 16 * u);
-            }
+    for (int i = 0; i < NBB; ++i) {
+        const int b = (bb0 + i) * 16 + r;
+        xrow[i] = x + (size_t)(b < B ? b : 0) * K + k0 + 4 * q;
+        xm[i] = b < B ? 1.f : 0.f;
+        acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // DH_UNR k-steps of loads in flight per wave
+    for (int k = 0; k < kc; k += 16 * DH_UNR) {
+        float4 wv[DH_UNR], xv[NBB][DH_UNR];
 #pragma unroll
-            for (int u = 0; u < DH_UNR; ++u) {
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].x, xv[u].x * xm, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].y, xv[u].y * xm, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].z, xv[u].z * xm, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].w, xv[u].w * xm, acc, 0, 0, 0);
-            }
+        for (int u = 0; u < DH_UNR; ++u) {
+            wv[u] = ld_nt4(wrow + k + 16 * u);
+#pragma unroll
+            for (int i = 0; i < NBB; ++i) xv[i][u] = *(const float4*)(xrow[i] + k + 16 * u);
         }
-        // lane holds D[n0 + 4q + t][b] for t = 0..3
-        if (b < B) *(float4*)(part + ((size_t)s * B + b) * N + n0 + 4 * q) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+#pragma unroll
+        for (int u = 0; u < DH_UNR; ++u)
+#pragma unroll
+            for (int i = 0; i < NBB; ++i) {
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].x, xv[i][u].x * xm[i], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].y, xv[i][u].y * xm[i], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].z, xv[i][u].z * xm[i], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u].w, xv[i][u].w * xm[i], acc[i], 0, 0, 0);
+            }
+    }
+    // lane holds D[n0 + 4q + t][b] for t = 0..3
+#pragma unroll
+    for (int i = 0; i < NBB; ++i) {
+        const int b = (bb0 + i) * 16 + r;
+        if (b < B)
+            *(float4*)(part + ((size_t)s * B + b) * N + n0 + 4 * q) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
     }
 }
 
@@ -926,7 +933,13 @@ extern "C" int fen_dhead_fwd(int B, int K, int N, const float* x, const float* w
     if (!x || !w1 || !b1 || !w2 || !b2 || !pre || !y || !work || B <= 0 || K <= 0 || N <= 0) return FEN_EINVAL;
     if (!dhead_shape_ok(B, K, N)) return FEN_EUNSUPPORTED;
     const int S = dhead_split(K), kc = K / S;
-    hipLaunchKernelGGL(k_dhead_mm, dim3(N / 64, S), dim3(256), 0, STREAM, B, K, N, kc, x, w1, work);
+    const int nbb = (B + 15) >> 4;
+    for (int bb = 0; bb < nbb; bb += DH_MAXBB) {             // one pass for B <= 32
+        if (nbb - bb >= 2)
+            hipLaunchKernelGGL(k_dhead_mm<2>, dim3(N / 64, S), dim3(256), 0, STREAM, B, K, N, kc, bb, x, w1, work);
+        else
+            hipLaunchKernelGGL(k_dhead_mm<1>, dim3(N / 64, S), dim3(256), 0, STREAM, B, K, N, kc, bb, x, w1, work);
+    }
     hipLaunchKernelGGL(k_dhead_fin, dim3(B), dim3(1024), 0, STREAM, B, N, S, work, b1, w2, b2, slope, sigmoid, pre, y);
     FEN_CHECK_LAUNCH();
     return FEN_OK;
