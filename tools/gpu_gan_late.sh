@@ -1,6 +1,6 @@
-# The grouped BN finalizes summing both batches' partials with their loads in flight together
-# (product) vs the library before the round's last GAN changes (base): BN / D / GAN parity, the
-# GAN iteration same box, then the configs[2] / configs[3] kernel breakdowns
+# Late round-6 GAN changes (grouped BN passes, per-batch finalizes, the D head's single weight
+# read) vs a base library built from an earlier commit (make ... OUT=build_var/libfen_hip_base.so):
+# BN / D / GAN parity, the GAN iteration same box, then the configs[2] / configs[3] breakdowns
 set -e
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
